@@ -1,0 +1,349 @@
+// dgs_internal.h -- shared definitions of libdgs.so (MI355X / gfx950).
+//
+// Opaque buffer layouts, the reference-literal arithmetic used by the binning kernels, the
+// fine-cell geometry used for exact culling, and small host helpers.  See DESIGN.md.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "dgs.h"
+
+#define DGS_NO_CONTRACT _Pragma("clang fp contract(off)")
+
+namespace dgs {
+
+// ---------------------------------------------------------------------------------------
+// Constants (config.h:18-20, forward.cu:21)
+// ---------------------------------------------------------------------------------------
+constexpr float kTile = 0.51f;         // BLOCK_SIZE
+constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
+constexpr uint32_t kVersion = 1;
+constexpr uint32_t kGeneral = 0x80000000u;  // entry flag: per-pair exact torus wrap needed
+constexpr uint32_t kIdMask = 0x7fffffffu;
+// Culling threshold on q = X^T A X.  power = -q/2 < -105 makes expf(power) exactly +0 in
+// fp32 (e^-105 < half of the smallest subnormal), so every forward and backward term of such
+// a pair is exactly zero in the reference (all of them carry the factor G); culling them
+// is result-preserving.
+constexpr double kQCut = 210.0;
+constexpr double kCellSlack = 1e-3;  // fraction of a fine cell tolerated outside its bounds
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// ---------------------------------------------------------------------------------------
+// Opaque buffer layout.  Gaussian-side buffer (DGS_BUF_BINNING):
+//   [header 256 B][counts int32[4]][perm int32[P]][cell_gbeg int32[ncells]]
+//   [cell_gend int32[ncells]][entries uint32[E]][bwd_units uint2[bwd_cap]]
+// Sample-side buffer (DGS_BUF_SAMPLE_BINNING):
+//   [header copy 256 B][sorted_sid int32[N]][cell_sbeg int32[ncells]][cell_send int32[ncells]]
+//   [fwd_units uint2[fwd_cap]]
+// ---------------------------------------------------------------------------------------
+struct Header {
+    uint32_t magic, version;
+    int32_t P, D, N, T;
+    int32_t grid[2];
+    float off[2];
+    int32_t n;       // fine cells per tile axis
+    int32_t CT;      // cells per tile = n^D + 1 (the last one is the tile's unculled fallback cell)
+    int32_t ncells;  // T * CT
+    int32_t pad0;
+    int64_t R;       // num_rendered (reference count)
+    int64_t E;       // fine (Gaussian, cell) entries
+    int64_t fwd_cap, bwd_cap;
+    uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gend, o_entries, o_bwd_units, g_bytes;
+    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
+    uint64_t stamp;  // identical in both buffers of one preprocess call
+};
+static_assert(sizeof(Header) <= 256, "header too large");
+constexpr size_t kHeaderBytes = 256;
+
+enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1 };
+
+__host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct Layout {  // byte offsets, computed on the host
+    uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gend, o_entries, o_bwd_units, g_bytes;
+    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
+};
+
+inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64_t fwd_cap,
+                          int64_t bwd_cap) {
+    Layout L;
+    size_t o = kHeaderBytes;
+    L.o_counts = o;    o = align_up(o + 16, 256);
+    L.o_perm = o;      o = align_up(o + 4 * (size_t)P, 256);
+    L.o_cell_gbeg = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_cell_gend = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_entries = o;   o = align_up(o + 4 * (size_t)E + 16, 256);
+    L.o_bwd_units = o; o = align_up(o + 8 * (size_t)bwd_cap, 256);
+    L.g_bytes = o;
+    o = kHeaderBytes;
+    L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);
+    L.o_cell_sbeg = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_cell_send = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_fwd_units = o; o = align_up(o + 8 * (size_t)fwd_cap, 256);
+    L.s_bytes = o;
+    return L;
+}
+
+// Device view of both buffers.
+struct Bins {
+    const Header *h;
+    const int32_t *counts;
+    const int32_t *perm;
+    const int32_t *cell_gbeg, *cell_gend;
+    const uint32_t *entries;
+    const uint2 *bwd_units;
+    const int32_t *sorted_sid;
+    const int32_t *cell_sbeg, *cell_send;
+    const uint2 *fwd_units;
+};
+
+// Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
+// address hipcc emits s_load_* into SGPRs (no VGPRs, no LDS, no vector-memory slot).
+template <typename T>
+__device__ __forceinline__ T sload(const T *p) {
+    return *(const __attribute__((address_space(4))) T *)(p);
+}
+template <>
+__device__ __forceinline__ float4 sload<float4>(const float4 *p) {
+    const float *f = reinterpret_cast<const float *>(p);
+    return make_float4(sload(f), sload(f + 1), sload(f + 2), sload(f + 3));
+}
+template <>
+__device__ __forceinline__ uint2 sload<uint2>(const uint2 *p) {
+    const uint64_t v = *(const __attribute__((address_space(4))) uint64_t *)(p);
+    return make_uint2((uint32_t)v, (uint32_t)(v >> 32));
+}
+
+__device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
+    Bins B;
+    B.h = reinterpret_cast<const Header *>(gb);
+    const uint64_t o_counts = sload(&B.h->o_counts), o_perm = sload(&B.h->o_perm);
+    const uint64_t o_gbeg = sload(&B.h->o_cell_gbeg), o_gend = sload(&B.h->o_cell_gend);
+    const uint64_t o_ent = sload(&B.h->o_entries), o_bu = sload(&B.h->o_bwd_units);
+    const uint64_t o_sorted = sload(&B.h->o_sorted), o_sbeg = sload(&B.h->o_cell_sbeg);
+    const uint64_t o_send = sload(&B.h->o_cell_send), o_fu = sload(&B.h->o_fwd_units);
+    B.counts = reinterpret_cast<const int32_t *>(gb + o_counts);
+    B.perm = reinterpret_cast<const int32_t *>(gb + o_perm);
+    B.cell_gbeg = reinterpret_cast<const int32_t *>(gb + o_gbeg);
+    B.cell_gend = reinterpret_cast<const int32_t *>(gb + o_gend);
+    B.entries = reinterpret_cast<const uint32_t *>(gb + o_ent);
+    B.bwd_units = reinterpret_cast<const uint2 *>(gb + o_bu);
+    B.sorted_sid = reinterpret_cast<const int32_t *>(sb + o_sorted);
+    B.cell_sbeg = reinterpret_cast<const int32_t *>(sb + o_sbeg);
+    B.cell_send = reinterpret_cast<const int32_t *>(sb + o_send);
+    B.fwd_units = reinterpret_cast<const uint2 *>(sb + o_fu);
+    return B;
+}
+
+// Wave index of this thread, provably uniform (readfirstlane), with the bijective XCD-aware
+// block remap (cdna_hip_programming.md T1): consecutive units -- neighbouring cells that
+// share Gaussians -- run on one XCD and share its L2.  Kernels grid-stride by
+// gridDim.x * kWavesPerBlock from here.
+__device__ __forceinline__ int wave_unit_index() {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    const int bb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    return bb * kWavesPerBlock + w;
+}
+
+// ---------------------------------------------------------------------------------------
+// Reference-literal arithmetic (binning).  hipcc inlines the __f*_rn intrinsics into plain
+// operators, which -ffp-contract=fast would then fuse into FMAs (measured: 28 % of 1e5
+// determinants differed by an ulp), so every function here also turns contraction off.
+// ---------------------------------------------------------------------------------------
+// float -> int like CUDA's cvt.{rzi,rmi,rpi}.s32.f32: saturating, NaN -> 0.
+__host__ __device__ inline int sat_int(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483647.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)v;
+}
+
+// IEEE single operations, never fused.  Not the __f*_rn intrinsics: they are OCML bitcode
+// whose instructions carry `contract` flags and fuse after inlining whatever the caller's
+// pragma.  sqrt and division go through double: double rounding through 53 >= 2*24+2 bits
+// is innocuous for + - * / sqrt, and the device's f64 sqrt is correctly rounded while its
+// f32 sqrt is not (tools/diag_radius.hip: 16 % of 1e5 results one ulp off).
+__device__ __forceinline__ float rsub(float a, float b) { DGS_NO_CONTRACT return a - b; }
+__device__ __forceinline__ float radd(float a, float b) { DGS_NO_CONTRACT return a + b; }
+__device__ __forceinline__ float rmul(float a, float b) { DGS_NO_CONTRACT return a * b; }
+__device__ __forceinline__ float rdiv(float a, float b) { return (float)((double)a / (double)b); }
+__device__ __forceinline__ float rsqrt_cr(float a) { return (float)__builtin_sqrt((double)a); }
+
+// forward.cu:52-61 (called only when not skipped by det == 0)
+__device__ inline float ref_radius(int D, const float *cov) {
+    DGS_NO_CONTRACT
+    if (D == 1) return (float)(3.0 * (double)rsqrt_cr(cov[0]));
+    const float det = rsub(rmul(cov[0], cov[2]), rmul(cov[1], cov[1]));
+    const float mid = rmul(0.5f, radd(cov[0], cov[2]));
+    const float disc = rsub(rmul(mid, mid), det);
+    const double fl = fmax(1e-6, (double)disc);
+    const float lambda = (float)((double)mid + sqrt(fl));
+    return (float)(3.0 * (double)rsqrt_cr(lambda));
+}
+
+// auxiliary.h:21-31 (TORUS)
+__device__ inline void ref_rect(int D, const float *p, float r, const float *off, int *rmin,
+                                int *rmax) {
+    DGS_NO_CONTRACT
+    for (int i = 0; i < D; ++i) {
+        const float d = rsub(p[i], off[i]);
+        rmin[i] = sat_int(floorf(rdiv(rsub(d, r), kTile)));
+        rmax[i] = sat_int(ceilf(rdiv(radd(d, r), kTile)));
+    }
+}
+
+// forward.cu:24-83: returns tiles touched and the stored radius (0 = Gaussian skipped).
+__device__ inline uint32_t ref_touched(int D, const float *mean, const float *cov,
+                                       const int *grid, const float *off, float *radius) {
+    DGS_NO_CONTRACT
+    *radius = 0.0f;
+    if (D == 2) {
+        const float det = rsub(rmul(cov[0], cov[2]), rmul(cov[1], cov[1]));
+        if (det == 0.0f) return 0;
+    }
+    const float r = ref_radius(D, cov);
+    int rmin[2], rmax[2];
+    ref_rect(D, mean, r, off, rmin, rmax);
+    int t0 = rmax[0] - rmin[0];
+    t0 = t0 < grid[0] ? t0 : grid[0];
+    uint32_t touched;
+    if (D == 1) {
+        touched = (uint32_t)t0;
+    } else {
+        int t1 = rmax[1] - rmin[1];
+        t1 = t1 < grid[1] ? t1 : grid[1];
+        touched = (uint32_t)(t1 * t0);
+    }
+    if (touched == 0) return 0;
+    *radius = r;
+    return touched;
+}
+
+__host__ __device__ inline int wrap_tile(int x, int g) { return x < 0 ? (g + (x % g)) : (x % g); }
+
+// sampler_impl.cu:54-129: the tile-key rectangle of one Gaussian (after the full-range rule).
+struct KeyRect {
+    int x0, x1, y0, y1;
+};
+__device__ inline KeyRect ref_key_rect(int D, const float *mean, float r, const int *grid,
+                                       const float *off) {
+    int rmin[2], rmax[2];
+    ref_rect(D, mean, r, off, rmin, rmax);
+    KeyRect k;
+    if (rmax[0] - rmin[0] >= grid[0]) { rmin[0] = 0; rmax[0] = grid[0]; }
+    k.x0 = rmin[0]; k.x1 = rmax[0];
+    k.y0 = 0; k.y1 = 1;
+    if (D == 2) {
+        if (rmax[1] - rmin[1] >= grid[1]) { rmin[1] = 0; rmax[1] = grid[1]; }
+        k.y0 = rmin[1]; k.y1 = rmax[1];
+    }
+    return k;
+}
+__device__ inline uint32_t key_of(int D, int x, int y, const int *grid) {
+    if (D == 1) return (uint32_t)wrap_tile(x, grid[0]);
+    return (uint32_t)(wrap_tile(y, grid[1]) * grid[0] + wrap_tile(x, grid[0]));
+}
+
+// sampler_impl.cu:155-189
+__device__ inline uint32_t ref_sample_key(int D, const float *s, const int *grid,
+                                          const float *off) {
+    DGS_NO_CONTRACT
+    uint32_t tile[2] = {0, 0};
+    for (int i = 0; i < D; ++i) {
+        int t = sat_int(rdiv(rsub(s[i], off[i]), kTile));
+        t = t < 0 ? 0 : t;
+        t = t > grid[i] ? grid[i] : t;
+        tile[i] = (uint32_t)t;
+    }
+    return D == 1 ? tile[0] : tile[1] * (uint32_t)grid[0] + tile[0];
+}
+
+// forward.cu:149-157: exact period-2 wrap of one displacement (general path only).
+__device__ __forceinline__ float ref_wrap(float x) {
+    DGS_NO_CONTRACT
+    if (fabsf(x) > 1.0f) {
+        const float ax = fabsf(x);
+        // |x| in (1, 2): fmod(x, 2) == x, so the result x -/+ 2 is exact in float.
+        float r = ax < 2.0f ? ax : fmodf(ax, 2.0f);
+        r = r - 2.0f;  // correctly rounded, same as the double computation rounded once
+        x = x >= 0.0f ? r : -r;
+    }
+    return x;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fine-cell geometry.  Every reference tile is cut into n x n (D=2) or n (D=1) fine cells
+// plus one unculled fallback cell for samples that lie outside their tile's nominal area
+// (the reference's clamp-to-grid aliasing, sampler_impl.cu:169).  Cell id = tile*CT + local.
+// ---------------------------------------------------------------------------------------
+struct Geom {
+    int D, T, n, CT, ncells;
+    int grid[2];
+    float off[2];
+    double fs;  // fine cell size = 0.51f / n
+};
+
+__device__ inline uint32_t sample_cell(const Geom &G, const float *s) {
+    DGS_NO_CONTRACT
+    const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
+    if (key >= (uint32_t)G.T) return (uint32_t)G.ncells;  // never rendered
+    const int tx = G.D == 1 ? (int)key : (int)(key % (uint32_t)G.grid[0]);
+    const int ty = G.D == 1 ? 0 : (int)(key / (uint32_t)G.grid[0]);
+    const int tc[2] = {tx, ty};
+    int f[2] = {0, 0};
+    for (int i = 0; i < G.D; ++i) {
+        const double d = (double)rsub(s[i], G.off[i]);
+        const double u = (d - (double)tc[i] * (double)kTile) / G.fs;
+        int fi = (int)floor(u);
+        if (fi < 0) {
+            if (u >= -kCellSlack) fi = 0;
+            else return key * (uint32_t)G.CT + (uint32_t)(G.CT - 1);
+        } else if (fi >= G.n) {
+            if (u <= G.n + kCellSlack) fi = G.n - 1;
+            else return key * (uint32_t)G.CT + (uint32_t)(G.CT - 1);
+        }
+        f[i] = fi;
+    }
+    return key * (uint32_t)G.CT + (uint32_t)(f[1] * G.n + f[0]);
+}
+
+// ---------------------------------------------------------------------------------------
+// Host-side launch hints.  preprocess records the exact work-unit counts of the buffers it
+// created; forward/backward size their grids from them.  The kernels grid-stride over the
+// device-side counts, so a missing or stale hint only costs speed, never correctness.
+// ---------------------------------------------------------------------------------------
+struct UnitHint {
+    const void *gbuf, *sbuf;
+    size_t gbytes, sbytes;
+    int64_t nfwd, nbwd;
+};
+void hint_put(const UnitHint &h);
+bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);
+
+// ---------------------------------------------------------------------------------------
+// Host-side error state
+// ---------------------------------------------------------------------------------------
+void set_error(const std::string &msg);
+int fail(int code, const std::string &msg);
+int check_hip(hipError_t e, const char *what);
+
+}  // namespace dgs
+
+#define DGS_TRY_HIP(expr)                                                        \
+    do {                                                                         \
+        int _rc = ::dgs::check_hip((expr), #expr);                               \
+        if (_rc) return _rc;                                                     \
+    } while (0)
+
+// Launch check; with debug, synchronise and surface asynchronous faults (auxiliary.h:33-40).
+#define DGS_LAUNCH_CHECK(stream, debug)                                          \
+    do {                                                                         \
+        DGS_TRY_HIP(hipGetLastError());                                          \
+        if (debug) DGS_TRY_HIP(hipStreamSynchronize(stream));                    \
+    } while (0)

@@ -1,0 +1,658 @@
+// dgs_preprocess.hip -- binning for the MI355X Gaussian sampler.
+//
+// Replaces PreprocessCUDA (sample_points.cu:38-98) and CudaSampler::Sampler::preprocess
+// (sampler_impl.cu:216-330).  The reference bins Gaussians into 0.51-wide tiles and renders
+// every (Gaussian, sample) pair of a tile -- 16 workgroups for a [-1,1)^2 domain.  Here the
+// reference tile membership is reproduced exactly (radius, rect, torus wrap, clamp rules;
+// num_rendered, radii, ranges are bit-identical), and each tile is refined into fine cells:
+// a Gaussian is listed in a cell only if some sample of the cell can see a non-zero
+// contribution (q = X^T A X <= 210, i.e. expf(power) != 0 in fp32).  Culled pairs are
+// exactly-zero pairs of the reference, so the sums are unchanged.
+//
+// Work lists produced here (see dgs_internal.h for the layout):
+//   * samples sorted by fine cell, per-cell sample ranges, forward work units (cell, 64 samples)
+//   * Gaussians renumbered by spatial home cell (perm), per-cell Gaussian lists in ascending
+//     internal id, backward work units (cell, 64 list entries)
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "dgs_internal.h"
+
+namespace dgs {
+
+// ------------------------------------------------------------------------------ errors
+static thread_local std::string g_last_error;
+void set_error(const std::string &msg) { g_last_error = msg; }
+int fail(int code, const std::string &msg) {
+    g_last_error = msg;
+    return code;
+}
+int check_hip(hipError_t e, const char *what) {
+    if (e == hipSuccess) return DGS_OK;
+    g_last_error = std::string("HIP error ") + hipGetErrorString(e) + " at " + what;
+    return DGS_ERR_HIP;
+}
+
+// ------------------------------------------------------------------------ launch hints
+static std::mutex g_hint_mu;
+static std::unordered_map<const void *, UnitHint> g_hints;
+void hint_put(const UnitHint &h) {
+    std::lock_guard<std::mutex> lk(g_hint_mu);
+    if (g_hints.size() > 4096) g_hints.clear();
+    g_hints[h.gbuf] = h;
+}
+bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out) {
+    std::lock_guard<std::mutex> lk(g_hint_mu);
+    auto it = g_hints.find(gbuf);
+    if (it == g_hints.end()) return false;
+    const UnitHint &h = it->second;
+    if (h.sbuf != sbuf || h.gbytes != gbytes || h.sbytes != sbytes) return false;
+    *out = h;
+    return true;
+}
+
+static int bit_length(uint64_t v) {
+    int b = 0;
+    while (v) { ++b; v >>= 1; }
+    return b < 1 ? 1 : b;
+}
+
+// ------------------------------------------------------------------------- tile grid
+// sample_points.cu:70-74 with torch's CUDA arithmetic (division by a CPU scalar is a
+// multiplication by the float reciprocal in ATen's div_true_kernel_cuda).
+__global__ void k_bounds_partial(int N, int D, const float *__restrict__ s, float *part) {
+    __shared__ float smin[2][kBlock], smax[2][kBlock];
+    float mn[2] = {INFINITY, INFINITY}, mx[2] = {-INFINITY, -INFINITY};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
+         i += (int64_t)gridDim.x * blockDim.x)
+        for (int d = 0; d < D; ++d) {
+            const float v = s[i * D + d];
+            mn[d] = fminf(mn[d], v);
+            mx[d] = fmaxf(mx[d], v);
+        }
+    for (int d = 0; d < 2; ++d) { smin[d][threadIdx.x] = mn[d]; smax[d][threadIdx.x] = mx[d]; }
+    __syncthreads();
+    for (int st = kBlock / 2; st > 0; st >>= 1) {
+        if ((int)threadIdx.x < st)
+            for (int d = 0; d < 2; ++d) {
+                smin[d][threadIdx.x] = fminf(smin[d][threadIdx.x], smin[d][threadIdx.x + st]);
+                smax[d][threadIdx.x] = fmaxf(smax[d][threadIdx.x], smax[d][threadIdx.x + st]);
+            }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0)
+        for (int d = 0; d < 2; ++d) {
+            part[blockIdx.x * 4 + d] = smin[d][0];
+            part[blockIdx.x * 4 + 2 + d] = smax[d][0];
+        }
+}
+
+__global__ void k_bounds_final(int nparts, int D, const float *part, int *grid, float *off) {
+    if (threadIdx.x != 0) return;
+    for (int d = 0; d < D; ++d) {
+        float mn = INFINITY, mx = -INFINITY;
+        for (int p = 0; p < nparts; ++p) {
+            mn = fminf(mn, part[p * 4 + d]);
+            mx = fmaxf(mx, part[p * 4 + 2 + d]);
+        }
+        const float ext = radd(rsub(mx, mn), 1e-6f);
+        const float inv = rdiv(1.0f, kTile);
+        grid[d] = (int)ceilf(rmul(ext, inv));
+        off[d] = mn;
+    }
+}
+
+// ---------------------------------------------------------------------- sample binning
+__global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
+                               uint32_t *__restrict__ keys, uint32_t *__restrict__ ids,
+                               uint32_t *__restrict__ tile_count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= N) return;
+    float s[2] = {samples[i * G.D], G.D == 2 ? samples[i * G.D + 1] : 0.0f};
+    const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
+    if (key < (uint32_t)G.T) atomicAdd(&tile_count[key], 1u);
+    keys[i] = sample_cell(G, s);
+    ids[i] = (uint32_t)i;
+}
+
+// identifyTileRanges (sampler_impl.cu:134-151) over sorted cell keys; keys >= limit ignored.
+__global__ void k_identify(int64_t L, const uint32_t *__restrict__ keys, uint32_t limit,
+                           int32_t *__restrict__ beg, int32_t *__restrict__ end) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= L) return;
+    const uint32_t k = keys[i];
+    if (i == 0) {
+        if (k < limit) beg[k] = 0;
+    } else {
+        const uint32_t p = keys[i - 1];
+        if (k != p) {
+            if (p < limit) end[p] = (int32_t)i;
+            if (k < limit) beg[k] = (int32_t)i;
+        }
+    }
+    if (i == L - 1 && k < limit) end[k] = (int32_t)L;
+}
+
+// ------------------------------------------------------------------- Gaussian binning
+// forward.cu:24-83 (radius, tiles touched) + the reference tile counts + spatial home key.
+__global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
+                             const float *__restrict__ covs, float *__restrict__ radii,
+                             uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
+                             uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
+                             int home_w, int home_h) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int D = G.D, S = D * (D + 1) / 2;
+    float m[2] = {means[i * D], D == 2 ? means[i * D + 1] : 0.0f};
+    float cv[3] = {covs[i * S], D == 2 ? covs[i * S + 1] : 0.0f, D == 2 ? covs[i * S + 2] : 0.0f};
+    float r;
+    const uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
+    radii[i] = r;
+    touched[i] = t;
+    ids[i] = (uint32_t)i;
+    if (!(r > 0.0f)) {
+        home[i] = 0xffffffffu;
+        return;
+    }
+    const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
+    for (int y = kr.y0; y < kr.y1; ++y)
+        for (int x = kr.x0; x < kr.x1; ++x) {
+            const uint32_t key = key_of(D, x, y, G.grid);
+            if (key < (uint32_t)G.T) atomicAdd(&tile_count[key], 1u);
+        }
+    int h[2] = {0, 0};
+    const int lim[2] = {home_w, home_h};
+    for (int d = 0; d < D; ++d) {
+        const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
+        int v = (u == u) ? (int)floor(fmin(fmax(u, -1.0), (double)lim[d])) : 0;
+        h[d] = v < 0 ? 0 : (v >= lim[d] ? lim[d] - 1 : v);
+    }
+    home[i] = (uint32_t)(h[1] * home_w + h[0]);
+}
+
+// Does [xa, xb] x [ya, yb] contain an X with X^T A X <= qcut?  (convex quadratic: the
+// minimum over a box is at the origin if inside, else on an edge at the clamped critical point)
+__device__ inline bool box_hits_ellipse(double xa, double xb, double ya, double yb, double c0,
+                                        double c1, double c2, double qcut) {
+    if (xa <= 0.0 && xb >= 0.0 && ya <= 0.0 && yb >= 0.0) return true;
+    double best = INFINITY;
+    const double xs[2] = {xa, xb}, ys[2] = {ya, yb};
+    for (int k = 0; k < 2; ++k) {
+        const double x = xs[k];
+        const double y = fmin(fmax(-c1 * x / c2, ya), yb);
+        best = fmin(best, c0 * x * x + 2.0 * c1 * x * y + c2 * y * y);
+        const double yy = ys[k];
+        const double xx = fmin(fmax(-c1 * yy / c0, xa), xb);
+        best = fmin(best, c0 * xx * xx + 2.0 * c1 * xx * yy + c2 * yy * yy);
+    }
+    return best <= qcut * (1.0 + 1e-6) + 1e-12;
+}
+
+// Enumerate the fine entries (cell, id|flag) of one Gaussian, in the reference's tile-key
+// order (sampler_impl.cu:94-124), restricted to non-empty cells that pass the exact cull.
+template <class Emit>
+__device__ inline void enumerate_fine(const Geom &G, const float *m, float r, const float *con,
+                                      const int32_t *__restrict__ sbeg,
+                                      const int32_t *__restrict__ send, uint32_t id, Emit emit) {
+    const int D = G.D;
+    const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
+    const double c0 = con[0], c1 = D == 2 ? con[1] : 0.0, c2 = D == 2 ? con[2] : 0.0;
+    double e[2] = {INFINITY, INFINITY};
+    bool pd;
+    if (D == 1) {
+        pd = c0 > 0.0 && c0 < INFINITY;
+        if (pd) e[0] = sqrt(kQCut / c0) * (1.0 + 1e-6);
+    } else {
+        const double det = c0 * c2 - c1 * c1;
+        pd = c0 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY;
+        if (pd) {
+            e[0] = sqrt(kQCut * c2 / det) * (1.0 + 1e-6);
+            e[1] = sqrt(kQCut * c0 / det) * (1.0 + 1e-6);
+        }
+    }
+    const bool cull = pd && e[0] < 0.5 && (D == 1 || e[1] < 0.5);
+    const double slack = kCellSlack * G.fs;
+    double md[2], epsx[2];
+    for (int d = 0; d < 2; ++d) {
+        md[d] = d < D ? (double)m[d] - (double)G.off[d] : 0.0;
+        epsx[d] = 1e-6 * (1.0 + fabs((double)m[d]) + fabs((double)G.off[d]));
+    }
+    const double BS = (double)kTile;
+    for (int y = kr.y0; y < kr.y1; ++y)
+        for (int x = kr.x0; x < kr.x1; ++x) {
+            const uint32_t key = key_of(D, x, y, G.grid);
+            if (key >= (uint32_t)G.T) continue;
+            const int tc[2] = {D == 1 ? (int)key : (int)(key % (uint32_t)G.grid[0]),
+                               D == 1 ? 0 : (int)(key / (uint32_t)G.grid[0])};
+            const uint32_t base = key * (uint32_t)G.CT;
+            int flo[2] = {0, 0}, fhi[2] = {0, 0}, ks[2] = {0, 0};
+            bool any = true;
+            for (int d = 0; d < D; ++d) {
+                const double o = tc[d] * BS;
+                if (!cull) {
+                    flo[d] = 0;
+                    fhi[d] = G.n - 1;
+                    continue;
+                }
+                const double xa = md[d] - (o + BS + slack) - epsx[d];
+                const double xb = md[d] - (o - slack) + epsx[d];
+                const double klo = ceil((xa - e[d]) * 0.5), khi = floor((xb + e[d]) * 0.5);
+                if (klo > khi) { any = false; break; }
+                ks[d] = (int)klo;  // e < 0.5 and a tile narrower than 1: at most one k
+                const double dl = md[d] - 2.0 * klo - e[d] - epsx[d];
+                const double dh = md[d] - 2.0 * klo + e[d] + epsx[d];
+                int lo = (int)floor(fmax((dl - o) / G.fs - kCellSlack, -1.0));
+                int hi = (int)floor(fmin((dh - o) / G.fs + kCellSlack, (double)G.n));
+                flo[d] = lo < 0 ? 0 : lo;
+                fhi[d] = hi > G.n - 1 ? G.n - 1 : hi;
+                if (flo[d] > fhi[d]) { any = false; break; }
+            }
+            if (any) {
+                const int ylo = D == 2 ? flo[1] : 0, yhi = D == 2 ? fhi[1] : 0;
+                for (int fy = ylo; fy <= yhi; ++fy)
+                    for (int fx = flo[0]; fx <= fhi[0]; ++fx) {
+                        const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
+                        if (send[cell] <= sbeg[cell]) continue;
+                        const int f[2] = {fx, fy};
+                        double xa[2] = {0, 0}, xb[2] = {0, 0};
+                        for (int d = 0; d < D; ++d) {
+                            const double o = tc[d] * BS;
+                            const double dlo = o + f[d] * G.fs - slack, dhi = o + (f[d] + 1) * G.fs + slack;
+                            xa[d] = md[d] - dhi - epsx[d];
+                            xb[d] = md[d] - dlo + epsx[d];
+                        }
+                        if (cull) {
+                            bool hit;
+                            if (D == 1) {
+                                hit = xa[0] - 2.0 * ks[0] <= e[0] && xb[0] - 2.0 * ks[0] >= -e[0];
+                            } else {
+                                hit = box_hits_ellipse(xa[0] - 2.0 * ks[0], xb[0] - 2.0 * ks[0],
+                                                       xa[1] - 2.0 * ks[1], xb[1] - 2.0 * ks[1],
+                                                       c0, c1, c2, kQCut);
+                            }
+                            if (!hit) continue;
+                        }
+                        bool inside = true;
+                        for (int d = 0; d < D; ++d) inside = inside && xa[d] >= -1.0 && xb[d] <= 1.0;
+                        emit(cell, id | (inside ? 0u : kGeneral));
+                    }
+            }
+            const uint32_t fb = base + (uint32_t)(G.CT - 1);
+            if (send[fb] > sbeg[fb]) emit(fb, id | kGeneral);
+        }
+}
+
+__device__ inline void load_gauss(int D, const float *__restrict__ means,
+                                  const float *__restrict__ conics, int64_t g, float *m, float *c) {
+    const int S = D * (D + 1) / 2;
+    m[0] = means[g * D];
+    m[1] = D == 2 ? means[g * D + 1] : 0.0f;
+    c[0] = conics[g * S];
+    c[1] = D == 2 ? conics[g * S + 1] : 0.0f;
+    c[2] = D == 2 ? conics[g * S + 2] : 0.0f;
+}
+
+__global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
+                             const float *__restrict__ means, const float *__restrict__ conics,
+                             const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+                             const int32_t *__restrict__ send, uint64_t *__restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int64_t g = perm[i];
+    const float r = radii[g];
+    uint64_t n = 0;
+    if (r > 0.0f) {
+        float m[2], c[3];
+        load_gauss(G.D, means, conics, g, m, c);
+        enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t, uint32_t) { ++n; });
+    }
+    counts[i] = n;
+}
+
+__global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
+                            const float *__restrict__ means, const float *__restrict__ conics,
+                            const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+                            const int32_t *__restrict__ send, const uint64_t *__restrict__ offs,
+                            uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int64_t g = perm[i];
+    const float r = radii[g];
+    if (!(r > 0.0f)) return;
+    float m[2], c[3];
+    load_gauss(G.D, means, conics, g, m, c);
+    uint64_t o = offs[i];
+    enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
+        ekeys[o] = cell;
+        evals[o] = val;
+        ++o;
+    });
+}
+
+__global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
+                         const uint64_t *__restrict__ rsum, int64_t *__restrict__ out) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    out[0] = (int64_t)rsum[0];
+    out[1] = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;
+}
+
+// ----------------------------------------------------------------------- work units
+__global__ void k_unit_counts(int ncells, const int32_t *__restrict__ sbeg,
+                              const int32_t *__restrict__ send, const int32_t *__restrict__ gbeg,
+                              const int32_t *__restrict__ gend, uint32_t *__restrict__ fcnt,
+                              uint32_t *__restrict__ bcnt) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int ns = send[c] - sbeg[c], ng = gend[c] - gbeg[c];
+    fcnt[c] = (uint32_t)((ns + kWave - 1) / kWave);
+    bcnt[c] = ns > 0 ? (uint32_t)((ng + kWave - 1) / kWave) : 0u;
+}
+
+__global__ void k_unit_fill(int ncells, const int32_t *__restrict__ sbeg,
+                            const int32_t *__restrict__ gbeg, const uint32_t *__restrict__ fcnt,
+                            const uint32_t *__restrict__ bcnt, const uint32_t *__restrict__ foff,
+                            const uint32_t *__restrict__ boff, uint2 *__restrict__ funits,
+                            uint2 *__restrict__ bunits, int32_t *__restrict__ counters) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    for (uint32_t b = 0; b < fcnt[c]; ++b)
+        funits[foff[c] + b] = make_uint2((uint32_t)c, (uint32_t)sbeg[c] + b * kWave);
+    for (uint32_t b = 0; b < bcnt[c]; ++b)
+        bunits[boff[c] + b] = make_uint2((uint32_t)c, (uint32_t)gbeg[c] + b * kWave);
+    if (c == ncells - 1) {
+        counters[kNumFwdUnits] = (int32_t)(foff[c] + fcnt[c]);
+        counters[kNumBwdUnits] = (int32_t)(boff[c] + bcnt[c]);
+    }
+}
+
+// Reference-layout ranges (identifyTileRanges semantics: empty tiles stay (0, 0)).
+__global__ void k_ref_ranges(int T, const uint32_t *__restrict__ cnt, uint2 *__restrict__ ranges) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    uint32_t acc = 0;
+    for (int t = 0; t < T; ++t) {
+        const uint32_t c = cnt[t];
+        ranges[t] = c ? make_uint2(acc, acc + c) : make_uint2(0u, 0u);
+        acc += c;
+    }
+}
+
+__global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
+    const int i = threadIdx.x;
+    const char *src = reinterpret_cast<const char *>(&h);
+    if (i < (int)sizeof(Header)) {
+        gbuf[i] = src[i];
+        sbuf[i] = src[i];
+    }
+}
+
+__global__ void k_copy_u32(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) b[i] = (int32_t)a[i];
+}
+
+static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
+// waves per cell), capped so that cells stay reasonably large for sparse sample sets.
+static int choose_n(int D, int64_t N, int64_t T) {
+    const double per_tile = (double)N / (double)(T > 0 ? T : 1);
+    const double target = 120.0;
+    if (D == 2) {
+        int n = (int)std::lround(std::sqrt(per_tile / target));
+        return std::max(1, std::min(n, 64));
+    }
+    int n = (int)std::lround(per_tile / target);
+    return std::max(1, std::min(n, 1 << 16));
+}
+
+// Scratch allocator: every piece comes from the caller's callback.
+struct Scratch {
+    dgs_alloc_fn fn;
+    void *ctx;
+    int rc = DGS_OK;
+    template <typename T>
+    T *get(size_t count) {
+        if (rc) return nullptr;
+        void *p = fn(ctx, DGS_BUF_SCRATCH, align_up(std::max<size_t>(count * sizeof(T), 16), 256));
+        if (!p) rc = fail(DGS_ERR_ALLOC, "scratch allocation failed");
+        return static_cast<T *>(p);
+    }
+};
+
+}  // namespace dgs
+
+using namespace dgs;
+
+extern "C" const char *dgs_last_error(void) { return g_last_error.c_str(); }
+extern "C" int dgs_version(void) { return (int)kVersion; }
+
+extern "C" int dgs_tile_grid(int N, int D, const float *samples, int *grid_out, float *off_out,
+                             dgs_stream_t stream) {
+    if (N <= 0 || (D != 1 && D != 2) || !samples) return fail(DGS_ERR_ARG, "dgs_tile_grid: bad arguments");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nparts = (int)std::min<int64_t>(1024, grid_for(N));
+    float *part = nullptr;
+    int *dgrid = nullptr;
+    float *doff = nullptr;
+    DGS_TRY_HIP(hipMallocAsync(&part, sizeof(float) * 4 * nparts, s));
+    DGS_TRY_HIP(hipMallocAsync(&dgrid, sizeof(int) * 2, s));
+    DGS_TRY_HIP(hipMallocAsync(&doff, sizeof(float) * 2, s));
+    k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, part);
+    k_bounds_final<<<1, 64, 0, s>>>(nparts, D, part, dgrid, doff);
+    DGS_TRY_HIP(hipGetLastError());
+    int hg[2];
+    float ho[2];
+    DGS_TRY_HIP(hipMemcpyAsync(hg, dgrid, sizeof(int) * D, hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipMemcpyAsync(ho, doff, sizeof(float) * D, hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    DGS_TRY_HIP(hipFreeAsync(part, s));
+    DGS_TRY_HIP(hipFreeAsync(dgrid, s));
+    DGS_TRY_HIP(hipFreeAsync(doff, s));
+    for (int d = 0; d < D; ++d) { grid_out[d] = hg[d]; off_out[d] = ho[d]; }
+    return DGS_OK;
+}
+
+extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
+                              const float *conics, const float *samples, const int *grid,
+                              const float *grid_offset, float *radii, dgs_alloc_fn alloc,
+                              void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream,
+                              int debug) {
+    if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
+    if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
+    *num_rendered = 0;
+    if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
+    if (!grid || !grid_offset) return fail(DGS_ERR_ARG, "dgs_preprocess: grid/offset required");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+
+    Geom G;
+    G.D = D;
+    G.grid[0] = grid[0];
+    G.grid[1] = D == 2 ? grid[1] : 1;
+    G.off[0] = grid_offset[0];
+    G.off[1] = D == 2 ? grid_offset[1] : 0.0f;
+    if (G.grid[0] <= 0 || G.grid[1] <= 0) return fail(DGS_ERR_ARG, "tile grid must be positive");
+    const int64_t T64 = (int64_t)G.grid[0] * G.grid[1];
+    if (T64 > (1 << 24)) return fail(DGS_ERR_ARG, "tile grid too large");
+    G.T = (int)T64;
+    G.n = choose_n(D, N, G.T);
+    G.CT = (D == 2 ? G.n * G.n : G.n) + 1;
+    const int64_t ncells64 = (int64_t)G.T * G.CT;
+    if (ncells64 >= (1LL << 31) - 1) return fail(DGS_ERR_ARG, "too many fine cells");
+    G.ncells = (int)ncells64;
+    G.fs = (double)kTile / G.n;
+    const int ncells = G.ncells;
+    const int home_w = G.grid[0] * G.n, home_h = D == 2 ? G.grid[1] * G.n : 1;
+
+    // ---- sample-side buffer (size known now) and the reference range buffers
+    const int64_t fwd_cap = (N + kWave - 1) / kWave + std::min<int64_t>(N, ncells) + 1;
+    Layout L0 = make_layout(P, N, ncells, 0, fwd_cap, 0);
+    char *sbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_BINNING, L0.s_bytes));
+    char *rbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_RANGES, (size_t)G.T * 8 + 8));
+    char *srbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_RANGES, (size_t)G.T * 8 + 8));
+    if (!sbuf || !rbuf || !srbuf) return fail(DGS_ERR_ALLOC, "buffer allocation failed");
+    int32_t *sorted_sid = reinterpret_cast<int32_t *>(sbuf + L0.o_sorted);
+    int32_t *cell_sbeg = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_sbeg);
+    int32_t *cell_send = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_send);
+    uint2 *fwd_units = reinterpret_cast<uint2 *>(sbuf + L0.o_fwd_units);
+
+    Scratch S{alloc, alloc_ctx};
+    uint32_t *skeys = S.get<uint32_t>(N), *skeys_sorted = S.get<uint32_t>(N), *sids = S.get<uint32_t>(N);
+    uint32_t *stile = S.get<uint32_t>(G.T + 1), *gtile = S.get<uint32_t>(G.T + 1);
+    uint32_t *home = S.get<uint32_t>(P), *home_sorted = S.get<uint32_t>(P), *gids = S.get<uint32_t>(P);
+    uint32_t *perm = S.get<uint32_t>(P);
+    uint64_t *touched = S.get<uint64_t>(P), *fcount = S.get<uint64_t>(P), *foffs = S.get<uint64_t>(P);
+    uint64_t *rsum = S.get<uint64_t>(1);
+    int64_t *totals = S.get<int64_t>(2);
+    if (S.rc) return S.rc;
+
+    // hipcub temp storage: one allocation sized for the largest phase-A primitive
+    size_t t_ssort = 0, t_hsort = 0, t_scan = 0, t_red = 0;
+    const int sbits = bit_length((uint64_t)ncells);
+    const int hbits = 32;  // home keys may be 0xffffffff for absent Gaussians
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_ssort, skeys, skeys_sorted, sids,
+                                                   (uint32_t *)sorted_sid, N, 0, sbits, s));
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_hsort, home, home_sorted, gids,
+                                                   perm, P, 0, hbits, s));
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, fcount, foffs, P, s));
+    DGS_TRY_HIP(hipcub::DeviceReduce::Sum(nullptr, t_red, touched, rsum, P, s));
+    const size_t t_a = std::max(std::max(t_ssort, t_hsort), std::max(t_scan, t_red));
+    void *tmp_a = S.get<char>(t_a);
+    if (S.rc) return S.rc;
+
+    DGS_TRY_HIP(hipMemsetAsync(stile, 0, sizeof(uint32_t) * (G.T + 1), s));
+    DGS_TRY_HIP(hipMemsetAsync(gtile, 0, sizeof(uint32_t) * (G.T + 1), s));
+    DGS_TRY_HIP(hipMemsetAsync(cell_sbeg, 0, sizeof(int32_t) * ncells, s));
+    DGS_TRY_HIP(hipMemsetAsync(cell_send, 0, sizeof(int32_t) * ncells, s));
+
+    // ---- samples: fine cell keys, stable radix sort, per-cell ranges
+    k_sample_cells<<<grid_for(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
+    DGS_LAUNCH_CHECK(s, debug);
+    size_t tb = t_a;
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, skeys, skeys_sorted, sids,
+                                                   (uint32_t *)sorted_sid, N, 0, sbits, s));
+    DGS_LAUNCH_CHECK(s, debug);
+    k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send);
+    DGS_LAUNCH_CHECK(s, debug);
+
+    // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
+    k_gauss_prep<<<grid_for(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
+                                                home, gids, home_w, home_h);
+    DGS_LAUNCH_CHECK(s, debug);
+    tb = t_a;
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
+                                                   hbits, s));
+    DGS_LAUNCH_CHECK(s, debug);
+    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
+                                                cell_send, fcount);
+    DGS_LAUNCH_CHECK(s, debug);
+    tb = t_a;
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, fcount, foffs, P, s));
+    tb = t_a;
+    DGS_TRY_HIP(hipcub::DeviceReduce::Sum(tmp_a, tb, touched, rsum, P, s));
+    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, rsum, totals);
+    DGS_LAUNCH_CHECK(s, debug);
+    int64_t htot[2] = {0, 0};
+    DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));  // the one host sync: num_rendered is a Python int
+    const int64_t R = htot[0], E = htot[1];
+    *num_rendered = R;
+    if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries");
+
+    // ---- Gaussian-side buffer
+    const int64_t bwd_cap = (E + kWave - 1) / kWave + std::min<int64_t>(E, ncells) + 1;
+    Layout L = make_layout(P, N, ncells, E, fwd_cap, bwd_cap);
+    char *gbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_BINNING, L.g_bytes));
+    if (!gbuf) return fail(DGS_ERR_ALLOC, "binning buffer allocation failed");
+    int32_t *counters = reinterpret_cast<int32_t *>(gbuf + L.o_counts);
+    int32_t *gperm = reinterpret_cast<int32_t *>(gbuf + L.o_perm);
+    int32_t *cell_gbeg = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gbeg);
+    int32_t *cell_gend = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gend);
+    uint32_t *entries = reinterpret_cast<uint32_t *>(gbuf + L.o_entries);
+    uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
+
+    uint32_t *ekeys = S.get<uint32_t>(E + 1), *evals = S.get<uint32_t>(E + 1);
+    uint32_t *ekeys_sorted = S.get<uint32_t>(E + 1);
+    uint32_t *fcnt = S.get<uint32_t>(ncells), *bcnt = S.get<uint32_t>(ncells);
+    uint32_t *foff = S.get<uint32_t>(ncells), *boff = S.get<uint32_t>(ncells);
+    if (S.rc) return S.rc;
+    size_t t_esort = 0, t_cscan = 0;
+    const int ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1));
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_esort, ekeys, ekeys_sorted, evals,
+                                                   entries, (int)E, 0, ebits, s));
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_cscan, fcnt, foff, ncells, s));
+    void *tmp_b = S.get<char>(std::max(t_esort, t_cscan));
+    if (S.rc) return S.rc;
+
+    DGS_TRY_HIP(hipMemsetAsync(counters, 0, 16, s));
+    DGS_TRY_HIP(hipMemsetAsync(cell_gbeg, 0, sizeof(int32_t) * ncells, s));
+    DGS_TRY_HIP(hipMemsetAsync(cell_gend, 0, sizeof(int32_t) * ncells, s));
+    k_copy_u32<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
+    DGS_LAUNCH_CHECK(s, debug);
+    if (E > 0) {
+        k_fine_fill<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
+                                                   cell_send, foffs, ekeys, evals);
+        DGS_LAUNCH_CHECK(s, debug);
+        tb = std::max(t_esort, t_cscan);
+        DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,
+                                                       entries, (int)E, 0, ebits, s));
+        DGS_LAUNCH_CHECK(s, debug);
+        k_identify<<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, (uint32_t)ncells, cell_gbeg, cell_gend);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
+    k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
+                                                      cell_gend, fcnt, bcnt);
+    DGS_LAUNCH_CHECK(s, debug);
+    tb = std::max(t_esort, t_cscan);
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, fcnt, foff, ncells, s));
+    tb = std::max(t_esort, t_cscan);
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, bcnt, boff, ncells, s));
+    k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
+                                                    boff, fwd_units, bwd_units, counters);
+    DGS_LAUNCH_CHECK(s, debug);
+
+    // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled)
+    DGS_TRY_HIP(hipMemsetAsync(rbuf, 0, (size_t)G.T * 8 + 8, s));
+    DGS_TRY_HIP(hipMemsetAsync(srbuf, 0, (size_t)G.T * 8 + 8, s));
+    k_ref_ranges<<<1, 64, 0, s>>>(G.T, gtile, reinterpret_cast<uint2 *>(rbuf));
+    k_ref_ranges<<<1, 64, 0, s>>>(G.T, stile, reinterpret_cast<uint2 *>(srbuf));
+    DGS_LAUNCH_CHECK(s, debug);
+
+    // ---- headers
+    static std::atomic<uint64_t> stamp_counter{0x5eed0000ull};
+    Header h;
+    std::memset(&h, 0, sizeof(h));
+    h.magic = kMagic;
+    h.version = kVersion;
+    h.P = P; h.D = D; h.N = N; h.T = G.T;
+    h.grid[0] = G.grid[0]; h.grid[1] = G.grid[1];
+    h.off[0] = G.off[0]; h.off[1] = G.off[1];
+    h.n = G.n; h.CT = G.CT; h.ncells = ncells;
+    h.R = R; h.E = E;
+    h.fwd_cap = fwd_cap; h.bwd_cap = bwd_cap;
+    h.o_counts = L.o_counts; h.o_perm = L.o_perm; h.o_cell_gbeg = L.o_cell_gbeg;
+    h.o_cell_gend = L.o_cell_gend; h.o_entries = L.o_entries; h.o_bwd_units = L.o_bwd_units;
+    h.g_bytes = L.g_bytes;
+    h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
+    h.o_fwd_units = L0.o_fwd_units; h.s_bytes = L0.s_bytes;
+    h.stamp = ++stamp_counter;
+    k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
+    DGS_LAUNCH_CHECK(s, debug);
+
+    // exact unit counts for the launch-size hint (second and last host sync)
+    int32_t hc[2] = {0, 0};
+    DGS_TRY_HIP(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    UnitHint uh;
+    uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
+    uh.nfwd = hc[kNumFwdUnits]; uh.nbwd = hc[kNumBwdUnits];
+    hint_put(uh);
+    return DGS_OK;
+}

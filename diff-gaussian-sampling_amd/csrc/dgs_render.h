@@ -1,0 +1,264 @@
+// dgs_render.h -- per-pair math of the four sampling functions (forward and backward) and
+// the packed row formats of the render kernels.
+//
+// Row formats (fp32, written per call by the pack kernels, read wave-uniformly through the
+// scalar cache in the forward and per lane in the backward):
+//   Gaussian row, D=2: [m0 m1 k0 k1 k2 flags v0..v(CB-1)]  padded to RS = 4k floats (8 at CB<=2)
+//   Gaussian row, D=1: [m0 k0 flags v0..]
+//     k = conic * (-log2 e) * {1/2, 1, 1/2}: power * log2(e) = X0 (k0 X0 + k1 X1) + k2 X1^2
+//     flags bit 0: "unsafe" conic (not well-conditioned PD) -> reference-literal power + mask
+//   Conic row: [c0 c1 c2 0] (D=2) / [c0 0 0 0] (D=1), read only where the raw conic is needed.
+//   Sample row (backward): [s0 (s1) dLsym[U][CB]], dL summed over symmetric components.
+#pragma once
+
+#include "dgs_internal.h"
+
+namespace dgs {
+
+constexpr float kLog2e = 1.4426950408889634f;
+
+template <int FN, int D>
+struct Traits {
+    static constexpr int K = FN == 0 ? 1 : FN == 1 ? D : FN == 2 ? D * D : D * D * D;  // out comps
+    static constexpr int U = D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4);  // unique
+    static constexpr int S = D * (D + 1) / 2;
+    static constexpr int GBASE = D == 2 ? 6 : 3;  // first value slot; flags at GBASE-1
+};
+
+// expanded component -> unique term (forward.cu:288-291, 322-329)
+template <int FN, int D>
+__host__ __device__ constexpr int unique_of(int k) {
+    if (D == 1 || FN <= 1) return k;
+    if constexpr (FN == 2) return k == 0 ? 0 : (k == 3 ? 2 : 1);
+    return k == 0 ? 0 : (k == 7 ? 3 : ((k == 1 || k == 2 || k == 4) ? 1 : 2));
+}
+
+template <int D, int CB>
+__host__ __device__ constexpr int grow_stride() { return (int)((D == 2 ? 6 : 3) + CB + 3) / 4 * 4; }
+template <int FN, int D, int CB>
+__host__ __device__ constexpr int srow_stride() { return (D + Traits<FN, D>::U * CB + 3) / 4 * 4; }
+
+__device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Reference-literal power (forward.cu:227/234/246/256, backward.cu:113/132/...): float
+// products without contraction, double scaling, rounded once to float.
+template <int FN, int D>
+__device__ __forceinline__ float ref_power(const float *X, const float *c) {
+    DGS_NO_CONTRACT
+    if constexpr (D == 1) {
+        if constexpr (FN == 0) return (float)(-0.5 * (double)c[0] * (double)X[0] * (double)X[0]);
+        else {
+            const float x1 = rmul(c[0], X[0]);
+            return (float)(-0.5 * (double)x1 * (double)X[0]);
+        }
+    } else {
+        // gaussian: c0*X0*X0 + c2*X1*X1; others: x1*X0 + x2*X1 with x1 = c0*X0 -- same ops
+        const float a = radd(rmul(rmul(c[0], X[0]), X[0]), rmul(rmul(c[2], X[1]), X[1]));
+        const float b = rmul(rmul(c[1], X[0]), X[1]);
+        return (float)(-0.5 * (double)a - (double)b);
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Forward (forward.cu:225-332): acc[U][CB] += v * G * term_u
+// ---------------------------------------------------------------------------------------
+template <int FN, int D, int CB>
+__device__ __forceinline__ void fwd_terms(const float *X, const float *c, float G, const float *v,
+                                          float (&acc)[Traits<FN, D>::U][CB]) {
+    if constexpr (FN == 0) {
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) acc[0][ch] = fmaf(v[ch], G, acc[0][ch]);
+    } else {
+    float t[4];
+    if constexpr (D == 1) {
+        const float x1 = c[0] * X[0];
+        if constexpr (FN == 1) t[0] = x1;
+        else if constexpr (FN == 2) t[0] = x1 * x1 - c[0];
+        else t[0] = 3.0f * c[0] * x1 - x1 * x1 * x1;  // 2 c x1 - x1^3 + c x1
+    } else {
+        const float a1 = fmaf(c[1], X[1], c[0] * X[0]);
+        const float a2 = fmaf(c[1], X[0], c[2] * X[1]);
+        if constexpr (FN == 1) {
+            t[0] = a1; t[1] = a2;
+        } else if constexpr (FN == 2) {
+            t[0] = fmaf(a1, a1, -c[0]);
+            t[1] = fmaf(a1, a2, -c[1]);
+            t[2] = fmaf(a2, a2, -c[2]);
+        } else {
+            const float a11 = a1 * a1, a22 = a2 * a2;
+            t[0] = a1 * (3.0f * c[0] - a11);
+            t[1] = fmaf(2.0f * c[1], a1, a2 * (c[0] - a11));
+            t[2] = fmaf(2.0f * c[1], a2, a1 * (c[2] - a22));
+            t[3] = a2 * (3.0f * c[2] - a22);
+        }
+    }
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) {
+        const float vg = v[ch] * G;
+#pragma unroll
+        for (int u = 0; u < Traits<FN, D>::U; ++u) acc[u][ch] = fmaf(vg, t[u], acc[u][ch]);
+    }
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+// Backward (backward.cu:108-416).  Lane = Gaussian, so every accumulator is per lane.
+// The gaussian function accumulates moments (gm/gc are linear in them, converted in the
+// epilogue); the others accumulate the reference's per-pair terms.
+//   gm[D], gc[S]: mean / conic gradient accumulators, gv[CB]: value gradient
+//   dl[U][CB]: this sample's dL/dout summed over symmetric components (wave-uniform)
+// ---------------------------------------------------------------------------------------
+template <int FN, int D, int CB>
+__device__ __forceinline__ void bwd_terms(const float *X, const float *c, float G, const float *v,
+                                          const float (&dl)[Traits<FN, D>::U][CB], float *gm,
+                                          float *gv, float *gc) {
+    constexpr int U = Traits<FN, D>::U;
+    float Gu[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        float s = 0.0f;
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) s = fmaf(v[ch], dl[u][ch], s);
+        Gu[u] = s;  // dL_dG (per unique component), reference's dL_dG* sums
+    }
+    if constexpr (FN == 0) {
+        // moments: gm = -[A (sum t X)], gc = -1/2 sum t X X^T (off-diagonal -sum t X0 X1)
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(G, dl[0][ch], gv[ch]);
+        const float t = G * Gu[0];
+        const float tx = t * X[0];
+        gm[0] += tx;                              // sum t X0
+        gc[0] = fmaf(tx, X[0], gc[0]);            // sum t X0^2
+        if constexpr (D == 2) {
+            const float ty = t * X[1];
+            gm[1] += ty;                          // sum t X1
+            gc[1] = fmaf(tx, X[1], gc[1]);        // sum t X0 X1
+            gc[2] = fmaf(ty, X[1], gc[2]);        // sum t X1^2
+        }
+    } else if constexpr (D == 1) {
+        const float x1 = c[0] * X[0];
+        const float GdLdG = G * Gu[0];
+        float f, dmx, dcc;
+        if constexpr (FN == 1) {
+            f = x1;
+            dmx = (x1 * x1 - c[0]);
+            dcc = X[0] - 0.5f * X[0] * X[0] * x1;
+        } else if constexpr (FN == 2) {
+            f = x1 * x1 - c[0];
+            dmx = x1 * x1 * x1 - 3.0f * c[0] * x1;
+            dcc = 2.0f * x1 * X[0] - 0.5f * (x1 * x1 - c[0]) * X[0] * X[0] - 1.0f;
+        } else {
+            f = 3.0f * c[0] * x1 - x1 * x1 * x1;
+            dmx = 6.0f * c[0] * x1 * x1 - x1 * x1 * x1 * x1 - 3.0f * c[0] * c[0];
+            // backward.cu:322-325, reproduced literally (not the true derivative)
+            dcc = 2.0f * X[0] * X[0] - 2.0f * x1 * x1 * X[0] - 0.5f * (2.0f * X[0] * x1 - X[0]) * X[0] * X[0]
+                + 0.5f * (x1 * x1 - c[0]) * x1 * X[0] * X[0];
+        }
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(f * dl[0][ch], G, gv[ch]);
+        gm[0] = fmaf(-dmx, GdLdG, gm[0]);
+        gc[0] = fmaf(dcc, GdLdG, gc[0]);
+    } else {
+    const float X0 = X[0], X1 = X[1];
+    const float a1 = fmaf(c[1], X1, c[0] * X0);
+    const float a2 = fmaf(c[1], X0, c[2] * X1);
+    if constexpr (FN == 1) {
+        const float Gx = Gu[0], Gy = Gu[1];
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(fmaf(a1, dl[0][ch], a2 * dl[1][ch]), G, gv[ch]);
+        const float gx = fmaf(a1, Gx, a2 * Gy);
+        const float axy = fmaf(a1, a2, -c[1]);
+        const float dLdx = fmaf(fmaf(a1, a1, -c[0]), Gx, axy * Gy) * G;
+        const float dLdy = fmaf(fmaf(a2, a2, -c[2]), Gy, axy * Gx) * G;
+        gm[0] -= dLdx;
+        gm[1] -= dLdy;
+        gc[0] = fmaf(fmaf(X0, Gx, -0.5f * X0 * X0 * gx), G, gc[0]);
+        gc[1] = fmaf(X1 * Gx + X0 * Gy - X0 * X1 * gx, G, gc[1]);
+        gc[2] = fmaf(fmaf(X1, Gy, -0.5f * X1 * X1 * gx), G, gc[2]);
+    } else if constexpr (FN == 2) {
+        const float dxx = fmaf(a1, a1, -c[0]), dxy = fmaf(a1, a2, -c[1]), dyy = fmaf(a2, a2, -c[2]);
+        const float Gxx = Gu[0], Sxy = Gu[1], Gyy = Gu[2];
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch)
+            gv[ch] = fmaf(dxx * dl[0][ch] + dxy * dl[1][ch] + dyy * dl[2][ch], G, gv[ch]);
+        const float dLdx = ((a1 * a1 * a1 - 3.0f * c[0] * a1) * Gxx
+                            + (a1 * a2 * a1 - c[1] * a1 - (c[1] * a1 + c[0] * a2)) * Sxy
+                            + (a2 * a2 * a1 - c[2] * a1 - 2.0f * c[1] * a2) * Gyy) * G;
+        const float dLdy = ((a1 * a1 * a2 - c[0] * a2 - 2.0f * c[1] * a1) * Gxx
+                            + (a1 * a2 * a2 - c[1] * a2 - (c[2] * a1 + c[1] * a2)) * Sxy
+                            + (a2 * a2 * a2 - 3.0f * c[2] * a2) * Gyy) * G;
+        gm[0] -= dLdx;
+        gm[1] -= dLdy;
+        const float xx_cxx = -0.5f * dxx * X0 * X0 + 2.0f * a1 * X0 - 1.0f;
+        const float xy_cxx = -0.5f * dxy * X0 * X0 + a2 * X0;
+        const float yy_cxx = -0.5f * dyy * X0 * X0;
+        const float xx_cxy = -dxx * X0 * X1 + 2.0f * a1 * X1;
+        const float xy_cxy = -dxy * X0 * X1 + a2 * X1 + a1 * X0 - 1.0f;
+        const float yy_cxy = -dyy * X0 * X1 + 2.0f * a2 * X0;
+        const float xx_cyy = -0.5f * dxx * X1 * X1;
+        const float xy_cyy = -0.5f * dxy * X1 * X1 + a1 * X1;
+        const float yy_cyy = -0.5f * dyy * X1 * X1 + 2.0f * a2 * X1 - 1.0f;
+        gc[0] = fmaf(xx_cxx * Gxx + xy_cxx * Sxy + yy_cxx * Gyy, G, gc[0]);
+        gc[1] = fmaf(xx_cxy * Gxx + xy_cxy * Sxy + yy_cxy * Gyy, G, gc[1]);
+        gc[2] = fmaf(xx_cyy * Gxx + xy_cyy * Sxy + yy_cyy * Gyy, G, gc[2]);
+    } else {
+    // third, D == 2
+    const float a11 = a1 * a1, a22 = a2 * a2, a12 = a1 * a2;
+    const float dxxx = 3.0f * c[0] * a1 - a11 * a1;
+    const float dxxy = 2.0f * c[1] * a1 - a11 * a2 + c[0] * a2;
+    const float dxyy = 2.0f * c[1] * a2 - a1 * a22 + c[2] * a1;
+    const float dyyy = 3.0f * c[2] * a2 - a22 * a2;
+    const float Gxxx = Gu[0], S1 = Gu[1], S2 = Gu[2], Gyyy = Gu[3];
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch)
+        gv[ch] = fmaf(dxxx * dl[0][ch] + dxxy * dl[1][ch] + dxyy * dl[2][ch] + dyyy * dl[3][ch], G, gv[ch]);
+    const float xxy_dx = 2.0f * a12 * c[0] + a11 * c[1] - 3.0f * c[0] * c[1];
+    const float xyy_dx = 2.0f * a12 * c[1] + a22 * c[0] - c[2] * c[0] - 2.0f * c[1] * c[1];
+    const float dLdx = ((dxxx * a1 - 3.0f * c[0] * c[0] + 3.0f * a11 * c[0]) * Gxxx
+                        + (dxxy * a1 + xxy_dx) * S1 + (dxyy * a1 + xyy_dx) * S2
+                        + (dyyy * a1 - 3.0f * c[2] * c[1] + 3.0f * a22 * c[1]) * Gyyy) * G;
+    const float xxy_dy = 2.0f * a12 * c[1] + a11 * c[2] - c[0] * c[2] - 2.0f * c[1] * c[1];
+    const float xyy_dy = 2.0f * a12 * c[2] + a22 * c[1] - 3.0f * c[2] * c[1];
+    const float dLdy = ((dxxx * a2 - 3.0f * c[0] * c[1] + 3.0f * a11 * c[1]) * Gxxx
+                        + (dxxy * a2 + xxy_dy) * S1 + (dxyy * a2 + xyy_dy) * S2
+                        + (dyyy * a2 - 3.0f * c[2] * c[2] + 3.0f * a22 * c[2]) * Gyyy) * G;
+    gm[0] -= dLdx;
+    gm[1] -= dLdy;
+    const float v0 = -0.5f * dxxx * X0 * X0 + 3.0f * c[0] * X0 + 3.0f * a1 - 3.0f * a11 * X0;
+    const float v1 = -0.5f * dxxy * X0 * X0 + 2.0f * c[1] * X0 - 2.0f * a12 * X0 + a2;
+    const float v2 = -0.5f * dxyy * X0 * X0 - a22 * X0 + c[2] * X0;
+    const float v3 = -0.5f * dyyy * X0 * X0;
+    const float w0 = -dxxx * X0 * X1 + 3.0f * c[0] * X1 - 3.0f * a11 * X1;
+    const float w1 = -dxxy * X0 * X1 + 2.0f * c[1] * X1 + 2.0f * a1 - 2.0f * a12 * X1 - a11 * X0 + c[0] * X0;
+    const float w2 = -dxyy * X0 * X1 + 2.0f * c[1] * X0 + 2.0f * a2 - a22 * X1 - 2.0f * a12 * X0 + c[2] * X1;
+    const float w3 = -dyyy * X0 * X1 + 3.0f * c[2] * X0 - 3.0f * a22 * X0;
+    const float z0 = -0.5f * dxxx * X1 * X1;
+    const float z1 = -0.5f * dxxy * X1 * X1 - a11 * X1 + c[0] * X1;
+    const float z2 = -0.5f * dxyy * X1 * X1 + 2.0f * c[1] * X1 - 2.0f * a12 * X1 + a1;
+    const float z3 = -0.5f * dyyy * X1 * X1 + 3.0f * c[2] * X1 + 3.0f * a2 - 3.0f * a22 * X1;
+    gc[0] = fmaf(v0 * Gxxx + v1 * S1 + v2 * S2 + v3 * Gyyy, G, gc[0]);
+    gc[1] = fmaf(w0 * Gxxx + w1 * S1 + w2 * S2 + w3 * Gyyy, G, gc[1]);
+    gc[2] = fmaf(z0 * Gxxx + z1 * S1 + z2 * S2 + z3 * Gyyy, G, gc[2]);
+    }
+    }
+}
+
+// Epilogue of the gaussian moment form: convert moments to gradients.
+template <int FN, int D>
+__device__ __forceinline__ void bwd_finish(const float *c, float *gm, float *gc) {
+    if constexpr (FN != 0) {
+        return;
+    } else if constexpr (D == 1) {
+        gm[0] = -c[0] * gm[0];
+        gc[0] = -0.5f * gc[0];
+    } else {
+    const float sx = gm[0], sy = gm[1];
+    gm[0] = -fmaf(c[0], sx, c[1] * sy);
+    gm[1] = -fmaf(c[1], sx, c[2] * sy);
+    gc[0] = -0.5f * gc[0];
+    gc[1] = -gc[1];
+    gc[2] = -0.5f * gc[2];
+    }
+}
+
+}  // namespace dgs

@@ -1,0 +1,625 @@
+// dgs_sample.hip -- forward and backward sampling kernels (gfx950).
+//
+// Replaces FORWARD::render / BACKWARD::render (forward.cu:87-166, 277-345;
+// backward.cu:26-106, 418-501) and the per-call host glue of sample_points.cu:100-372.
+//
+// Work decomposition (one wave64 per work unit, 4 independent waves per 256-thread block):
+//   forward : unit = (fine cell, up to 64 of its samples).  Lane = sample.  The cell's
+//             Gaussian list is walked wave-uniformly: each Gaussian's packed row comes in
+//             through the scalar cache (s_load) into SGPRs, so the per-pair work is pure VALU
+//             and the accumulation stays in registers (no atomics, no global RMW per pair).
+//   backward: unit = (fine cell, up to 64 entries of its Gaussian list).  Lane = Gaussian.
+//             The cell's samples (position + dL/dout) are walked wave-uniformly through the
+//             scalar cache; every lane accumulates its own Gaussian's gradient in registers
+//             and issues one atomic add per gradient component at the end of the unit.
+//             Gaussians are renumbered spatially at preprocess, so a wave's 64 lanes add to
+//             nearly contiguous addresses (coalesced atomics).
+#include <algorithm>
+#include <mutex>
+#include <utility>
+#include <vector>
+
+#include "dgs_render.h"
+
+namespace dgs {
+
+static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// --------------------------------------------------------------------------- packing
+template <int D, int CB>
+__global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *__restrict__ means,
+                             const float *__restrict__ conics, const float *__restrict__ values,
+                             int C, int cbase, float *__restrict__ rows, float4 *__restrict__ crows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const Header *h = reinterpret_cast<const Header *>(gbuf);
+    const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
+    const int64_t g = perm[i];
+    constexpr int S = D * (D + 1) / 2, RS = grow_stride<D, CB>(), B = Traits<0, D>::GBASE;
+    float c[3] = {conics[g * S], D == 2 ? conics[g * S + 1] : 0.0f, D == 2 ? conics[g * S + 2] : 0.0f};
+    bool safe;
+    if constexpr (D == 1) {
+        safe = c[0] >= 0.0f && c[0] < INFINITY;
+    } else {
+        const double c0 = c[0], c1 = c[1], c2 = c[2];
+        safe = c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
+               c1 * c1 < 0.98 * c0 * c2;
+    }
+    float out[RS];
+#pragma unroll
+    for (int k = 0; k < RS; ++k) out[k] = 0.0f;
+    if constexpr (D == 2) {
+        out[0] = means[g * 2];
+        out[1] = means[g * 2 + 1];
+        out[2] = -0.5f * kLog2e * c[0];
+        out[3] = -kLog2e * c[1];
+        out[4] = -0.5f * kLog2e * c[2];
+    } else {
+        out[0] = means[g];
+        out[1] = -0.5f * kLog2e * c[0];
+    }
+    out[B - 1] = __int_as_float(safe ? 0 : 1);
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) {
+        const int gc = cbase + ch;
+        out[B + ch] = gc < C ? values[g * C + gc] : 0.0f;
+    }
+    float *row = rows + i * RS;
+#pragma unroll
+    for (int k = 0; k < RS; k += 4)
+        *reinterpret_cast<float4 *>(row + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+    crows[i] = make_float4(c[0], c[1], c[2], 0.0f);
+}
+
+template <int FN, int D, int CB>
+__global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
+                               const float *__restrict__ samples, const float *__restrict__ dL,
+                               int C, int cbase, float *__restrict__ rows) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= N) return;
+    const Header *h = reinterpret_cast<const Header *>(gbuf);
+    const int32_t *sorted = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted);
+    const int64_t sid = sorted[j];
+    constexpr int K = Traits<FN, D>::K, RSS = srow_stride<FN, D, CB>();
+    float out[RSS];
+#pragma unroll
+    for (int k = 0; k < RSS; ++k) out[k] = 0.0f;
+    out[0] = samples[sid * D];
+    if constexpr (D == 2) out[1] = samples[sid * D + 1];
+    const float *d = dL + sid * K * C;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        const int u = unique_of<FN, D>(k);
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) {
+            const int gc = cbase + ch;
+            if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
+        }
+    }
+    float *row = rows + j * RSS;
+#pragma unroll
+    for (int k = 0; k < RSS; k += 4)
+        *reinterpret_cast<float4 *>(row + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+}
+
+// ------------------------------------------------------------------- pair probability
+// Fast path: no torus wrap in this (Gaussian, cell) entry and a well-conditioned PD conic, so
+// power <= 0 is guaranteed and G = 2^(power*log2e) is one v_exp_f32.  General path: the
+// reference's exact wrap and, for other conics, the reference-literal power with its
+// `power > 0 -> skip` rule (forward.cu:228) and an accurate expf.
+template <int D>
+__device__ __forceinline__ float fast_prob(const float *X, const float *k) {
+    if constexpr (D == 2) return fast_exp2(fmaf(X[0], fmaf(k[0], X[0], k[1] * X[1]), k[2] * X[1] * X[1]));
+    else return fast_exp2(k[0] * X[0] * X[0]);
+}
+
+template <int FN, int D>
+__device__ __forceinline__ float general_prob(float *X, const float *c, const float *k, bool wrap,
+                                              bool unsafe) {
+    if (wrap) {
+        X[0] = ref_wrap(X[0]);
+        if constexpr (D == 2) X[1] = ref_wrap(X[1]);
+    }
+    if (unsafe) {
+        const float p = ref_power<FN, D>(X, c);
+        return p > 0.0f ? 0.0f : expf(p);
+    }
+    return fast_prob<D>(X, k);
+}
+
+// ------------------------------------------------------------------- forward kernel
+// Gaussians per scalar-load batch (its rows occupy SGPRs: smaller for wide channel blocks)
+template <int CB>
+__host__ __device__ constexpr int fwd_batch() { return CB <= 2 ? 8 : CB <= 4 ? 4 : 2; }
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbuf,
+                                                    const char *__restrict__ sbuf,
+                                                    const float *__restrict__ grows,
+                                                    const float4 *__restrict__ crows,
+                                                    const float *__restrict__ samples,
+                                                    float *__restrict__ out, int C, int cbase) {
+    using Tr = Traits<FN, D>;
+    constexpr int RS = grow_stride<D, CB>(), B = Tr::GBASE, U = Tr::U, K = Tr::K;
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumFwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.fwd_units[unit]);
+        const int cell = (int)u.x, sb = (int)u.y;
+        const int se = min(sb + kWave, sload(&bins.cell_send[cell]));
+        const int j = sb + lane;
+        const bool active = j < se;
+        const int64_t sid = bins.sorted_sid[active ? j : sb];
+        const float s0 = samples[sid * D], s1 = D == 2 ? samples[sid * D + 1] : 0.0f;
+        const int gb = sload(&bins.cell_gbeg[cell]), ge = sload(&bins.cell_gend[cell]);
+
+        float acc[U][CB];
+#pragma unroll
+        for (int a = 0; a < U; ++a)
+#pragma unroll
+            for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
+
+        constexpr int NB = fwd_batch<CB>();
+        for (int e0 = gb; e0 < ge; e0 += NB) {
+            uint32_t ent[NB];
+#pragma unroll
+            for (int q = 0; q < NB; ++q) ent[q] = sload(&bins.entries[min(e0 + q, ge - 1)]);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                const int64_t id = ent[q] & kIdMask;
+                const float *row = grows + id * RS;
+                float r[RS];
+#pragma unroll
+                for (int k = 0; k < RS; ++k) r[k] = sload(row + k);
+                const bool live = e0 + q < ge;  // wave-uniform tail mask (scalar select)
+                float v[CB];
+#pragma unroll
+                for (int ch = 0; ch < CB; ++ch) v[ch] = live ? r[B + ch] : 0.0f;
+                const bool unsafe = __float_as_int(r[B - 1]) & 1;
+                const bool wrap = (ent[q] & kGeneral) != 0;
+                float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
+                const float kk[3] = {r[D == 2 ? 2 : 1], D == 2 ? r[3] : 0.0f, D == 2 ? r[4] : 0.0f};
+                float c[3] = {0.0f, 0.0f, 0.0f};
+                if (FN != 0 || unsafe) {
+                    const float4 cr = sload(&crows[id]);
+                    c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
+                }
+                float G;
+                if (!(wrap || unsafe)) {
+                    G = fast_prob<D>(X, kk);
+                } else {
+                    if (!live) continue;
+                    G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
+                }
+                fwd_terms<FN, D, CB>(X, c, G, v, acc);
+            }
+        }
+        if (active) {
+            float *o = out + sid * K * C;
+            const int nch = min(CB, C - cbase);
+#pragma unroll
+            for (int k = 0; k < K; ++k) {
+                const int ui = unique_of<FN, D>(k);
+#pragma unroll
+                for (int ch = 0; ch < CB; ++ch)
+                    if (ch < nch) o[k * C + cbase + ch] = acc[ui][ch];
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------ backward kernel
+template <int FN, int CB>
+__host__ __device__ constexpr int bwd_batch() { return (CB <= 2 && FN <= 1) ? 4 : CB <= 4 ? 2 : 1; }
+
+template <int FN, int D, int CB, bool SLOW>
+__device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict__ srows,
+                                         const float *m, const float *c, const float *kk,
+                                         const float *v, bool wrap, bool unsafe, float *gm,
+                                         float *gv, float *gc) {
+    constexpr int U = Traits<FN, D>::U, RSS = srow_stride<FN, D, CB>(), NB = bwd_batch<FN, CB>();
+    for (int j0 = sb; j0 < se; j0 += NB) {
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const float *sr = srows + (int64_t)min(j0 + q, se - 1) * RSS;
+            const bool live = j0 + q < se;  // wave-uniform tail mask: dL -> 0
+            float srow[RSS];
+#pragma unroll
+            for (int k = 0; k < RSS; ++k) srow[k] = sload(sr + k);
+            float dl[U][CB];
+#pragma unroll
+            for (int a = 0; a < U; ++a)
+#pragma unroll
+                for (int ch = 0; ch < CB; ++ch) dl[a][ch] = live ? srow[D + a * CB + ch] : 0.0f;
+            float X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : 0.0f};
+            float G;
+            if constexpr (SLOW) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
+            else G = fast_prob<D>(X, kk);
+            bwd_terms<FN, D, CB>(X, c, G, v, dl, gm, gv, gc);
+        }
+    }
+}
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gbuf,
+                                                     const char *__restrict__ sbuf,
+                                                     const float *__restrict__ grows,
+                                                     const float4 *__restrict__ crows,
+                                                     const float *__restrict__ srows,
+                                                     float *__restrict__ acc, int P, int vrow0) {
+    using Tr = Traits<FN, D>;
+    constexpr int RS = grow_stride<D, CB>(), B = Tr::GBASE, S = Tr::S;
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumBwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1);
+    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.bwd_units[unit]);
+        const int cell = (int)u.x, eb = (int)u.y;
+        const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
+        const bool active = eb + lane < ee;
+        const uint32_t ent = bins.entries[active ? eb + lane : eb];
+        const int64_t id = ent & kIdMask;
+        const float *grow = grows + id * RS;
+        float r[RS];
+#pragma unroll
+        for (int k = 0; k < RS; k += 4) {
+            const float4 q = *reinterpret_cast<const float4 *>(grow + k);
+            r[k] = q.x; r[k + 1] = q.y; r[k + 2] = q.z; r[k + 3] = q.w;
+        }
+        const float4 cr = crows[id];
+        const bool wrap = (ent & kGeneral) != 0;
+        const bool unsafe = __float_as_int(r[B - 1]) & 1;
+        const float c[3] = {cr.x, cr.y, cr.z};
+        const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
+        const float kk[3] = {r[D == 2 ? 2 : 1], D == 2 ? r[3] : 0.0f, D == 2 ? r[4] : 0.0f};
+        const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+        float gm[2] = {0.0f, 0.0f}, gc[3] = {0.0f, 0.0f, 0.0f}, gv[CB];
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = 0.0f;
+        if (__any(active && (wrap || unsafe)))
+            bwd_loop<FN, D, CB, true>(sb, se, srows, m, c, kk, r + B, wrap, unsafe, gm, gv, gc);
+        else
+            bwd_loop<FN, D, CB, false>(sb, se, srows, m, c, kk, r + B, false, false, gm, gv, gc);
+        if (active) {
+            bwd_finish<FN, D>(c, gm, gc);
+#pragma unroll
+            for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, gm[d]);
+#pragma unroll
+            for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, gc[k]);
+#pragma unroll
+            for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, gv[ch]);
+        }
+    }
+}
+
+// Internal (spatial) order -> caller order.
+__global__ void k_finalize(int P, int D, int C, const char *__restrict__ gbuf,
+                           const float *__restrict__ acc, float *__restrict__ dmeans,
+                           float *__restrict__ dvalues, float *__restrict__ dconics) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const Header *h = reinterpret_cast<const Header *>(gbuf);
+    const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
+    const int64_t g = perm[i];
+    const int S = D * (D + 1) / 2;
+    for (int d = 0; d < D; ++d) dmeans[g * D + d] = acc[(int64_t)d * P + i];
+    for (int k = 0; k < S; ++k) dconics[g * S + k] = acc[(int64_t)(D + k) * P + i];
+    for (int ch = 0; ch < C; ++ch) dvalues[g * C + ch] = acc[(int64_t)(D + S + ch) * P + i];
+}
+
+// ------------------------------------------------------------- diagnostic pair count
+template <int D>
+__global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
+                                                  const char *__restrict__ sbuf,
+                                                  const float *__restrict__ grows,
+                                                  const float4 *__restrict__ crows,
+                                                  const float *__restrict__ samples, float thr,
+                                                  unsigned long long *__restrict__ counts) {
+    constexpr int RS = grow_stride<D, 1>();
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumFwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.fwd_units[unit]);
+        const int cell = (int)u.x, sb = (int)u.y;
+        const int se = min(sb + kWave, sload(&bins.cell_send[cell]));
+        const int j = sb + (threadIdx.x & (kWave - 1));
+        const bool active = j < se;
+        const int64_t sid = bins.sorted_sid[active ? j : sb];
+        const float s0 = samples[sid * D], s1 = D == 2 ? samples[sid * D + 1] : 0.0f;
+        const int gb = sload(&bins.cell_gbeg[cell]), ge = sload(&bins.cell_gend[cell]);
+        unsigned long long live = 0;
+        for (int e = gb; e < ge; ++e) {
+            const int64_t id = sload(&bins.entries[e]) & kIdMask;
+            const float *row = grows + id * RS;
+            const float4 cr = sload(&crows[id]);
+            const float c[3] = {cr.x, cr.y, cr.z};
+            float X[2] = {ref_wrap(sload(row) - s0), D == 2 ? ref_wrap(sload(row + 1) - s1) : 0.0f};
+            const float p = ref_power<0, D>(X, c);
+            live += (p >= thr && p <= 0.0f) ? 1ull : 0ull;
+        }
+        if (active) {
+            atomicAdd(&counts[0], (unsigned long long)(ge - gb));
+            atomicAdd(&counts[1], live);
+        }
+    }
+}
+
+// ------------------------------------------------------------------ kernel timing
+// Optional HIP-event brackets around the render kernels (bench.py: the dominant kernel's
+// average duration on the stream it runs on).  Off by default.
+static std::mutex g_tmu;
+static bool g_timing = false;
+static std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tev[2];
+
+struct KernelTimer {
+    int which;
+    hipStream_t s;
+    hipEvent_t a = nullptr, b = nullptr;
+    KernelTimer(int w, hipStream_t st) : which(w), s(st) {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        if (!g_timing) return;
+        if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
+        (void)hipEventRecord(a, s);
+    }
+    ~KernelTimer() {
+        if (!a) return;
+        (void)hipEventRecord(b, s);
+        std::lock_guard<std::mutex> lk(g_tmu);
+        g_tev[which].push_back({a, b});
+    }
+};
+
+// ------------------------------------------------------------------ host dispatch
+static int channel_block(int C) { return C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : 16; }
+static int grow_stride_rt(int D, int CB) { return ((D == 2 ? 6 : 3) + CB + 3) / 4 * 4; }
+static int unique_rt(int FN, int D) { return D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4); }
+static int srow_stride_rt(int FN, int D, int CB) { return (D + unique_rt(FN, D) * CB + 3) / 4 * 4; }
+static size_t a256(size_t x) { return align_up(x, 256); }
+
+struct WsLayout {
+    size_t grows, crows, srows, acc, total;
+};
+static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
+    const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
+    WsLayout w;
+    w.grows = a256((size_t)P * grow_stride_rt(D, CB) * 4 + 64);
+    w.crows = a256((size_t)P * 16 + 64);
+    w.srows = backward ? a256((size_t)N * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;
+    w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
+    w.total = w.grows + w.crows + w.srows + w.acc;
+    return w;
+}
+
+// Grid size in blocks: exact (from the preprocess hint) or a persistent-size fallback; the
+// kernels grid-stride over the device-side unit count either way.
+static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_t sbytes, bool bwd) {
+    UnitHint h;
+    int64_t units;
+    if (hint_get(gb, gbytes, sb, sbytes, &h)) {
+        units = bwd ? h.nbwd : h.nfwd;
+    } else {
+        units = 256 * 8 * kWavesPerBlock;  // 8 blocks per CU, striding
+    }
+    int64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+    if (blocks < 1) blocks = 1;
+    if (blocks > (1 << 30)) blocks = 1 << 30;
+    return (unsigned)blocks;
+}
+
+struct Call {
+    int FN, P, D, N, C;
+    const float *means, *values, *conics, *samples, *dL;
+    const char *gb, *sb;
+    size_t gbytes, sbytes;
+    float *out, *dm, *dv, *dc;
+    char *ws;
+    hipStream_t s;
+    int debug;
+};
+
+template <int FN, int D, int CB>
+static int run_forward(const Call &a) {
+    const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, false);
+    float *grows = reinterpret_cast<float *>(a.ws);
+    float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
+    const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
+    for (int cbase = 0; cbase < a.C; cbase += CB) {
+        k_pack_gauss<D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
+                                                                 a.values, a.C, cbase, grows, crows);
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+        {
+            KernelTimer t(0, a.s);
+            k_forward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows, a.samples,
+                                                               a.out, a.C, cbase);
+        }
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+    }
+    return DGS_OK;
+}
+
+template <int FN, int D, int CB>
+static int run_backward(const Call &a) {
+    const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, true);
+    float *grows = reinterpret_cast<float *>(a.ws);
+    float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
+    float *srows = reinterpret_cast<float *>(a.ws + w.grows + w.crows);
+    float *acc = reinterpret_cast<float *>(a.ws + w.grows + w.crows + w.srows);
+    constexpr int S = D * (D + 1) / 2;
+    DGS_TRY_HIP(hipMemsetAsync(acc, 0, w.acc, a.s));
+    const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
+    for (int cbase = 0; cbase < a.C; cbase += CB) {
+        k_pack_gauss<D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
+                                                                 a.values, a.C, cbase, grows, crows);
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+        k_pack_samples<FN, D, CB><<<grid_for(a.N), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
+                                                                      a.dL, a.C, cbase, srows);
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+        // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
+        {
+            KernelTimer t(1, a.s);
+            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows, srows, acc,
+                                                                a.P, D + S + cbase);
+        }
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+    }
+    k_finalize<<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, D, a.C, a.gb, acc, a.dm, a.dv, a.dc);
+    DGS_LAUNCH_CHECK(a.s, a.debug);
+    return DGS_OK;
+}
+
+template <int FN, int D>
+static int dispatch_cb(const Call &a, bool bwd) {
+    switch (channel_block(a.C)) {
+    case 1: return bwd ? run_backward<FN, D, 1>(a) : run_forward<FN, D, 1>(a);
+    case 2: return bwd ? run_backward<FN, D, 2>(a) : run_forward<FN, D, 2>(a);
+    case 4: return bwd ? run_backward<FN, D, 4>(a) : run_forward<FN, D, 4>(a);
+    case 8: return bwd ? run_backward<FN, D, 8>(a) : run_forward<FN, D, 8>(a);
+    default: return bwd ? run_backward<FN, D, 16>(a) : run_forward<FN, D, 16>(a);
+    }
+}
+
+template <int FN>
+static int dispatch_d(const Call &a, bool bwd) {
+    return a.D == 1 ? dispatch_cb<FN, 1>(a, bwd) : dispatch_cb<FN, 2>(a, bwd);
+}
+
+static int dispatch(const Call &a, bool bwd) {
+    switch (a.FN) {
+    case DGS_GAUSSIAN: return dispatch_d<0>(a, bwd);
+    case DGS_DERIVATIVE: return dispatch_d<1>(a, bwd);
+    case DGS_LAPLACIAN: return dispatch_d<2>(a, bwd);
+    default: return dispatch_d<3>(a, bwd);
+    }
+}
+
+static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t gbytes,
+                    const void *sb, size_t sbytes, size_t need, size_t have) {
+    if (FN < 0 || FN > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
+    if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported");
+    if (P < 0 || N < 0 || C < 0) return fail(DGS_ERR_ARG, "negative size");
+    if (P == 0 || N == 0 || C == 0) return DGS_OK;
+    if (!gb || !sb || gbytes < kHeaderBytes || sbytes < kHeaderBytes)
+        return fail(DGS_ERR_BUFFER, "binning buffers missing or too small (run preprocess first)");
+    if (have < need) return fail(DGS_ERR_ARG, "workspace too small");
+    return DGS_OK;
+}
+
+}  // namespace dgs
+
+using namespace dgs;
+
+extern "C" size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward) {
+    if (P <= 0 || N <= 0 || C <= 0 || (D != 1 && D != 2)) return 256;
+    return ws_layout(function, P, D, N, C, backward != 0).total;
+}
+
+extern "C" int dgs_sample_forward(int function, int P, int D, int N, int C, const float *means,
+                                  const float *values, const float *conics, const float *samples,
+                                  const void *binning, size_t binning_bytes,
+                                  const void *sample_binning, size_t sample_binning_bytes,
+                                  float *out, void *workspace, size_t workspace_bytes,
+                                  dgs_stream_t stream, int debug) {
+    const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 0);
+    int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
+                      sample_binning_bytes, need, workspace_bytes);
+    if (rc || P == 0 || N == 0 || C == 0) return rc;
+    Call a{function, P, D, N, C, means, values, conics, samples, nullptr,
+           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
+           binning_bytes, sample_binning_bytes, out, nullptr, nullptr, nullptr,
+           static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
+    return dispatch(a, false);
+}
+
+extern "C" int dgs_sample_backward(int function, int P, int D, int N, int C, const float *means,
+                                   const float *values, const float *conics, const float *samples,
+                                   const float *dL_dout, const void *binning, size_t binning_bytes,
+                                   const void *sample_binning, size_t sample_binning_bytes,
+                                   float *dL_dmeans, float *dL_dvalues, float *dL_dconics,
+                                   void *workspace, size_t workspace_bytes, dgs_stream_t stream,
+                                   int debug) {
+    const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 1);
+    int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
+                      sample_binning_bytes, need, workspace_bytes);
+    if (rc) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0 || N == 0 || C == 0) {
+        // sample_points.cu:165-167: zero gradients
+        const int S = D * (D + 1) / 2;
+        if (P > 0) {
+            DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, sizeof(float) * (size_t)P * D, s));
+            DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, sizeof(float) * (size_t)P * S, s));
+            if (C > 0) DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, sizeof(float) * (size_t)P * C, s));
+        }
+        return DGS_OK;
+    }
+    Call a{function, P, D, N, C, means, values, conics, samples, dL_dout,
+           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
+           binning_bytes, sample_binning_bytes, nullptr, dL_dmeans, dL_dvalues, dL_dconics,
+           static_cast<char *>(workspace), s, debug};
+    return dispatch(a, true);
+}
+
+extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics,
+                               const float *samples, const void *binning, size_t binning_bytes,
+                               const void *sample_binning, size_t sample_binning_bytes, float thr,
+                               int64_t *counts, void *workspace, size_t workspace_bytes,
+                               dgs_stream_t stream) {
+    counts[0] = counts[1] = 0;
+    const size_t need = dgs_sample_workspace_size(0, P, D, N, 1, 0) + 256;
+    int rc = validate(0, P, D, N, 1, binning, binning_bytes, sample_binning, sample_binning_bytes,
+                      need, workspace_bytes);
+    if (rc || P == 0 || N == 0) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const char *gb = static_cast<const char *>(binning), *sb = static_cast<const char *>(sample_binning);
+    const WsLayout w = ws_layout(0, P, D, N, 1, false);
+    float *grows = static_cast<float *>(workspace);
+    float4 *crows = reinterpret_cast<float4 *>(static_cast<char *>(workspace) + w.grows);
+    unsigned long long *dcnt = reinterpret_cast<unsigned long long *>(
+        static_cast<char *>(workspace) + need - 256);
+    DGS_TRY_HIP(hipMemsetAsync(dcnt, 0, 16, s));
+    const unsigned blocks = unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false);
+    if (D == 2) {
+        k_pack_gauss<2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
+        k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
+    } else {
+        k_pack_gauss<1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
+        k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
+    }
+    DGS_TRY_HIP(hipGetLastError());
+    unsigned long long h[2];
+    DGS_TRY_HIP(hipMemcpyAsync(h, dcnt, sizeof(h), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    counts[0] = (int64_t)h[0];
+    counts[1] = (int64_t)h[1];
+    return DGS_OK;
+}
+
+extern "C" void dgs_timing_enable(int on) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_timing = on != 0;
+}
+
+// Sums the recorded durations of kernel `which` (0 = forward render, 1 = backward render),
+// waiting for their events, and clears the record.  Returns the number of launches.
+extern "C" int dgs_timing_read(int which, double *total_ms) {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev;
+    {
+        std::lock_guard<std::mutex> lk(g_tmu);
+        if (which < 0 || which > 1) return -1;
+        ev.swap(g_tev[which]);
+    }
+    double tot = 0.0;
+    for (auto &p : ev) {
+        float ms = 0.0f;
+        (void)hipEventSynchronize(p.second);
+        if (hipEventElapsedTime(&ms, p.first, p.second) == hipSuccess) tot += ms;
+        (void)hipEventDestroy(p.first);
+        (void)hipEventDestroy(p.second);
+    }
+    *total_ms = tot;
+    return (int)ev.size();
+}

@@ -1,0 +1,273 @@
+// torch_ext.cpp -- diff_gaussian_sampling._C: the reference's pybind surface (ext.cpp:19-32)
+// mapped onto the C ABI of libdgs.so (include/dgs.h).
+//
+// Same function names, argument order and meaning, return arity and error behaviour as the
+// reference host glue (sample_points.{h,cu}, aggregate_neighbors.{h,cu}):
+//   * inputs are borrowed, made contiguous; wrong dtypes raise RuntimeError (the reference's
+//     data<float>() check); P == 0 or N == 0 returns zero/empty results without launching;
+//   * the tile grid is computed with the reference's own torch ops (sample_points.cu:70-74);
+//   * opaque u8 buffers come back to Python and are handed back verbatim;
+//   * everything runs on torch's current HIP stream; `debug` synchronises and checks after
+//     every launch (auxiliary.h:33-40).
+#include <ATen/hip/HIPContext.h>
+#include <torch/extension.h>
+
+#include <stdexcept>
+#include <tuple>
+#include <vector>
+
+#include "dgs.h"
+
+namespace {
+
+using torch::Tensor;
+
+hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+dgs_stream_t as_dgs(hipStream_t s) { return reinterpret_cast<dgs_stream_t>(s); }
+
+void check(int rc, const char *what) {
+    if (rc != DGS_OK) throw std::runtime_error(std::string(what) + ": " + dgs_last_error());
+}
+
+Tensor f32(const Tensor &t, const char *name) {
+    TORCH_CHECK(t.scalar_type() == torch::kFloat32, name, " must be a float32 tensor (got ",
+                t.scalar_type(), ")");
+    TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+    return t.contiguous();
+}
+
+Tensor u8(const Tensor &t, const char *name) {
+    TORCH_CHECK(t.scalar_type() == torch::kUInt8, name, " must be the uint8 buffer returned by preprocess");
+    return t.contiguous();
+}
+
+struct AllocCtx {
+    torch::Device device;
+    Tensor bufs[4];
+    std::vector<Tensor> scratch;
+};
+
+void *alloc_cb(void *vctx, int which, size_t bytes) {
+    auto *ctx = static_cast<AllocCtx *>(vctx);
+    try {
+        Tensor t = torch::empty({(int64_t)bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(ctx->device));
+        void *p = t.data_ptr();
+        if (which >= 0 && which < 4) ctx->bufs[which] = t;
+        else ctx->scratch.push_back(t);
+        return p;
+    } catch (...) {
+        return nullptr;
+    }
+}
+
+Tensor empty_u8(const torch::Device &dev) {
+    return torch::empty({0}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
+}
+
+// sample_points.cu:70-74, literally (torch ops on the device, then to the host).
+std::pair<std::vector<int>, std::vector<float>> tile_grid_torch(const Tensor &samples) {
+    const Tensor min_bound = std::get<0>(samples.min(0));
+    const Tensor max_bound = std::get<0>(samples.max(0));
+    const Tensor tile_grid = torch::ceil((max_bound - min_bound + 1e-6f) / 0.51f).to(torch::kInt32);
+    const Tensor g = tile_grid.cpu(), o = min_bound.cpu();
+    const int D = (int)g.numel();
+    std::vector<int> grid(D);
+    std::vector<float> off(D);
+    for (int d = 0; d < D; ++d) {
+        grid[d] = g.data_ptr<int>()[d];
+        off[d] = o.data_ptr<float>()[d];
+    }
+    return {grid, off};
+}
+
+using PreOut = std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor>;
+
+PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Tensor &cov_in,
+                       const Tensor &conics_in, const Tensor &samples_in, const std::vector<int> *grid_in,
+                       const std::vector<float> *off_in, bool debug) {
+    const Tensor means = f32(means_in, "means"), covs = f32(cov_in, "covariances");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    (void)values_in;
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    Tensor radii = torch::full({P}, 0, means.options());
+    AllocCtx ctx{means.device()};
+    for (int i = 0; i < 4; ++i) ctx.bufs[i] = empty_u8(means.device());
+    int64_t rendered = 0;
+    if (P != 0 && N != 0) {
+        TORCH_CHECK(D == 1 || D == 2, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
+        TORCH_CHECK(samples.size(-1) == D, "samples must have the same dimension as means");
+        std::vector<int> grid;
+        std::vector<float> off;
+        if (grid_in) {
+            grid = *grid_in;
+            off = *off_in;
+        } else {
+            std::tie(grid, off) = tile_grid_torch(samples);
+        }
+        TORCH_CHECK((int)grid.size() == D && (int)off.size() == D, "grid/offset must have D entries");
+        check(dgs_preprocess(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
+                             conics.data_ptr<float>(), samples.data_ptr<float>(), grid.data(),
+                             off.data(), radii.data_ptr<float>(), alloc_cb, &ctx, &rendered,
+                             as_dgs(cur_stream()), debug ? 1 : 0),
+              "preprocess_gaussians");
+    }
+    return std::make_tuple(rendered, ctx.bufs[DGS_BUF_BINNING], ctx.bufs[DGS_BUF_SAMPLE_BINNING],
+                           ctx.bufs[DGS_BUF_RANGES], ctx.bufs[DGS_BUF_SAMPLE_RANGES], radii);
+}
+
+// PreprocessCUDA (sample_points.h:20-27)
+PreOut PreprocessCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances,
+                      const Tensor &conics, const Tensor &samples, const bool debug) {
+    return preprocess_impl(means, values, covariances, conics, samples, nullptr, nullptr, debug);
+}
+
+// Sharded extension: the same with a caller-given (global) tile grid and offset.
+PreOut PreprocessBoundedCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances,
+                             const Tensor &conics, const Tensor &samples, std::vector<int> grid,
+                             std::vector<float> offset, const bool debug) {
+    return preprocess_impl(means, values, covariances, conics, samples, &grid, &offset, debug);
+}
+
+Tensor sample_generic(int fn, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
+                      const Tensor &samples_in, const Tensor &binning_in, const Tensor &sbinning_in,
+                      bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    const int C = (int)values.size(-1);
+    std::vector<int64_t> shape{N};
+    for (int k = 0; k < fn; ++k) shape.push_back(D);
+    shape.push_back(C);
+    Tensor out = torch::full(shape, 0.0, means.options());
+    if (P != 0 && N != 0) {
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        const size_t ws = dgs_sample_workspace_size(fn, P, D, N, C, 0);
+        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_sample_forward(fn, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                 conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(),
+                                 (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
+                                 out.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
+                                 debug ? 1 : 0),
+              "sample_gaussians");
+    }
+    return out;
+}
+
+using Grads = std::tuple<Tensor, Tensor, Tensor>;
+
+Grads sample_backward_generic(int fn, const Tensor &means_in, const Tensor &values_in,
+                              const Tensor &conics_in, const Tensor &samples_in, const Tensor &dL_in,
+                              const Tensor &binning_in, const Tensor &sbinning_in, bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    const int C = (int)values.size(-1);
+    Tensor dmeans = torch::zeros({P, D}, means.options());
+    Tensor dvalues = torch::zeros({P, C}, means.options());
+    Tensor dconics = torch::zeros({P, D * (D + 1) / 2}, means.options());
+    if (P != 0 && N != 0) {
+        const Tensor dL = f32(dL_in, "dL_dout_values");
+        int64_t K = 1;
+        for (int k = 0; k < fn; ++k) K *= D;
+        TORCH_CHECK(dL.numel() == (int64_t)N * K * C, "dL_dout has the wrong number of elements");
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        const size_t ws = dgs_sample_workspace_size(fn, P, D, N, C, 1);
+        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_sample_backward(fn, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                  conics.data_ptr<float>(), samples.data_ptr<float>(), dL.data_ptr<float>(),
+                                  gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
+                                  dmeans.data_ptr<float>(), dvalues.data_ptr<float>(),
+                                  dconics.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
+                                  debug ? 1 : 0),
+              "sample_gaussians_backward");
+    }
+    return std::make_tuple(dmeans, dvalues, dconics);
+}
+
+#define DGS_FWD(NAME, FN)                                                                       \
+    Tensor NAME(const Tensor &means, const Tensor &values, const Tensor &conics,                \
+                const Tensor &samples, const int64_t num_rendered, const Tensor &binning_buffer, \
+                const Tensor &sample_binning_buffer, const Tensor &ranges,                      \
+                const Tensor &sample_ranges, const bool debug) {                                \
+        (void)num_rendered; (void)ranges; (void)sample_ranges;                                  \
+        return sample_generic(FN, means, values, conics, samples, binning_buffer,              \
+                              sample_binning_buffer, debug);                                    \
+    }
+#define DGS_BWD(NAME, FN)                                                                       \
+    Grads NAME(const Tensor &means, const Tensor &values, const Tensor &conics,                 \
+               const Tensor &samples, const int64_t num_rendered, const Tensor &dL_dout_values, \
+               const Tensor &binning_buffer, const Tensor &sample_binning_buffer,               \
+               const Tensor &ranges, const Tensor &sample_ranges, const bool debug) {           \
+        (void)num_rendered; (void)ranges; (void)sample_ranges;                                  \
+        return sample_backward_generic(FN, means, values, conics, samples, dL_dout_values,     \
+                                       binning_buffer, sample_binning_buffer, debug);           \
+    }
+
+// sample_points.h:29-131
+DGS_FWD(SampleGaussiansCUDA, DGS_GAUSSIAN)
+DGS_FWD(SampleGaussiansDerivativeCUDA, DGS_DERIVATIVE)
+DGS_FWD(SampleGaussiansLaplacianCUDA, DGS_LAPLACIAN)
+DGS_FWD(SampleGaussiansThirdCUDA, DGS_THIRD)
+DGS_BWD(SampleGaussiansBackwardCUDA, DGS_GAUSSIAN)
+DGS_BWD(SampleGaussiansDerivativeBackwardCUDA, DGS_DERIVATIVE)
+DGS_BWD(SampleGaussiansLaplacianBackwardCUDA, DGS_LAPLACIAN)
+DGS_BWD(SampleGaussiansThirdBackwardCUDA, DGS_THIRD)
+
+// Diagnostics: (W_cand, W_live) over the pairs the forward evaluates.
+std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &conics_in,
+                                        const Tensor &samples_in, const Tensor &binning_in,
+                                        const Tensor &sbinning_in, double thr) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    int64_t counts[2] = {0, 0};
+    if (P != 0 && N != 0) {
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        const size_t ws = dgs_sample_workspace_size(0, P, D, N, 1, 0) + 256;
+        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_count_pairs(P, D, N, means.data_ptr<float>(), conics.data_ptr<float>(),
+                              samples.data_ptr<float>(), gb.data_ptr(), (size_t)gb.numel(),
+                              sb.data_ptr(), (size_t)sb.numel(), (float)thr, counts, work.data_ptr(),
+                              ws, as_dgs(cur_stream())),
+              "count_pairs");
+    }
+    return std::make_tuple(counts[0], counts[1]);
+}
+
+// The C-ABI tile grid (device min/max, torch-CUDA arithmetic) -- for tests of dgs_tile_grid.
+std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_in) {
+    const Tensor samples = f32(samples_in, "samples");
+    const int N = (int)samples.size(0), D = (int)samples.size(-1);
+    std::vector<int> grid(D);
+    std::vector<float> off(D);
+    check(dgs_tile_grid(N, D, samples.data_ptr<float>(), grid.data(), off.data(), as_dgs(cur_stream())),
+          "tile_grid");
+    return std::make_tuple(grid, off);
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+    m.doc() = "MI355X-native differentiable Gaussian sampling (HIP / gfx950)";
+    // ext.cpp:20-31
+    m.def("preprocess_gaussians", &PreprocessCUDA);
+    m.def("sample_gaussians", &SampleGaussiansCUDA);
+    m.def("sample_gaussians_backward", &SampleGaussiansBackwardCUDA);
+    m.def("sample_gaussians_derivative", &SampleGaussiansDerivativeCUDA);
+    m.def("sample_gaussians_derivative_backward", &SampleGaussiansDerivativeBackwardCUDA);
+    m.def("sample_gaussians_laplacian", &SampleGaussiansLaplacianCUDA);
+    m.def("sample_gaussians_laplacian_backward", &SampleGaussiansLaplacianBackwardCUDA);
+    m.def("sample_gaussians_third_derivative", &SampleGaussiansThirdCUDA);
+    m.def("sample_gaussians_third_derivative_backward", &SampleGaussiansThirdBackwardCUDA);
+    // extensions (not on the reference surface)
+    m.def("preprocess_gaussians_bounded", &PreprocessBoundedCUDA);
+    m.def("count_pairs", &CountPairs);
+    m.def("tile_grid", &TileGrid);
+    m.def("library_version", []() { return dgs_version(); });
+    m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });
+    m.def("timing_read", [](int which) {
+        double ms = 0.0;
+        const int n = dgs_timing_read(which, &ms);
+        return std::make_tuple(n, ms);
+    });
+}

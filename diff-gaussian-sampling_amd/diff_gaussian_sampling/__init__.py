@@ -1,0 +1,214 @@
+"""diff_gaussian_sampling -- MI355X-native drop-in for kr4b/diff-gaussian-sampling.
+
+Same public surface as the reference package (diff_gaussian_sampling/__init__.py:1-317):
+the functional entry points, `call_debug`, the autograd Functions and `GaussianSampler`,
+with the same argument order, return arity and debug behaviour.  The compute is the HIP
+library libdgs.so behind `diff_gaussian_sampling._C` (csrc/torch_ext.cpp); there is no CPU
+fallback -- importing this package without the built extension raises ImportError.
+"""
+import torch
+
+try:
+    from . import _C
+except ImportError as exc:  # pragma: no cover - exercised on an unbuilt tree
+    raise ImportError(
+        "diff_gaussian_sampling._C is not built; run `python diff-gaussian-sampling_amd/build.py` "
+        "(hipcc, gfx950) first") from exc
+
+__all__ = [
+    "sample_gaussians", "sample_gaussians_derivative", "sample_gaussians_laplacian",
+    "sample_gaussians_third_derivative", "aggregate_neighbors", "preprocess_gaussians",
+    "preprocess_aggregate", "call_debug", "cpu_deep_copy_tuple", "GaussianSampler",
+]
+
+
+def cpu_deep_copy_tuple(input_tuple):
+    """CPU clones of the tensor members of a tuple (py:17-19)."""
+    return tuple(x.cpu().clone() if isinstance(x, torch.Tensor) else x for x in input_tuple)
+
+
+# The first parameter is named `debug` in the reference but receives `means` (py:21-31).
+def sample_gaussians(debug, *args):
+    return _SampleGaussians.apply(debug, *args)
+
+
+def sample_gaussians_derivative(debug, *args):
+    return _SampleGaussiansDerivative.apply(debug, *args)
+
+
+def sample_gaussians_laplacian(debug, *args):
+    return _SampleGaussiansLaplacian.apply(debug, *args)
+
+
+def sample_gaussians_third_derivative(debug, *args):
+    return _SampleGaussiansThirdDerivative.apply(debug, *args)
+
+
+def aggregate_neighbors(features, transform, queries, keys, frequencies, distance_transform,
+                        indices, ranges, dists, densities, inv_total_densities, debug):
+    return _AggregateNeighbors.apply(features, transform, queries, keys, frequencies,
+                                     distance_transform, indices, ranges, dists, densities,
+                                     inv_total_densities, debug)
+
+
+def call_debug(func, debug, name, *args):
+    """Runs func(*args); with debug, a CPU snapshot of the arguments is written to
+    snapshot_<name>.dump when it raises, and the exception is re-raised (py:38-50)."""
+    if not debug:
+        return func(*args)
+    snapshot = cpu_deep_copy_tuple(args)  # copied before the call can corrupt them
+    try:
+        return func(*args)
+    except Exception:
+        torch.save(snapshot, "snapshot_{}.dump".format(name))
+        print("\nAn error occured in {}. Please forward snapshot_{}.dump for debugging.".format(name, name))
+        raise
+
+
+def preprocess_gaussians(means, values, covariances, conics, samples, debug):
+    """Tile binning (py:52-65).  Returns (num_rendered, binning_buffer, sample_binning_buffer,
+    ranges, sample_ranges, radii)."""
+    args = (means, values, covariances, conics, samples, debug)
+    return call_debug(_C.preprocess_gaussians, debug, "preprocess", *args)
+
+
+def preprocess_aggregate(means, conics, radii, debug):
+    """Neighbour lists for aggregate_neighbors (py:67-77)."""
+    args = (means, conics, radii, debug)
+    return call_debug(_C.preprocess_aggregate, debug, "preprocess_agg", *args)
+
+
+def call_forward(ctx, func, name, *args):
+    (means, values, conics, samples, num_rendered, binning_buffer, sample_binning_buffer,
+     ranges, sample_ranges, debug) = args
+    out = call_debug(func, debug, name, *args)
+    ctx.debug = debug
+    ctx.num_rendered = num_rendered
+    ctx.save_for_backward(means, values, conics, samples, binning_buffer, sample_binning_buffer,
+                          ranges, sample_ranges)
+    return out
+
+
+def call_backward(ctx, func, grad_out, name):
+    (means, values, conics, samples, binning_buffer, sample_binning_buffer, ranges,
+     sample_ranges) = ctx.saved_tensors
+    args = (means, values, conics, samples, ctx.num_rendered, grad_out, binning_buffer,
+            sample_binning_buffer, ranges, sample_ranges, ctx.debug)
+    grad_means, grad_values, grad_conics = call_debug(func, ctx.debug, name, *args)
+    # gradients for (means, values, conics); None for the remaining inputs (py:114-126)
+    return (grad_means, grad_values, grad_conics) + (None,) * 8
+
+
+class _SampleGaussians(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *args):
+        return call_forward(ctx, _C.sample_gaussians, "fw", *args)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        return call_backward(ctx, _C.sample_gaussians_backward, grad_out, "bw")
+
+
+class _SampleGaussiansDerivative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *args):
+        return call_forward(ctx, _C.sample_gaussians_derivative, "der_fw", *args)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        return call_backward(ctx, _C.sample_gaussians_derivative_backward, grad_out, "der_bw")
+
+
+class _SampleGaussiansLaplacian(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *args):
+        return call_forward(ctx, _C.sample_gaussians_laplacian, "lap_fw", *args)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        return call_backward(ctx, _C.sample_gaussians_laplacian_backward, grad_out, "lap_bw")
+
+
+class _SampleGaussiansThirdDerivative(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, *args):
+        return call_forward(ctx, _C.sample_gaussians_third_derivative, "3_fw", *args)
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        return call_backward(ctx, _C.sample_gaussians_third_derivative_backward, grad_out, "3_bw")
+
+
+class _AggregateNeighbors(torch.autograd.Function):
+    """py:165-212: tensors are kept as ctx attributes, as in the reference."""
+
+    @staticmethod
+    def forward(ctx, features, transform, queries, keys, frequencies, distance_transform,
+                indices, ranges, dists, densities, inv_total_densities, debug):
+        ctx.features, ctx.transform, ctx.queries, ctx.keys = features, transform, queries, keys
+        ctx.frequencies, ctx.distance_transform = frequencies, distance_transform
+        ctx.indices, ctx.ranges, ctx.dists, ctx.densities = indices, ranges, dists, densities
+        ctx.inv_total_densities, ctx.debug = inv_total_densities, debug
+        args = (features, transform, queries, keys, frequencies, distance_transform, indices,
+                ranges, dists, densities, inv_total_densities, debug)
+        weights, embeddings, factors, neighbor_features = call_debug(
+            _C.aggregate_neighbors, debug, "aggregate", *args)
+        if torch.isnan(neighbor_features.mean()):
+            # The reference prints conics[i] here, a name undefined in that scope (py:188);
+            # the diagnostic is kept without it.
+            for i in range(neighbor_features.shape[0]):
+                if torch.isnan(neighbor_features[i].mean()):
+                    print(i, neighbor_features[i])
+        ctx.weights, ctx.embeddings, ctx.factors = weights, embeddings, factors
+        return neighbor_features
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        grads = call_debug(
+            _C.aggregate_neighbors_backward, ctx.debug, "aggregate_bw",
+            ctx.features, ctx.transform, ctx.queries, ctx.keys, ctx.frequencies,
+            ctx.distance_transform, ctx.indices, ctx.ranges, ctx.dists, ctx.densities,
+            ctx.weights, ctx.embeddings, ctx.factors, ctx.inv_total_densities, grad_out, ctx.debug)
+        return tuple(grads) + (None,) * 6
+
+
+class GaussianSampler:
+    """Per-step state holder (py:214-317): preprocess once, then sample/aggregate."""
+
+    def __init__(self, debug):
+        self.debug = debug
+
+    def preprocess(self, means, values, covariances, conics, samples):
+        (self.num_rendered, self.binning_buffer, self.sample_binning_buffer, self.ranges,
+         self.sample_ranges, self.radii) = preprocess_gaussians(
+            means, values, covariances, conics, samples, self.debug)
+        self.means, self.values, self.conics, self.samples = means, values, conics, samples
+
+    def _args(self):
+        return (self.means, self.values, self.conics, self.samples, self.num_rendered,
+                self.binning_buffer, self.sample_binning_buffer, self.ranges,
+                self.sample_ranges, self.debug)
+
+    def sample_gaussians(self):
+        return sample_gaussians(*self._args())
+
+    def sample_gaussians_derivative(self):
+        return sample_gaussians_derivative(*self._args())
+
+    def sample_gaussians_laplacian(self):
+        return sample_gaussians_laplacian(*self._args())
+
+    def sample_gaussians_third_derivative(self):
+        return sample_gaussians_third_derivative(*self._args())
+
+    def preprocess_aggregate(self):
+        (self.indices, self.ranges_agg, self.dists, self.densities,
+         self.inv_total_densities) = preprocess_aggregate(self.means, self.conics, self.radii,
+                                                          self.debug)
+        # the reference overwrites self.ranges with the aggregate CSR ranges (py:294-298)
+        self.ranges = self.ranges_agg
+
+    def aggregate_neighbors(self, features, transform, queries, keys, frequencies, distance_transform):
+        return aggregate_neighbors(features, transform, queries, keys, frequencies,
+                                   distance_transform, self.indices, self.ranges, self.dists,
+                                   self.densities, self.inv_total_densities, self.debug)

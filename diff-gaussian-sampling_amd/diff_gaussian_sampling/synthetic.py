@@ -1,0 +1,65 @@
+"""Seeded synthetic Gaussian fields, generated on the CPU so that the
+GPU path and the CPU oracle see identical bits.
+
+    means     ~ U[-1, 1)^D                                   (seed + 0)
+    sigma_d   ~ h * U[0.5, 1.5],  h = 2 / P^(1/D)             (seed + 1)
+    theta     ~ U[0, pi)  (D = 2; anisotropic rotation)      (seed + 2)
+    cov       = R diag(sigma^2) R^T, packed [xx, xy, yy] (D=2) / [xx] (D=1)
+    conics    = exact inverse, packed [yy, -xy, xx] / det    (float64, then rounded)
+    values    ~ N(0, 1) [P, C]                                (seed + 3)
+    samples   ~ U[-1, 1)^D [N, D]                              (seed + 4)
+    dL_dout   ~ N(0, 1) [N, K, C]                             (seed + 5)
+"""
+import math
+
+import torch
+
+
+def _gen(seed):
+    g = torch.Generator()
+    g.manual_seed(int(seed))
+    return g
+
+
+def gaussians(P, D=2, C=1, seed=0, scale=1.0):
+    """Returns float32 CPU tensors (means, values, covariances, conics)."""
+    means = torch.rand(P, D, generator=_gen(seed), dtype=torch.float64) * 2.0 - 1.0
+    h = 2.0 / (max(P, 1) ** (1.0 / D)) * scale
+    sig = h * (0.5 + torch.rand(P, D, generator=_gen(seed + 1), dtype=torch.float64))
+    if D == 1:
+        var = sig[:, 0] ** 2
+        cov = var[:, None]
+        con = (1.0 / var)[:, None]
+    else:
+        th = torch.rand(P, generator=_gen(seed + 2), dtype=torch.float64) * math.pi
+        c, s = torch.cos(th), torch.sin(th)
+        s0, s1 = sig[:, 0] ** 2, sig[:, 1] ** 2
+        xx = c * c * s0 + s * s * s1
+        xy = c * s * (s0 - s1)
+        yy = s * s * s0 + c * c * s1
+        det = xx * yy - xy * xy
+        cov = torch.stack([xx, xy, yy], -1)
+        con = torch.stack([yy / det, -xy / det, xx / det], -1)
+    values = torch.randn(P, C, generator=_gen(seed + 3), dtype=torch.float64)
+    return (means.float(), values.float(), cov.float(), con.float())
+
+
+def samples(N, D=2, seed=4):
+    return (torch.rand(N, D, generator=_gen(seed), dtype=torch.float64) * 2.0 - 1.0).float()
+
+
+def grid_samples(n, D=2):
+    """A regular n^D lattice on [-1, 1)^D (the physics-informed collocation grid)."""
+    ax = torch.arange(n, dtype=torch.float64) * (2.0 / n) - 1.0
+    if D == 1:
+        return ax[:, None].float()
+    yy, xx = torch.meshgrid(ax, ax, indexing="ij")
+    return torch.stack([xx.reshape(-1), yy.reshape(-1)], -1).float()
+
+
+def out_components(function, D):
+    return D ** {"gaussian": 0, "derivative": 1, "laplacian": 2, "third": 3}[function]
+
+
+def grad_out(N, K, C, seed=5):
+    return torch.randn(N, K, C, generator=_gen(seed), dtype=torch.float64).float()

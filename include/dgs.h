@@ -1,0 +1,121 @@
+/*
+ * dgs.h -- C ABI of the MI355X-native differentiable Gaussian sampler (libdgs.so).
+ *
+ * Plain pointers, sizes and a HIP stream; no torch types.  Every device pointer is global
+ * memory on the current HIP device; every array is dense row-major fp32 unless stated.
+ * All entry points are asynchronous on `stream` except where a host value is returned
+ * (dgs_tile_grid, dgs_preprocess), and none allocates memory on its own: buffers come from
+ * the caller through `dgs_alloc_fn` (mirroring the reference's resize_functional lambdas,
+ * sample_points.cu:29-35) or as explicit workspaces.
+ *
+ * Each function names the reference interface it replaces.  The torch extension
+ * diff_gaussian_sampling._C (csrc/torch_ext.cpp) maps the 12 pybind entry points of the
+ * reference (ext.cpp:19-32) onto these functions; INTEGRATION.md shows the ctypes binding.
+ *
+ * Return value: DGS_OK (0) or a dgs_status code; dgs_last_error() describes the failure
+ * (thread-local).  With debug != 0 every launch is followed by a stream synchronisation
+ * and a HIP error check, as the reference's CHECK_CUDA(…, debug) does (auxiliary.h:33-40).
+ */
+#ifndef DGS_H_INCLUDED
+#define DGS_H_INCLUDED
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *dgs_stream_t; /* == hipStream_t; NULL = default stream */
+
+enum dgs_status {
+    DGS_OK = 0,
+    DGS_ERR_ARG = 1,     /* invalid argument (shape, dimension, size)                */
+    DGS_ERR_HIP = 2,     /* HIP runtime / kernel error                               */
+    DGS_ERR_ALLOC = 3,   /* the allocation callback returned NULL                    */
+    DGS_ERR_BUFFER = 4   /* an opaque binning buffer is missing, stale or corrupted  */
+};
+
+/* CudaSampler::Function (sampler.h:23) */
+enum dgs_function { DGS_GAUSSIAN = 0, DGS_DERIVATIVE = 1, DGS_LAPLACIAN = 2, DGS_THIRD = 3 };
+
+/* Which buffer the allocation callback is asked for. */
+enum dgs_buffer {
+    DGS_BUF_BINNING = 0,        /* opaque Gaussian-side binning state (returned to Python) */
+    DGS_BUF_SAMPLE_BINNING = 1, /* opaque sample-side binning state (returned to Python)   */
+    DGS_BUF_RANGES = 2,         /* uint2[T] + 8 B, reference layout (sample_points.cu:76)  */
+    DGS_BUF_SAMPLE_RANGES = 3,  /* uint2[T] + 8 B, reference layout (sample_points.cu:77)  */
+    DGS_BUF_SCRATCH = 4         /* temporary, released by the caller after the call        */
+};
+
+/* Returns device memory of at least `bytes` bytes (16-byte aligned), or NULL on failure.
+ * It may be called several times per buffer kind only for DGS_BUF_SCRATCH. */
+typedef void *(*dgs_alloc_fn)(void *ctx, int which, size_t bytes);
+
+const char *dgs_last_error(void);
+int dgs_version(void);
+
+/* Tile grid of the reference host glue (sample_points.cu:70-74), computed on the device with
+ * torch's CUDA-path arithmetic: grid[d] = ceil((max_d - min_d + 1e-6f) * (1.0f / 0.51f)),
+ * offset[d] = min_d.  Synchronises `stream`; grid_out/offset_out are host arrays of D. */
+int dgs_tile_grid(int N, int D, const float *samples, int *grid_out, float *offset_out,
+                  dgs_stream_t stream);
+
+/* Binning: replaces PreprocessCUDA (sample_points.cu:38-98) and
+ * CudaSampler::Sampler::preprocess (sampler_impl.cu:216-330).
+ *   means[P][D], covariances[P][S], conics[P][S], samples[N][D]   (S = D(D+1)/2, D in {1,2})
+ *   grid[D], grid_offset[D]: host arrays (dgs_tile_grid, or the global grid of a sharded run)
+ *   radii[P]: out, reference radii (0 for skipped Gaussians)
+ *   num_rendered: out (host), the reference's R = sum of tiles touched
+ * Buffers are requested through `alloc`.  Synchronises `stream` once (to size the lists).
+ * Contract: the forward/backward calls that use these buffers must pass the same means,
+ * conics and samples (GaussianSampler guarantees it; values may differ). */
+int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
+                   const float *conics, const float *samples, const int *grid,
+                   const float *grid_offset, float *radii, dgs_alloc_fn alloc, void *alloc_ctx,
+                   int64_t *num_rendered, dgs_stream_t stream, int debug);
+
+/* Workspace bytes needed by dgs_sample_forward (backward == 0) or dgs_sample_backward. */
+size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward);
+
+/* Forward: replaces SampleGaussians{,Derivative,Laplacian,Third}CUDA (sample_points.cu:100-143,
+ * 198-296), CudaSampler::Sampler::forward (sampler_impl.cu:333-364) and FORWARD::render
+ * (forward.cu:277-345).  out[N][K][C], K = D^function, must be zero-filled by the caller
+ * (samples outside every tile stay 0, as in the reference). */
+int dgs_sample_forward(int function, int P, int D, int N, int C, const float *means,
+                       const float *values, const float *conics, const float *samples,
+                       const void *binning, size_t binning_bytes, const void *sample_binning,
+                       size_t sample_binning_bytes, float *out, void *workspace,
+                       size_t workspace_bytes, dgs_stream_t stream, int debug);
+
+/* Backward: replaces SampleGaussians*BackwardCUDA (sample_points.cu:145-196, 298-372),
+ * CudaSampler::Sampler::backward (sampler_impl.cu:368-405) and BACKWARD::render
+ * (backward.cu:418-501).  dL_dout[N][K][C]; writes (overwrites) dL_dmeans[P][D],
+ * dL_dvalues[P][C], dL_dconics[P][S]. */
+int dgs_sample_backward(int function, int P, int D, int N, int C, const float *means,
+                        const float *values, const float *conics, const float *samples,
+                        const float *dL_dout, const void *binning, size_t binning_bytes,
+                        const void *sample_binning, size_t sample_binning_bytes,
+                        float *dL_dmeans, float *dL_dvalues, float *dL_dconics, void *workspace,
+                        size_t workspace_bytes, dgs_stream_t stream, int debug);
+
+/* Diagnostics (not on the reference API): counts, over the pairs the forward evaluates,
+ * W_cand (candidate pairs after culling) and W_live (pairs with power >= thr, the survey's
+ * live-pair count for thr = -104).  counts[0] = W_cand, counts[1] = W_live (host, syncs). */
+int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics,
+                    const float *samples, const void *binning, size_t binning_bytes,
+                    const void *sample_binning, size_t sample_binning_bytes, float thr,
+                    int64_t *counts, void *workspace, size_t workspace_bytes,
+                    dgs_stream_t stream);
+
+/* Benchmark support: bracket every forward (which = 0) / backward (which = 1) render-kernel
+ * launch with HIP events on its stream.  dgs_timing_read waits for the recorded events, adds
+ * their durations into *total_ms, clears the record and returns the launch count. */
+void dgs_timing_enable(int on);
+int dgs_timing_read(int which, double *total_ms);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* DGS_H_INCLUDED */

@@ -1,0 +1,572 @@
+/*
+ * oracle.c -- CPU restatement of the kr4b/diff-gaussian-sampling sampler path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library, and only as the checker (or as the timed CPU
+ * baseline).  The product path (diff_gaussian_sampling + libdgs.so) never links or calls it.
+ *
+ * PARITY STATUS: "parity unpinned".  The reference is CUDA-only (nvcc, cub, cooperative
+ * groups, an un-vendored glm submodule) and cannot be built or run in this image, and it
+ * ships no tests, fixtures or golden vectors.  This restatement is
+ * instead pinned by (a) autograd: every backward formula equals torch.autograd of the
+ * matching forward (except the reference's own D=1 third-derivative conic gradient,
+ * backward.cu:322-325, which is reproduced literally and pinned by a literal transcription
+ * test), (b) closed-form known answers, and (c) torch's own CUDA-path arithmetic for the
+ * tile grid (tests/test_gpu_parity.py::test_tile_grid_matches_torch_cuda_semantics).
+ *
+ * Arithmetic is literal: float where the reference uses FLOAT, double where the reference's
+ * double literals promote (e.g. `-0.5 * (...)`, `3.0 * sqrt(...)`), expf/sqrtf/floorf for the
+ * CUDA float overloads of exp/sqrt/floor.  Build with -ffp-contract=off so that no product
+ * is fused into an FMA (nvcc's contraction choices are unknowable without the toolchain).
+ *
+ * Every function cites the reference file:line it follows.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define ORC_TILE 0.51f /* config.h:18 BLOCK_SIZE */
+
+typedef struct {
+    int P, D, N;
+    int grid[2];
+    int T;
+    float off[2];
+    int64_t R;        /* num_rendered: sum of tiles_touched (sampler_impl.cu:253-257) */
+    int64_t *gstart;  /* [T+1] CSR over tiles of the per-tile Gaussian lists         */
+    int32_t *glist;   /* ascending gid inside each tile (unique (tile<<32|gid) keys) */
+    int64_t *sstart;  /* [T+1] CSR over tiles of the per-tile sample lists           */
+    int32_t *slist;   /* ascending sid inside each tile                              */
+    int32_t *skey;    /* [N] sample tile key (may be >= T: never rendered)           */
+    uint32_t *ranges; /* [2T] reference-layout uint2 ranges (sampler_impl.cu:134-151) */
+    uint32_t *sranges;
+} orc_bins;
+
+/* float -> int as the CUDA cvt.rzi/rmi.s32.f32 instructions do it: saturating, NaN -> 0. */
+static int sat_int(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483647.0f) return 2147483647;
+    if (v <= -2147483648.0f) return (-2147483647 - 1);
+    return (int)v;
+}
+
+/* sample_points.cu:70-74.  min/max over samples, then
+ *   tile_grid = ceil((max - min + 1e-6f) / BLOCK_SIZE)
+ * evaluated by torch on the CUDA device.  ATen's div_true_kernel_cuda turns division by a
+ * CPU scalar into a multiplication by the opmath (float) reciprocal, so the CUDA result is
+ * ceil(ext * (1.0f / 0.51f)); tests pin this against torch's own GPU op. */
+void orc_tile_grid(int N, int D, const float *samples, int *grid, float *off) {
+    for (int d = 0; d < 2; ++d) { grid[d] = 1; off[d] = 0.0f; }
+    for (int d = 0; d < D; ++d) {
+        float mn = samples[d], mx = samples[d];
+        for (int i = 1; i < N; ++i) {
+            float v = samples[(int64_t)i * D + d];
+            if (v < mn) mn = v;
+            if (v > mx) mx = v;
+        }
+        volatile float ext = (mx - mn) + 1e-6f;
+        volatile float inv = 1.0f / ORC_TILE;
+        volatile float q = ext * inv;
+        grid[d] = (int)ceilf(q);
+        off[d] = mn;
+    }
+}
+
+/* forward.cu:52-61 -- radius of the 3-sigma box; returns 0 when the Gaussian is skipped. */
+static float ref_radius(int D, const float *cov) {
+    if (D == 1) return (float)(3.0 * (double)sqrtf(cov[0]));
+    float det = cov[0] * cov[2] - cov[1] * cov[1];
+    if (det == 0.0f) return 0.0f;
+    float mid = 0.5f * (cov[0] + cov[2]);
+    float disc = mid * mid - det;
+    double floor_disc = fmax(1e-6, (double)disc); /* CUDA max(double, float) */
+    float lambda = (float)((double)mid + sqrt(floor_disc));
+    return (float)(3.0 * (double)sqrtf(lambda));
+}
+
+/* auxiliary.h:21-31 (TORUS branch) */
+static void ref_rect(int D, const float *p, float r, const float *off, int *rmin, int *rmax) {
+    for (int i = 0; i < D; ++i) {
+        float lo = ((p[i] - off[i]) - r) / ORC_TILE;
+        float hi = ((p[i] - off[i]) + r) / ORC_TILE;
+        rmin[i] = sat_int(floorf(lo));
+        rmax[i] = sat_int(ceilf(hi));
+    }
+}
+
+/* forward.cu:24-83 -- tiles touched; radius stored only when touched != 0. */
+static uint32_t ref_touched(int D, const float *mean, const float *cov, const int *grid,
+                            const float *off, float *radius_out) {
+    *radius_out = 0.0f;
+    if (D == 2) {
+        float det = cov[0] * cov[2] - cov[1] * cov[1];
+        if (det == 0.0f) return 0;
+    }
+    float r = ref_radius(D, cov);
+    int rmin[2], rmax[2];
+    ref_rect(D, mean, r, off, rmin, rmax);
+    int t0 = rmax[0] - rmin[0];
+    if (t0 > grid[0]) t0 = grid[0];
+    uint32_t touched;
+    if (D == 1) {
+        touched = (uint32_t)t0;
+    } else {
+        int t1 = rmax[1] - rmin[1];
+        if (t1 > grid[1]) t1 = grid[1];
+        touched = (uint32_t)(t1 * t0);
+    }
+    if (touched == 0) return 0;
+    *radius_out = r;
+    return touched;
+}
+
+static int wrap_tile(int x, int g) { return x < 0 ? (g + (x % g)) : (x % g); } /* sampler_impl.cu:88-89 */
+
+/* sampler_impl.cu:54-129 -- enumerate the tile keys of one Gaussian, in emission order. */
+static int ref_keys(int D, const float *mean, float r, const int *grid, const float *off,
+                    uint32_t *keys) {
+    int rmin[2], rmax[2], n = 0;
+    ref_rect(D, mean, r, off, rmin, rmax);
+    if (rmax[0] - rmin[0] >= grid[0]) { rmin[0] = 0; rmax[0] = grid[0]; }
+    if (D == 1) {
+        for (int x = rmin[0]; x < rmax[0]; ++x) keys[n++] = (uint32_t)wrap_tile(x, grid[0]);
+        return n;
+    }
+    if (rmax[1] - rmin[1] >= grid[1]) { rmin[1] = 0; rmax[1] = grid[1]; }
+    for (int y = rmin[1]; y < rmax[1]; ++y)
+        for (int x = rmin[0]; x < rmax[0]; ++x)
+            keys[n++] = (uint32_t)(wrap_tile(y, grid[1]) * grid[0] + wrap_tile(x, grid[0]));
+    return n;
+}
+
+/* sampler_impl.cu:155-189 -- sample tile key (clamped to [0, grid], not grid-1). */
+static uint32_t ref_sample_key(int D, const float *s, const int *grid, const float *off) {
+    uint32_t tile[2] = {0, 0};
+    for (int i = 0; i < D; ++i) {
+        int t = sat_int((s[i] - off[i]) / ORC_TILE);
+        if (t < 0) t = 0;
+        if (t > grid[i]) t = grid[i];
+        tile[i] = (uint32_t)t;
+    }
+    return D == 1 ? tile[0] : tile[1] * (uint32_t)grid[0] + tile[0];
+}
+
+void orc_free(orc_bins *b) {
+    if (!b) return;
+    free(b->gstart); free(b->glist); free(b->sstart); free(b->slist); free(b->skey);
+    free(b->ranges); free(b->sranges); free(b);
+}
+
+/* sample_points.cu:38-98 + sampler_impl.cu:216-330.  grid/off may be given (sharded runs
+ * use the global grid); pass grid == NULL to derive them from `samples` as the reference
+ * does.  Writes radii[P].  Returns NULL on allocation failure. */
+orc_bins *orc_bin(int P, int D, int N, const float *means, const float *covs,
+                  const float *samples, const int *grid_in, const float *off_in, float *radii) {
+    orc_bins *b = (orc_bins *)calloc(1, sizeof(orc_bins));
+    if (!b) return NULL;
+    b->P = P; b->D = D; b->N = N;
+    if (grid_in) {
+        b->grid[0] = grid_in[0]; b->grid[1] = D == 2 ? grid_in[1] : 1;
+        b->off[0] = off_in[0]; b->off[1] = D == 2 ? off_in[1] : 0.0f;
+    } else {
+        orc_tile_grid(N, D, samples, b->grid, b->off);
+    }
+    b->T = D == 1 ? b->grid[0] : b->grid[0] * b->grid[1];
+    const int T = b->T, S = D * (D + 1) / 2;
+    b->gstart = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
+    b->sstart = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
+    b->ranges = (uint32_t *)calloc((size_t)2 * T, sizeof(uint32_t));
+    b->sranges = (uint32_t *)calloc((size_t)2 * T, sizeof(uint32_t));
+    b->skey = (int32_t *)calloc((size_t)N + 1, sizeof(int32_t));
+    uint32_t *keys = (uint32_t *)malloc(sizeof(uint32_t) * ((size_t)T + 1));
+    if (!b->gstart || !b->sstart || !b->ranges || !b->sranges || !b->skey || !keys) {
+        free(keys); orc_free(b); return NULL;
+    }
+    /* pass 1: radii, R, per-tile counts */
+    int64_t *gcount = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
+    for (int g = 0; g < P; ++g) {
+        float r;
+        uint32_t touched = ref_touched(D, means + (int64_t)g * D, covs + (int64_t)g * S,
+                                       b->grid, b->off, &r);
+        radii[g] = r;
+        b->R += touched;
+        if (r > 0.0f) {
+            int n = ref_keys(D, means + (int64_t)g * D, r, b->grid, b->off, keys);
+            for (int k = 0; k < n; ++k)
+                if (keys[k] < (uint32_t)T) gcount[keys[k]]++;
+        }
+    }
+    for (int t = 0; t < T; ++t) b->gstart[t + 1] = b->gstart[t] + gcount[t];
+    b->glist = (int32_t *)malloc(sizeof(int32_t) * ((size_t)b->gstart[T] + 1));
+    memset(gcount, 0, sizeof(int64_t) * ((size_t)T + 1));
+    /* pass 2: fill -- gid-ascending scan gives the (tile<<32 | gid) sorted order per tile */
+    for (int g = 0; g < P; ++g) {
+        if (!(radii[g] > 0.0f)) continue;
+        int n = ref_keys(D, means + (int64_t)g * D, radii[g], b->grid, b->off, keys);
+        for (int k = 0; k < n; ++k)
+            if (keys[k] < (uint32_t)T) b->glist[b->gstart[keys[k]] + gcount[keys[k]]++] = g;
+    }
+    /* samples */
+    int64_t *scount = (int64_t *)calloc((size_t)T + 1, sizeof(int64_t));
+    for (int i = 0; i < N; ++i) {
+        uint32_t k = ref_sample_key(D, samples + (int64_t)i * D, b->grid, b->off);
+        b->skey[i] = (int32_t)k;
+        if (k < (uint32_t)T) scount[k]++;
+    }
+    for (int t = 0; t < T; ++t) b->sstart[t + 1] = b->sstart[t] + scount[t];
+    b->slist = (int32_t *)malloc(sizeof(int32_t) * ((size_t)b->sstart[T] + 1));
+    memset(scount, 0, sizeof(int64_t) * ((size_t)T + 1));
+    for (int i = 0; i < N; ++i) {
+        uint32_t k = (uint32_t)b->skey[i];
+        if (k < (uint32_t)T) b->slist[b->sstart[k] + scount[k]++] = i;
+    }
+    /* identifyTileRanges (sampler_impl.cu:134-151): empty tiles keep (0,0) */
+    for (int t = 0; t < T; ++t) {
+        if (b->gstart[t + 1] > b->gstart[t]) {
+            b->ranges[2 * t] = (uint32_t)b->gstart[t];
+            b->ranges[2 * t + 1] = (uint32_t)b->gstart[t + 1];
+        }
+        if (b->sstart[t + 1] > b->sstart[t]) {
+            b->sranges[2 * t] = (uint32_t)b->sstart[t];
+            b->sranges[2 * t + 1] = (uint32_t)b->sstart[t + 1];
+        }
+    }
+    free(gcount); free(scount); free(keys);
+    return b;
+}
+
+int orc_T(const orc_bins *b) { return b->T; }
+int64_t orc_R(const orc_bins *b) { return b->R; }
+void orc_grid(const orc_bins *b, int *grid, float *off) {
+    grid[0] = b->grid[0]; grid[1] = b->grid[1]; off[0] = b->off[0]; off[1] = b->off[1];
+}
+void orc_ranges(const orc_bins *b, uint32_t *ranges, uint32_t *sranges) {
+    memcpy(ranges, b->ranges, sizeof(uint32_t) * 2 * (size_t)b->T);
+    memcpy(sranges, b->sranges, sizeof(uint32_t) * 2 * (size_t)b->T);
+}
+void orc_sample_keys(const orc_bins *b, int32_t *keys) {
+    memcpy(keys, b->skey, sizeof(int32_t) * (size_t)b->N);
+}
+int64_t orc_tile_gaussians(const orc_bins *b, int t, int32_t *out) {
+    int64_t n = b->gstart[t + 1] - b->gstart[t];
+    if (out) memcpy(out, b->glist + b->gstart[t], sizeof(int32_t) * (size_t)n);
+    return n;
+}
+
+/* forward.cu:149-157 / backward.cu:89-97 -- period-2 torus wrap of one displacement. */
+static float ref_wrap(float x) {
+    if (fabsf(x) > 1.0) {
+        if (x >= 0) x = (float)(fmod((double)x, 2.0) - 2.0);
+        else x = (float)(fmod((double)x, 2.0) + 2.0);
+    }
+    return x;
+}
+
+enum { F_GAUSS = 0, F_DERIV = 1, F_LAPL = 2, F_THIRD = 3 };
+
+static int out_comps(int fn, int D) {
+    int k = 1;
+    for (int i = 0; i < fn; ++i) k *= D;
+    return k;
+}
+
+/* forward.cu:168-275 -- one pair's contribution, accumulated into o[comp*C + ch]. */
+static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const float *v, float *o) {
+    if (D == 1) {
+        float x1 = c[0] * X[0];
+        float power = fn == F_GAUSS ? (float)(-0.5 * c[0] * X[0] * X[0]) : (float)(-0.5 * x1 * X[0]);
+        if (power > 0.0) return;
+        float a = expf(power);
+        for (int ch = 0; ch < C; ++ch) {
+            float va = v[ch] * a;
+            switch (fn) {
+            case F_GAUSS: o[ch] += va; break;
+            case F_DERIV: o[ch] += va * x1; break;
+            case F_LAPL: o[ch] += va * (x1 * x1 - c[0]); break;
+            default: o[ch] = (float)((double)o[ch] + (double)va * (2.0 * c[0] * x1 - (double)(x1 * x1 * x1) + (double)(c[0] * x1)));
+            }
+        }
+        return;
+    }
+    float power;
+    float x1 = c[0] * X[0], x2 = c[2] * X[1];
+    if (fn == F_GAUSS)
+        power = (float)(-0.5 * (double)(c[0] * X[0] * X[0] + c[2] * X[1] * X[1]) - (double)(c[1] * X[0] * X[1]));
+    else
+        power = (float)(-0.5 * (double)(x1 * X[0] + x2 * X[1]) - (double)(c[1] * X[0] * X[1]));
+    if (power > 0.0) return;
+    float a = expf(power);
+    float a1 = x1 + c[1] * X[1], a2 = x2 + c[1] * X[0];
+    float t[4];
+    int nt = 0;
+    switch (fn) {
+    case F_GAUSS: break;
+    case F_DERIV: nt = 2; t[0] = x1 + c[1] * X[1]; t[1] = x2 + c[1] * X[0]; break;
+    case F_LAPL: nt = 3; t[0] = a1 * a1 - c[0]; t[1] = a1 * a2 - c[1]; t[2] = a2 * a2 - c[2]; break;
+    default:
+        nt = 4;
+        t[0] = (float)(3.0 * c[0] * a1 - (double)(a1 * a1 * a1));
+        t[1] = (float)(2.0 * c[1] * a1 - (double)(a1 * a1 * a2) + (double)(c[0] * a2));
+        t[2] = (float)(2.0 * c[1] * a2 - (double)(a1 * a2 * a2) + (double)(c[2] * a1));
+        t[3] = (float)(3.0 * c[2] * a2 - (double)(a2 * a2 * a2));
+    }
+    /* expanded component -> unique term: laplacian [xx,xy,yx,yy]; third [xxx,xxy,xyx,xyy,yxx,yxy,yyx,yyy] */
+    static const int lap_map[4] = {0, 1, 1, 2};
+    static const int third_map[8] = {0, 1, 1, 2, 1, 2, 2, 3};
+    for (int ch = 0; ch < C; ++ch) {
+        float va = v[ch] * a;
+        switch (fn) {
+        case F_GAUSS: o[ch] += va; break;
+        case F_DERIV: o[ch] += va * t[0]; o[C + ch] += va * t[1]; break;
+        case F_LAPL: for (int k = 0; k < 4; ++k) o[k * C + ch] += va * t[lap_map[k]]; break;
+        default: for (int k = 0; k < 8; ++k) o[k * C + ch] += va * t[third_map[k]];
+        }
+    }
+    (void)nt;
+}
+
+/* backward.cu:108-416 -- one pair's gradient contributions (literal formulas, including the
+ * reference's D=1 third-derivative conic gradient at backward.cu:322-325). */
+static void bwd_pair(int fn, int D, int C, const float *X, const float *c, const float *v,
+                     const float *dL /* [K][C] of this sample */, float *gm, float *gv, float *gc) {
+    if (D == 1) {
+        float x1 = c[0] * X[0];
+        float power = fn == F_GAUSS ? (float)(-0.5 * c[0] * X[0] * X[0]) : (float)(-0.5 * x1 * X[0]);
+        if (power > 0.0) return;
+        float G = expf(power);
+        float dLdG = 0.0f;
+        for (int ch = 0; ch < C; ++ch) {
+            float d = dL[ch];
+            switch (fn) {
+            case F_GAUSS: gv[ch] += G * d; break;
+            case F_DERIV: gv[ch] += x1 * d * G; break;
+            case F_LAPL: { float gx = (x1 * x1 - c[0]) * d; gv[ch] += gx * G; } break;
+            default: { float gx = (float)((3.0 * c[0] * x1 - (double)(x1 * x1 * x1)) * d); gv[ch] += gx * G; }
+            }
+            dLdG += v[ch] * d;
+        }
+        switch (fn) {
+        case F_GAUSS: {
+            float gdx = G * X[0];
+            float dG = gdx * c[0];
+            float dLdx = dLdG * dG;
+            gm[0] += -dLdx;
+            gc[0] += (float)(-0.5 * gdx * X[0] * dLdG);
+        } break;
+        case F_DERIV: {
+            float dLdx = (x1 * x1 - c[0]) * dLdG * G;
+            gm[0] += -dLdx;
+            gc[0] += (float)(((double)X[0] - 0.5 * X[0] * X[0] * x1) * dLdG * G);
+        } break;
+        case F_LAPL: {
+            float dLdx = (float)(((double)(x1 * x1 * x1) - 3.0 * c[0] * x1) * dLdG * G);
+            float dVdc = (float)((2.0 * x1 * X[0] - 0.5 * (x1 * x1 - c[0]) * X[0] * X[0] - 1.0) * dLdG * G);
+            gm[0] += -dLdx;
+            gc[0] += dVdc;
+        } break;
+        default: {
+            float dLdx = (float)((6.0 * c[0] * x1 * x1 - (double)(x1 * x1 * x1 * x1) - 3.0 * c[0] * c[0]) * dLdG * G);
+            /* backward.cu:322-325: not the true derivative; reproduced literally */
+            float dVdc = (float)((2.0 * X[0] * X[0] - 2.0 * x1 * x1 * X[0] - 0.5 * (2.0 * X[0] * x1 - X[0]) * X[0] * X[0]
+                                  + 0.5 * (x1 * x1 - c[0]) * x1 * X[0] * X[0]) * dLdG * G);
+            gm[0] += -dLdx;
+            gc[0] += dVdc;
+        }
+        }
+        return;
+    }
+    float x1 = c[0] * X[0], x2 = c[2] * X[1];
+    float power;
+    if (fn == F_GAUSS)
+        power = (float)(-0.5 * (double)(c[0] * X[0] * X[0] + c[2] * X[1] * X[1]) - (double)(c[1] * X[0] * X[1]));
+    else
+        power = (float)(-0.5 * (double)(x1 * X[0] + x2 * X[1]) - (double)(c[1] * X[0] * X[1]));
+    if (power > 0.0) return;
+    float G = expf(power);
+    float a1 = x1 + c[1] * X[1], a2 = x2 + c[1] * X[0];
+    if (fn == F_GAUSS) {
+        float dLdG = 0.0f;
+        for (int ch = 0; ch < C; ++ch) { gv[ch] += G * dL[ch]; dLdG += v[ch] * dL[ch]; }
+        float gdx = G * X[0], gdy = G * X[1];
+        gm[0] += -dLdG * (gdx * c[0] + gdy * c[1]);
+        gm[1] += -dLdG * (gdx * c[1] + gdy * c[2]);
+        gc[0] += (float)(-0.5 * gdx * X[0] * dLdG);
+        gc[1] += -gdy * X[0] * dLdG;
+        gc[2] += (float)(-0.5 * gdy * X[1] * dLdG);
+        return;
+    }
+    if (fn == F_DERIV) {
+        float Gx = 0.0f, Gy = 0.0f;
+        for (int ch = 0; ch < C; ++ch) {
+            float dx = dL[ch], dy = dL[C + ch];
+            float gx = a1 * dx + a2 * dy;
+            gv[ch] += gx * G;
+            Gx += v[ch] * dx;
+            Gy += v[ch] * dy;
+        }
+        float gx = a1 * Gx + a2 * Gy;
+        float dLdx = ((a1 * a1 - c[0]) * Gx + (a1 * a2 - c[1]) * Gy) * G;
+        float dLdy = ((a2 * a2 - c[2]) * Gy + (a1 * a2 - c[1]) * Gx) * G;
+        gm[0] += -dLdx;
+        gm[1] += -dLdy;
+        gc[0] += (float)(((double)(X[0] * Gx) - 0.5 * X[0] * X[0] * gx) * G);
+        gc[1] += (X[1] * Gx + X[0] * Gy - X[0] * X[1] * gx) * G;
+        gc[2] += (float)(((double)(X[1] * Gy) - 0.5 * X[1] * X[1] * gx) * G);
+        return;
+    }
+    if (fn == F_LAPL) {
+        float dxx = a1 * a1 - c[0], dxy = a1 * a2 - c[1], dyy = a2 * a2 - c[2];
+        float Gxx = 0.0f, Gxy = 0.0f, Gyx = 0.0f, Gyy = 0.0f;
+        for (int ch = 0; ch < C; ++ch) {
+            float d0 = dL[ch], d1 = dL[C + ch], d2 = dL[2 * C + ch], d3 = dL[3 * C + ch];
+            float g = dxx * d0 + dxy * d1 + dxy * d2 + dyy * d3;
+            gv[ch] += g * G;
+            Gxx += v[ch] * d0; Gxy += v[ch] * d1; Gyx += v[ch] * d2; Gyy += v[ch] * d3;
+        }
+        float dLdx = (float)(((double)(a1 * a1 * a1) - 3.0 * c[0] * a1) * Gxx
+                             + (double)((a1 * a2 * a1 - c[1] * a1 - (c[1] * a1 + c[0] * a2)) * (Gxy + Gyx))
+                             + ((double)(a2 * a2 * a1 - c[2] * a1) - 2.0 * c[1] * a2) * Gyy) * G;
+        float dLdy = (float)(((double)(a1 * a1 * a2 - c[0] * a2) - 2.0 * c[1] * a1) * Gxx
+                             + (double)((a1 * a2 * a2 - c[1] * a2 - (c[2] * a1 + c[1] * a2)) * (Gxy + Gyx))
+                             + ((double)(a2 * a2 * a2) - 3.0 * c[2] * a2) * Gyy) * G;
+        gm[0] += -dLdx;
+        gm[1] += -dLdy;
+        float S = Gxy + Gyx;
+        float xx_cxx = (float)(-0.5 * dxx * X[0] * X[0] + 2.0 * a1 * X[0] - 1.0);
+        float xy_cxx = (float)(-0.5 * dxy * X[0] * X[0] + (double)(a2 * X[0]));
+        float yy_cxx = (float)(-0.5 * dyy * X[0] * X[0]);
+        float xx_cxy = (float)((double)(-dxx * X[0] * X[1]) + 2.0 * a1 * X[1]);
+        float xy_cxy = -dxy * X[0] * X[1] + a2 * X[1] + a1 * X[0] - 1.0f;
+        float yy_cxy = (float)((double)(-dyy * X[0] * X[1]) + 2.0 * a2 * X[0]);
+        float xx_cyy = (float)(-0.5 * dxx * X[1] * X[1]);
+        float xy_cyy = (float)(-0.5 * dxy * X[1] * X[1] + (double)(a1 * X[1]));
+        float yy_cyy = (float)(-0.5 * dyy * X[1] * X[1] + 2.0 * a2 * X[1] - 1.0);
+        gc[0] += (xx_cxx * Gxx + xy_cxx * S + yy_cxx * Gyy) * G;
+        gc[1] += (xx_cxy * Gxx + xy_cxy * S + yy_cxy * Gyy) * G;
+        gc[2] += (xx_cyy * Gxx + xy_cyy * S + yy_cyy * Gyy) * G;
+        return;
+    }
+    /* third, D == 2 (backward.cu:329-415) */
+    float dxxx = (float)(3.0 * c[0] * a1 - (double)(a1 * a1 * a1));
+    float dxxy = (float)(2.0 * c[1] * a1 - (double)(a1 * a1 * a2) + (double)(c[0] * a2));
+    float dxyy = (float)(2.0 * c[1] * a2 - (double)(a1 * a2 * a2) + (double)(c[2] * a1));
+    float dyyy = (float)(3.0 * c[2] * a2 - (double)(a2 * a2 * a2));
+    float Gk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int ch = 0; ch < C; ++ch) {
+        const float *d = dL + ch;
+        float g = dxxx * d[0] + dxxy * d[C] + dxxy * d[2 * C] + dxyy * d[3 * C]
+                + dxxy * d[4 * C] + dxyy * d[5 * C] + dxyy * d[6 * C] + dyyy * d[7 * C];
+        gv[ch] += g * G;
+        for (int k = 0; k < 8; ++k) Gk[k] += v[ch] * d[k * C];
+    }
+    float S1 = Gk[1] + Gk[2] + Gk[4], S2 = Gk[3] + Gk[5] + Gk[6];
+    float xxy_dx = (float)(2.0 * a1 * a2 * c[0] + (double)(a1 * a1 * c[1]) - 3.0 * c[0] * c[1]);
+    float xyy_dx = (float)(2.0 * a1 * a2 * c[1] + (double)(a2 * a2 * c[0]) - (double)(c[2] * c[0]) - 2.0 * c[1] * c[1]);
+    /* left-to-right sum in double: each float term is promoted on its own */
+    float dLdx = (float)((((double)(dxxx * a1) - 3.0 * c[0] * c[0] + 3.0 * a1 * a1 * c[0]) * Gk[0]
+                          + (double)((dxxy * a1 + xxy_dx) * Gk[1]) + (double)((dxxy * a1 + xxy_dx) * Gk[2])
+                          + (double)((dxyy * a1 + xyy_dx) * Gk[3]) + (double)((dxxy * a1 + xxy_dx) * Gk[4])
+                          + (double)((dxyy * a1 + xyy_dx) * Gk[5]) + (double)((dxyy * a1 + xyy_dx) * Gk[6])
+                          + ((double)(dyyy * a1) - 3.0 * c[2] * c[1] + 3.0 * a2 * a2 * c[1]) * Gk[7]) * G);
+    float xxy_dy = (float)(2.0 * a1 * a2 * c[1] + (double)(a1 * a1 * c[2]) - (double)(c[0] * c[2]) - 2.0 * c[1] * c[1]);
+    float xyy_dy = (float)(2.0 * a1 * a2 * c[2] + (double)(a2 * a2 * c[1]) - 3.0 * c[2] * c[1]);
+    float dLdy = (float)((((double)(dxxx * a2) - 3.0 * c[0] * c[1] + 3.0 * a1 * a1 * c[1]) * Gk[0]
+                          + (double)((dxxy * a2 + xxy_dy) * Gk[1]) + (double)((dxxy * a2 + xxy_dy) * Gk[2])
+                          + (double)((dxyy * a2 + xyy_dy) * Gk[3]) + (double)((dxxy * a2 + xxy_dy) * Gk[4])
+                          + (double)((dxyy * a2 + xyy_dy) * Gk[5]) + (double)((dxyy * a2 + xyy_dy) * Gk[6])
+                          + ((double)(dyyy * a2) - 3.0 * c[2] * c[2] + 3.0 * a2 * a2 * c[2]) * Gk[7]) * G);
+    gm[0] += -dLdx;
+    gm[1] += -dLdy;
+    float X0 = X[0], X1 = X[1];
+    float v_cxx[4], v_cxy[4], v_cyy[4];
+    v_cxx[0] = (float)(-0.5 * dxxx * X0 * X0 + 3.0 * c[0] * X0 + 3.0 * a1 - 3.0 * a1 * a1 * X0);
+    v_cxx[1] = (float)(-0.5 * dxxy * X0 * X0 + 2.0 * c[1] * X0 - 2.0 * a1 * a2 * X0 + a2);
+    v_cxx[2] = (float)(-0.5 * dxyy * X0 * X0 - (double)(a2 * a2 * X0) + (double)(c[2] * X0));
+    v_cxx[3] = (float)(-0.5 * dyyy * X0 * X0);
+    v_cxy[0] = (float)((double)(-dxxx * X0 * X1) + 3.0 * c[0] * X1 - 3.0 * a1 * a1 * X1);
+    v_cxy[1] = (float)((double)(-dxxy * X0 * X1) + 2.0 * c[1] * X1 + 2.0 * a1 - 2.0 * a1 * a2 * X1 - (double)(a1 * a1 * X0) + (double)(c[0] * X0));
+    v_cxy[2] = (float)((double)(-dxyy * X0 * X1) + 2.0 * c[1] * X0 + 2.0 * a2 - (double)(a2 * a2 * X1) - 2.0 * a1 * a2 * X0 + (double)(c[2] * X1));
+    v_cxy[3] = (float)((double)(-dyyy * X0 * X1) + 3.0 * c[2] * X0 - 3.0 * a2 * a2 * X0);
+    v_cyy[0] = (float)(-0.5 * dxxx * X1 * X1);
+    v_cyy[1] = (float)(-0.5 * dxxy * X1 * X1 - (double)(a1 * a1 * X1) + (double)(c[0] * X1));
+    v_cyy[2] = (float)(-0.5 * dxyy * X1 * X1 + 2.0 * c[1] * X1 - 2.0 * a1 * a2 * X1 + a1);
+    v_cyy[3] = (float)(-0.5 * dyyy * X1 * X1 + 3.0 * c[2] * X1 + 3.0 * a2 - 3.0 * a2 * a2 * X1);
+    gc[0] += (v_cxx[0] * Gk[0] + v_cxx[1] * S1 + v_cxx[2] * S2 + v_cxx[3] * Gk[7]) * G;
+    gc[1] += (v_cxy[0] * Gk[0] + v_cxy[1] * S1 + v_cxy[2] * S2 + v_cxy[3] * Gk[7]) * G;
+    gc[2] += (v_cyy[0] * Gk[0] + v_cyy[1] * S1 + v_cyy[2] * S2 + v_cyy[3] * Gk[7]) * G;
+}
+
+static void displacement(int D, const float *m, const float *s, float *X) {
+    for (int k = 0; k < D; ++k) X[k] = ref_wrap(m[k] - s[k]);
+}
+
+/* forward.cu:87-166 (render) for samples `sub` (NULL = all); out is [N][K][C], accumulated
+ * in ascending-gid order exactly like the reference's per-thread loop.  Samples whose key
+ * is >= T are never rendered (left untouched). */
+void orc_forward(const orc_bins *b, int fn, int C, const float *means, const float *values,
+                 const float *conics, const float *samples, float *out, int nsub, const int32_t *sub) {
+    const int D = b->D, S = D * (D + 1) / 2, K = out_comps(fn, D);
+    int count = sub ? nsub : b->N;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        float *o = out + (int64_t)sid * K * C;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            fwd_pair(fn, D, C, X, conics + (int64_t)g * S, values + (int64_t)g * C, o);
+        }
+    }
+}
+
+/* backward.cu:26-106 -- gradient accumulation (serial order; the reference's atomic order
+ * is nondeterministic).  Grads are accumulated into dmeans[P][D], dvalues[P][C], dconics[P][S]
+ * (caller zero-initialises).  Only samples in `sub` contribute (NULL = all). */
+void orc_backward(const orc_bins *b, int fn, int C, const float *means, const float *values,
+                  const float *conics, const float *samples, const float *dL_dout, float *dmeans,
+                  float *dvalues, float *dconics, int nsub, const int32_t *sub) {
+    const int D = b->D, S = D * (D + 1) / 2, K = out_comps(fn, D);
+    int count = sub ? nsub : b->N;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        const float *dL = dL_dout + (int64_t)sid * K * C;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            bwd_pair(fn, D, C, X, conics + (int64_t)g * S, values + (int64_t)g * C, dL,
+                     dmeans + (int64_t)g * D, dvalues + (int64_t)g * C, dconics + (int64_t)g * S);
+        }
+    }
+}
+
+/* Diagnostic: pairs of the reference pair set with power >= thr (W_live for thr = -104) and
+ * the total pair count (W_ref), over samples `sub` (NULL = all). */
+void orc_count_pairs(const orc_bins *b, const float *means, const float *conics, const float *samples,
+                     double thr, int nsub, const int32_t *sub, int64_t *w_ref, int64_t *w_live) {
+    const int D = b->D, S = D * (D + 1) / 2;
+    int count = sub ? nsub : b->N;
+    int64_t ref = 0, live = 0;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            const float *c = conics + (int64_t)g * S;
+            double p = D == 1 ? -0.5 * c[0] * X[0] * X[0]
+                              : -0.5 * ((double)c[0] * X[0] * X[0] + (double)c[2] * X[1] * X[1]) - (double)c[1] * X[0] * X[1];
+            ref++;
+            if (p >= thr && p <= 0.0) live++;
+        }
+    }
+    *w_ref = ref;
+    *w_live = live;
+}

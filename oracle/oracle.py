@@ -1,0 +1,167 @@
+"""ctypes wrapper around oracle/_build/liboracle.so -- the CPU restatement of the reference.
+
+TEST INFRASTRUCTURE ONLY (see oracle.c header): imported by tests/, __graft_entry__.smoke()
+and bench.py's cpu_baseline leg, never by the product package.
+
+Parity status: "parity unpinned" -- no reference outputs exist (see oracle.c).
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+_lib = None
+
+FUNCTIONS = {"gaussian": 0, "derivative": 1, "laplacian": 2, "third": 3}
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def _load():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        build()
+    lib = ctypes.CDLL(_LIB_PATH)
+    P = ctypes.c_void_p
+    i32, i64 = ctypes.c_int, ctypes.c_int64
+    lib.orc_bin.restype = P
+    lib.orc_bin.argtypes = [i32, i32, i32, P, P, P, P, P, P]
+    lib.orc_free.argtypes = [P]
+    lib.orc_T.argtypes = [P]
+    lib.orc_R.argtypes = [P]
+    lib.orc_R.restype = i64
+    lib.orc_grid.argtypes = [P, P, P]
+    lib.orc_ranges.argtypes = [P, P, P]
+    lib.orc_sample_keys.argtypes = [P, P]
+    lib.orc_tile_gaussians.argtypes = [P, i32, P]
+    lib.orc_tile_gaussians.restype = i64
+    lib.orc_forward.argtypes = [P, i32, i32, P, P, P, P, P, i32, P]
+    lib.orc_backward.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
+    lib.orc_count_pairs.argtypes = [P, P, P, P, ctypes.c_double, i32, P, P, P]
+    lib.orc_tile_grid.argtypes = [i32, i32, P, P, P]
+    _lib = lib
+    return lib
+
+
+def _f32(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+
+
+def _ptr(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def out_components(function, D):
+    return D ** FUNCTIONS[function]
+
+
+def tile_grid(samples):
+    lib = _load()
+    s = _f32(samples)
+    N, D = s.shape
+    grid = np.zeros(2, np.int32)
+    off = np.zeros(2, np.float32)
+    lib.orc_tile_grid(N, D, _ptr(s), _ptr(grid), _ptr(off))
+    return grid[:D].copy(), off[:D].copy()
+
+
+class OracleBins:
+    """Reference binning (sample_points.cu:38-98, sampler_impl.cu:216-330) on the CPU."""
+
+    def __init__(self, means, covariances, samples, grid=None, offset=None):
+        lib = _load()
+        self.means = _f32(means)
+        self.covariances = _f32(covariances)
+        self.samples = _f32(samples)
+        self.P, self.D = self.means.shape
+        self.N = self.samples.shape[0]
+        self.radii = np.zeros(self.P, np.float32)
+        g = o = None
+        if grid is not None:
+            g = np.zeros(2, np.int32)
+            g[: len(grid)] = grid
+            o = np.zeros(2, np.float32)
+            o[: len(offset)] = offset
+        self._h = lib.orc_bin(self.P, self.D, self.N, _ptr(self.means), _ptr(self.covariances),
+                              _ptr(self.samples), _ptr(g), _ptr(o), _ptr(self.radii))
+        if not self._h:
+            raise MemoryError("orc_bin failed")
+        self.T = lib.orc_T(self._h)
+        self.num_rendered = int(lib.orc_R(self._h))
+        grid2 = np.zeros(2, np.int32)
+        off2 = np.zeros(2, np.float32)
+        lib.orc_grid(self._h, _ptr(grid2), _ptr(off2))
+        self.grid = grid2[: self.D].copy()
+        self.offset = off2[: self.D].copy()
+
+    def __del__(self):
+        if getattr(self, "_h", None):
+            _load().orc_free(self._h)
+            self._h = None
+
+    def ranges(self):
+        r = np.zeros(2 * self.T, np.uint32)
+        s = np.zeros(2 * self.T, np.uint32)
+        _load().orc_ranges(self._h, _ptr(r), _ptr(s))
+        return r.reshape(self.T, 2), s.reshape(self.T, 2)
+
+    def sample_keys(self):
+        k = np.zeros(self.N, np.int32)
+        _load().orc_sample_keys(self._h, _ptr(k))
+        return k
+
+    def tile_gaussians(self, t):
+        n = _load().orc_tile_gaussians(self._h, t, None)
+        out = np.zeros(max(n, 1), np.int32)
+        _load().orc_tile_gaussians(self._h, t, _ptr(out))
+        return out[:n]
+
+    def forward(self, function, values, conics, subset=None, samples=None, means=None):
+        lib = _load()
+        v = _f32(values)
+        c = _f32(conics)
+        m = self.means if means is None else _f32(means)
+        s = self.samples if samples is None else _f32(samples)
+        C = v.shape[1]
+        K = out_components(function, self.D)
+        out = np.zeros((self.N, K, C), np.float32)
+        sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
+        lib.orc_forward(self._h, FUNCTIONS[function], C, _ptr(m), _ptr(v), _ptr(c), _ptr(s),
+                        _ptr(out), 0 if sub is None else len(sub), _ptr(sub))
+        return out
+
+    def backward(self, function, values, conics, dL_dout, subset=None, samples=None, means=None):
+        lib = _load()
+        v = _f32(values)
+        c = _f32(conics)
+        m = self.means if means is None else _f32(means)
+        s = self.samples if samples is None else _f32(samples)
+        C = v.shape[1]
+        S = self.D * (self.D + 1) // 2
+        dL = _f32(dL_dout).reshape(self.N, -1)
+        dm = np.zeros((self.P, self.D), np.float32)
+        dv = np.zeros((self.P, C), np.float32)
+        dc = np.zeros((self.P, S), np.float32)
+        sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
+        lib.orc_backward(self._h, FUNCTIONS[function], C, _ptr(m), _ptr(v), _ptr(c), _ptr(s),
+                         _ptr(dL), _ptr(dm), _ptr(dv), _ptr(dc),
+                         0 if sub is None else len(sub), _ptr(sub))
+        return dm, dv, dc
+
+    def count_pairs(self, conics, thr=-104.0, subset=None):
+        lib = _load()
+        c = _f32(conics)
+        sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
+        w_ref = ctypes.c_int64()
+        w_live = ctypes.c_int64()
+        lib.orc_count_pairs(self._h, _ptr(self.means), _ptr(c), _ptr(self.samples), thr,
+                            0 if sub is None else len(sub), _ptr(sub),
+                            ctypes.byref(w_ref), ctypes.byref(w_live))
+        return w_ref.value, w_live.value

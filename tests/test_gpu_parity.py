@@ -1,0 +1,253 @@
+"""GPU parity: the HIP path (through diff_gaussian_sampling._C / libdgs.so) against the CPU
+oracle (oracle/oracle.c, the restatement of the reference), on identical seeded inputs.
+
+Integer / index outputs (num_rendered, radii, reference-layout ranges) must be bit-identical.
+Floating-point outputs use the SURVEY 8c tolerance, per tensor:
+    |gpu - ref| <= RTOL * |ref| + ATOL * max|ref|,   RTOL = 1e-5, ATOL = 1e-6 (forward)
+and the same with ATOL = 1e-5 for gradients, whose reference order is atomic (nondeterministic)
+and whose terms cancel heavily (values ~ N(0,1), dL ~ N(0,1)).
+"""
+import numpy as np
+import pytest
+import torch
+
+from diff_gaussian_sampling import synthetic as syn
+from helpers import FUNCS, close, gpu_run, ref_ranges_bytes
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-5
+ATOL_FWD = 1e-6
+ATOL_BWD = 1e-5
+
+
+def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=None,
+                atol_fwd=ATOL_FWD, atol_bwd=ATOL_BWD):
+    """Runs every check and reports all failures together."""
+    ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+    res = gpu_run(dgs._C, function, means, values, covs, conics, samples, dL)
+    errors = []
+
+    def attempt(fn, *a):
+        try:
+            fn(*a)
+        except AssertionError as e:
+            errors.append(str(e).strip().splitlines()[0] + " " + " ".join(str(e).split())[:300])
+
+    def eq(a, b, what):
+        if not np.array_equal(a, b):
+            raise AssertionError(f"{what}: {int(np.sum(np.asarray(a) != np.asarray(b)))} mismatches")
+
+    # integer parity
+    attempt(eq, res["R"], ob.num_rendered, "num_rendered")
+    attempt(eq, res["radii"], ob.radii, "radii")
+    rg, srg = ref_ranges_bytes(ob)
+    attempt(eq, res["ranges"], rg, "ranges")
+    attempt(eq, res["sample_ranges"], srg, "sample_ranges")
+    # forward
+    N = samples.shape[0]
+    ref_out = ob.forward(function, values.numpy(), conics.numpy(), subset=subset)
+    got = res["out"].reshape(N, -1, values.shape[1])
+    if subset is not None:
+        got, ref_out = got[subset], ref_out[subset]
+    attempt(close, got, ref_out, RTOL, atol_fwd, f"{function} forward")
+    # backward
+    dm, dv, dc = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
+    gm, gv, gc = res["grads"]
+    attempt(close, gm, dm, RTOL, atol_bwd, f"{function} dL/dmeans")
+    attempt(close, gv, dv, RTOL, atol_bwd, f"{function} dL/dvalues")
+    attempt(close, gc, dc, RTOL, atol_bwd, f"{function} dL/dconics")
+    assert not errors, "\n".join(errors)
+    return res, ob
+
+
+@pytest.mark.parametrize("function", FUNCS)
+@pytest.mark.parametrize("D,P,N,C", [(2, 1000, 4000, 1), (2, 3000, 20000, 3), (2, 800, 6000, 16),
+                                     (1, 300, 5000, 1), (1, 200, 3000, 5)])
+def test_parity_synthetic(dgs, oracle, function, D, P, N, C):
+    means, values, covs, conics = syn.gaussians(P, D, C, seed=11)
+    samples = syn.samples(N, D, seed=12)
+    K = syn.out_components(function, D)
+    dL = syn.grad_out(N, K, C, seed=13)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
+@pytest.mark.parametrize("function", ["gaussian", "laplacian"])
+def test_parity_small_gaussians_fine_cells(dgs, oracle, function):
+    """Many small Gaussians: exercises the fine-cell culling (several cells per tile)."""
+    means, values, covs, conics = syn.gaussians(20000, 2, 2, seed=21)
+    samples = syn.samples(60000, 2, seed=22)
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(60000, K, 2, seed=23)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
+def _edge_gaussians():
+    """Hand-made edge cases: torus wrap at +-1, huge Gaussian (full tile range), det == 0
+    covariance (absent), non-PD conic (power > 0 skip), radius floor (tiny Gaussian)."""
+    means = torch.tensor([[0.995, 0.0], [-0.999, 0.998], [0.1, -0.2], [0.3, 0.3],
+                          [-0.5, 0.7], [0.0, -0.999], [0.25, 0.25], [0.6, -0.6]])
+    covs = torch.tensor([[1e-3, 0.0, 1e-3], [2e-3, 5e-4, 1e-3], [0.25, 0.0, 0.25], [1.0, 1.0, 1.0],
+                         [1e-3, 0.0, 1e-3], [1e-8, 0.0, 1e-8], [1e-3, 0.0, 2e-3], [1e-2, 0.0, 1e-2]])
+    conics = torch.tensor([[1e3, 0.0, 1e3], [571.4286, -285.7143, 1142.8572], [4.0, 0.0, 4.0],
+                           [1.0, 0.0, 1.0], [50.0, 80.0, 50.0], [1e8, 0.0, 1e8], [1e3, 0.0, 5e2],
+                           [-10.0, 0.0, 100.0]])
+    values = torch.tensor([[1.0], [-2.0], [0.5], [3.0], [1.5], [2.5], [-1.0], [0.75]])
+    return means, values, covs, conics
+
+
+@pytest.mark.parametrize("function", FUNCS)
+def test_parity_edge_cases(dgs, oracle, function):
+    means, values, covs, conics = _edge_gaussians()
+    s = syn.samples(3000, 2, seed=31)
+    extra = torch.tensor([[-0.999, 0.0], [0.999, 0.998], [0.995, 0.0], [0.0, 0.999], [0.25, 0.25],
+                          [0.3, 0.3], [-1.0, -1.0], [0.99999, 0.99999]])
+    samples = torch.cat([s, extra])
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(samples.shape[0], K, 1, seed=32)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
+def _aliasing_domain():
+    """A sample domain wide enough (> 32 units) that adding 1e-6f to the extent is absorbed,
+    so the sample at the maximum lands in tile `grid` and aliases (sampler_impl.cu:169)."""
+    f32 = np.float32
+    inv = f32(1.0) / f32(0.51)
+    for k in range(64, 400):
+        d = f32(k) * f32(0.51)
+        for cand in (d, np.nextafter(d, f32(np.inf)), np.nextafter(d, f32(0))):
+            ext = f32(cand + f32(1e-6))
+            g = int(np.ceil(f32(ext * inv)))
+            t = int(f32(cand / f32(0.51)))
+            if t >= g:
+                return float(cand)
+    return None
+
+
+@pytest.mark.parametrize("function", ["gaussian", "derivative"])
+def test_parity_sample_clamp_aliasing(dgs, oracle, function):
+    d = _aliasing_domain()
+    assert d is not None
+    g = torch.Generator().manual_seed(41)
+    s = torch.rand(4000, 2, generator=g) * torch.tensor([d, 1.0])
+    s = torch.cat([s, torch.tensor([[0.0, 0.0], [d, 0.5], [d, 0.0], [d * 0.5, 1.0]])]).float()
+    P = 600
+    means = (torch.rand(P, 2, generator=g) * torch.tensor([d, 1.0])).float()
+    sig = 0.05 + 0.05 * torch.rand(P, 1, generator=g)
+    covs = torch.cat([sig ** 2, torch.zeros(P, 1), sig ** 2], 1).float()
+    conics = torch.cat([1 / sig ** 2, torch.zeros(P, 1), 1 / sig ** 2], 1).float()
+    values = torch.randn(P, 1, generator=g).float()
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(s.shape[0], K, 1, seed=42)
+    _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
+
+
+def test_parity_d1_zero_variance(dgs, oracle):
+    """D = 1 zero variance: the reference counts a tile (num_rendered) but emits no key."""
+    means = torch.tensor([[0.3], [-0.2], [0.7]])
+    covs = torch.tensor([[0.0], [1e-3], [4e-3]])
+    conics = torch.tensor([[1e9], [1e3], [250.0]])
+    values = torch.tensor([[1.0], [2.0], [-1.0]])
+    samples = syn.samples(500, 1, seed=51)
+    dL = syn.grad_out(500, 1, 1, seed=52)
+    _check_case(dgs, oracle, "gaussian", means, values, covs, conics, samples, dL)
+
+
+def test_empty_inputs(dgs):
+    C = dgs._C
+    dev = "cuda:0"
+    m = torch.zeros(0, 2, device=dev)
+    v = torch.zeros(0, 1, device=dev)
+    cv = torch.zeros(0, 3, device=dev)
+    s = torch.rand(10, 2, device=dev)
+    R, gb, sb, rg, srg, radii = C.preprocess_gaussians(m, v, cv, cv, s, False)
+    assert R == 0 and gb.numel() == 0 and radii.numel() == 0
+    out = C.sample_gaussians(m, v, cv, s, R, gb, sb, rg, srg, False)
+    assert out.shape == (10, 1) and float(out.abs().sum()) == 0.0
+    gm, gv, gc = C.sample_gaussians_backward(m, v, cv, s, R, torch.ones(10, 1, device=dev), gb, sb, rg, srg, False)
+    assert gm.shape == (0, 2) and gv.shape == (0, 1) and gc.shape == (0, 3)
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(5, 2, 1))
+    s0 = torch.zeros(0, 2, device=dev)
+    R, gb, sb, rg, srg, radii = C.preprocess_gaussians(means, values, covs, conics, s0, False)
+    assert R == 0 and float(radii.abs().sum()) == 0.0
+    out = C.sample_gaussians_laplacian(means, values, conics, s0, R, gb, sb, rg, srg, False)
+    assert out.shape == (0, 2, 2, 1)
+
+
+def test_dtype_error(dgs):
+    means, values, covs, conics = (t.cuda() for t in syn.gaussians(10, 2, 1))
+    with pytest.raises(RuntimeError):
+        dgs._C.preprocess_gaussians(means.double(), values, covs, conics, syn.samples(50).cuda(), False)
+
+
+def test_tile_grid_matches_torch_cuda_semantics(dgs, oracle):
+    """Pins the reference glue's grid arithmetic (sample_points.cu:73): torch's GPU division by
+    a scalar equals multiplication by the float reciprocal; the C-ABI, the shim and the oracle
+    all agree on it."""
+    g = torch.Generator().manual_seed(61)
+    x = (torch.rand(200000, generator=g) * 50).float()
+    gpu_div = (x.cuda() / 0.51).cpu()
+    recip = x * torch.tensor(np.float32(1.0) / np.float32(0.51), dtype=torch.float32)
+    assert torch.equal(gpu_div, recip), "torch GPU division by a scalar is not reciprocal-multiply"
+    for seed in range(5):
+        s = syn.samples(5000, 2, seed=70 + seed) * (1 + 10 * seed)
+        grid, off = dgs._C.tile_grid(s.cuda())
+        ogrid, ooff = oracle.tile_grid(s.numpy())
+        assert list(grid) == list(ogrid) and np.array_equal(np.float32(off), ooff)
+
+
+def test_autograd_through_package(dgs, oracle):
+    """GaussianSampler + loss.backward() returns the _C gradients (py:128-162, 214-289)."""
+    P, N, C = 2000, 10000, 2
+    means, values, covs, conics = (t.cuda() for t in syn.gaussians(P, 2, C, seed=81))
+    samples = syn.samples(N, 2, seed=82).cuda()
+    means.requires_grad_(True)
+    values.requires_grad_(True)
+    conics.requires_grad_(True)
+    sampler = dgs.GaussianSampler(False)
+    sampler.preprocess(means, values, covs, conics, samples)
+    out = sampler.sample_gaussians_derivative()
+    w = syn.grad_out(N, 2, C, seed=83).cuda().reshape(out.shape)
+    (out * w).sum().backward()
+    R, gb, sb, rg, srg = (sampler.num_rendered, sampler.binning_buffer, sampler.sample_binning_buffer,
+                          sampler.ranges, sampler.sample_ranges)
+    gm, gv, gc = dgs._C.sample_gaussians_derivative_backward(
+        means.detach(), values.detach(), conics.detach(), samples, R, w, gb, sb, rg, srg, False)
+    close(means.grad.cpu(), gm.cpu(), 1e-6, 1e-7, "means.grad")
+    close(values.grad.cpu(), gv.cpu(), 1e-6, 1e-7, "values.grad")
+    close(conics.grad.cpu(), gc.cpu(), 1e-6, 1e-7, "conics.grad")
+
+
+def test_debug_mode(dgs, oracle):
+    means, values, covs, conics = syn.gaussians(500, 2, 1, seed=91)
+    samples = syn.samples(2000, 2, seed=92)
+    dL = syn.grad_out(2000, 1, 1, seed=93)
+    res = gpu_run(dgs._C, "gaussian", means, values, covs, conics, samples, dL, debug=True)
+    ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+    close(res["out"].reshape(2000, 1, 1), ob.forward("gaussian", values.numpy(), conics.numpy()),
+          RTOL, ATOL_FWD, "debug forward")
+
+
+def test_repeatable(dgs):
+    """The forward is deterministic run to run (fixed per-sample order)."""
+    means, values, covs, conics = syn.gaussians(3000, 2, 1, seed=101)
+    samples = syn.samples(20000, 2, seed=102)
+    a = gpu_run(dgs._C, "gaussian", means, values, covs, conics, samples)["out"]
+    b = gpu_run(dgs._C, "gaussian", means, values, covs, conics, samples)["out"]
+    assert np.array_equal(a, b)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("function", ["gaussian", "third"])
+def test_parity_headline_size_subset(dgs, oracle, function):
+    """BASELINE config 3 (1M Gaussians x 2M samples): forward checked on 1500 samples, backward
+    with dL/dout non-zero only on those samples (grads then depend on them alone)."""
+    P, N = 1_000_000, 2_000_000
+    means, values, covs, conics = syn.gaussians(P, 2, 1, seed=0)
+    samples = syn.samples(N, 2, seed=4)
+    K = syn.out_components(function, 2)
+    g = torch.Generator().manual_seed(111)
+    subset = torch.randperm(N, generator=g)[:1500].sort().values.numpy().astype(np.int32)
+    dL = torch.zeros(N, K, 1)
+    dL[subset] = syn.grad_out(len(subset), K, 1, seed=112)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=subset)
