@@ -20,8 +20,13 @@ namespace dgs {
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
 constexpr uint32_t kVersion = 1;
-constexpr uint32_t kGeneral = 0x80000000u;  // entry flag: per-pair exact torus wrap needed
-constexpr uint32_t kIdMask = 0x7fffffffu;
+// Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
+// flagged ones come last (the render kernels then see whole flag-free batches).
+constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
+constexpr uint32_t kUnsafe = 0x40000000u;   // conic not well-conditioned PD: reference-literal power
+constexpr uint32_t kSlow = kGeneral | kUnsafe;
+constexpr uint32_t kIdMask = 0x3fffffffu;
+constexpr int64_t kMaxGaussians = (int64_t)kIdMask;
 // Culling threshold on q = X^T A X.  power = -q/2 < -105 makes expf(power) exactly +0 in
 // fp32 (e^-105 < half of the smallest subnormal), so every forward and backward term of such
 // a pair is exactly zero in the reference (all of them carry the factor G); culling them
@@ -35,7 +40,8 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // ---------------------------------------------------------------------------------------
 // Opaque buffer layout.  Gaussian-side buffer (DGS_BUF_BINNING):
 //   [header 256 B][counts int32[4]][perm int32[P]][cell_gbeg int32[ncells]]
-//   [cell_gend int32[ncells]][entries uint32[E]][bwd_units uint2[bwd_cap]]
+//   [cell_gmid int32[ncells]][cell_gend int32[ncells]][entries uint32[E]][bwd_units uint2[bwd_cap]]
+// A cell's list is [gbeg, gend); its flag-free entries come first, [gbeg, gmid).
 // Sample-side buffer (DGS_BUF_SAMPLE_BINNING):
 //   [header copy 256 B][sorted_sid int32[N]][cell_sbeg int32[ncells]][cell_send int32[ncells]]
 //   [fwd_units uint2[fwd_cap]]
@@ -55,6 +61,7 @@ struct Header {
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gend, o_entries, o_bwd_units, g_bytes;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
     uint64_t stamp;  // identical in both buffers of one preprocess call
+    uint64_t o_cell_gmid;
 };
 static_assert(sizeof(Header) <= 256, "header too large");
 constexpr size_t kHeaderBytes = 256;
@@ -64,7 +71,7 @@ enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1 };
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {  // byte offsets, computed on the host
-    uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gend, o_entries, o_bwd_units, g_bytes;
+    uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
 };
 
@@ -75,8 +82,9 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_counts = o;    o = align_up(o + 16, 256);
     L.o_perm = o;      o = align_up(o + 4 * (size_t)P, 256);
     L.o_cell_gbeg = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_cell_gmid = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_cell_gend = o; o = align_up(o + 4 * (size_t)ncells, 256);
-    L.o_entries = o;   o = align_up(o + 4 * (size_t)E + 16, 256);
+    L.o_entries = o;   o = align_up(o + 4 * (size_t)E + 64, 256);  // slack: 8-entry scalar loads
     L.o_bwd_units = o; o = align_up(o + 8 * (size_t)bwd_cap, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
@@ -93,7 +101,7 @@ struct Bins {
     const Header *h;
     const int32_t *counts;
     const int32_t *perm;
-    const int32_t *cell_gbeg, *cell_gend;
+    const int32_t *cell_gbeg, *cell_gmid, *cell_gend;
     const uint32_t *entries;
     const uint2 *bwd_units;
     const int32_t *sorted_sid;
@@ -123,6 +131,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.h = reinterpret_cast<const Header *>(gb);
     const uint64_t o_counts = sload(&B.h->o_counts), o_perm = sload(&B.h->o_perm);
     const uint64_t o_gbeg = sload(&B.h->o_cell_gbeg), o_gend = sload(&B.h->o_cell_gend);
+    const uint64_t o_gmid = sload(&B.h->o_cell_gmid);
     const uint64_t o_ent = sload(&B.h->o_entries), o_bu = sload(&B.h->o_bwd_units);
     const uint64_t o_sorted = sload(&B.h->o_sorted), o_sbeg = sload(&B.h->o_cell_sbeg);
     const uint64_t o_send = sload(&B.h->o_cell_send), o_fu = sload(&B.h->o_fwd_units);
@@ -130,6 +139,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.perm = reinterpret_cast<const int32_t *>(gb + o_perm);
     B.cell_gbeg = reinterpret_cast<const int32_t *>(gb + o_gbeg);
     B.cell_gend = reinterpret_cast<const int32_t *>(gb + o_gend);
+    B.cell_gmid = reinterpret_cast<const int32_t *>(gb + o_gmid);
     B.entries = reinterpret_cast<const uint32_t *>(gb + o_ent);
     B.bwd_units = reinterpret_cast<const uint2 *>(gb + o_bu);
     B.sorted_sid = reinterpret_cast<const int32_t *>(sb + o_sorted);
@@ -223,6 +233,16 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
     if (touched == 0) return 0;
     *radius = r;
     return touched;
+}
+
+// A conic whose power = -X^T A X / 2 cannot come out > 0 under fp32 rounding: positive
+// definite with |c1|^2 < 0.98 c0 c2 (D = 2), or c0 >= 0 (D = 1).  Other conics take the
+// reference-literal power evaluation with its `power > 0 -> skip` rule (forward.cu:228).
+__host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float c2f) {
+    const double c0 = c0f, c1 = c1f, c2 = c2f;
+    if (D == 1) return !(c0 >= 0.0 && c0 < INFINITY);
+    return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
+             c1 * c1 < 0.98 * c0 * c2);
 }
 
 __host__ __device__ inline int wrap_tile(int x, int g) { return x < 0 ? (g + (x % g)) : (x % g); }

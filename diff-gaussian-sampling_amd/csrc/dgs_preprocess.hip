@@ -111,28 +111,45 @@ __global__ void k_bounds_final(int nparts, int D, const float *part, int *grid, 
 }
 
 // ---------------------------------------------------------------------- sample binning
+// Per-block tile histograms in LDS (a [-1,1)^2 domain has 16 tiles: global atomics on 16
+// words serialise), flushed with one atomic per non-empty bin.
+constexpr int kHistBins = 4096;
+
 __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids,
                                uint32_t *__restrict__ tile_count) {
+    __shared__ uint32_t hist[kHistBins];
+    const bool lds = G.T <= kHistBins;
+    if (lds)
+        for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= N) return;
-    float s[2] = {samples[i * G.D], G.D == 2 ? samples[i * G.D + 1] : 0.0f};
-    const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
-    if (key < (uint32_t)G.T) atomicAdd(&tile_count[key], 1u);
-    keys[i] = sample_cell(G, s);
-    ids[i] = (uint32_t)i;
+    if (i < N) {
+        float s[2] = {samples[i * G.D], G.D == 2 ? samples[i * G.D + 1] : 0.0f};
+        const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
+        if (key < (uint32_t)G.T) {
+            if (lds) atomicAdd(&hist[key], 1u);
+            else atomicAdd(&tile_count[key], 1u);
+        }
+        keys[i] = sample_cell(G, s);
+        ids[i] = (uint32_t)i;
+    }
+    __syncthreads();
+    if (lds)
+        for (int t = threadIdx.x; t < G.T; t += blockDim.x)
+            if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
 }
 
 // identifyTileRanges (sampler_impl.cu:134-151) over sorted cell keys; keys >= limit ignored.
 __global__ void k_identify(int64_t L, const uint32_t *__restrict__ keys, uint32_t limit,
-                           int32_t *__restrict__ beg, int32_t *__restrict__ end) {
+                           int32_t *__restrict__ beg, int32_t *__restrict__ end, int shift) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L) return;
-    const uint32_t k = keys[i];
+    const uint32_t k = keys[i] >> shift;
     if (i == 0) {
         if (k < limit) beg[k] = 0;
     } else {
-        const uint32_t p = keys[i - 1];
+        const uint32_t p = keys[i - 1] >> shift;
         if (k != p) {
             if (p < limit) end[p] = (int32_t)i;
             if (k < limit) beg[k] = (int32_t)i;
@@ -148,26 +165,44 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
                              uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
                              uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
                              int home_w, int home_h) {
+    __shared__ uint32_t hist[kHistBins];
+    const bool lds = G.T <= kHistBins;
+    if (lds)
+        for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
+    __syncthreads();
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
     const int D = G.D, S = D * (D + 1) / 2;
-    float m[2] = {means[i * D], D == 2 ? means[i * D + 1] : 0.0f};
-    float cv[3] = {covs[i * S], D == 2 ? covs[i * S + 1] : 0.0f, D == 2 ? covs[i * S + 2] : 0.0f};
-    float r;
-    const uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
-    radii[i] = r;
-    touched[i] = t;
-    ids[i] = (uint32_t)i;
+    float r = 0.0f;
+    float m[2] = {0.0f, 0.0f};
+    if (i < P) {
+        m[0] = means[i * D];
+        m[1] = D == 2 ? means[i * D + 1] : 0.0f;
+        float cv[3] = {covs[i * S], D == 2 ? covs[i * S + 1] : 0.0f, D == 2 ? covs[i * S + 2] : 0.0f};
+        const uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
+        radii[i] = r;
+        touched[i] = t;
+        ids[i] = (uint32_t)i;
+        if (r > 0.0f) {
+            const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
+            for (int y = kr.y0; y < kr.y1; ++y)
+                for (int x = kr.x0; x < kr.x1; ++x) {
+                    const uint32_t key = key_of(D, x, y, G.grid);
+                    if (key < (uint32_t)G.T) {
+                        if (lds) atomicAdd(&hist[key], 1u);
+                        else atomicAdd(&tile_count[key], 1u);
+                    }
+                }
+        }
+    }
+    __syncthreads();
+    if (lds)
+        for (int t = threadIdx.x; t < G.T; t += blockDim.x)
+            if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
+    if (i >= P) return;
     if (!(r > 0.0f)) {
         home[i] = 0xffffffffu;
         return;
     }
-    const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
-    for (int y = kr.y0; y < kr.y1; ++y)
-        for (int x = kr.x0; x < kr.x1; ++x) {
-            const uint32_t key = key_of(D, x, y, G.grid);
-            if (key < (uint32_t)G.T) atomicAdd(&tile_count[key], 1u);
-        }
     int h[2] = {0, 0};
     const int lim[2] = {home_w, home_h};
     for (int d = 0; d < D; ++d) {
@@ -219,6 +254,7 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
         }
     }
     const bool cull = pd && e[0] < 0.5 && (D == 1 || e[1] < 0.5);
+    const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
     const double slack = kCellSlack * G.fs;
     double md[2], epsx[2];
     for (int d = 0; d < 2; ++d) {
@@ -282,11 +318,11 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                         }
                         bool inside = true;
                         for (int d = 0; d < D; ++d) inside = inside && xa[d] >= -1.0 && xb[d] <= 1.0;
-                        emit(cell, id | (inside ? 0u : kGeneral));
+                        emit(cell, id | uflag | (inside ? 0u : kGeneral));
                     }
             }
             const uint32_t fb = base + (uint32_t)(G.CT - 1);
-            if (send[fb] > sbeg[fb]) emit(fb, id | kGeneral);
+            if (send[fb] > sbeg[fb]) emit(fb, id | uflag | kGeneral);
         }
 }
 
@@ -331,10 +367,24 @@ __global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
     load_gauss(G.D, means, conics, g, m, c);
     uint64_t o = offs[i];
     enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
-        ekeys[o] = cell;
+        ekeys[o] = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
         evals[o] = val;
         ++o;
     });
+}
+
+// Half-cell ranges (key = cell << 1 | flagged) -> per-cell [gbeg, gmid, gend).
+__global__ void k_cell_ranges(int ncells, const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
+                              int32_t *__restrict__ gbeg, int32_t *__restrict__ gmid,
+                              int32_t *__restrict__ gend) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int fb = hb[2 * c], fe = he[2 * c], sb = hb[2 * c + 1], se = he[2 * c + 1];
+    const bool fast = fe > fb, slow = se > sb;
+    const int b = fast ? fb : (slow ? sb : 0);
+    gbeg[c] = b;
+    gmid[c] = fast ? fe : b;
+    gend[c] = slow ? se : (fast ? fe : 0);
 }
 
 __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
@@ -467,6 +517,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
                               int debug) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
+    if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^30 - 1)");
     *num_rendered = 0;
     if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
     if (!grid || !grid_offset) return fail(DGS_ERR_ARG, "dgs_preprocess: grid/offset required");
@@ -485,7 +536,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     G.n = choose_n(D, N, G.T);
     G.CT = (D == 2 ? G.n * G.n : G.n) + 1;
     const int64_t ncells64 = (int64_t)G.T * G.CT;
-    if (ncells64 >= (1LL << 31) - 1) return fail(DGS_ERR_ARG, "too many fine cells");
+    if (ncells64 >= (1LL << 30)) return fail(DGS_ERR_ARG, "too many fine cells");
     G.ncells = (int)ncells64;
     G.fs = (double)kTile / G.n;
     const int ncells = G.ncells;
@@ -539,7 +590,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, skeys, skeys_sorted, sids,
                                                    (uint32_t *)sorted_sid, N, 0, sbits, s));
     DGS_LAUNCH_CHECK(s, debug);
-    k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send);
+    k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
@@ -574,6 +625,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     int32_t *counters = reinterpret_cast<int32_t *>(gbuf + L.o_counts);
     int32_t *gperm = reinterpret_cast<int32_t *>(gbuf + L.o_perm);
     int32_t *cell_gbeg = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gbeg);
+    int32_t *cell_gmid = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gmid);
     int32_t *cell_gend = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gend);
     uint32_t *entries = reinterpret_cast<uint32_t *>(gbuf + L.o_entries);
     uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
@@ -581,10 +633,11 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     uint32_t *ekeys = S.get<uint32_t>(E + 1), *evals = S.get<uint32_t>(E + 1);
     uint32_t *ekeys_sorted = S.get<uint32_t>(E + 1);
     uint32_t *fcnt = S.get<uint32_t>(ncells), *bcnt = S.get<uint32_t>(ncells);
+    int32_t *hbeg = S.get<int32_t>(2 * (size_t)ncells), *hend = S.get<int32_t>(2 * (size_t)ncells);
     uint32_t *foff = S.get<uint32_t>(ncells), *boff = S.get<uint32_t>(ncells);
     if (S.rc) return S.rc;
     size_t t_esort = 0, t_cscan = 0;
-    const int ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1));
+    const int ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_esort, ekeys, ekeys_sorted, evals,
                                                    entries, (int)E, 0, ebits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_cscan, fcnt, foff, ncells, s));
@@ -592,8 +645,8 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     if (S.rc) return S.rc;
 
     DGS_TRY_HIP(hipMemsetAsync(counters, 0, 16, s));
-    DGS_TRY_HIP(hipMemsetAsync(cell_gbeg, 0, sizeof(int32_t) * ncells, s));
-    DGS_TRY_HIP(hipMemsetAsync(cell_gend, 0, sizeof(int32_t) * ncells, s));
+    DGS_TRY_HIP(hipMemsetAsync(hbeg, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
+    DGS_TRY_HIP(hipMemsetAsync(hend, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
     k_copy_u32<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
@@ -604,9 +657,11 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
         DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,
                                                        entries, (int)E, 0, ebits, s));
         DGS_LAUNCH_CHECK(s, debug);
-        k_identify<<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, (uint32_t)ncells, cell_gbeg, cell_gend);
+        k_identify<<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
         DGS_LAUNCH_CHECK(s, debug);
     }
+    k_cell_ranges<<<grid_for(ncells), kBlock, 0, s>>>(ncells, hbeg, hend, cell_gbeg, cell_gmid, cell_gend);
+    DGS_LAUNCH_CHECK(s, debug);
     k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
                                                       cell_gend, fcnt, bcnt);
     DGS_LAUNCH_CHECK(s, debug);
@@ -639,6 +694,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     h.fwd_cap = fwd_cap; h.bwd_cap = bwd_cap;
     h.o_counts = L.o_counts; h.o_perm = L.o_perm; h.o_cell_gbeg = L.o_cell_gbeg;
     h.o_cell_gend = L.o_cell_gend; h.o_entries = L.o_entries; h.o_bwd_units = L.o_bwd_units;
+    h.o_cell_gmid = L.o_cell_gmid;
     h.g_bytes = L.g_bytes;
     h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
     h.o_fwd_units = L0.o_fwd_units; h.s_bytes = L0.s_bytes;

@@ -1,13 +1,12 @@
 // dgs_render.h -- per-pair math of the four sampling functions (forward and backward) and
 // the packed row formats of the render kernels.
 //
-// Row formats (fp32, written per call by the pack kernels, read wave-uniformly through the
-// scalar cache in the forward and per lane in the backward):
-//   Gaussian row, D=2: [m0 m1 k0 k1 k2 flags v0..v(CB-1)]  padded to RS = 4k floats (8 at CB<=2)
-//   Gaussian row, D=1: [m0 k0 flags v0..]
+// Row formats (fp32, written per call by the pack kernels; read wave-uniformly through the
+// scalar cache in the forward, per lane in the backward):
+//   Gaussian row  D=2: [m0 m1 k0 k1 k2 (c0 c1 c2) v0..v(CB-1)]   (c only for FN != gaussian)
+//                 D=1: [m0 k0 (c0) v0..]                           padded to RS = 4k floats
 //     k = conic * (-log2 e) * {1/2, 1, 1/2}: power * log2(e) = X0 (k0 X0 + k1 X1) + k2 X1^2
-//     flags bit 0: "unsafe" conic (not well-conditioned PD) -> reference-literal power + mask
-//   Conic row: [c0 c1 c2 0] (D=2) / [c0 0 0 0] (D=1), read only where the raw conic is needed.
+//   Conic row:    [c0 c1 c2 0] / [c0 0 0 0]  (unsafe/general paths and the backward)
 //   Sample row (backward): [s0 (s1) dLsym[U][CB]], dL summed over symmetric components.
 #pragma once
 
@@ -22,7 +21,7 @@ struct Traits {
     static constexpr int K = FN == 0 ? 1 : FN == 1 ? D : FN == 2 ? D * D : D * D * D;  // out comps
     static constexpr int U = D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4);  // unique
     static constexpr int S = D * (D + 1) / 2;
-    static constexpr int GBASE = D == 2 ? 6 : 3;  // first value slot; flags at GBASE-1
+    static constexpr int GBASE = D == 2 ? (FN == 0 ? 5 : 8) : (FN == 0 ? 2 : 3);  // first value slot
 };
 
 // expanded component -> unique term (forward.cu:288-291, 322-329)
@@ -33,12 +32,80 @@ __host__ __device__ constexpr int unique_of(int k) {
     return k == 0 ? 0 : (k == 7 ? 3 : ((k == 1 || k == 2 || k == 4) ? 1 : 2));
 }
 
-template <int D, int CB>
-__host__ __device__ constexpr int grow_stride() { return (int)((D == 2 ? 6 : 3) + CB + 3) / 4 * 4; }
+template <int FN, int D, int CB>
+__host__ __device__ constexpr int grow_stride() { return (Traits<FN, D>::GBASE + CB + 3) / 4 * 4; }
 template <int FN, int D, int CB>
 __host__ __device__ constexpr int srow_stride() { return (D + Traits<FN, D>::U * CB + 3) / 4 * 4; }
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// Batch sizes of the wave-uniform scalar loads: the batch's rows occupy SGPRs (<= ~64).
+template <int RS>
+__host__ __device__ constexpr int fwd_batch() { return RS <= 8 ? 8 : RS <= 16 ? 4 : 2; }
+template <int RSS>
+__host__ __device__ constexpr int bwd_batch() { return RSS <= 4 ? 8 : RSS <= 8 ? 4 : RSS <= 16 ? 2 : 1; }
+
+template <int N> struct U32s { uint32_t v[N]; };
+template <int N> struct F32s { float v[N]; };
+
+// N consecutive wave-uniform dwords as whole vector loads from the constant address space:
+// one s_load_dwordx{4,8,16} per 4/8/16 dwords.  (Element-wise loads get shrunk to the dwords
+// actually used -- e.g. a 6-of-8-dword row became x4 + x2 -- doubling the scalar-cache
+// requests, which were the forward kernel's bottleneck.)
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x16_t __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x8_t __attribute__((ext_vector_type(8)));
+typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+
+template <typename V>
+__device__ __forceinline__ V sload_vec(const void *p) {
+    return *(const __attribute__((address_space(4))) V *)(p);
+}
+
+template <int N>
+__device__ __forceinline__ F32s<N> sload_f(const float *p) {
+    static_assert(N % 4 == 0, "rows are padded to 4 dwords");
+    F32s<N> r;
+    int k = 0;
+#pragma unroll
+    for (; k + 16 <= N; k += 16) {
+        const f32x16_t v = sload_vec<f32x16_t>(p + k);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) r.v[k + i] = v[i];
+    }
+#pragma unroll
+    for (; k + 8 <= N; k += 8) {
+        const f32x8_t v = sload_vec<f32x8_t>(p + k);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[k + i] = v[i];
+    }
+#pragma unroll
+    for (; k + 4 <= N; k += 4) {
+        const f32x4_t v = sload_vec<f32x4_t>(p + k);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r.v[k + i] = v[i];
+    }
+    return r;
+}
+template <int N>
+__device__ __forceinline__ U32s<N> sload_u(const uint32_t *p) {
+    static_assert(N == 8 || N == 4 || N == 2, "entry batches of 2, 4 or 8");
+    U32s<N> r;
+    if constexpr (N == 8) {
+        const u32x8_t v = sload_vec<u32x8_t>(p);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r.v[i] = v[i];
+    } else if constexpr (N == 4) {
+        const u32x4_t v = sload_vec<u32x4_t>(p);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) r.v[i] = v[i];
+    } else {
+        r.v[0] = sload(p);
+        r.v[1] = sload(p + 1);
+    }
+    return r;
+}
 
 // Reference-literal power (forward.cu:227/234/246/256, backward.cu:113/132/...): float
 // products without contraction, double scaling, rounded once to float.

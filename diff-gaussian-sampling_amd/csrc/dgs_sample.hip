@@ -26,7 +26,7 @@ namespace dgs {
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
 // --------------------------------------------------------------------------- packing
-template <int D, int CB>
+template <int FN, int D, int CB>
 __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *__restrict__ means,
                              const float *__restrict__ conics, const float *__restrict__ values,
                              int C, int cbase, float *__restrict__ rows, float4 *__restrict__ crows) {
@@ -35,16 +35,8 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
     const Header *h = reinterpret_cast<const Header *>(gbuf);
     const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
     const int64_t g = perm[i];
-    constexpr int S = D * (D + 1) / 2, RS = grow_stride<D, CB>(), B = Traits<0, D>::GBASE;
-    float c[3] = {conics[g * S], D == 2 ? conics[g * S + 1] : 0.0f, D == 2 ? conics[g * S + 2] : 0.0f};
-    bool safe;
-    if constexpr (D == 1) {
-        safe = c[0] >= 0.0f && c[0] < INFINITY;
-    } else {
-        const double c0 = c[0], c1 = c[1], c2 = c[2];
-        safe = c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
-               c1 * c1 < 0.98 * c0 * c2;
-    }
+    constexpr int S = D * (D + 1) / 2, RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    const float c[3] = {conics[g * S], D == 2 ? conics[g * S + 1] : 0.0f, D == 2 ? conics[g * S + 2] : 0.0f};
     float out[RS];
 #pragma unroll
     for (int k = 0; k < RS; ++k) out[k] = 0.0f;
@@ -54,11 +46,12 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
         out[2] = -0.5f * kLog2e * c[0];
         out[3] = -kLog2e * c[1];
         out[4] = -0.5f * kLog2e * c[2];
+        if constexpr (FN != 0) { out[5] = c[0]; out[6] = c[1]; out[7] = c[2]; }
     } else {
         out[0] = means[g];
         out[1] = -0.5f * kLog2e * c[0];
+        if constexpr (FN != 0) out[2] = c[0];
     }
-    out[B - 1] = __int_as_float(safe ? 0 : 1);
 #pragma unroll
     for (int ch = 0; ch < CB; ++ch) {
         const int gc = cbase + ch;
@@ -127,11 +120,18 @@ __device__ __forceinline__ float general_prob(float *X, const float *c, const fl
     return fast_prob<D>(X, k);
 }
 
-// ------------------------------------------------------------------- forward kernel
-// Gaussians per scalar-load batch (its rows occupy SGPRs: smaller for wide channel blocks)
-template <int CB>
-__host__ __device__ constexpr int fwd_batch() { return CB <= 2 ? 8 : CB <= 4 ? 4 : 2; }
+// Raw conic of a Gaussian row (FN != gaussian keeps it in the row).
+template <int FN, int D, int RS>
+__device__ __forceinline__ void row_conic(const float (&r)[RS], float *c) {
+    if constexpr (FN != 0) {
+        if constexpr (D == 2) { c[0] = r[5]; c[1] = r[6]; c[2] = r[7]; }
+        else { c[0] = r[2]; c[1] = c[2] = 0.0f; }
+    } else {
+        c[0] = c[1] = c[2] = 0.0f;
+    }
+}
 
+// ------------------------------------------------------------------- forward kernel
 template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbuf,
                                                     const char *__restrict__ sbuf,
@@ -140,7 +140,8 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
                                                     const float *__restrict__ samples,
                                                     float *__restrict__ out, int C, int cbase) {
     using Tr = Traits<FN, D>;
-    constexpr int RS = grow_stride<D, CB>(), B = Tr::GBASE, U = Tr::U, K = Tr::K;
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE, U = Tr::U, K = Tr::K;
+    constexpr int NB = fwd_batch<RS>();
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
@@ -161,40 +162,46 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
 #pragma unroll
             for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
 
-        constexpr int NB = fwd_batch<CB>();
-        for (int e0 = gb; e0 < ge; e0 += NB) {
-            uint32_t ent[NB];
+        const int gm = sload(&bins.cell_gmid[cell]);
+        const char *gbase = reinterpret_cast<const char *>(grows);
+        // (1) flag-free entries in full batches: NB entries, then NB rows in flight, then math
+        int e0 = gb;
+        for (; e0 + NB <= gm; e0 += NB) {
+            const U32s<NB> E = sload_u<NB>(bins.entries + e0);
+            F32s<RS> rows[NB];
 #pragma unroll
-            for (int q = 0; q < NB; ++q) ent[q] = sload(&bins.entries[min(e0 + q, ge - 1)]);
+            for (int q = 0; q < NB; ++q)  // 32-bit byte offset: folds into the s_load (soffset)
+                rows[q] = sload_f<RS>(reinterpret_cast<const float *>(gbase + E.v[q] * (uint32_t)(RS * 4)));
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
-                const int64_t id = ent[q] & kIdMask;
-                const float *row = grows + id * RS;
-                float r[RS];
-#pragma unroll
-                for (int k = 0; k < RS; ++k) r[k] = sload(row + k);
-                const bool live = e0 + q < ge;  // wave-uniform tail mask (scalar select)
-                float v[CB];
-#pragma unroll
-                for (int ch = 0; ch < CB; ++ch) v[ch] = live ? r[B + ch] : 0.0f;
-                const bool unsafe = __float_as_int(r[B - 1]) & 1;
-                const bool wrap = (ent[q] & kGeneral) != 0;
+                const float(&r)[RS] = rows[q].v;
+                float c[3];
+                row_conic<FN, D, RS>(r, c);
                 float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
-                const float kk[3] = {r[D == 2 ? 2 : 1], D == 2 ? r[3] : 0.0f, D == 2 ? r[4] : 0.0f};
-                float c[3] = {0.0f, 0.0f, 0.0f};
-                if (FN != 0 || unsafe) {
+                const float G = fast_prob<D>(X, &r[D]);
+                fwd_terms<FN, D, CB>(X, c, G, &r[B], acc);
+            }
+        }
+        // (2) the rest one by one: fast tail, then the flagged entries (wrap / unsafe conic)
+        for (; e0 < ge; ++e0) {
+            const uint32_t e = sload(&bins.entries[e0]);
+            const uint32_t id = e & kIdMask;
+            const F32s<RS> row = sload_f<RS>(reinterpret_cast<const float *>(gbase + id * (uint32_t)(RS * 4)));
+            const float(&r)[RS] = row.v;
+            float c[3];
+            row_conic<FN, D, RS>(r, c);
+            float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
+            float G;
+            if (!(e & kSlow)) {
+                G = fast_prob<D>(X, &r[D]);
+            } else {
+                if (e & kUnsafe) {
                     const float4 cr = sload(&crows[id]);
                     c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
                 }
-                float G;
-                if (!(wrap || unsafe)) {
-                    G = fast_prob<D>(X, kk);
-                } else {
-                    if (!live) continue;
-                    G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
-                }
-                fwd_terms<FN, D, CB>(X, c, G, v, acc);
+                G = general_prob<FN, D>(X, c, &r[D], (e & kGeneral) != 0, (e & kUnsafe) != 0);
             }
+            fwd_terms<FN, D, CB>(X, c, G, &r[B], acc);
         }
         if (active) {
             float *o = out + sid * K * C;
@@ -211,34 +218,41 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
 }
 
 // ------------------------------------------------------------------ backward kernel
-template <int FN, int CB>
-__host__ __device__ constexpr int bwd_batch() { return (CB <= 2 && FN <= 1) ? 4 : CB <= 4 ? 2 : 1; }
+template <int FN, int D, int CB, bool SLOW>
+__device__ __forceinline__ void bwd_sample(const float *srow, const float *m, const float *c,
+                                           const float *kk, const float *v, bool wrap, bool unsafe,
+                                           float *gm, float *gv, float *gc) {
+    constexpr int U = Traits<FN, D>::U;
+    float dl[U][CB];
+#pragma unroll
+    for (int a = 0; a < U; ++a)
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) dl[a][ch] = srow[D + a * CB + ch];
+    float X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : 0.0f};
+    float G;
+    if constexpr (SLOW) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
+    else G = fast_prob<D>(X, kk);
+    bwd_terms<FN, D, CB>(X, c, G, v, dl, gm, gv, gc);
+}
 
+// The cell's samples, wave-uniform: full batches of NB contiguous sample rows (one or two
+// s_load_dwordx16), then the tail one by one.
 template <int FN, int D, int CB, bool SLOW>
 __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict__ srows,
                                          const float *m, const float *c, const float *kk,
                                          const float *v, bool wrap, bool unsafe, float *gm,
                                          float *gv, float *gc) {
-    constexpr int U = Traits<FN, D>::U, RSS = srow_stride<FN, D, CB>(), NB = bwd_batch<FN, CB>();
-    for (int j0 = sb; j0 < se; j0 += NB) {
+    constexpr int RSS = srow_stride<FN, D, CB>(), NB = bwd_batch<RSS>();
+    int j0 = sb;
+    for (; j0 + NB <= se; j0 += NB) {
+        const F32s<NB * RSS> sr = sload_f<NB * RSS>(srows + (int64_t)j0 * RSS);
 #pragma unroll
-        for (int q = 0; q < NB; ++q) {
-            const float *sr = srows + (int64_t)min(j0 + q, se - 1) * RSS;
-            const bool live = j0 + q < se;  // wave-uniform tail mask: dL -> 0
-            float srow[RSS];
-#pragma unroll
-            for (int k = 0; k < RSS; ++k) srow[k] = sload(sr + k);
-            float dl[U][CB];
-#pragma unroll
-            for (int a = 0; a < U; ++a)
-#pragma unroll
-                for (int ch = 0; ch < CB; ++ch) dl[a][ch] = live ? srow[D + a * CB + ch] : 0.0f;
-            float X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : 0.0f};
-            float G;
-            if constexpr (SLOW) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
-            else G = fast_prob<D>(X, kk);
-            bwd_terms<FN, D, CB>(X, c, G, v, dl, gm, gv, gc);
-        }
+        for (int q = 0; q < NB; ++q)
+            bwd_sample<FN, D, CB, SLOW>(&sr.v[q * RSS], m, c, kk, v, wrap, unsafe, gm, gv, gc);
+    }
+    for (; j0 < se; ++j0) {
+        const F32s<RSS> sr = sload_f<RSS>(srows + (int64_t)j0 * RSS);
+        bwd_sample<FN, D, CB, SLOW>(sr.v, m, c, kk, v, wrap, unsafe, gm, gv, gc);
     }
 }
 
@@ -250,7 +264,7 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0) {
     using Tr = Traits<FN, D>;
-    constexpr int RS = grow_stride<D, CB>(), B = Tr::GBASE, S = Tr::S;
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE, S = Tr::S;
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumBwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
@@ -271,18 +285,17 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
         }
         const float4 cr = crows[id];
         const bool wrap = (ent & kGeneral) != 0;
-        const bool unsafe = __float_as_int(r[B - 1]) & 1;
+        const bool unsafe = (ent & kUnsafe) != 0;
         const float c[3] = {cr.x, cr.y, cr.z};
         const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
-        const float kk[3] = {r[D == 2 ? 2 : 1], D == 2 ? r[3] : 0.0f, D == 2 ? r[4] : 0.0f};
         const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
         float gm[2] = {0.0f, 0.0f}, gc[3] = {0.0f, 0.0f, 0.0f}, gv[CB];
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) gv[ch] = 0.0f;
         if (__any(active && (wrap || unsafe)))
-            bwd_loop<FN, D, CB, true>(sb, se, srows, m, c, kk, r + B, wrap, unsafe, gm, gv, gc);
+            bwd_loop<FN, D, CB, true>(sb, se, srows, m, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
         else
-            bwd_loop<FN, D, CB, false>(sb, se, srows, m, c, kk, r + B, false, false, gm, gv, gc);
+            bwd_loop<FN, D, CB, false>(sb, se, srows, m, c, &r[D], &r[B], false, false, gm, gv, gc);
         if (active) {
             bwd_finish<FN, D>(c, gm, gc);
 #pragma unroll
@@ -318,7 +331,7 @@ __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
                                                   const float4 *__restrict__ crows,
                                                   const float *__restrict__ samples, float thr,
                                                   unsigned long long *__restrict__ counts) {
-    constexpr int RS = grow_stride<D, 1>();
+    constexpr int RS = grow_stride<0, D, 1>();
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
@@ -375,7 +388,10 @@ struct KernelTimer {
 
 // ------------------------------------------------------------------ host dispatch
 static int channel_block(int C) { return C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : 16; }
-static int grow_stride_rt(int D, int CB) { return ((D == 2 ? 6 : 3) + CB + 3) / 4 * 4; }
+static int grow_stride_rt(int FN, int D, int CB) {
+    const int base = D == 2 ? (FN == 0 ? 5 : 8) : (FN == 0 ? 2 : 3);
+    return (base + CB + 3) / 4 * 4;
+}
 static int unique_rt(int FN, int D) { return D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4); }
 static int srow_stride_rt(int FN, int D, int CB) { return (D + unique_rt(FN, D) * CB + 3) / 4 * 4; }
 static size_t a256(size_t x) { return align_up(x, 256); }
@@ -386,7 +402,7 @@ struct WsLayout {
 static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
     WsLayout w;
-    w.grows = a256((size_t)P * grow_stride_rt(D, CB) * 4 + 64);
+    w.grows = a256((size_t)P * grow_stride_rt(FN, D, CB) * 4 + 64);
     w.crows = a256((size_t)P * 16 + 64);
     w.srows = backward ? a256((size_t)N * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;
     w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
@@ -428,7 +444,7 @@ static int run_forward(const Call &a) {
     float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
                                                                  a.values, a.C, cbase, grows, crows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         {
@@ -452,7 +468,7 @@ static int run_backward(const Call &a) {
     DGS_TRY_HIP(hipMemsetAsync(acc, 0, w.acc, a.s));
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
                                                                  a.values, a.C, cbase, grows, crows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         k_pack_samples<FN, D, CB><<<grid_for(a.N), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
@@ -498,6 +514,8 @@ static int dispatch(const Call &a, bool bwd) {
 
 static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t gbytes,
                     const void *sb, size_t sbytes, size_t need, size_t have) {
+    if ((uint64_t)P * grow_stride_rt(FN, D, channel_block(C)) * 4 >= (1ull << 32))
+        return fail(DGS_ERR_ARG, "Gaussian rows exceed 4 GiB (32-bit scalar offsets)");
     if (FN < 0 || FN > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported");
     if (P < 0 || N < 0 || C < 0) return fail(DGS_ERR_ARG, "negative size");
@@ -583,10 +601,10 @@ extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const fl
     DGS_TRY_HIP(hipMemsetAsync(dcnt, 0, 16, s));
     const unsigned blocks = unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false);
     if (D == 2) {
-        k_pack_gauss<2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
+        k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
         k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
     } else {
-        k_pack_gauss<1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
+        k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
         k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
     }
     DGS_TRY_HIP(hipGetLastError());
