@@ -514,12 +514,12 @@ static int dispatch(const Call &a, bool bwd) {
 
 static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t gbytes,
                     const void *sb, size_t sbytes, size_t need, size_t have) {
-    if ((uint64_t)P * grow_stride_rt(FN, D, channel_block(C)) * 4 >= (1ull << 32))
-        return fail(DGS_ERR_ARG, "Gaussian rows exceed 4 GiB (32-bit scalar offsets)");
     if (FN < 0 || FN > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported");
     if (P < 0 || N < 0 || C < 0) return fail(DGS_ERR_ARG, "negative size");
     if (P == 0 || N == 0 || C == 0) return DGS_OK;
+    if ((uint64_t)P * grow_stride_rt(FN, D, channel_block(C)) * 4 >= (1ull << 32))
+        return fail(DGS_ERR_ARG, "Gaussian rows exceed 4 GiB (32-bit scalar offsets)");
     if (!gb || !sb || gbytes < kHeaderBytes || sbytes < kHeaderBytes)
         return fail(DGS_ERR_BUFFER, "binning buffers missing or too small (run preprocess first)");
     if (have < need) return fail(DGS_ERR_ARG, "workspace too small");

@@ -102,9 +102,12 @@ class OracleBins:
         self.offset = off2[: self.D].copy()
 
     def __del__(self):
-        if getattr(self, "_h", None):
-            _load().orc_free(self._h)
-            self._h = None
+        h, self._h = getattr(self, "_h", None), None
+        if h and _lib is not None:
+            try:
+                _lib.orc_free(h)
+            except Exception:  # interpreter shutdown
+                pass
 
     def ranges(self):
         r = np.zeros(2 * self.T, np.uint32)

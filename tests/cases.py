@@ -1,0 +1,87 @@
+"""Hand-made input cases shared by the oracle tests, the golden-vector generator and the GPU
+parity tests.  Each returns float32 CPU tensors (means, values, covariances, conics, samples).
+
+They cover the edge cases SURVEY.md section 8c lists: torus wrap at +-1, a Gaussian whose
+rect spans the whole grid (full range), det == 0 covariance (absent), a non-PD conic (the
+`power > 0` skip), the radius floor (tiny Gaussian), the sample clamp to `grid` (aliasing,
+sampler_impl.cu:169-177), D = 1 zero variance, and means far outside the sample domain
+(rect indices that are negative multiples of the grid: C's `%` wraps them to `grid`).
+"""
+import numpy as np
+import torch
+
+from diff_gaussian_sampling import synthetic as syn
+
+
+def edge_gaussians():
+    means = torch.tensor([[0.995, 0.0], [-0.999, 0.998], [0.1, -0.2], [0.3, 0.3],
+                          [-0.5, 0.7], [0.0, -0.999], [0.25, 0.25], [0.6, -0.6]])
+    covs = torch.tensor([[1e-3, 0.0, 1e-3], [2e-3, 5e-4, 1e-3], [0.25, 0.0, 0.25], [1.0, 1.0, 1.0],
+                         [1e-3, 0.0, 1e-3], [1e-8, 0.0, 1e-8], [1e-3, 0.0, 2e-3], [1e-2, 0.0, 1e-2]])
+    conics = torch.tensor([[1e3, 0.0, 1e3], [571.4286, -285.7143, 1142.8572], [4.0, 0.0, 4.0],
+                           [1.0, 0.0, 1.0], [50.0, 80.0, 50.0], [1e8, 0.0, 1e8], [1e3, 0.0, 5e2],
+                           [-10.0, 0.0, 100.0]])
+    values = torch.tensor([[1.0], [-2.0], [0.5], [3.0], [1.5], [2.5], [-1.0], [0.75]])
+    return means, values, covs, conics
+
+
+def edge_case(n_random=3000):
+    """Edge Gaussians over random samples plus samples placed on the wrap seams."""
+    means, values, covs, conics = edge_gaussians()
+    s = syn.samples(n_random, 2, seed=31)
+    extra = torch.tensor([[-0.999, 0.0], [0.999, 0.998], [0.995, 0.0], [0.0, 0.999], [0.25, 0.25],
+                          [0.3, 0.3], [-1.0, -1.0], [0.99999, 0.99999]])
+    return means, values, covs, conics, torch.cat([s, extra])
+
+
+def aliasing_domain():
+    """An x-extent wide enough (> 32 units) that adding 1e-6f is absorbed, so the sample at
+    the maximum lands in tile `grid` and aliases into the next row (sampler_impl.cu:169)."""
+    f32 = np.float32
+    inv = f32(1.0) / f32(0.51)
+    for k in range(64, 400):
+        d = f32(k) * f32(0.51)
+        for cand in (d, np.nextafter(d, f32(np.inf)), np.nextafter(d, f32(0))):
+            ext = f32(cand + f32(1e-6))
+            g = int(np.ceil(f32(ext * inv)))
+            t = int(f32(cand / f32(0.51)))
+            if t >= g:
+                return float(cand)
+    return None
+
+
+def aliasing_case(n=4000, P=600):
+    d = aliasing_domain()
+    g = torch.Generator().manual_seed(41)
+    s = torch.rand(n, 2, generator=g) * torch.tensor([d, 1.0])
+    s = torch.cat([s, torch.tensor([[0.0, 0.0], [d, 0.5], [d, 0.0], [d * 0.5, 1.0]])]).float()
+    means = (torch.rand(P, 2, generator=g) * torch.tensor([d, 1.0])).float()
+    sig = 0.05 + 0.05 * torch.rand(P, 1, generator=g)
+    covs = torch.cat([sig ** 2, torch.zeros(P, 1), sig ** 2], 1).float()
+    conics = torch.cat([1 / sig ** 2, torch.zeros(P, 1), 1 / sig ** 2], 1).float()
+    values = torch.randn(P, 1, generator=g).float()
+    return means, values, covs, conics, s
+
+
+def d1_zero_variance_case(n=500):
+    """D = 1 zero variance: the reference counts a tile (num_rendered) but emits no key."""
+    means = torch.tensor([[0.3], [-0.2], [0.7]])
+    covs = torch.tensor([[0.0], [1e-3], [4e-3]])
+    conics = torch.tensor([[1e9], [1e3], [250.0]])
+    values = torch.tensor([[1.0], [2.0], [-1.0]])
+    return means, values, covs, conics, syn.samples(n, 1, seed=51)
+
+
+def far_means_case(n=3000):
+    """Means outside [-1, 1): rects start at negative multiples of the grid (C's `%` then
+    gives key `grid`, i.e. the next row / past the end) and X wraps by more than one period."""
+    g = torch.Generator().manual_seed(121)
+    P = 64
+    means = (torch.rand(P, 2, generator=g) * 8.0 - 5.0).float()
+    means[:8, 0] = torch.tensor([-1.0 - 4 * 0.51, -1.0 - 8 * 0.51, -1.0 - 4 * 0.51 + 0.1, 3.3,
+                                 -3.05, -5.1, 2.9, 1.02]).float()
+    sig = 0.1 + 0.2 * torch.rand(P, 1, generator=g)
+    covs = torch.cat([sig ** 2, torch.zeros(P, 1), 1.5 * sig ** 2], 1).float()
+    conics = torch.cat([1 / sig ** 2, torch.zeros(P, 1), 1 / (1.5 * sig ** 2)], 1).float()
+    values = torch.randn(P, 1, generator=g).float()
+    return means, values, covs, conics, syn.samples(n, 2, seed=122)

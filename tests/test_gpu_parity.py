@@ -12,6 +12,7 @@ import pytest
 import torch
 
 from diff_gaussian_sampling import synthetic as syn
+import cases
 from helpers import FUNCS, close, gpu_run, ref_ranges_bytes
 
 pytestmark = pytest.mark.gpu
@@ -82,74 +83,34 @@ def test_parity_small_gaussians_fine_cells(dgs, oracle, function):
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
-def _edge_gaussians():
-    """Hand-made edge cases: torus wrap at +-1, huge Gaussian (full tile range), det == 0
-    covariance (absent), non-PD conic (power > 0 skip), radius floor (tiny Gaussian)."""
-    means = torch.tensor([[0.995, 0.0], [-0.999, 0.998], [0.1, -0.2], [0.3, 0.3],
-                          [-0.5, 0.7], [0.0, -0.999], [0.25, 0.25], [0.6, -0.6]])
-    covs = torch.tensor([[1e-3, 0.0, 1e-3], [2e-3, 5e-4, 1e-3], [0.25, 0.0, 0.25], [1.0, 1.0, 1.0],
-                         [1e-3, 0.0, 1e-3], [1e-8, 0.0, 1e-8], [1e-3, 0.0, 2e-3], [1e-2, 0.0, 1e-2]])
-    conics = torch.tensor([[1e3, 0.0, 1e3], [571.4286, -285.7143, 1142.8572], [4.0, 0.0, 4.0],
-                           [1.0, 0.0, 1.0], [50.0, 80.0, 50.0], [1e8, 0.0, 1e8], [1e3, 0.0, 5e2],
-                           [-10.0, 0.0, 100.0]])
-    values = torch.tensor([[1.0], [-2.0], [0.5], [3.0], [1.5], [2.5], [-1.0], [0.75]])
-    return means, values, covs, conics
-
-
 @pytest.mark.parametrize("function", FUNCS)
 def test_parity_edge_cases(dgs, oracle, function):
-    means, values, covs, conics = _edge_gaussians()
-    s = syn.samples(3000, 2, seed=31)
-    extra = torch.tensor([[-0.999, 0.0], [0.999, 0.998], [0.995, 0.0], [0.0, 0.999], [0.25, 0.25],
-                          [0.3, 0.3], [-1.0, -1.0], [0.99999, 0.99999]])
-    samples = torch.cat([s, extra])
+    """Torus wrap at +-1, full-range Gaussian, det == 0, non-PD conic, radius floor."""
+    means, values, covs, conics, samples = cases.edge_case()
     K = syn.out_components(function, 2)
     dL = syn.grad_out(samples.shape[0], K, 1, seed=32)
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
-def _aliasing_domain():
-    """A sample domain wide enough (> 32 units) that adding 1e-6f to the extent is absorbed,
-    so the sample at the maximum lands in tile `grid` and aliases (sampler_impl.cu:169)."""
-    f32 = np.float32
-    inv = f32(1.0) / f32(0.51)
-    for k in range(64, 400):
-        d = f32(k) * f32(0.51)
-        for cand in (d, np.nextafter(d, f32(np.inf)), np.nextafter(d, f32(0))):
-            ext = f32(cand + f32(1e-6))
-            g = int(np.ceil(f32(ext * inv)))
-            t = int(f32(cand / f32(0.51)))
-            if t >= g:
-                return float(cand)
-    return None
-
-
 @pytest.mark.parametrize("function", ["gaussian", "derivative"])
 def test_parity_sample_clamp_aliasing(dgs, oracle, function):
-    d = _aliasing_domain()
-    assert d is not None
-    g = torch.Generator().manual_seed(41)
-    s = torch.rand(4000, 2, generator=g) * torch.tensor([d, 1.0])
-    s = torch.cat([s, torch.tensor([[0.0, 0.0], [d, 0.5], [d, 0.0], [d * 0.5, 1.0]])]).float()
-    P = 600
-    means = (torch.rand(P, 2, generator=g) * torch.tensor([d, 1.0])).float()
-    sig = 0.05 + 0.05 * torch.rand(P, 1, generator=g)
-    covs = torch.cat([sig ** 2, torch.zeros(P, 1), sig ** 2], 1).float()
-    conics = torch.cat([1 / sig ** 2, torch.zeros(P, 1), 1 / sig ** 2], 1).float()
-    values = torch.randn(P, 1, generator=g).float()
+    means, values, covs, conics, s = cases.aliasing_case()
     K = syn.out_components(function, 2)
     dL = syn.grad_out(s.shape[0], K, 1, seed=42)
     _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
 
 
+@pytest.mark.parametrize("function", ["gaussian", "laplacian"])
+def test_parity_far_means(dgs, oracle, function):
+    means, values, covs, conics, s = cases.far_means_case()
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(s.shape[0], K, 1, seed=123)
+    _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
+
+
 def test_parity_d1_zero_variance(dgs, oracle):
-    """D = 1 zero variance: the reference counts a tile (num_rendered) but emits no key."""
-    means = torch.tensor([[0.3], [-0.2], [0.7]])
-    covs = torch.tensor([[0.0], [1e-3], [4e-3]])
-    conics = torch.tensor([[1e9], [1e3], [250.0]])
-    values = torch.tensor([[1.0], [2.0], [-1.0]])
-    samples = syn.samples(500, 1, seed=51)
-    dL = syn.grad_out(500, 1, 1, seed=52)
+    means, values, covs, conics, samples = cases.d1_zero_variance_case()
+    dL = syn.grad_out(samples.shape[0], 1, 1, seed=52)
     _check_case(dgs, oracle, "gaussian", means, values, covs, conics, samples, dL)
 
 
