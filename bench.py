@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--N", type=int, default=2_000_000, help="query points per GPU")
     ap.add_argument("--C", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
-    ap.add_argument("--cpu-samples", type=int, default=1024)
+    ap.add_argument("--cpu-samples", type=int, default=3072)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -48,6 +48,7 @@ def build_lib(force=False, debug=False):
     flags = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
              "-Wall", "-Wno-unused-function", "-Wno-unused-variable"]
     flags += ["-O1", "-g"] if debug else ["-O3"]
+    flags += os.environ.get("DGS_EXTRA_CFLAGS", "").split()  # experiments / tuning builds
     objs = []
     jobs = []
     for src in sources:

@@ -34,6 +34,10 @@ constexpr int64_t kMaxGaussians = (int64_t)kIdMask;
 constexpr double kQCut = 210.0;
 constexpr double kCellSlack = 1e-3;  // fraction of a fine cell tolerated outside its bounds
 constexpr int kWave = 64;
+// Forward work unit: a block of up to 32 sample PAIRS of one cell, pair-aligned in the sorted
+// sample order (pairs (2p, 2p+1) are packed fp32 operands; a pair may straddle a cell edge,
+// its foreign sample is evaluated but not written).
+constexpr int kFwdUnit = kWave;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
@@ -66,7 +70,7 @@ struct Header {
 static_assert(sizeof(Header) <= 256, "header too large");
 constexpr size_t kHeaderBytes = 256;
 
-enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1 };
+enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1, kNumUnsafe = 2 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -159,6 +163,13 @@ __device__ __forceinline__ int wave_unit_index() {
     const int bb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
     const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     return bb * kWavesPerBlock + w;
+}
+
+// The same remap at block granularity (one unit per block; kernels stride by gridDim.x).
+__device__ __forceinline__ int block_unit_index() {
+    const int nb = gridDim.x, b = blockIdx.x;
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -297,6 +308,31 @@ __device__ __forceinline__ float ref_wrap(float x) {
     return x;
 }
 
+// The even shift the reference's wrap applies to a displacement x (X' = x - shift): 0 for
+// |x| <= 1, else sign(x) * 2 (floor(|x| / 2) + 1) -- fmod(x, 2) -/+ 2 in closed form.  On an
+// interval of x that crosses none of the breakpoints |x| = 1, 2, 4, ... the shift is constant,
+// and fl(m - s) - shift is then exact (Sterbenz), i.e. bit-identical to the reference.
+__host__ __device__ inline double wrap_shift(double x) {
+    const double ax = fabs(x);
+    if (!(ax > 1.0)) return 0.0;
+    return copysign(2.0 * (floor(ax * 0.5) + 1.0), x);
+}
+__device__ __forceinline__ float wrap_shift_f(float x) {
+    const float ax = fabsf(x);
+    return ax > 1.0f ? copysignf(2.0f * (floorf(ax * 0.5f) + 1.0f), x) : 0.0f;
+}
+
+// ref_wrap in closed form, branch-free and exact: fmod(|x|, 2) = |x| - 2 trunc(|x| / 2) is
+// representable, so every step below is exact except the final `- 2`, which rounds once,
+// like the reference's double expression rounded to float.  Identity for |x| <= 1.
+__device__ __forceinline__ float wrap_exact(float x) {
+    DGS_NO_CONTRACT
+    const float ax = fabsf(x);
+    const float f = ax - 2.0f * truncf(0.5f * ax);
+    const float w = f - 2.0f;
+    return ax > 1.0f ? (x >= 0.0f ? w : -w) : x;
+}
+
 // ---------------------------------------------------------------------------------------
 // Fine-cell geometry.  Every reference tile is cut into n x n (D=2) or n (D=1) fine cells
 // plus one unculled fallback cell for samples that lie outside their tile's nominal area
@@ -342,6 +378,7 @@ struct UnitHint {
     const void *gbuf, *sbuf;
     size_t gbytes, sbytes;
     int64_t nfwd, nbwd;
+    int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);

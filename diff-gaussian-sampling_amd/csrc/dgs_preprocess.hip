@@ -16,6 +16,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
+#include <cstdlib>
 #include <atomic>
 #include <cmath>
 #include <cstring>
@@ -316,13 +317,19 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                             }
                             if (!hit) continue;
                         }
-                        bool inside = true;
-                        for (int d = 0; d < D; ++d) inside = inside && xa[d] >= -1.0 && xb[d] <= 1.0;
-                        emit(cell, id | uflag | (inside ? 0u : kGeneral));
+                        // kGeneral: some |X| in the cell may exceed 1 (torus wrap); the shift is
+                        // constant over the cell unless [xa, xb] crosses a wrap breakpoint, in
+                        // which case the entry takes the fully general per-pair path (kUnsafe).
+                        bool inside = true, constant = true;
+                        for (int d = 0; d < D; ++d) {
+                            inside = inside && xa[d] >= -1.0 && xb[d] <= 1.0;
+                            constant = constant && wrap_shift(xa[d]) == wrap_shift(xb[d]);
+                        }
+                        emit(cell, id | uflag | (inside ? 0u : (constant ? kGeneral : kGeneral | kUnsafe)));
                     }
             }
             const uint32_t fb = base + (uint32_t)(G.CT - 1);
-            if (send[fb] > sbeg[fb]) emit(fb, id | uflag | kGeneral);
+            if (send[fb] > sbeg[fb]) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
         }
 }
 
@@ -357,7 +364,8 @@ __global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
                             const float *__restrict__ means, const float *__restrict__ conics,
                             const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
                             const int32_t *__restrict__ send, const uint64_t *__restrict__ offs,
-                            uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals) {
+                            uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals,
+                            int32_t *__restrict__ counters) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -366,11 +374,14 @@ __global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
     float m[2], c[3];
     load_gauss(G.D, means, conics, g, m, c);
     uint64_t o = offs[i];
+    uint32_t nunsafe = 0;
     enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
         ekeys[o] = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
         evals[o] = val;
+        nunsafe += (val & kUnsafe) ? 1u : 0u;
         ++o;
     });
+    if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
 }
 
 // Half-cell ranges (key = cell << 1 | flagged) -> per-cell [gbeg, gmid, gend).
@@ -402,7 +413,8 @@ __global__ void k_unit_counts(int ncells, const int32_t *__restrict__ sbeg,
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     const int ns = send[c] - sbeg[c], ng = gend[c] - gbeg[c];
-    fcnt[c] = (uint32_t)((ns + kWave - 1) / kWave);
+    const int npairs = ((send[c] + 1) >> 1) - (sbeg[c] >> 1);
+    fcnt[c] = ns > 0 && ng > 0 ? (uint32_t)((npairs + kFwdUnit / 2 - 1) / (kFwdUnit / 2)) : 0u;
     bcnt[c] = ns > 0 ? (uint32_t)((ng + kWave - 1) / kWave) : 0u;
 }
 
@@ -414,7 +426,7 @@ __global__ void k_unit_fill(int ncells, const int32_t *__restrict__ sbeg,
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= ncells) return;
     for (uint32_t b = 0; b < fcnt[c]; ++b)
-        funits[foff[c] + b] = make_uint2((uint32_t)c, (uint32_t)sbeg[c] + b * kWave);
+        funits[foff[c] + b] = make_uint2((uint32_t)c, (uint32_t)(sbeg[c] & ~1) + b * kFwdUnit);
     for (uint32_t b = 0; b < bcnt[c]; ++b)
         bunits[boff[c] + b] = make_uint2((uint32_t)c, (uint32_t)gbeg[c] + b * kWave);
     if (c == ncells - 1) {
@@ -452,9 +464,22 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
 // waves per cell), capped so that cells stay reasonably large for sparse sample sets.
+// Fine cells per tile axis.  A forward unit holds up to kFwdUnit = 128 samples of one cell and
+// walks the cell's whole Gaussian list, so the mean cell population is set a few Poisson
+// deviations below 128 (a cell just over 128 pays a second full walk for a few samples);
+// smaller cells also cull more.  DGS_CELL_TARGET overrides the mean (tuning).
+static double cell_target() {
+    static const double t = [] {
+        const char *e = std::getenv("DGS_CELL_TARGET");
+        const double v = e ? std::atof(e) : 0.0;
+        return v > 0.0 ? v : 100.0;
+    }();
+    return t;
+}
+
 static int choose_n(int D, int64_t N, int64_t T) {
     const double per_tile = (double)N / (double)(T > 0 ? T : 1);
-    const double target = 120.0;
+    const double target = cell_target();
     if (D == 2) {
         int n = (int)std::lround(std::sqrt(per_tile / target));
         return std::max(1, std::min(n, 64));
@@ -543,7 +568,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     const int home_w = G.grid[0] * G.n, home_h = D == 2 ? G.grid[1] * G.n : 1;
 
     // ---- sample-side buffer (size known now) and the reference range buffers
-    const int64_t fwd_cap = (N + kWave - 1) / kWave + std::min<int64_t>(N, ncells) + 1;
+    const int64_t fwd_cap = (N + kFwdUnit - 1) / kFwdUnit + 2 * std::min<int64_t>(N, ncells) + 1;
     Layout L0 = make_layout(P, N, ncells, 0, fwd_cap, 0);
     char *sbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_BINNING, L0.s_bytes));
     char *rbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_RANGES, (size_t)G.T * 8 + 8));
@@ -651,7 +676,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
         k_fine_fill<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                   cell_send, foffs, ekeys, evals);
+                                                   cell_send, foffs, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = std::max(t_esort, t_cscan);
         DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,
@@ -703,12 +728,12 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
 
     // exact unit counts for the launch-size hint (second and last host sync)
-    int32_t hc[2] = {0, 0};
+    int32_t hc[3] = {0, 0, 0};
     DGS_TRY_HIP(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
-    uh.nfwd = hc[kNumFwdUnits]; uh.nbwd = hc[kNumBwdUnits];
+    uh.nfwd = hc[kNumFwdUnits]; uh.nbwd = hc[kNumBwdUnits]; uh.nunsafe = hc[kNumUnsafe];
     hint_put(uh);
     return DGS_OK;
 }

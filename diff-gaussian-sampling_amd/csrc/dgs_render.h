@@ -39,6 +39,31 @@ __host__ __device__ constexpr int srow_stride() { return (D + Traits<FN, D>::U *
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// ---------------------------------------------------------------------------------------
+// Lane values: `float` (one pair per lane) or `f2` (two pairs per lane).  The per-pair math
+// below is written once over V; with V = f2 the compiler emits packed fp32 VALU ops
+// (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32, wave-uniform operands broadcast from SGPR
+// pairs with op_sel), which is what the 157 TFLOP/s fp32 vector peak of MI355X counts.  Each
+// component goes through exactly the operations of the scalar form, so results are
+// bit-identical to V = float.
+// ---------------------------------------------------------------------------------------
+typedef float f2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float vfma(float a, float b, float c) { return fmaf(a, b, c); }
+__device__ __forceinline__ f2 vfma(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+
+template <typename V> __device__ __forceinline__ V bc(float x);
+template <> __device__ __forceinline__ float bc<float>(float x) { return x; }
+template <> __device__ __forceinline__ f2 bc<f2>(float x) { return f2{x, x}; }
+
+__device__ __forceinline__ float vexp2(float x) { return fast_exp2(x); }
+__device__ __forceinline__ f2 vexp2(f2 x) { return f2{fast_exp2(x.x), fast_exp2(x.y)}; }
+
+__device__ __forceinline__ float lo(float x) { return x; }
+__device__ __forceinline__ float lo(f2 x) { return x.x; }
+__device__ __forceinline__ float hsum(float x) { return x; }
+__device__ __forceinline__ float hsum(f2 x) { return x.x + x.y; }
+
 // Batch sizes of the wave-uniform scalar loads: the batch's rows occupy SGPRs (<= ~64).
 template <int RS>
 __host__ __device__ constexpr int fwd_batch() { return RS <= 8 ? 8 : RS <= 16 ? 4 : 2; }
@@ -77,6 +102,9 @@ __device__ __forceinline__ F32s<N> sload_f(const float *p) {
 #pragma unroll
     for (; k + 8 <= N; k += 8) {
         const f32x8_t v = sload_vec<f32x8_t>(p + k);
+        // Mark all 8 dwords live (no instruction is emitted): otherwise the load is shrunk
+        // to the dwords the caller reads (x4 + x2 for a 6-dword row), two requests instead of one.
+        asm volatile("" ::"s"(v));
 #pragma unroll
         for (int i = 0; i < 8; ++i) r.v[k + i] = v[i];
     }
@@ -107,6 +135,55 @@ __device__ __forceinline__ U32s<N> sload_u(const uint32_t *p) {
     return r;
 }
 
+// ---------------------------------------------------------------------------------------
+// Cross-lane reduce-scatter of a wave: every lane holds 64 partial sums v[0..63]; afterwards
+// lane l holds v[l] summed over all 64 lanes (returned).  Six halving stages, each adding a
+// lane's kept half to its partner's copy of the same half: distance 32 and 16 with the gfx950
+// half-swap instructions (v_permlane32_swap / v_permlane16_swap move a whole register half
+// between lane halves), distance 8/4/2/1 inside 16-lane rows with DPP (row_mirror,
+// row_half_mirror, quad_perm xor 2 / xor 1).  At every stage the lane whose partner-distance
+// bit is set keeps the upper half, so the surviving index equals the lane id.  ~140 VALU ops
+// per 64 x 64 sums; the order of the additions is fixed (deterministic).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float rs_partner(float x, int ctrl) {
+    switch (ctrl) {  // the DPP control must be a constant at the builtin
+    case 0x140: return __builtin_amdgcn_update_dpp(0.0f, x, 0x140, 0xf, 0xf, false);  // row_mirror
+    case 0x141: return __builtin_amdgcn_update_dpp(0.0f, x, 0x141, 0xf, 0xf, false);  // row_half_mirror
+    case 0x4e: return __builtin_amdgcn_update_dpp(0.0f, x, 0x4e, 0xf, 0xf, false);    // quad_perm xor 2
+    default: return __builtin_amdgcn_update_dpp(0.0f, x, 0xb1, 0xf, 0xf, false);      // quad_perm xor 1
+    }
+}
+
+template <int N>
+__device__ __forceinline__ void rs_dpp_stage(float (&x)[64], int lane, int bit, int ctrl) {
+    // x[0..2N) -> x[0..N): keep own half, add the partner's copy of it
+    const bool hi = (lane & bit) != 0;
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+        const float keep = hi ? x[i + N] : x[i];
+        const float send = hi ? x[i] : x[i + N];
+        x[i] = keep + rs_partner(send, ctrl);
+    }
+}
+
+__device__ __forceinline__ float reduce_scatter64(float (&x)[64], int lane) {
+#pragma unroll
+    for (int i = 0; i < 32; ++i) {  // distance 32: lanes >= 32 keep values 32..63
+        const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x[i]), __float_as_uint(x[i + 32]), false, false);
+        x[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {  // distance 16: odd 16-lane rows keep the upper half
+        const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x[i]), __float_as_uint(x[i + 16]), false, false);
+        x[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+    }
+    rs_dpp_stage<8>(x, lane, 8, 0x140);
+    rs_dpp_stage<4>(x, lane, 4, 0x141);
+    rs_dpp_stage<2>(x, lane, 2, 0x4e);
+    rs_dpp_stage<1>(x, lane, 1, 0xb1);
+    return x[0];
+}
+
 // Reference-literal power (forward.cu:227/234/246/256, backward.cu:113/132/...): float
 // products without contraction, double scaling, rounded once to float.
 template <int FN, int D>
@@ -129,41 +206,41 @@ __device__ __forceinline__ float ref_power(const float *X, const float *c) {
 // ---------------------------------------------------------------------------------------
 // Forward (forward.cu:225-332): acc[U][CB] += v * G * term_u
 // ---------------------------------------------------------------------------------------
-template <int FN, int D, int CB>
-__device__ __forceinline__ void fwd_terms(const float *X, const float *c, float G, const float *v,
-                                          float (&acc)[Traits<FN, D>::U][CB]) {
+template <int FN, int D, int CB, typename V>
+__device__ __forceinline__ void fwd_terms(const V *X, const float *c, V G, const float *v,
+                                          V (&acc)[Traits<FN, D>::U][CB]) {
     if constexpr (FN == 0) {
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) acc[0][ch] = fmaf(v[ch], G, acc[0][ch]);
+        for (int ch = 0; ch < CB; ++ch) acc[0][ch] = vfma(bc<V>(v[ch]), G, acc[0][ch]);
     } else {
-    float t[4];
+    V t[4];
     if constexpr (D == 1) {
-        const float x1 = c[0] * X[0];
+        const V x1 = c[0] * X[0];
         if constexpr (FN == 1) t[0] = x1;
         else if constexpr (FN == 2) t[0] = x1 * x1 - c[0];
         else t[0] = 3.0f * c[0] * x1 - x1 * x1 * x1;  // 2 c x1 - x1^3 + c x1
     } else {
-        const float a1 = fmaf(c[1], X[1], c[0] * X[0]);
-        const float a2 = fmaf(c[1], X[0], c[2] * X[1]);
+        const V a1 = vfma(bc<V>(c[1]), X[1], c[0] * X[0]);
+        const V a2 = vfma(bc<V>(c[1]), X[0], c[2] * X[1]);
         if constexpr (FN == 1) {
             t[0] = a1; t[1] = a2;
         } else if constexpr (FN == 2) {
-            t[0] = fmaf(a1, a1, -c[0]);
-            t[1] = fmaf(a1, a2, -c[1]);
-            t[2] = fmaf(a2, a2, -c[2]);
+            t[0] = vfma(a1, a1, bc<V>(-c[0]));
+            t[1] = vfma(a1, a2, bc<V>(-c[1]));
+            t[2] = vfma(a2, a2, bc<V>(-c[2]));
         } else {
-            const float a11 = a1 * a1, a22 = a2 * a2;
+            const V a11 = a1 * a1, a22 = a2 * a2;
             t[0] = a1 * (3.0f * c[0] - a11);
-            t[1] = fmaf(2.0f * c[1], a1, a2 * (c[0] - a11));
-            t[2] = fmaf(2.0f * c[1], a2, a1 * (c[2] - a22));
+            t[1] = vfma(bc<V>(2.0f * c[1]), a1, a2 * (c[0] - a11));
+            t[2] = vfma(bc<V>(2.0f * c[1]), a2, a1 * (c[2] - a22));
             t[3] = a2 * (3.0f * c[2] - a22);
         }
     }
 #pragma unroll
     for (int ch = 0; ch < CB; ++ch) {
-        const float vg = v[ch] * G;
+        const V vg = v[ch] * G;
 #pragma unroll
-        for (int u = 0; u < Traits<FN, D>::U; ++u) acc[u][ch] = fmaf(vg, t[u], acc[u][ch]);
+        for (int u = 0; u < Traits<FN, D>::U; ++u) acc[u][ch] = vfma(vg, t[u], acc[u][ch]);
     }
     }
 }
@@ -175,37 +252,37 @@ __device__ __forceinline__ void fwd_terms(const float *X, const float *c, float 
 //   gm[D], gc[S]: mean / conic gradient accumulators, gv[CB]: value gradient
 //   dl[U][CB]: this sample's dL/dout summed over symmetric components (wave-uniform)
 // ---------------------------------------------------------------------------------------
-template <int FN, int D, int CB>
-__device__ __forceinline__ void bwd_terms(const float *X, const float *c, float G, const float *v,
-                                          const float (&dl)[Traits<FN, D>::U][CB], float *gm,
-                                          float *gv, float *gc) {
+template <int FN, int D, int CB, typename V>
+__device__ __forceinline__ void bwd_terms(const V *X, const float *c, V G, const float *v,
+                                          const V (&dl)[Traits<FN, D>::U][CB], V *gm, V *gv,
+                                          V *gc) {
     constexpr int U = Traits<FN, D>::U;
-    float Gu[U];
+    V Gu[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-        float s = 0.0f;
+        V s = bc<V>(0.0f);
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) s = fmaf(v[ch], dl[u][ch], s);
+        for (int ch = 0; ch < CB; ++ch) s = vfma(bc<V>(v[ch]), dl[u][ch], s);
         Gu[u] = s;  // dL_dG (per unique component), reference's dL_dG* sums
     }
     if constexpr (FN == 0) {
         // moments: gm = -[A (sum t X)], gc = -1/2 sum t X X^T (off-diagonal -sum t X0 X1)
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(G, dl[0][ch], gv[ch]);
-        const float t = G * Gu[0];
-        const float tx = t * X[0];
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = vfma(G, dl[0][ch], gv[ch]);
+        const V t = G * Gu[0];
+        const V tx = t * X[0];
         gm[0] += tx;                              // sum t X0
-        gc[0] = fmaf(tx, X[0], gc[0]);            // sum t X0^2
+        gc[0] = vfma(tx, X[0], gc[0]);            // sum t X0^2
         if constexpr (D == 2) {
-            const float ty = t * X[1];
+            const V ty = t * X[1];
             gm[1] += ty;                          // sum t X1
-            gc[1] = fmaf(tx, X[1], gc[1]);        // sum t X0 X1
-            gc[2] = fmaf(ty, X[1], gc[2]);        // sum t X1^2
+            gc[1] = vfma(tx, X[1], gc[1]);        // sum t X0 X1
+            gc[2] = vfma(ty, X[1], gc[2]);        // sum t X1^2
         }
     } else if constexpr (D == 1) {
-        const float x1 = c[0] * X[0];
-        const float GdLdG = G * Gu[0];
-        float f, dmx, dcc;
+        const V x1 = c[0] * X[0];
+        const V GdLdG = G * Gu[0];
+        V f, dmx, dcc;
         if constexpr (FN == 1) {
             f = x1;
             dmx = (x1 * x1 - c[0]);
@@ -222,90 +299,91 @@ __device__ __forceinline__ void bwd_terms(const float *X, const float *c, float 
                 + 0.5f * (x1 * x1 - c[0]) * x1 * X[0] * X[0];
         }
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(f * dl[0][ch], G, gv[ch]);
-        gm[0] = fmaf(-dmx, GdLdG, gm[0]);
-        gc[0] = fmaf(dcc, GdLdG, gc[0]);
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = vfma(f * dl[0][ch], G, gv[ch]);
+        gm[0] = vfma(-dmx, GdLdG, gm[0]);
+        gc[0] = vfma(dcc, GdLdG, gc[0]);
     } else {
-    const float X0 = X[0], X1 = X[1];
-    const float a1 = fmaf(c[1], X1, c[0] * X0);
-    const float a2 = fmaf(c[1], X0, c[2] * X1);
+    const V X0 = X[0], X1 = X[1];
+    const V a1 = vfma(bc<V>(c[1]), X1, c[0] * X0);
+    const V a2 = vfma(bc<V>(c[1]), X0, c[2] * X1);
     if constexpr (FN == 1) {
-        const float Gx = Gu[0], Gy = Gu[1];
+        const V Gx = Gu[0], Gy = Gu[1];
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = fmaf(fmaf(a1, dl[0][ch], a2 * dl[1][ch]), G, gv[ch]);
-        const float gx = fmaf(a1, Gx, a2 * Gy);
-        const float axy = fmaf(a1, a2, -c[1]);
-        const float dLdx = fmaf(fmaf(a1, a1, -c[0]), Gx, axy * Gy) * G;
-        const float dLdy = fmaf(fmaf(a2, a2, -c[2]), Gy, axy * Gx) * G;
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = vfma(vfma(a1, dl[0][ch], a2 * dl[1][ch]), G, gv[ch]);
+        const V gx = vfma(a1, Gx, a2 * Gy);
+        const V axy = vfma(a1, a2, bc<V>(-c[1]));
+        const V dLdx = vfma(vfma(a1, a1, bc<V>(-c[0])), Gx, axy * Gy) * G;
+        const V dLdy = vfma(vfma(a2, a2, bc<V>(-c[2])), Gy, axy * Gx) * G;
         gm[0] -= dLdx;
         gm[1] -= dLdy;
-        gc[0] = fmaf(fmaf(X0, Gx, -0.5f * X0 * X0 * gx), G, gc[0]);
-        gc[1] = fmaf(X1 * Gx + X0 * Gy - X0 * X1 * gx, G, gc[1]);
-        gc[2] = fmaf(fmaf(X1, Gy, -0.5f * X1 * X1 * gx), G, gc[2]);
+        gc[0] = vfma(vfma(X0, Gx, -0.5f * X0 * X0 * gx), G, gc[0]);
+        gc[1] = vfma(X1 * Gx + X0 * Gy - X0 * X1 * gx, G, gc[1]);
+        gc[2] = vfma(vfma(X1, Gy, -0.5f * X1 * X1 * gx), G, gc[2]);
     } else if constexpr (FN == 2) {
-        const float dxx = fmaf(a1, a1, -c[0]), dxy = fmaf(a1, a2, -c[1]), dyy = fmaf(a2, a2, -c[2]);
-        const float Gxx = Gu[0], Sxy = Gu[1], Gyy = Gu[2];
+        const V dxx = vfma(a1, a1, bc<V>(-c[0])), dxy = vfma(a1, a2, bc<V>(-c[1])),
+                dyy = vfma(a2, a2, bc<V>(-c[2]));
+        const V Gxx = Gu[0], Sxy = Gu[1], Gyy = Gu[2];
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch)
-            gv[ch] = fmaf(dxx * dl[0][ch] + dxy * dl[1][ch] + dyy * dl[2][ch], G, gv[ch]);
-        const float dLdx = ((a1 * a1 * a1 - 3.0f * c[0] * a1) * Gxx
+            gv[ch] = vfma(dxx * dl[0][ch] + dxy * dl[1][ch] + dyy * dl[2][ch], G, gv[ch]);
+        const V dLdx = ((a1 * a1 * a1 - 3.0f * c[0] * a1) * Gxx
                             + (a1 * a2 * a1 - c[1] * a1 - (c[1] * a1 + c[0] * a2)) * Sxy
                             + (a2 * a2 * a1 - c[2] * a1 - 2.0f * c[1] * a2) * Gyy) * G;
-        const float dLdy = ((a1 * a1 * a2 - c[0] * a2 - 2.0f * c[1] * a1) * Gxx
+        const V dLdy = ((a1 * a1 * a2 - c[0] * a2 - 2.0f * c[1] * a1) * Gxx
                             + (a1 * a2 * a2 - c[1] * a2 - (c[2] * a1 + c[1] * a2)) * Sxy
                             + (a2 * a2 * a2 - 3.0f * c[2] * a2) * Gyy) * G;
         gm[0] -= dLdx;
         gm[1] -= dLdy;
-        const float xx_cxx = -0.5f * dxx * X0 * X0 + 2.0f * a1 * X0 - 1.0f;
-        const float xy_cxx = -0.5f * dxy * X0 * X0 + a2 * X0;
-        const float yy_cxx = -0.5f * dyy * X0 * X0;
-        const float xx_cxy = -dxx * X0 * X1 + 2.0f * a1 * X1;
-        const float xy_cxy = -dxy * X0 * X1 + a2 * X1 + a1 * X0 - 1.0f;
-        const float yy_cxy = -dyy * X0 * X1 + 2.0f * a2 * X0;
-        const float xx_cyy = -0.5f * dxx * X1 * X1;
-        const float xy_cyy = -0.5f * dxy * X1 * X1 + a1 * X1;
-        const float yy_cyy = -0.5f * dyy * X1 * X1 + 2.0f * a2 * X1 - 1.0f;
-        gc[0] = fmaf(xx_cxx * Gxx + xy_cxx * Sxy + yy_cxx * Gyy, G, gc[0]);
-        gc[1] = fmaf(xx_cxy * Gxx + xy_cxy * Sxy + yy_cxy * Gyy, G, gc[1]);
-        gc[2] = fmaf(xx_cyy * Gxx + xy_cyy * Sxy + yy_cyy * Gyy, G, gc[2]);
+        const V xx_cxx = -0.5f * dxx * X0 * X0 + 2.0f * a1 * X0 - 1.0f;
+        const V xy_cxx = -0.5f * dxy * X0 * X0 + a2 * X0;
+        const V yy_cxx = -0.5f * dyy * X0 * X0;
+        const V xx_cxy = -dxx * X0 * X1 + 2.0f * a1 * X1;
+        const V xy_cxy = -dxy * X0 * X1 + a2 * X1 + a1 * X0 - 1.0f;
+        const V yy_cxy = -dyy * X0 * X1 + 2.0f * a2 * X0;
+        const V xx_cyy = -0.5f * dxx * X1 * X1;
+        const V xy_cyy = -0.5f * dxy * X1 * X1 + a1 * X1;
+        const V yy_cyy = -0.5f * dyy * X1 * X1 + 2.0f * a2 * X1 - 1.0f;
+        gc[0] = vfma(xx_cxx * Gxx + xy_cxx * Sxy + yy_cxx * Gyy, G, gc[0]);
+        gc[1] = vfma(xx_cxy * Gxx + xy_cxy * Sxy + yy_cxy * Gyy, G, gc[1]);
+        gc[2] = vfma(xx_cyy * Gxx + xy_cyy * Sxy + yy_cyy * Gyy, G, gc[2]);
     } else {
     // third, D == 2
-    const float a11 = a1 * a1, a22 = a2 * a2, a12 = a1 * a2;
-    const float dxxx = 3.0f * c[0] * a1 - a11 * a1;
-    const float dxxy = 2.0f * c[1] * a1 - a11 * a2 + c[0] * a2;
-    const float dxyy = 2.0f * c[1] * a2 - a1 * a22 + c[2] * a1;
-    const float dyyy = 3.0f * c[2] * a2 - a22 * a2;
-    const float Gxxx = Gu[0], S1 = Gu[1], S2 = Gu[2], Gyyy = Gu[3];
+    const V a11 = a1 * a1, a22 = a2 * a2, a12 = a1 * a2;
+    const V dxxx = 3.0f * c[0] * a1 - a11 * a1;
+    const V dxxy = 2.0f * c[1] * a1 - a11 * a2 + c[0] * a2;
+    const V dxyy = 2.0f * c[1] * a2 - a1 * a22 + c[2] * a1;
+    const V dyyy = 3.0f * c[2] * a2 - a22 * a2;
+    const V Gxxx = Gu[0], S1 = Gu[1], S2 = Gu[2], Gyyy = Gu[3];
 #pragma unroll
     for (int ch = 0; ch < CB; ++ch)
-        gv[ch] = fmaf(dxxx * dl[0][ch] + dxxy * dl[1][ch] + dxyy * dl[2][ch] + dyyy * dl[3][ch], G, gv[ch]);
-    const float xxy_dx = 2.0f * a12 * c[0] + a11 * c[1] - 3.0f * c[0] * c[1];
-    const float xyy_dx = 2.0f * a12 * c[1] + a22 * c[0] - c[2] * c[0] - 2.0f * c[1] * c[1];
-    const float dLdx = ((dxxx * a1 - 3.0f * c[0] * c[0] + 3.0f * a11 * c[0]) * Gxxx
+        gv[ch] = vfma(dxxx * dl[0][ch] + dxxy * dl[1][ch] + dxyy * dl[2][ch] + dyyy * dl[3][ch], G, gv[ch]);
+    const V xxy_dx = 2.0f * a12 * c[0] + a11 * c[1] - 3.0f * c[0] * c[1];
+    const V xyy_dx = 2.0f * a12 * c[1] + a22 * c[0] - c[2] * c[0] - 2.0f * c[1] * c[1];
+    const V dLdx = ((dxxx * a1 - 3.0f * c[0] * c[0] + 3.0f * a11 * c[0]) * Gxxx
                         + (dxxy * a1 + xxy_dx) * S1 + (dxyy * a1 + xyy_dx) * S2
                         + (dyyy * a1 - 3.0f * c[2] * c[1] + 3.0f * a22 * c[1]) * Gyyy) * G;
-    const float xxy_dy = 2.0f * a12 * c[1] + a11 * c[2] - c[0] * c[2] - 2.0f * c[1] * c[1];
-    const float xyy_dy = 2.0f * a12 * c[2] + a22 * c[1] - 3.0f * c[2] * c[1];
-    const float dLdy = ((dxxx * a2 - 3.0f * c[0] * c[1] + 3.0f * a11 * c[1]) * Gxxx
+    const V xxy_dy = 2.0f * a12 * c[1] + a11 * c[2] - c[0] * c[2] - 2.0f * c[1] * c[1];
+    const V xyy_dy = 2.0f * a12 * c[2] + a22 * c[1] - 3.0f * c[2] * c[1];
+    const V dLdy = ((dxxx * a2 - 3.0f * c[0] * c[1] + 3.0f * a11 * c[1]) * Gxxx
                         + (dxxy * a2 + xxy_dy) * S1 + (dxyy * a2 + xyy_dy) * S2
                         + (dyyy * a2 - 3.0f * c[2] * c[2] + 3.0f * a22 * c[2]) * Gyyy) * G;
     gm[0] -= dLdx;
     gm[1] -= dLdy;
-    const float v0 = -0.5f * dxxx * X0 * X0 + 3.0f * c[0] * X0 + 3.0f * a1 - 3.0f * a11 * X0;
-    const float v1 = -0.5f * dxxy * X0 * X0 + 2.0f * c[1] * X0 - 2.0f * a12 * X0 + a2;
-    const float v2 = -0.5f * dxyy * X0 * X0 - a22 * X0 + c[2] * X0;
-    const float v3 = -0.5f * dyyy * X0 * X0;
-    const float w0 = -dxxx * X0 * X1 + 3.0f * c[0] * X1 - 3.0f * a11 * X1;
-    const float w1 = -dxxy * X0 * X1 + 2.0f * c[1] * X1 + 2.0f * a1 - 2.0f * a12 * X1 - a11 * X0 + c[0] * X0;
-    const float w2 = -dxyy * X0 * X1 + 2.0f * c[1] * X0 + 2.0f * a2 - a22 * X1 - 2.0f * a12 * X0 + c[2] * X1;
-    const float w3 = -dyyy * X0 * X1 + 3.0f * c[2] * X0 - 3.0f * a22 * X0;
-    const float z0 = -0.5f * dxxx * X1 * X1;
-    const float z1 = -0.5f * dxxy * X1 * X1 - a11 * X1 + c[0] * X1;
-    const float z2 = -0.5f * dxyy * X1 * X1 + 2.0f * c[1] * X1 - 2.0f * a12 * X1 + a1;
-    const float z3 = -0.5f * dyyy * X1 * X1 + 3.0f * c[2] * X1 + 3.0f * a2 - 3.0f * a22 * X1;
-    gc[0] = fmaf(v0 * Gxxx + v1 * S1 + v2 * S2 + v3 * Gyyy, G, gc[0]);
-    gc[1] = fmaf(w0 * Gxxx + w1 * S1 + w2 * S2 + w3 * Gyyy, G, gc[1]);
-    gc[2] = fmaf(z0 * Gxxx + z1 * S1 + z2 * S2 + z3 * Gyyy, G, gc[2]);
+    const V v0 = -0.5f * dxxx * X0 * X0 + 3.0f * c[0] * X0 + 3.0f * a1 - 3.0f * a11 * X0;
+    const V v1 = -0.5f * dxxy * X0 * X0 + 2.0f * c[1] * X0 - 2.0f * a12 * X0 + a2;
+    const V v2 = -0.5f * dxyy * X0 * X0 - a22 * X0 + c[2] * X0;
+    const V v3 = -0.5f * dyyy * X0 * X0;
+    const V w0 = -dxxx * X0 * X1 + 3.0f * c[0] * X1 - 3.0f * a11 * X1;
+    const V w1 = -dxxy * X0 * X1 + 2.0f * c[1] * X1 + 2.0f * a1 - 2.0f * a12 * X1 - a11 * X0 + c[0] * X0;
+    const V w2 = -dxyy * X0 * X1 + 2.0f * c[1] * X0 + 2.0f * a2 - a22 * X1 - 2.0f * a12 * X0 + c[2] * X1;
+    const V w3 = -dyyy * X0 * X1 + 3.0f * c[2] * X0 - 3.0f * a22 * X0;
+    const V z0 = -0.5f * dxxx * X1 * X1;
+    const V z1 = -0.5f * dxxy * X1 * X1 - a11 * X1 + c[0] * X1;
+    const V z2 = -0.5f * dxyy * X1 * X1 + 2.0f * c[1] * X1 - 2.0f * a12 * X1 + a1;
+    const V z3 = -0.5f * dyyy * X1 * X1 + 3.0f * c[2] * X1 + 3.0f * a2 - 3.0f * a22 * X1;
+    gc[0] = vfma(v0 * Gxxx + v1 * S1 + v2 * S2 + v3 * Gyyy, G, gc[0]);
+    gc[1] = vfma(w0 * Gxxx + w1 * S1 + w2 * S2 + w3 * Gyyy, G, gc[1]);
+    gc[2] = vfma(z0 * Gxxx + z1 * S1 + z2 * S2 + z3 * Gyyy, G, gc[2]);
     }
     }
 }

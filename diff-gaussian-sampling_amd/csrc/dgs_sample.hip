@@ -4,18 +4,23 @@
 // backward.cu:26-106, 418-501) and the per-call host glue of sample_points.cu:100-372.
 //
 // Work decomposition (one wave64 per work unit, 4 independent waves per 256-thread block):
-//   forward : unit = (fine cell, up to 64 of its samples).  Lane = sample.  The cell's
-//             Gaussian list is walked wave-uniformly: each Gaussian's packed row comes in
-//             through the scalar cache (s_load) into SGPRs, so the per-pair work is pure VALU
-//             and the accumulation stays in registers (no atomics, no global RMW per pair).
+//   forward : unit = (fine cell, up to 128 of its samples).  Lane l holds samples l and l+64
+//             and evaluates both with packed fp32 ops (v_pk_*; a unit of <= 64 samples runs
+//             the one-sample-per-lane instance).  The cell's Gaussian list is walked
+//             wave-uniformly: each Gaussian's packed row comes in through the scalar cache
+//             (s_load) into SGPRs, so the per-pair work is pure VALU and the accumulation
+//             stays in registers (no atomics, no global RMW per pair).
 //   backward: unit = (fine cell, up to 64 entries of its Gaussian list).  Lane = Gaussian.
 //             The cell's samples (position + dL/dout) are walked wave-uniformly through the
-//             scalar cache; every lane accumulates its own Gaussian's gradient in registers
-//             and issues one atomic add per gradient component at the end of the unit.
-//             Gaussians are renumbered spatially at preprocess, so a wave's 64 lanes add to
-//             nearly contiguous addresses (coalesced atomics).
+//             scalar cache, two at a time with packed ops where the sample rows are small
+//             enough to be stored as interleaved pairs; every lane accumulates its own
+//             Gaussian's gradient in registers and issues one atomic add per gradient
+//             component at the end of the unit.  Gaussians are renumbered spatially at
+//             preprocess, so a wave's 64 lanes add to nearly contiguous addresses.
 #include <algorithm>
+#include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <utility>
 #include <vector>
 
@@ -64,35 +69,50 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
     crows[i] = make_float4(c[0], c[1], c[2], 0.0f);
 }
 
+// Sample rows of the backward.  Packed layout (kPairRows): samples j = 2p, 2p+1 share the
+// pair row p, field-interleaved [f0(2p) f0(2p+1) f1(2p) f1(2p+1) ...], so that a wave-uniform
+// s_load puts each field of both samples into an aligned SGPR pair (a packed-op operand).
+template <int FN, int D, int CB>
+__host__ __device__ constexpr bool pair_rows() { return srow_stride<FN, D, CB>() <= 16; }
+
 template <int FN, int D, int CB>
 __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
                                const float *__restrict__ samples, const float *__restrict__ dL,
                                int C, int cbase, float *__restrict__ rows) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= N) return;
-    const Header *h = reinterpret_cast<const Header *>(gbuf);
-    const int32_t *sorted = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted);
-    const int64_t sid = sorted[j];
+    constexpr bool PK = pair_rows<FN, D, CB>();
+    if (j >= (PK ? (int64_t)(N + 1) / 2 * 2 : (int64_t)N)) return;
     constexpr int K = Traits<FN, D>::K, RSS = srow_stride<FN, D, CB>();
     float out[RSS];
 #pragma unroll
     for (int k = 0; k < RSS; ++k) out[k] = 0.0f;
-    out[0] = samples[sid * D];
-    if constexpr (D == 2) out[1] = samples[sid * D + 1];
-    const float *d = dL + sid * K * C;
+    if (j < N) {  // j == N (odd N, packed): the zero second half of the last pair
+        const Header *h = reinterpret_cast<const Header *>(gbuf);
+        const int32_t *sorted = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted);
+        const int64_t sid = sorted[j];
+        out[0] = samples[sid * D];
+        if constexpr (D == 2) out[1] = samples[sid * D + 1];
+        const float *d = dL + sid * K * C;
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-        const int u = unique_of<FN, D>(k);
+        for (int k = 0; k < K; ++k) {
+            const int u = unique_of<FN, D>(k);
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) {
-            const int gc = cbase + ch;
-            if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
+            for (int ch = 0; ch < CB; ++ch) {
+                const int gc = cbase + ch;
+                if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
+            }
         }
     }
-    float *row = rows + j * RSS;
+    if constexpr (PK) {
+        float *row = rows + (j >> 1) * (2 * RSS) + (j & 1);
 #pragma unroll
-    for (int k = 0; k < RSS; k += 4)
-        *reinterpret_cast<float4 *>(row + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+        for (int k = 0; k < RSS; ++k) row[2 * k] = out[k];
+    } else {
+        float *row = rows + j * RSS;
+#pragma unroll
+        for (int k = 0; k < RSS; k += 4)
+            *reinterpret_cast<float4 *>(row + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
+    }
 }
 
 // ------------------------------------------------------------------- pair probability
@@ -100,10 +120,10 @@ __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char 
 // power <= 0 is guaranteed and G = 2^(power*log2e) is one v_exp_f32.  General path: the
 // reference's exact wrap and, for other conics, the reference-literal power with its
 // `power > 0 -> skip` rule (forward.cu:228) and an accurate expf.
-template <int D>
-__device__ __forceinline__ float fast_prob(const float *X, const float *k) {
-    if constexpr (D == 2) return fast_exp2(fmaf(X[0], fmaf(k[0], X[0], k[1] * X[1]), k[2] * X[1] * X[1]));
-    else return fast_exp2(k[0] * X[0] * X[0]);
+template <int D, typename V>
+__device__ __forceinline__ V fast_prob(const V *X, const float *k) {
+    if constexpr (D == 2) return vexp2(vfma(X[0], vfma(bc<V>(k[0]), X[0], k[1] * X[1]), k[2] * X[1] * X[1]));
+    else return vexp2(k[0] * X[0] * X[0]);
 }
 
 template <int FN, int D>
@@ -117,7 +137,18 @@ __device__ __forceinline__ float general_prob(float *X, const float *c, const fl
         const float p = ref_power<FN, D>(X, c);
         return p > 0.0f ? 0.0f : expf(p);
     }
-    return fast_prob<D>(X, k);
+    return fast_prob<D, float>(X, k);
+}
+
+template <int FN, int D>
+__device__ __forceinline__ f2 general_prob(f2 *X, const float *c, const float *k, bool wrap,
+                                           bool unsafe) {
+    float Xa[2] = {X[0].x, D == 2 ? X[1].x : 0.0f}, Xb[2] = {X[0].y, D == 2 ? X[1].y : 0.0f};
+    const float Ga = general_prob<FN, D>(Xa, c, k, wrap, unsafe);
+    const float Gb = general_prob<FN, D>(Xb, c, k, wrap, unsafe);
+    X[0] = f2{Xa[0], Xb[0]};
+    if constexpr (D == 2) X[1] = f2{Xa[1], Xb[1]};
+    return f2{Ga, Gb};
 }
 
 // Raw conic of a Gaussian row (FN != gaussian keeps it in the row).
@@ -131,128 +162,381 @@ __device__ __forceinline__ void row_conic(const float (&r)[RS], float *c) {
     }
 }
 
-// ------------------------------------------------------------------- forward kernel
+// ------------------------------------------------------------------- forward kernels
+// A forward unit is (cell, pair-aligned block of up to 64 sorted samples); the samples it
+// writes are those of the block that belong to the cell.
+struct FwdUnit {
+    int cell, sb, lo, hi;  // block start (even), written sample range [lo, hi)
+};
+
+__device__ __forceinline__ FwdUnit fwd_unit_at(const Bins &bins, int unit) {
+    const uint2 u = sload(&bins.fwd_units[unit]);
+    FwdUnit f;
+    f.cell = (int)u.x;
+    f.sb = (int)u.y;
+    f.lo = max(f.sb, sload(&bins.cell_sbeg[f.cell]));
+    f.hi = min(f.sb + kFwdUnit, sload(&bins.cell_send[f.cell]));
+    return f;
+}
+
+// Centre of a fine cell in sample coordinates (float; used only to pick wrap shifts, which
+// are constant over the cell with a margin).
+template <int D>
+__device__ __forceinline__ void cell_center(const Header *h, int cell, float *ctr) {
+    const int CT = sload(&h->CT), n = sload(&h->n), gx = sload(&h->grid[0]);
+    const int tile = cell / CT, loc = cell - tile * CT;
+    const int t[2] = {D == 1 ? tile : tile % gx, D == 1 ? 0 : tile / gx};
+    const int f[2] = {D == 1 ? loc : loc % n, D == 1 ? 0 : loc / n};
+    const float fs = kTile / (float)n;
+#pragma unroll
+    for (int d = 0; d < D; ++d) ctr[d] = sload(&h->off[d]) + t[d] * kTile + (f[d] + 0.5f) * fs;
+}
+
+// (a) Transposed form (small accumulators, U * CB <= 4).  Lane = Gaussian of the cell list,
+// 64 at a time (rows by vector gather); the block's samples are wave-uniform, read in order
+// as packed pair rows [s0(2p) s0(2p+1) s1(2p) s1(2p+1)] through the scalar cache, and the
+// pair math is packed fp32.  Every lane keeps a partial sum per (sample, component) over the
+// whole cell list; one cross-lane reduce-scatter per pass then leaves sum (sample, comp) =
+// value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
+// bound by the scalar cache's random-row throughput, tools/ubench.hip).
 template <int FN, int D, int CB>
+__host__ __device__ constexpr bool fwd_transposed() { return Traits<FN, D>::U * CB <= 4; }
+
+// The pass's first `np` (<= NP, wave-uniform) sample pairs against the lane's Gaussian.
+// WRAP: some lane's entry crosses the torus seam.  Its wrap (forward.cu:149-157) is a
+// constant even shift over the cell (preprocess sends the other seam entries to the general
+// path), subtracted exactly: sh = 0 for every other lane.
+template <int FN, int D, int CB, int NP, bool WRAP>
+__device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, int p0, int np,
+                                            const float *m, const float *sh, const float *c,
+                                            const float *kk, const float *v,
+                                            f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
+    constexpr int PRF = 2 * D, PPL = 16 / PRF;  // floats per pair row, pairs per s_load_dwordx16
+#pragma unroll
+    for (int q = 0; q < NP; q += PPL) {
+        if (q >= np) break;
+        const F32s<16> sr = sload_f<16>(fsrows + (int64_t)(p0 + q) * PRF);
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) {
+            if (q + j < NP) {
+                const float *pr = &sr.v[j * PRF];
+                f2 X[2] = {m[0] - f2{pr[0], pr[1]}, D == 2 ? m[1] - f2{pr[2], pr[3]} : bc<f2>(0.0f)};
+                if constexpr (WRAP) {
+                    X[0] = X[0] - sh[0];
+                    if constexpr (D == 2) X[1] = X[1] - sh[1];
+                }
+                const f2 G = fast_prob<D, f2>(X, kk);
+                fwd_terms<FN, D, CB, f2>(X, c, G, v, acc[q + j]);
+            }
+        }
+    }
+}
+
+// Cell-list entries [eb, ee) against the pass's sample pairs, 64 Gaussians (lanes) at a time.
+template <int FN, int D, int CB, int NP, bool FLAGGED>
+__device__ __forceinline__ void fwd_t_groups(const Bins &bins, const float *__restrict__ grows,
+                                             const float *__restrict__ fsrows, int eb, int ee,
+                                             int p0, int np, int lane, const float *ctr,
+                                             f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    for (int g0 = eb; g0 < ee; g0 += kWave) {
+        const bool active = g0 + lane < ee;
+        const uint32_t ent = bins.entries[active ? g0 + lane : eb];
+        const int64_t id = ent & kIdMask;
+        const float *grow = grows + id * RS;
+        float r[RS];
+#pragma unroll
+        for (int k = 0; k < RS; k += 4) {
+            const float4 qv = *reinterpret_cast<const float4 *>(grow + k);
+            r[k] = qv.x; r[k + 1] = qv.y; r[k + 2] = qv.z; r[k + 3] = qv.w;
+        }
+        // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0: its row
+        // is zeroed (finite, zero values)
+        if (!active || (FLAGGED && (ent & kUnsafe))) {
+#pragma unroll
+            for (int k = 0; k < RS; ++k) r[k] = 0.0f;
+        }
+        float c[3];
+        row_conic<FN, D, RS>(r, c);
+        const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
+        float sh[2] = {0.0f, 0.0f};  // the lane's constant wrap shift (kGeneral entries)
+        if constexpr (FLAGGED) {
+            if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+            }
+        }
+        fwd_t_pairs<FN, D, CB, NP, FLAGGED>(fsrows, p0, np, m, sh, c, &r[D], &r[B], acc);
+    }
+}
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ gbuf,
+                                                      const char *__restrict__ sbuf,
+                                                      const float *__restrict__ grows,
+                                                      const float *__restrict__ fsrows,
+                                                      float *__restrict__ out, int C, int cbase) {
+    using Tr = Traits<FN, D>;
+    constexpr int U = Tr::U, K = Tr::K, UC = U * CB, RS = grow_stride<FN, D, CB>(), B = Tr::GBASE;
+    constexpr int NP = 32 / UC, NS = 2 * NP;  // sample pairs / samples per pass
+    static_assert(NP >= 1 && NS * UC <= 64, "accumulator does not fit the reduce-scatter");
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumFwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nch = min(CB, C - cbase);
+    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+        const FwdUnit fu = fwd_unit_at(bins, unit);
+        // every entry but the kUnsafe ones (added by k_forward<..., TAIL = true>)
+        const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
+        const int gm = sload(&bins.cell_gmid[fu.cell]);
+        float ctr[2];
+        cell_center<D>(bins.h, fu.cell, ctr);
+        for (int ps = fu.sb; ps < fu.hi; ps += NS) {
+            const int np = min(NP, (fu.hi - ps + 1) >> 1);
+            f2 acc[NP][U][CB];
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+#pragma unroll
+                for (int a = 0; a < U; ++a)
+#pragma unroll
+                    for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
+            // flag-free prefix [gb, gm), then the flagged suffix [gm, ge) (seam wraps; the kUnsafe
+            // entries there are left to the tail pass)
+            fwd_t_groups<FN, D, CB, NP, false>(bins, grows, fsrows, gb, gm, ps >> 1, np, lane, ctr, acc);
+            if (gm < ge)
+                fwd_t_groups<FN, D, CB, NP, true>(bins, grows, fsrows, gm, ge, ps >> 1, np, lane, ctr, acc);
+            // value index = (2 * pair + half) * UC + (u * CB + ch)
+            float x[64];
+#pragma unroll
+            for (int i = 0; i < 64; ++i) x[i] = 0.0f;
+#pragma unroll
+            for (int q = 0; q < NP; ++q)
+#pragma unroll
+                for (int a = 0; a < U; ++a)
+#pragma unroll
+                    for (int ch = 0; ch < CB; ++ch) {
+                        x[(2 * q) * UC + a * CB + ch] = acc[q][a][ch].x;
+                        x[(2 * q + 1) * UC + a * CB + ch] = acc[q][a][ch].y;
+                    }
+            const float sum = reduce_scatter64(x, lane);
+            const int slot = lane / UC, comp = lane - slot * UC;
+            const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
+            if (lane < NS * UC && j >= fu.lo && j < fu.hi && ch < nch) {
+                float *o = out + (int64_t)bins.sorted_sid[j] * K * C + cbase + ch;
+#pragma unroll
+                for (int k = 0; k < K; ++k)
+                    if (unique_of<FN, D>(k) == ui) o[k * C] = sum;
+            }
+        }
+    }
+}
+
+// (b) Lane-per-sample form (wide accumulators, U * CB > 4): lane = sample of the block, the
+// cell's Gaussian rows are walked wave-uniformly through the scalar cache.
+template <int FN, int D, int CB, bool UNSAFE_ONLY>
+__device__ __forceinline__ void fwd_accumulate(const Bins &bins, const float *__restrict__ grows,
+                                               const float4 *__restrict__ crows, int eb, int ee,
+                                               int gm, float s0, float s1,
+                                               float (&acc)[Traits<FN, D>::U][CB]) {
+    using Tr = Traits<FN, D>;
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE;
+    constexpr int NB = fwd_batch<RS>();
+    const char *gbase = reinterpret_cast<const char *>(grows);
+    // (1) flag-free entries in full batches: NB entries, then NB rows in flight, then math
+    const int fe = min(ee, gm);
+    int e0 = eb;
+    for (; e0 + NB <= fe; e0 += NB) {
+        const U32s<NB> E = sload_u<NB>(bins.entries + e0);
+        F32s<RS> rows[NB];
+#pragma unroll
+        for (int q = 0; q < NB; ++q)  // 32-bit byte offset: folds into the s_load (soffset)
+            rows[q] = sload_f<RS>(reinterpret_cast<const float *>(gbase + E.v[q] * (uint32_t)(RS * 4)));
+#pragma unroll
+        for (int q = 0; q < NB; ++q) {
+            const float(&r)[RS] = rows[q].v;
+            float c[3];
+            row_conic<FN, D, RS>(r, c);
+            float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
+            const float G = fast_prob<D, float>(X, &r[D]);
+            fwd_terms<FN, D, CB, float>(X, c, G, &r[B], acc);
+        }
+    }
+    // (2) the rest one by one: fast tail, then the flagged entries (wrap / unsafe conic)
+    for (; e0 < ee; ++e0) {
+        const uint32_t e = sload(&bins.entries[e0]);
+        if (UNSAFE_ONLY && !(e & kUnsafe)) continue;
+        const uint32_t id = e & kIdMask;
+        const F32s<RS> row = sload_f<RS>(reinterpret_cast<const float *>(gbase + id * (uint32_t)(RS * 4)));
+        const float(&r)[RS] = row.v;
+        float c[3];
+        row_conic<FN, D, RS>(r, c);
+        float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
+        float G;
+        if (!(e & kSlow)) {
+            G = fast_prob<D, float>(X, &r[D]);
+        } else {
+            if (e & kUnsafe) {
+                const float4 cr = sload(&crows[id]);
+                c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
+            }
+            G = general_prob<FN, D>(X, c, &r[D], (e & kGeneral) != 0, (e & kUnsafe) != 0);
+        }
+        fwd_terms<FN, D, CB, float>(X, c, G, &r[B], acc);
+    }
+}
+
+// TAIL = true: only the unsafe-conic entries (all in the flagged tail [gm, ge) of a list),
+// added onto the transposed kernel's output, which covered every other entry.
+template <int FN, int D, int CB, bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbuf,
                                                     const char *__restrict__ sbuf,
                                                     const float *__restrict__ grows,
                                                     const float4 *__restrict__ crows,
                                                     const float *__restrict__ samples,
                                                     float *__restrict__ out, int C, int cbase) {
-    using Tr = Traits<FN, D>;
-    constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE, U = Tr::U, K = Tr::K;
-    constexpr int NB = fwd_batch<RS>();
+    constexpr int U = Traits<FN, D>::U, K = Traits<FN, D>::K;
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
+    const int nch = min(CB, C - cbase);
     for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
-        const uint2 u = sload(&bins.fwd_units[unit]);
-        const int cell = (int)u.x, sb = (int)u.y;
-        const int se = min(sb + kWave, sload(&bins.cell_send[cell]));
-        const int j = sb + lane;
-        const bool active = j < se;
-        const int64_t sid = bins.sorted_sid[active ? j : sb];
+        const FwdUnit fu = fwd_unit_at(bins, unit);
+        if (TAIL && sload(&bins.cell_gmid[fu.cell]) == sload(&bins.cell_gend[fu.cell])) continue;
+        const int j = fu.sb + lane;
+        const bool active = j >= fu.lo && j < fu.hi;
+        const int64_t sid = bins.sorted_sid[active ? j : fu.lo];
         const float s0 = samples[sid * D], s1 = D == 2 ? samples[sid * D + 1] : 0.0f;
-        const int gb = sload(&bins.cell_gbeg[cell]), ge = sload(&bins.cell_gend[cell]);
-
+        const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
+        const int gm = sload(&bins.cell_gmid[fu.cell]);
         float acc[U][CB];
 #pragma unroll
         for (int a = 0; a < U; ++a)
 #pragma unroll
             for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
-
-        const int gm = sload(&bins.cell_gmid[cell]);
-        const char *gbase = reinterpret_cast<const char *>(grows);
-        // (1) flag-free entries in full batches: NB entries, then NB rows in flight, then math
-        int e0 = gb;
-        for (; e0 + NB <= gm; e0 += NB) {
-            const U32s<NB> E = sload_u<NB>(bins.entries + e0);
-            F32s<RS> rows[NB];
-#pragma unroll
-            for (int q = 0; q < NB; ++q)  // 32-bit byte offset: folds into the s_load (soffset)
-                rows[q] = sload_f<RS>(reinterpret_cast<const float *>(gbase + E.v[q] * (uint32_t)(RS * 4)));
-#pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                const float(&r)[RS] = rows[q].v;
-                float c[3];
-                row_conic<FN, D, RS>(r, c);
-                float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
-                const float G = fast_prob<D>(X, &r[D]);
-                fwd_terms<FN, D, CB>(X, c, G, &r[B], acc);
-            }
-        }
-        // (2) the rest one by one: fast tail, then the flagged entries (wrap / unsafe conic)
-        for (; e0 < ge; ++e0) {
-            const uint32_t e = sload(&bins.entries[e0]);
-            const uint32_t id = e & kIdMask;
-            const F32s<RS> row = sload_f<RS>(reinterpret_cast<const float *>(gbase + id * (uint32_t)(RS * 4)));
-            const float(&r)[RS] = row.v;
-            float c[3];
-            row_conic<FN, D, RS>(r, c);
-            float X[2] = {r[0] - s0, D == 2 ? r[1] - s1 : 0.0f};
-            float G;
-            if (!(e & kSlow)) {
-                G = fast_prob<D>(X, &r[D]);
-            } else {
-                if (e & kUnsafe) {
-                    const float4 cr = sload(&crows[id]);
-                    c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
-                }
-                G = general_prob<FN, D>(X, c, &r[D], (e & kGeneral) != 0, (e & kUnsafe) != 0);
-            }
-            fwd_terms<FN, D, CB>(X, c, G, &r[B], acc);
-        }
+        fwd_accumulate<FN, D, CB, TAIL>(bins, grows, crows, TAIL ? gm : gb, ge, gm, s0, s1, acc);
         if (active) {
             float *o = out + sid * K * C;
-            const int nch = min(CB, C - cbase);
 #pragma unroll
             for (int k = 0; k < K; ++k) {
                 const int ui = unique_of<FN, D>(k);
 #pragma unroll
-                for (int ch = 0; ch < CB; ++ch)
-                    if (ch < nch) o[k * C + cbase + ch] = acc[ui][ch];
+                for (int ch = 0; ch < CB; ++ch) {
+                    if (ch < nch) {
+                        if constexpr (TAIL) o[k * C + cbase + ch] += acc[ui][ch];
+                        else o[k * C + cbase + ch] = acc[ui][ch];
+                    }
+                }
             }
         }
     }
 }
 
+// Forward sample pair rows (transposed form): pair p = sorted samples (2p, 2p+1), fields
+// interleaved [s0 s0' (s1 s1')]; a missing second sample (odd N) is 0.
+template <int D>
+__global__ void k_pack_fsamples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
+                                const float *__restrict__ samples, float *__restrict__ rows) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (int64_t)(N + 1) / 2 * 2) return;
+    float s[2] = {0.0f, 0.0f};
+    if (j < N) {
+        const Header *h = reinterpret_cast<const Header *>(gbuf);
+        const int64_t sid = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted)[j];
+        s[0] = samples[sid * D];
+        if constexpr (D == 2) s[1] = samples[sid * D + 1];
+    }
+    float *row = rows + (j >> 1) * (2 * D) + (j & 1);
+#pragma unroll
+    for (int f = 0; f < D; ++f) row[2 * f] = s[f];
+}
+
 // ------------------------------------------------------------------ backward kernel
-template <int FN, int D, int CB, bool SLOW>
-__device__ __forceinline__ void bwd_sample(const float *srow, const float *m, const float *c,
+template <int FN, int D, int CB, bool SLOW, typename V>
+__device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *c,
                                            const float *kk, const float *v, bool wrap, bool unsafe,
-                                           float *gm, float *gv, float *gc) {
+                                           V *gm, V *gv, V *gc) {
     constexpr int U = Traits<FN, D>::U;
-    float dl[U][CB];
+    V dl[U][CB];
 #pragma unroll
     for (int a = 0; a < U; ++a)
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) dl[a][ch] = srow[D + a * CB + ch];
-    float X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : 0.0f};
-    float G;
+    V X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : bc<V>(0.0f)};
+    V G;
     if constexpr (SLOW) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
-    else G = fast_prob<D>(X, kk);
-    bwd_terms<FN, D, CB>(X, c, G, v, dl, gm, gv, gc);
+    else G = fast_prob<D, V>(X, kk);
+    bwd_terms<FN, D, CB, V>(X, c, G, v, dl, gm, gv, gc);
 }
 
-// The cell's samples, wave-uniform: full batches of NB contiguous sample rows (one or two
-// s_load_dwordx16), then the tail one by one.
-template <int FN, int D, int CB, bool SLOW>
+// One sample pair (packed layout) as RSS f2 fields; `drop` = 1 / 2 zeroes the dL fields of the
+// first / second sample (a pair straddling the cell boundary: the foreign sample then adds 0).
+template <int RSS, int D>
+__device__ __forceinline__ void pair_fields(const float *p, f2 (&f)[RSS], int drop) {
+#pragma unroll
+    for (int k = 0; k < RSS; ++k) {
+        float a = p[2 * k], b = p[2 * k + 1];
+        if (k >= D) {
+            a = drop == 1 ? 0.0f : a;
+            b = drop == 2 ? 0.0f : b;
+        }
+        f[k] = f2{a, b};
+    }
+}
+
+// The cell's samples [sb, se), wave-uniform through the scalar cache.
+//   scalar layout: NB sample rows per batch, then the tail one by one;
+//   pair layout  : pairs (2p, 2p+1) covering [sb, se), packed; the boundary pairs are masked.
+template <int FN, int D, int CB, bool SLOW, typename V>
 __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict__ srows,
                                          const float *m, const float *c, const float *kk,
-                                         const float *v, bool wrap, bool unsafe, float *gm,
-                                         float *gv, float *gc) {
-    constexpr int RSS = srow_stride<FN, D, CB>(), NB = bwd_batch<RSS>();
-    int j0 = sb;
-    for (; j0 + NB <= se; j0 += NB) {
-        const F32s<NB * RSS> sr = sload_f<NB * RSS>(srows + (int64_t)j0 * RSS);
+                                         const float *v, bool wrap, bool unsafe, V *gm, V *gv,
+                                         V *gc) {
+    constexpr int RSS = srow_stride<FN, D, CB>();
+    if constexpr (sizeof(V) == 4) {
+        constexpr int NB = bwd_batch<RSS>();
+        int j0 = sb;
+        for (; j0 + NB <= se; j0 += NB) {
+            const F32s<NB * RSS> sr = sload_f<NB * RSS>(srows + (int64_t)j0 * RSS);
 #pragma unroll
-        for (int q = 0; q < NB; ++q)
-            bwd_sample<FN, D, CB, SLOW>(&sr.v[q * RSS], m, c, kk, v, wrap, unsafe, gm, gv, gc);
-    }
-    for (; j0 < se; ++j0) {
-        const F32s<RSS> sr = sload_f<RSS>(srows + (int64_t)j0 * RSS);
-        bwd_sample<FN, D, CB, SLOW>(sr.v, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            for (int q = 0; q < NB; ++q)
+                bwd_sample<FN, D, CB, SLOW, V>(&sr.v[q * RSS], m, c, kk, v, wrap, unsafe, gm, gv, gc);
+        }
+        for (; j0 < se; ++j0) {
+            const F32s<RSS> sr = sload_f<RSS>(srows + (int64_t)j0 * RSS);
+            bwd_sample<FN, D, CB, SLOW, V>(sr.v, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+        }
+    } else {
+        constexpr int PR = 2 * RSS, NB = bwd_batch<PR>();
+        int p = sb >> 1;
+        const int pe = (se + 1) >> 1;
+        const int pf = (se & 1) ? pe - 1 : pe;  // end of the pairs fully inside [sb, se)
+        f2 f[RSS];
+        if (sb & 1) {
+            const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
+            pair_fields<RSS, D>(sr.v, f, 1);
+            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            ++p;
+        }
+        for (; p + NB <= pf; p += NB) {
+            const F32s<NB * PR> sr = sload_f<NB * PR>(srows + (int64_t)p * PR);
+#pragma unroll
+            for (int q = 0; q < NB; ++q) {
+                pair_fields<RSS, D>(&sr.v[q * PR], f, 0);
+                bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            }
+        }
+        for (; p < pf; ++p) {
+            const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
+            pair_fields<RSS, D>(sr.v, f, 0);
+            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+        }
+        if (se & 1) {
+            const F32s<PR> sr = sload_f<PR>(srows + (int64_t)(pe - 1) * PR);
+            pair_fields<RSS, D>(sr.v, f, 2);
+            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+        }
     }
 }
 
@@ -264,6 +548,7 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0) {
     using Tr = Traits<FN, D>;
+    using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
     constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE, S = Tr::S;
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumBwdUnits]);
@@ -289,21 +574,22 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
         const float c[3] = {cr.x, cr.y, cr.z};
         const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
         const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
-        float gm[2] = {0.0f, 0.0f}, gc[3] = {0.0f, 0.0f, 0.0f}, gv[CB];
+        V gm[2] = {bc<V>(0.0f), bc<V>(0.0f)}, gc[3] = {bc<V>(0.0f), bc<V>(0.0f), bc<V>(0.0f)}, gv[CB];
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = 0.0f;
+        for (int ch = 0; ch < CB; ++ch) gv[ch] = bc<V>(0.0f);
         if (__any(active && (wrap || unsafe)))
-            bwd_loop<FN, D, CB, true>(sb, se, srows, m, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
+            bwd_loop<FN, D, CB, true, V>(sb, se, srows, m, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
         else
-            bwd_loop<FN, D, CB, false>(sb, se, srows, m, c, &r[D], &r[B], false, false, gm, gv, gc);
+            bwd_loop<FN, D, CB, false, V>(sb, se, srows, m, c, &r[D], &r[B], false, false, gm, gv, gc);
         if (active) {
-            bwd_finish<FN, D>(c, gm, gc);
+            float sm[2] = {hsum(gm[0]), hsum(gm[1])}, sc[3] = {hsum(gc[0]), hsum(gc[1]), hsum(gc[2])};
+            bwd_finish<FN, D>(c, sm, sc);
 #pragma unroll
-            for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, gm[d]);
+            for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
 #pragma unroll
-            for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, gc[k]);
+            for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, gv[ch]);
+            for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, hsum(gv[ch]));
         }
     }
 }
@@ -336,14 +622,12 @@ __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
     for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
-        const uint2 u = sload(&bins.fwd_units[unit]);
-        const int cell = (int)u.x, sb = (int)u.y;
-        const int se = min(sb + kWave, sload(&bins.cell_send[cell]));
-        const int j = sb + (threadIdx.x & (kWave - 1));
-        const bool active = j < se;
-        const int64_t sid = bins.sorted_sid[active ? j : sb];
+        const FwdUnit fu = fwd_unit_at(bins, unit);
+        const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
+        const int j = fu.sb + (threadIdx.x & (kWave - 1));
+        const bool active = j >= fu.lo && j < fu.hi;
+        const int64_t sid = bins.sorted_sid[active ? j : fu.lo];
         const float s0 = samples[sid * D], s1 = D == 2 ? samples[sid * D + 1] : 0.0f;
-        const int gb = sload(&bins.cell_gbeg[cell]), ge = sload(&bins.cell_gend[cell]);
         unsigned long long live = 0;
         for (int e = gb; e < ge; ++e) {
             const int64_t id = sload(&bins.entries[e]) & kIdMask;
@@ -397,22 +681,25 @@ static int srow_stride_rt(int FN, int D, int CB) { return (D + unique_rt(FN, D) 
 static size_t a256(size_t x) { return align_up(x, 256); }
 
 struct WsLayout {
-    size_t grows, crows, srows, acc, total;
+    size_t grows, crows, fsrows, srows, acc, total;
 };
 static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
     WsLayout w;
     w.grows = a256((size_t)P * grow_stride_rt(FN, D, CB) * 4 + 64);
     w.crows = a256((size_t)P * 16 + 64);
-    w.srows = backward ? a256((size_t)N * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;
+    // forward pair rows; a pass reads up to 32 pairs (+ one x16 load) past the last pair
+    w.fsrows = backward ? 0 : a256(((size_t)N + 1) * D * 4 + 36 * 16);
+    w.srows = backward ? a256(((size_t)N + 1) * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;  // pair rows: N rounded up to even
     w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
-    w.total = w.grows + w.crows + w.srows + w.acc;
+    w.total = w.grows + w.crows + w.fsrows + w.srows + w.acc;
     return w;
 }
 
 // Grid size in blocks: exact (from the preprocess hint) or a persistent-size fallback; the
 // kernels grid-stride over the device-side unit count either way.
-static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_t sbytes, bool bwd) {
+static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_t sbytes, bool bwd,
+                            int units_per_block = kWavesPerBlock) {
     UnitHint h;
     int64_t units;
     if (hint_get(gb, gbytes, sb, sbytes, &h)) {
@@ -420,7 +707,12 @@ static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_
     } else {
         units = 256 * 8 * kWavesPerBlock;  // 8 blocks per CU, striding
     }
-    int64_t blocks = (units + kWavesPerBlock - 1) / kWavesPerBlock;
+    int64_t blocks = (units + units_per_block - 1) / units_per_block;
+    static const int64_t cap = [] {  // DGS_BLOCKS_PER_CU: persistent grid (tuning)
+        const char *e = std::getenv("DGS_BLOCKS_PER_CU");
+        return e ? (int64_t)std::atoi(e) * 256 : (int64_t)0;
+    }();
+    if (cap > 0 && blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
     if (blocks > (1 << 30)) blocks = 1 << 30;
     return (unsigned)blocks;
@@ -442,17 +734,36 @@ static int run_forward(const Call &a) {
     const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, false);
     float *grows = reinterpret_cast<float *>(a.ws);
     float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
+    float *fsrows = reinterpret_cast<float *>(a.ws + w.grows + w.crows);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
+    constexpr bool T = fwd_transposed<FN, D, CB>();
+    UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
+    const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
+    if constexpr (T) {
+        k_pack_fsamples<D><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples, fsrows);
+        DGS_LAUNCH_CHECK(a.s, a.debug);
+    }
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
                                                                  a.values, a.C, cbase, grows, crows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         {
             KernelTimer t(0, a.s);
-            k_forward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows, a.samples,
-                                                               a.out, a.C, cbase);
+            if constexpr (T)
+                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, fsrows, a.out,
+                                                                     a.C, cbase);
+            else
+                k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows,
+                                                                          a.samples, a.out, a.C, cbase);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
+        if constexpr (T) {
+            if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
+                k_forward<FN, D, CB, true><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows,
+                                                                         a.samples, a.out, a.C, cbase);
+                DGS_LAUNCH_CHECK(a.s, a.debug);
+            }
+        }
     }
     return DGS_OK;
 }
@@ -471,7 +782,7 @@ static int run_backward(const Call &a) {
         k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
                                                                  a.values, a.C, cbase, grows, crows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        k_pack_samples<FN, D, CB><<<grid_for(a.N), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
+        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
                                                                       a.dL, a.C, cbase, srows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
