@@ -66,6 +66,7 @@ struct Header {
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
     uint64_t stamp;  // identical in both buffers of one preprocess call
     uint64_t o_cell_gmid;
+    uint64_t o_cell_box;  // sample buffer: per-cell bounding box of the cell's samples
 };
 static_assert(sizeof(Header) <= 256, "header too large");
 constexpr size_t kHeaderBytes = 256;
@@ -76,7 +77,7 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
-    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, s_bytes;
+    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, s_bytes;
 };
 
 inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64_t fwd_cap,
@@ -96,6 +97,7 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_cell_sbeg = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_cell_send = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_fwd_units = o; o = align_up(o + 8 * (size_t)fwd_cap, 256);
+    L.o_cell_box = o;  o = align_up(o + 16 * (size_t)ncells, 256);
     L.s_bytes = o;
     return L;
 }
@@ -111,6 +113,7 @@ struct Bins {
     const int32_t *sorted_sid;
     const int32_t *cell_sbeg, *cell_send;
     const uint2 *fwd_units;
+    const float4 *cell_box;  // [min0 min1 max0 max1] of each cell's samples
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -139,6 +142,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     const uint64_t o_ent = sload(&B.h->o_entries), o_bu = sload(&B.h->o_bwd_units);
     const uint64_t o_sorted = sload(&B.h->o_sorted), o_sbeg = sload(&B.h->o_cell_sbeg);
     const uint64_t o_send = sload(&B.h->o_cell_send), o_fu = sload(&B.h->o_fwd_units);
+    const uint64_t o_box = sload(&B.h->o_cell_box);
     B.counts = reinterpret_cast<const int32_t *>(gb + o_counts);
     B.perm = reinterpret_cast<const int32_t *>(gb + o_perm);
     B.cell_gbeg = reinterpret_cast<const int32_t *>(gb + o_gbeg);
@@ -150,6 +154,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.cell_sbeg = reinterpret_cast<const int32_t *>(sb + o_sbeg);
     B.cell_send = reinterpret_cast<const int32_t *>(sb + o_send);
     B.fwd_units = reinterpret_cast<const uint2 *>(sb + o_fu);
+    B.cell_box = reinterpret_cast<const float4 *>(sb + o_box);
     return B;
 }
 

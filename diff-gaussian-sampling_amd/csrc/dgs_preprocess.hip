@@ -237,7 +237,8 @@ __device__ inline bool box_hits_ellipse(double xa, double xb, double ya, double 
 template <class Emit>
 __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, const float *con,
                                       const int32_t *__restrict__ sbeg,
-                                      const int32_t *__restrict__ send, uint32_t id, Emit emit) {
+                                      const int32_t *__restrict__ send,
+                                      const float4 *__restrict__ box, uint32_t id, Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
     const double c0 = con[0], c1 = D == 2 ? con[1] : 0.0, c2 = D == 2 ? con[2] : 0.0;
@@ -317,13 +318,19 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                             }
                             if (!hit) continue;
                         }
-                        // kGeneral: some |X| in the cell may exceed 1 (torus wrap); the shift is
-                        // constant over the cell unless [xa, xb] crosses a wrap breakpoint, in
-                        // which case the entry takes the fully general per-pair path (kUnsafe).
+                        // Wrap class from the cell's actual samples (box = their bounding box;
+                        // the nominal cell may reach past the last sample): kGeneral when some
+                        // |X| may exceed 1 (torus wrap) -- a constant shift over the cell unless
+                        // the X range crosses a wrap breakpoint, which takes the fully general
+                        // per-pair path (kUnsafe).  eps covers the float rounding of m - s.
+                        const float4 bx = box[cell];
+                        const double blo[2] = {bx.x, bx.y}, bhi[2] = {bx.z, bx.w};
                         bool inside = true, constant = true;
                         for (int d = 0; d < D; ++d) {
-                            inside = inside && xa[d] >= -1.0 && xb[d] <= 1.0;
-                            constant = constant && wrap_shift(xa[d]) == wrap_shift(xb[d]);
+                            const double eps = 1e-6 * (1.0 + fabs((double)m[d]) + fmax(fabs(blo[d]), fabs(bhi[d])));
+                            const double wa = (double)m[d] - bhi[d] - eps, wb = (double)m[d] - blo[d] + eps;
+                            inside = inside && wa >= -1.0 && wb <= 1.0;
+                            constant = constant && wrap_shift(wa) == wrap_shift(wb);
                         }
                         emit(cell, id | uflag | (inside ? 0u : (constant ? kGeneral : kGeneral | kUnsafe)));
                     }
@@ -343,10 +350,30 @@ __device__ inline void load_gauss(int D, const float *__restrict__ means,
     c[2] = D == 2 ? conics[g * S + 2] : 0.0f;
 }
 
+// Bounding box of each cell's samples [min0 min1 max0 max1] (empty cells: unused).
+__global__ void k_cell_box(int ncells, int D, const int32_t *__restrict__ sbeg,
+                           const int32_t *__restrict__ send, const int32_t *__restrict__ sorted,
+                           const float *__restrict__ samples, float4 *__restrict__ box) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    float lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+    for (int j = sbeg[c]; j < send[c]; ++j) {
+        const int64_t sid = sorted[j];
+        for (int d = 0; d < D; ++d) {
+            const float v = samples[sid * D + d];
+            lo[d] = fminf(lo[d], v);
+            hi[d] = fmaxf(hi[d], v);
+        }
+    }
+    if (D == 1) { lo[1] = hi[1] = 0.0f; }
+    box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
+}
+
 __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
                              const float *__restrict__ means, const float *__restrict__ conics,
                              const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
-                             const int32_t *__restrict__ send, uint64_t *__restrict__ counts) {
+                             const int32_t *__restrict__ send, const float4 *__restrict__ box,
+                             uint64_t *__restrict__ counts) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -355,7 +382,7 @@ __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
     if (r > 0.0f) {
         float m[2], c[3];
         load_gauss(G.D, means, conics, g, m, c);
-        enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t, uint32_t) { ++n; });
+        enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t, uint32_t) { ++n; });
     }
     counts[i] = n;
 }
@@ -363,9 +390,9 @@ __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
 __global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
                             const float *__restrict__ means, const float *__restrict__ conics,
                             const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
-                            const int32_t *__restrict__ send, const uint64_t *__restrict__ offs,
-                            uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals,
-                            int32_t *__restrict__ counters) {
+                            const int32_t *__restrict__ send, const float4 *__restrict__ box,
+                            const uint64_t *__restrict__ offs, uint32_t *__restrict__ ekeys,
+                            uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -375,7 +402,7 @@ __global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
     load_gauss(G.D, means, conics, g, m, c);
     uint64_t o = offs[i];
     uint32_t nunsafe = 0;
-    enumerate_fine(G, m, r, c, sbeg, send, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
+    enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
         ekeys[o] = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
         evals[o] = val;
         nunsafe += (val & kUnsafe) ? 1u : 0u;
@@ -575,6 +602,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     char *srbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_RANGES, (size_t)G.T * 8 + 8));
     if (!sbuf || !rbuf || !srbuf) return fail(DGS_ERR_ALLOC, "buffer allocation failed");
     int32_t *sorted_sid = reinterpret_cast<int32_t *>(sbuf + L0.o_sorted);
+    float4 *cell_box = reinterpret_cast<float4 *>(sbuf + L0.o_cell_box);
     int32_t *cell_sbeg = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_sbeg);
     int32_t *cell_send = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_send);
     uint2 *fwd_units = reinterpret_cast<uint2 *>(sbuf + L0.o_fwd_units);
@@ -586,6 +614,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     uint32_t *perm = S.get<uint32_t>(P);
     uint64_t *touched = S.get<uint64_t>(P), *fcount = S.get<uint64_t>(P), *foffs = S.get<uint64_t>(P);
     uint64_t *rsum = S.get<uint64_t>(1);
+
     int64_t *totals = S.get<int64_t>(2);
     if (S.rc) return S.rc;
 
@@ -617,6 +646,9 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
+    k_cell_box<<<grid_for(ncells), kBlock, 0, s>>>(ncells, D, cell_sbeg, cell_send, sorted_sid,
+                                                  samples, cell_box);
+    DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
     k_gauss_prep<<<grid_for(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
@@ -627,7 +659,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                cell_send, fcount);
+                                                cell_send, cell_box, fcount);
     DGS_LAUNCH_CHECK(s, debug);
     tb = t_a;
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, fcount, foffs, P, s));
@@ -676,7 +708,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
         k_fine_fill<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                   cell_send, foffs, ekeys, evals, counters);
+                                                   cell_send, cell_box, foffs, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = std::max(t_esort, t_cscan);
         DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,
@@ -722,7 +754,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     h.o_cell_gmid = L.o_cell_gmid;
     h.g_bytes = L.g_bytes;
     h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
-    h.o_fwd_units = L0.o_fwd_units; h.s_bytes = L0.s_bytes;
+    h.o_fwd_units = L0.o_fwd_units; h.o_cell_box = L0.o_cell_box; h.s_bytes = L0.s_bytes;
     h.stamp = ++stamp_counter;
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);

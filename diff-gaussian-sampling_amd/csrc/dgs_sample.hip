@@ -179,17 +179,15 @@ __device__ __forceinline__ FwdUnit fwd_unit_at(const Bins &bins, int unit) {
     return f;
 }
 
-// Centre of a fine cell in sample coordinates (float; used only to pick wrap shifts, which
-// are constant over the cell with a margin).
+// Centre of a cell's sample bounding box: preprocess classified each kGeneral entry's wrap
+// shift as constant over exactly that box (plus rounding margin), so the shift at the centre
+// is the shift of every sample of the cell.  (The nominal cell may reach past the last
+// sample and across a wrap breakpoint; its centre would not do.)
 template <int D>
-__device__ __forceinline__ void cell_center(const Header *h, int cell, float *ctr) {
-    const int CT = sload(&h->CT), n = sload(&h->n), gx = sload(&h->grid[0]);
-    const int tile = cell / CT, loc = cell - tile * CT;
-    const int t[2] = {D == 1 ? tile : tile % gx, D == 1 ? 0 : tile / gx};
-    const int f[2] = {D == 1 ? loc : loc % n, D == 1 ? 0 : loc / n};
-    const float fs = kTile / (float)n;
-#pragma unroll
-    for (int d = 0; d < D; ++d) ctr[d] = sload(&h->off[d]) + t[d] * kTile + (f[d] + 0.5f) * fs;
+__device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *ctr) {
+    const float4 b = sload(&bins.cell_box[cell]);
+    ctr[0] = 0.5f * (b.x + b.z);
+    ctr[1] = 0.5f * (b.y + b.w);
 }
 
 // (a) Transposed form (small accumulators, U * CB <= 4).  Lane = Gaussian of the cell list,
@@ -291,7 +289,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
         const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
         const int gm = sload(&bins.cell_gmid[fu.cell]);
         float ctr[2];
-        cell_center<D>(bins.h, fu.cell, ctr);
+        cell_center<D>(bins, fu.cell, ctr);
         for (int ps = fu.sb; ps < fu.hi; ps += NS) {
             const int np = min(NP, (fu.hi - ps + 1) >> 1);
             f2 acc[NP][U][CB];
@@ -453,10 +451,12 @@ __global__ void k_pack_fsamples(int N, const char *__restrict__ gbuf, const char
 }
 
 // ------------------------------------------------------------------ backward kernel
-template <int FN, int D, int CB, bool SLOW, typename V>
-__device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *c,
-                                           const float *kk, const float *v, bool wrap, bool unsafe,
-                                           V *gm, V *gv, V *gc) {
+// MODE 0: fast path; 1: plus the lane's constant torus-wrap shift sh (kGeneral entries);
+// 2: the fully general per-pair path (some lane has a kUnsafe entry).
+template <int FN, int D, int CB, int MODE, typename V>
+__device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *sh,
+                                           const float *c, const float *kk, const float *v,
+                                           bool wrap, bool unsafe, V *gm, V *gv, V *gc) {
     constexpr int U = Traits<FN, D>::U;
     V dl[U][CB];
 #pragma unroll
@@ -464,8 +464,12 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) dl[a][ch] = srow[D + a * CB + ch];
     V X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : bc<V>(0.0f)};
+    if constexpr (MODE == 1) {
+        X[0] = X[0] - sh[0];
+        if constexpr (D == 2) X[1] = X[1] - sh[1];
+    }
     V G;
-    if constexpr (SLOW) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
+    if constexpr (MODE == 2) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
     else G = fast_prob<D, V>(X, kk);
     bwd_terms<FN, D, CB, V>(X, c, G, v, dl, gm, gv, gc);
 }
@@ -488,9 +492,9 @@ __device__ __forceinline__ void pair_fields(const float *p, f2 (&f)[RSS], int dr
 // The cell's samples [sb, se), wave-uniform through the scalar cache.
 //   scalar layout: NB sample rows per batch, then the tail one by one;
 //   pair layout  : pairs (2p, 2p+1) covering [sb, se), packed; the boundary pairs are masked.
-template <int FN, int D, int CB, bool SLOW, typename V>
+template <int FN, int D, int CB, int MODE, typename V>
 __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict__ srows,
-                                         const float *m, const float *c, const float *kk,
+                                         const float *m, const float *sh, const float *c, const float *kk,
                                          const float *v, bool wrap, bool unsafe, V *gm, V *gv,
                                          V *gc) {
     constexpr int RSS = srow_stride<FN, D, CB>();
@@ -501,11 +505,11 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
             const F32s<NB * RSS> sr = sload_f<NB * RSS>(srows + (int64_t)j0 * RSS);
 #pragma unroll
             for (int q = 0; q < NB; ++q)
-                bwd_sample<FN, D, CB, SLOW, V>(&sr.v[q * RSS], m, c, kk, v, wrap, unsafe, gm, gv, gc);
+                bwd_sample<FN, D, CB, MODE, V>(&sr.v[q * RSS], m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
         }
         for (; j0 < se; ++j0) {
             const F32s<RSS> sr = sload_f<RSS>(srows + (int64_t)j0 * RSS);
-            bwd_sample<FN, D, CB, SLOW, V>(sr.v, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(sr.v, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
         }
     } else {
         constexpr int PR = 2 * RSS, NB = bwd_batch<PR>();
@@ -516,7 +520,7 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
         if (sb & 1) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
             pair_fields<RSS, D>(sr.v, f, 1);
-            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
             ++p;
         }
         for (; p + NB <= pf; p += NB) {
@@ -524,18 +528,18 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 pair_fields<RSS, D>(&sr.v[q * PR], f, 0);
-                bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+                bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
             }
         }
         for (; p < pf; ++p) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
             pair_fields<RSS, D>(sr.v, f, 0);
-            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
         }
         if (se & 1) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)(pe - 1) * PR);
             pair_fields<RSS, D>(sr.v, f, 2);
-            bwd_sample<FN, D, CB, SLOW, V>(f, m, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
         }
     }
 }
@@ -577,10 +581,20 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
         V gm[2] = {bc<V>(0.0f), bc<V>(0.0f)}, gc[3] = {bc<V>(0.0f), bc<V>(0.0f), bc<V>(0.0f)}, gv[CB];
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) gv[ch] = bc<V>(0.0f);
-        if (__any(active && (wrap || unsafe)))
-            bwd_loop<FN, D, CB, true, V>(sb, se, srows, m, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
-        else
-            bwd_loop<FN, D, CB, false, V>(sb, se, srows, m, c, &r[D], &r[B], false, false, gm, gv, gc);
+        float sh[2] = {0.0f, 0.0f};
+        if (__any(active && unsafe)) {
+            bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
+        } else if (__any(active && wrap)) {
+            if (active && wrap) {
+                float ctr[2];
+                cell_center<D>(bins, cell, ctr);
+#pragma unroll
+                for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+            }
+            bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+        } else {
+            bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+        }
         if (active) {
             float sm[2] = {hsum(gm[0]), hsum(gm[1])}, sc[3] = {hsum(gc[0]), hsum(gc[1]), hsum(gc[2])};
             bwd_finish<FN, D>(c, sm, sc);

@@ -85,3 +85,25 @@ def far_means_case(n=3000):
     conics = torch.cat([1 / sig ** 2, torch.zeros(P, 1), 1 / (1.5 * sig ** 2)], 1).float()
     values = torch.randn(P, 1, generator=g).float()
     return means, values, covs, conics, syn.samples(n, 2, seed=122)
+
+
+def seam_case(D=2, P=400, n=4000, C=1, seed=131):
+    """Gaussians hugging the domain edges (|m| within 0.02 of 1): their torus wraps onto the
+    cells of the opposite edge, whose nominal extent reaches past the last sample (the tile
+    grid spans 2.04 for samples spanning 2) -- the wrap shift must follow the samples."""
+    g = torch.Generator().manual_seed(seed)
+    side = torch.where(torch.rand(P, D, generator=g) < 0.5, -1.0, 1.0)
+    means = (side * (1.0 - 0.02 * torch.rand(P, D, generator=g))).float()
+    if D == 2:  # half of them only on one edge, free along the other axis
+        free = torch.rand(P, generator=g) < 0.5
+        means[free, 1] = (torch.rand(int(free.sum()), generator=g) * 2 - 1).float()
+    sig = 0.004 + 0.01 * torch.rand(P, 1, generator=g)
+    if D == 1:
+        covs = (sig ** 2).float()
+        conics = (1 / sig ** 2).float()
+    else:
+        covs = torch.cat([sig ** 2, 0.3 * sig ** 2, 1.2 * sig ** 2], 1).float()
+        det = covs[:, 0] * covs[:, 2] - covs[:, 1] ** 2
+        conics = torch.stack([covs[:, 2] / det, -covs[:, 1] / det, covs[:, 0] / det], 1).float()
+    values = torch.randn(P, C, generator=g).float()
+    return means, values, covs, conics, syn.samples(n, D, seed=seed + 1)

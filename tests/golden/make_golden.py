@@ -72,6 +72,8 @@ def golden_cases():
         "aliasing": lambda: cases.aliasing_case(n=1000, P=200),
         "far_means": lambda: cases.far_means_case(n=1000),
         "d1_zero_variance": cases.d1_zero_variance_case,
+        "seam_d1": lambda: cases.seam_case(D=1, n=1500),
+        "seam_d2": lambda: cases.seam_case(D=2, n=1500),
     }
 
 

@@ -108,6 +108,17 @@ def test_parity_far_means(dgs, oracle, function):
     _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
 
 
+@pytest.mark.parametrize("function", FUNCS)
+@pytest.mark.parametrize("D,C", [(1, 1), (1, 5), (2, 1), (2, 5)])
+def test_parity_torus_seam(dgs, oracle, function, D, C):
+    """Seam Gaussians: constant-shift wraps (transposed forward for C = 1, the lane-per-sample
+    forward for C = 5, the backward's shift path), incl. cells past the last sample."""
+    means, values, covs, conics, s = cases.seam_case(D=D, C=C)
+    K = syn.out_components(function, D)
+    dL = syn.grad_out(s.shape[0], K, C, seed=132)
+    _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
+
+
 def test_parity_d1_zero_variance(dgs, oracle):
     means, values, covs, conics, samples = cases.d1_zero_variance_case()
     dL = syn.grad_out(samples.shape[0], 1, 1, seed=52)

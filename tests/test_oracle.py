@@ -35,6 +35,8 @@ BIN_CASES = {
     "aliasing": cases.aliasing_case,
     "d1_zero_variance": cases.d1_zero_variance_case,
     "far_means": cases.far_means_case,
+    "seam_d1": lambda: cases.seam_case(D=1),
+    "seam_d2": lambda: cases.seam_case(D=2),
 }
 
 
