@@ -1,0 +1,36 @@
+"""The ctypes binding of the C ABI (tools/dgs_ctypes.py, shown in INTEGRATION.md) against the
+compiled torch extension: same binning bytes, same outputs, same gradients."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from diff_gaussian_sampling import synthetic as syn
+from helpers import FUNCS, FWD_NAME
+
+pytestmark = pytest.mark.gpu
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+
+
+@pytest.mark.parametrize("function", FUNCS)
+def test_ctypes_binding_matches_extension(dgs, function):
+    import dgs_ctypes
+    dev = "cuda:0"
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(2000, 2, 2, seed=141))
+    samples = syn.samples(8000, 2, seed=142).to(dev)
+    a = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
+    b = dgs_ctypes.preprocess_gaussians(means, values, covs, conics, samples, False)
+    assert a[0] == b[0]
+    for x, y in zip(a[3:], b[3:]):  # ranges, sample_ranges, radii
+        assert torch.equal(x, y)
+    fa = getattr(dgs._C, FWD_NAME[function])(means, values, conics, samples, *a[:5], False)
+    fb = getattr(dgs_ctypes, FWD_NAME[function])(means, values, conics, samples, *b[:5], False)
+    assert torch.equal(fa, fb)
+    dL = torch.randn_like(fa)
+    ga = getattr(dgs._C, FWD_NAME[function] + "_backward")(means, values, conics, samples, a[0], dL, *a[1:5], False)
+    gb = getattr(dgs_ctypes, FWD_NAME[function] + "_backward")(means, values, conics, samples, b[0], dL, *b[1:5], False)
+    for x, y in zip(ga, gb):  # atomics: order-dependent in the last bits
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5,
+                                   atol=1e-6 * float(x.abs().max()))

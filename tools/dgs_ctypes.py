@@ -1,0 +1,133 @@
+"""ctypes binding of libdgs.so (include/dgs.h) exposing the reference's `_C` surface.
+
+This is the binding a maintainer of kr4b/diff-gaussian-sampling would add in place of the
+CUDA extension (`diff_gaussian_sampling/_C`, ext.cpp:20-31) when the torch C++ extension
+cannot be built: it needs only ctypes, torch tensors for memory, and libdgs.so.  Install it as
+`diff_gaussian_sampling/_C.py` (or `sys.modules["diff_gaussian_sampling._C"] = dgs_ctypes`)
+and the reference's Python layer runs unchanged.  tests/test_gpu_ctypes.py checks it against
+the compiled extension.
+
+Every function takes and returns torch tensors exactly as the reference's `_C` does.  Device
+memory comes from torch (the allocation callback hands out uint8 tensors that this module keeps
+alive and returns); kernels run on torch's current stream.
+"""
+import ctypes
+import os
+
+import torch
+
+_LIB_PATH = os.environ.get("DGS_LIB") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "..", "diff-gaussian-sampling_amd",
+    "diff_gaussian_sampling", "libdgs.so")
+_lib = ctypes.CDLL(os.path.abspath(_LIB_PATH))
+
+_P, _I, _I64, _SZ, _F = ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_size_t, ctypes.c_float
+ALLOC_FN = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+_lib.dgs_last_error.restype = ctypes.c_char_p
+_lib.dgs_tile_grid.argtypes = [_I, _I, _P, _P, _P, _P]
+_lib.dgs_preprocess.argtypes = [_I, _I, _I, _P, _P, _P, _P, _P, _P, _P, ALLOC_FN, _P,
+                                ctypes.POINTER(_I64), _P, _I]
+_lib.dgs_sample_workspace_size.restype = _SZ
+_lib.dgs_sample_workspace_size.argtypes = [_I] * 6
+_lib.dgs_sample_forward.argtypes = [_I] * 5 + [_P] * 4 + [_P, _SZ, _P, _SZ, _P, _P, _SZ, _P, _I]
+_lib.dgs_sample_backward.argtypes = [_I] * 5 + [_P] * 5 + [_P, _SZ, _P, _SZ, _P, _P, _P, _P, _SZ, _P, _I]
+
+FUNCTIONS = {"sample_gaussians": 0, "sample_gaussians_derivative": 1,
+             "sample_gaussians_laplacian": 2, "sample_gaussians_third_derivative": 3}
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(_lib.dgs_last_error().decode())
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else None
+
+
+def _stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def _f32(t):
+    if t.dtype != torch.float32:
+        raise RuntimeError("expected float32 tensors")
+    return t.contiguous()
+
+
+def preprocess_gaussians(means, values, covariances, conics, samples, debug):
+    """sample_points.h:20-27 -> (num_rendered, binning, sample_binning, ranges, sample_ranges, radii)."""
+    means, covariances, conics, samples = map(_f32, (means, covariances, conics, samples))
+    P, D = means.shape
+    N = samples.shape[0]
+    dev = means.device
+    radii = torch.zeros(P, device=dev)
+    buffers = {}
+
+    def alloc(ctx, which, nbytes):  # DGS_BUF_* -> device memory owned by torch
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        buffers.setdefault(which, []).append(t)
+        return t.data_ptr()
+
+    cb = ALLOC_FN(alloc)
+    grid = (ctypes.c_int * 2)()
+    off = (ctypes.c_float * 2)()
+    if N > 0:
+        _check(_lib.dgs_tile_grid(N, D, _ptr(samples), grid, off, _stream()))
+    R = ctypes.c_int64(0)
+    _check(_lib.dgs_preprocess(P, D, N, _ptr(means), _ptr(covariances), _ptr(conics),
+                               _ptr(samples), grid, off, _ptr(radii), cb, None,
+                               ctypes.byref(R), _stream(), int(bool(debug))))
+    empty = torch.empty(0, dtype=torch.uint8, device=dev)
+    get = lambda k: buffers[k][-1] if k in buffers else empty
+    return R.value, get(0), get(1), get(2), get(3), radii
+
+
+def _forward(name, means, values, conics, samples, num_rendered, binning, sample_binning,
+             ranges, sample_ranges, debug):
+    means, values, conics, samples = map(_f32, (means, values, conics, samples))
+    fn = FUNCTIONS[name]
+    P, D = means.shape
+    N, C = samples.shape[0], values.shape[1]
+    out = torch.zeros((N,) + (D,) * fn + (C,), device=means.device)
+    ws = torch.empty(_lib.dgs_sample_workspace_size(fn, P, D, N, C, 0), dtype=torch.uint8,
+                     device=means.device)
+    _check(_lib.dgs_sample_forward(fn, P, D, N, C, _ptr(means), _ptr(values), _ptr(conics),
+                                   _ptr(samples), _ptr(binning), binning.numel(),
+                                   _ptr(sample_binning), sample_binning.numel(), _ptr(out),
+                                   _ptr(ws), ws.numel(), _stream(), int(bool(debug))))
+    return out
+
+
+def _backward(name, means, values, conics, samples, num_rendered, dL_dout, binning,
+              sample_binning, ranges, sample_ranges, debug):
+    means, values, conics, samples, dL_dout = map(_f32, (means, values, conics, samples, dL_dout))
+    fn = FUNCTIONS[name]
+    P, D = means.shape
+    N, C = samples.shape[0], values.shape[1]
+    S = D * (D + 1) // 2
+    dm = torch.zeros(P, D, device=means.device)
+    dv = torch.zeros(P, C, device=means.device)
+    dc = torch.zeros(P, S, device=means.device)
+    ws = torch.empty(_lib.dgs_sample_workspace_size(fn, P, D, N, C, 1), dtype=torch.uint8,
+                     device=means.device)
+    _check(_lib.dgs_sample_backward(fn, P, D, N, C, _ptr(means), _ptr(values), _ptr(conics),
+                                    _ptr(samples), _ptr(dL_dout), _ptr(binning), binning.numel(),
+                                    _ptr(sample_binning), sample_binning.numel(), _ptr(dm),
+                                    _ptr(dv), _ptr(dc), _ptr(ws), ws.numel(), _stream(),
+                                    int(bool(debug))))
+    return dm, dv, dc
+
+
+def _make(name):
+    fwd = lambda *a: _forward(name, *a)
+    bwd = lambda *a: _backward(name, *a)
+    fwd.__name__, bwd.__name__ = name, name + "_backward"
+    return fwd, bwd
+
+
+sample_gaussians, sample_gaussians_backward = _make("sample_gaussians")
+sample_gaussians_derivative, sample_gaussians_derivative_backward = _make("sample_gaussians_derivative")
+sample_gaussians_laplacian, sample_gaussians_laplacian_backward = _make("sample_gaussians_laplacian")
+sample_gaussians_third_derivative, sample_gaussians_third_derivative_backward = _make(
+    "sample_gaussians_third_derivative")
