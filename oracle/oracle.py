@@ -46,6 +46,10 @@ def _load():
     lib.orc_backward.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
     lib.orc_count_pairs.argtypes = [P, P, P, P, ctypes.c_double, i32, P, P, P]
     lib.orc_tile_grid.argtypes = [i32, i32, P, P, P]
+    lib.orc_agg_counts.argtypes = [i32, i32, P, P, P]
+    lib.orc_agg_fill.argtypes = [i32, i32, P, P, P, P, P, P, P, P]
+    lib.orc_agg_forward.argtypes = [i32] * 5 + [P] * 15
+    lib.orc_agg_backward.argtypes = [i32] * 5 + [P] * 21
     _lib = lib
     return lib
 
@@ -168,3 +172,68 @@ class OracleBins:
                             0 if sub is None else len(sub), _ptr(sub),
                             ctypes.byref(w_ref), ctypes.byref(w_live))
         return w_ref.value, w_live.value
+
+
+# ------------------------------------------------------------------ neighbour aggregation
+def _i64(a):
+    return np.ascontiguousarray(np.asarray(a, dtype=np.int64))
+
+
+def agg_preprocess(means, conics, radii):
+    """preprocess_aggregate (aggregate_neighbors.cu:323-367): (indices i64[Lnb], ranges
+    i64[P] inclusive cumsum, dists [Lnb, D], densities [Lnb], inv_total [P])."""
+    lib = _load()
+    m, c, r = _f32(means), _f32(conics), _f32(radii)
+    P, D = m.shape
+    counts = np.zeros(P, np.int64)
+    lib.orc_agg_counts(P, D, _ptr(m), _ptr(r), _ptr(counts))
+    ranges = np.cumsum(counts).astype(np.int64)
+    n = int(ranges[-1]) if P else 0
+    indices = np.full(n, -1, np.int64)
+    dists = np.zeros((n, D), np.float32)
+    dens = np.zeros(n, np.float32)
+    inv = np.zeros(P, np.float32)
+    lib.orc_agg_fill(P, D, _ptr(m), _ptr(c), _ptr(r), _ptr(ranges), _ptr(indices), _ptr(dists),
+                     _ptr(dens), _ptr(inv))
+    return indices, ranges, dists, dens, inv
+
+
+def agg_forward(features, transform, queries, keys, frequencies, distance_transform, indices,
+                ranges, dists, densities, inv_total):
+    """aggregate_neighbors forward: (weights, embeddings, factors, neighbor_features)."""
+    lib = _load()
+    f, T, q, k = _f32(features), _f32(transform), _f32(queries), _f32(keys)
+    fr, dt = _f32(frequencies), _f32(distance_transform)
+    idx, rg, X, dn, inv = _i64(indices), _i64(ranges), _f32(dists), _f32(densities), _f32(inv_total)
+    P, L = f.shape
+    K = q.shape[1]
+    D = X.shape[1] if X.ndim == 2 else 1
+    E = dt.size // 2
+    n = idx.size
+    w, emb, fac = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    out = np.zeros((P, L), np.float32)
+    lib.orc_agg_forward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+                        _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(w), _ptr(emb),
+                        _ptr(fac), _ptr(out))
+    return w, emb, fac, out
+
+
+def agg_backward(features, transform, queries, keys, frequencies, distance_transform, indices,
+                 ranges, dists, densities, weights, embeddings, factors, inv_total, dL):
+    """aggregate_neighbors backward: the six gradients (features, transform, queries, keys,
+    frequencies, distance_transform)."""
+    lib = _load()
+    f, T, q, k = _f32(features), _f32(transform), _f32(queries), _f32(keys)
+    fr, dt = _f32(frequencies), _f32(distance_transform)
+    idx, rg, X, dn = _i64(indices), _i64(ranges), _f32(dists), _f32(densities)
+    w, emb, fac, inv, g = _f32(weights), _f32(embeddings), _f32(factors), _f32(inv_total), _f32(dL)
+    P, L = f.shape
+    K = q.shape[1]
+    D = X.shape[1] if X.ndim == 2 else 1
+    E = dt.size // 2
+    outs = [np.zeros_like(f), np.zeros_like(T), np.zeros_like(q), np.zeros_like(k),
+            np.zeros_like(fr), np.zeros_like(dt)]
+    lib.orc_agg_backward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+                         _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
+                         _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
+    return tuple(outs)

@@ -1,0 +1,190 @@
+/*
+ * oracle_agg.c -- CPU restatement of the reference's neighbour aggregation
+ * (aggregate_neighbors.cu, kr4b/diff-gaussian-sampling).
+ *
+ * TEST INFRASTRUCTURE ONLY (see oracle.c): used by tests/ as the checker of the HIP path.
+ * PARITY STATUS: "parity unpinned" -- the reference is CUDA-only and ships no fixtures; this
+ * restatement is pinned by torch autograd of its forward (tests/test_oracle_agg.py) and by
+ * hand-checked predicate cases (asymmetric torus wrap, radius skip, power > 0 slots).
+ *
+ * FLOAT = float as in the reference (config.h:20); double where its double literals promote
+ * (`radii * 0.2`, `1.0 / (r + 1e-6)`, `-0.5 * ...`, `fmod(x, 2.0)`, `frequencies * M_PI * X`,
+ * `sin`/`cos` of that double).  Atomic float accumulations of the reference are serial here.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#ifndef M_PI
+#define M_PI 3.14159265358979323846
+#endif
+
+/* findCollisions, aggregate_neighbors.cu:18-50: is j a neighbour of i? */
+static int agg_collides(int D, const float *means, const float *radii, int i, int j) {
+    const float my_radius = (float)((double)radii[i] * 0.2);
+    if ((double)my_radius < 1e-6) return 0;
+    const float other_radius = (float)((double)radii[j] * 0.2);
+    if ((double)other_radius < 1e-6) return 0;
+    float dist = 0.0f;
+    for (int d = 0; d < D; ++d) {
+        float dx = means[(int64_t)j * D + d] - means[(int64_t)i * D + d];
+        /* TORUS: min(dx, abs(2.0 - fmod(abs(dx), 2.0))) -- only a positive dx can shrink */
+        const double w = fabs(2.0 - fmod((double)fabsf(dx), 2.0));
+        dx = (float)fmin((double)dx, w);
+        dist += dx * dx;
+    }
+    const float radius = my_radius + other_radius;
+    return !(dist > radius * radius);
+}
+
+/* Pass 1: neighbour counts per row (the reference's bool_indices.sum(-1)). */
+void orc_agg_counts(int P, int D, const float *means, const float *radii, int64_t *counts) {
+    for (int i = 0; i < P; ++i) {
+        int64_t n = 0;
+        for (int j = 0; j < P; ++j) n += agg_collides(D, means, radii, i, j);
+        counts[i] = n;
+    }
+}
+
+/* Pass 2: preprocess, aggregate_neighbors.cu:52-127.  ranges = inclusive cumsum of counts;
+ * indices pre-filled with -1, dists / densities with 0 (the host glue at 336-341). */
+void orc_agg_fill(int P, int D, const float *means, const float *conics, const float *radii,
+                  const int64_t *ranges, int64_t *indices, float *dists, float *densities,
+                  float *inv_total) {
+    const int S = D * (D + 1) / 2;
+    for (int i = 0; i < P; ++i) {
+        const float my_radius = (float)((double)radii[i] * 0.333);
+        const float my_inv_radius = (float)(1.0 / ((double)my_radius + 1e-6));
+        const int64_t start = i == 0 ? 0 : ranges[i - 1];
+        float total = 0.0f;
+        int64_t current = -1;
+        for (int j = 0; j < P; ++j) {
+            if (!agg_collides(D, means, radii, i, j)) continue;
+            current += 1;
+            const float *con = conics + (int64_t)j * S;
+            float *X = dists + (start + current) * D;
+            for (int d = 0; d < D; ++d) {
+                X[d] = means[(int64_t)j * D + d] - means[(int64_t)i * D + d];
+                if (fabsf(X[d]) > 1.0f) {
+                    if (X[d] >= 0) X[d] = (float)(fmod((double)X[d], 2.0) - 2.0);
+                    else X[d] = (float)(fmod((double)X[d], 2.0) + 2.0);
+                }
+            }
+            float power;
+            if (D == 1) {
+                power = (float)(-0.5 * con[0] * X[0] * X[0]);
+            } else {
+                power = (float)(-0.5 * (double)(con[0] * X[0] * X[0] + con[2] * X[1] * X[1])
+                                - (double)(con[1] * X[0] * X[1]));
+            }
+            for (int d = 0; d < D; ++d) X[d] *= my_inv_radius;
+            if (power > 0) continue;
+            densities[start + current] = expf(power);
+            indices[start + current] = j;
+            total += densities[start + current];
+        }
+        inv_total[i] = (float)(1.0 / ((double)total + 1e-6));
+    }
+}
+
+/* aggregateNeighbors, aggregate_neighbors.cu:129-208.  E = distance_transform.size / 2. */
+void orc_agg_forward(int P, int D, int L, int K, int E, const float *features,
+                     const float *transform, const float *queries, const float *keys,
+                     const float *frequencies, const float *dt, const int64_t *indices,
+                     const int64_t *ranges, const float *dists, const float *densities,
+                     const float *inv_total, float *weights, float *embeddings, float *factors,
+                     float *out) {
+    const int F = (E - 1) / D / 2, stride = (E - 1) / D;
+    for (int i = 0; i < P; ++i) {
+        const float *q = queries + (int64_t)i * K;
+        const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
+        float *o = out + (int64_t)i * L;
+        for (int64_t s = start; s < end; ++s) {
+            const int64_t idx = indices[s];
+            if (idx == -1) continue;
+            const float *feat = features + idx * L, *key = keys + idx * K, *X = dists + s * D;
+            float weight = 0.0f;
+            for (int k = 0; k < K; ++k) weight += q[k] * key[k];
+            weights[s] = weight;
+            float emb = 0.0f, fac = 0.0f;
+            for (int d = 0; d < D; ++d)
+                for (int e = 0; e < F; ++e) {
+                    const float sn = (float)sin((double)frequencies[e] * M_PI * (double)X[d]);
+                    const float cs = (float)cos((double)frequencies[e] * M_PI * (double)X[d]);
+                    emb += dt[d * stride + e * 2 + 0] * sn;
+                    emb += dt[d * stride + e * 2 + 1] * cs;
+                    fac += dt[E + d * stride + e * 2 + 0] * sn;
+                    fac += dt[E + d * stride + e * 2 + 1] * cs;
+                }
+            emb += dt[E - 1];
+            fac += dt[2 * E - 1];
+            embeddings[s] = emb;
+            factors[s] = fac;
+            const float dw = inv_total[i] * densities[s] * weight;
+            const float dwf = dw * fac, dwe = dw * emb;
+            for (int j = 0; j < L; ++j) {
+                const float embedded = dwe + dwf * feat[j];
+                for (int k = 0; k < L; ++k) o[k] += transform[j * L + k] * embedded;
+            }
+        }
+    }
+}
+
+/* aggregateNeighborsBackward, aggregate_neighbors.cu:210-321 (atomics in serial order). */
+void orc_agg_backward(int P, int D, int L, int K, int E, const float *features,
+                      const float *transform, const float *queries, const float *keys,
+                      const float *frequencies, const float *dt, const int64_t *indices,
+                      const int64_t *ranges, const float *dists, const float *densities,
+                      const float *weights, const float *embeddings, const float *factors,
+                      const float *inv_total, const float *dL, float *dfeat, float *dtrans,
+                      float *dq, float *dkeys, float *dfreq, float *ddt) {
+    const int F = (E - 1) / D / 2, stride = (E - 1) / D;
+    float st[1024];
+    for (int i = 0; i < P; ++i) {
+        const float *q = queries + (int64_t)i * K, *g = dL + (int64_t)i * L;
+        const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
+        for (int j = 0; j < L; ++j) {
+            st[j] = 0.0f;
+            for (int k = 0; k < L; ++k) st[j] += transform[j * L + k] * g[k];
+        }
+        for (int64_t s = start; s < end; ++s) {
+            const int64_t idx = indices[s];
+            if (idx == -1) continue;
+            const float *feat = features + idx * L, *key = keys + idx * K, *X = dists + s * D;
+            const float dc = densities[s] * inv_total[i];
+            const float dcw = dc * weights[s];
+            for (int d = 0; d < D; ++d)
+                for (int e = 0; e < F; ++e) {
+                    const float sn = (float)sin((double)frequencies[e] * M_PI * (double)X[d]);
+                    const float cs = (float)cos((double)frequencies[e] * M_PI * (double)X[d]);
+                    const int a = d * stride + e * 2;
+                    for (int j = 0; j < L; ++j) {
+                        const float dct = dcw * st[j];
+                        ddt[a + 0] += dct * sn;
+                        ddt[E + a + 0] += dct * sn * feat[j];
+                        dfreq[e] += (float)((double)cs * M_PI * (double)X[d] * (double)dct *
+                                            (double)(dt[a + 0] + dt[E + a + 0] * feat[j]));
+                        ddt[a + 1] += dct * cs;
+                        ddt[E + a + 1] += dct * cs * feat[j];
+                        dfreq[e] += (float)((double)-sn * M_PI * (double)X[d] * (double)dct *
+                                            (double)(dt[a + 1] + dt[E + a + 1] * feat[j]));
+                    }
+                }
+            const float dce = dc * embeddings[s], dcf = dc * factors[s];
+            for (int j = 0; j < L; ++j) {
+                const float dct = dcw * st[j];
+                ddt[E - 1] += dct;
+                ddt[2 * E - 1] += dct * feat[j];
+                dfeat[idx * L + j] += dct * factors[s];
+                const float embedded = dce + dcf * feat[j];
+                const float we = weights[s] * embedded;
+                for (int k = 0; k < L; ++k) dtrans[j * L + k] += we * g[k];
+                const float te = st[j] * embedded;
+                for (int k = 0; k < K; ++k) {
+                    dq[(int64_t)i * K + k] += key[k] * te;
+                    dkeys[idx * K + k] += q[k] * te;
+                }
+            }
+        }
+    }
+}
