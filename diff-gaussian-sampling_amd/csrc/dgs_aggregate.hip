@@ -1,0 +1,768 @@
+// dgs_aggregate.hip -- neighbour aggregation (gfx950).
+//
+// Replaces aggregate_neighbors.cu (kr4b/diff-gaussian-sampling):
+//   findCollisions + preprocess (18-127, 323-367) -> dgs_agg_preprocess
+//   aggregateNeighbors        (129-208, 369-415) -> dgs_agg_forward
+//   aggregateNeighborsBackward (210-321, 417-475) -> dgs_agg_backward
+//
+// Neighbour lists.  The reference tests every (i, j) pair into a P x P bool matrix (1 TB at
+// P = 1M).  Here the Gaussians are radix-sorted into a uniform grid whose cell is at least
+// twice the largest search radius 0.2 * radius, packed in cell order as {x, y, r, id}, and one
+// wave per row walks the cells that can hold a neighbour -- the direct neighbourhood and, per
+// axis, the images at +2k that the reference's one-sided torus wrap
+// `min(dx, |2 - fmod(|dx|, 2)|)` can bring close (only a positive dx wraps) -- evaluating the
+// reference predicate bit-exactly.  Pass 1 counts; pass 2 collects the row's neighbours in LDS,
+// bitonic-sorts them into the reference's ascending-j slot order and writes the slots.  Rows
+// with more neighbours than the wave's LDS holds are emitted in id windows.
+//
+// Forward.  One wave per row, lanes over slots.  The reference adds transform^T * embedded
+// into the output for every slot (2 L^2 FLOP per slot); here each lane accumulates
+// a[j] += dw (emb + fac * features[idx][j]) over its slots, one cross-lane reduce-scatter per
+// row forms a, and out = transform^T a (same sum, different rounding order).
+//
+// Backward.  One wave per row.  Per slot the reference's j-loops collapse onto two row sums,
+// S1 = sum_j st[j] and S2 = sum_j st[j] features[idx][j] (st = transform dL_row):
+// sum_j te_j = dc (emb S1 + fac S2), and the distance-transform / frequency terms need only
+// dcw S1 and dcw S2.  Query gradients and the row's a are reduced in registers; transform's
+// gradient is A^T dL over the rows' a (a second, small kernel); the neighbours' feature and
+// key gradients are scattered with float atomics as in the reference; the distance-transform
+// and frequency gradients are per-lane LDS partials, flushed once per wave.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "dgs_internal.h"
+#include "dgs_render.h"
+
+namespace dgs {
+
+constexpr int kAggNMax = 4096;  // neighbour ids a wave sorts in LDS at once
+constexpr int kAggMaxCells = 1 << 24;
+
+struct AggGeom {
+    int D;
+    int nc[2];     // grid cells per axis
+    double lo[2];  // grid origin (min of the valid means)
+    double hi[2];  // max of the valid means
+    double cs;     // cell size
+    float rmax;    // max 0.2 * radius over valid Gaussians
+};
+
+// float <-> order-preserving uint (min/max atomics on floats of any sign)
+__device__ __forceinline__ uint32_t f2o(float f) {
+    const uint32_t b = __float_as_uint(f);
+    return (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+}
+static inline float o2f(uint32_t o) {
+    const uint32_t b = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+    float f;
+    std::memcpy(&f, &b, 4);
+    return f;
+}
+
+// aggregate_neighbors.cu:29-34: r = radii * 0.2 (double literal, rounded to float); r < 1e-6
+// takes no part.
+__device__ __forceinline__ float agg_r(float radius) { return (float)((double)radius * 0.2); }
+__device__ __forceinline__ bool agg_valid(float r) { return (double)r >= 1e-6; }
+
+__global__ void k_agg_prep(int P, int D, const float *__restrict__ means, const float *__restrict__ radii,
+                           uint32_t *__restrict__ stats /* rmax, min[2], max[2] */) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const float r = agg_r(radii[i]);
+    if (!agg_valid(r)) return;
+    atomicMax(&stats[0], f2o(r));
+    for (int d = 0; d < D; ++d) {
+        const float m = means[(int64_t)i * D + d];
+        atomicMin(&stats[1 + d], f2o(m));
+        atomicMax(&stats[3 + d], f2o(m));
+    }
+}
+
+__device__ __forceinline__ int agg_cell_1d(const AggGeom &g, int d, double x) {
+    const double c = floor((x - g.lo[d]) / g.cs);
+    return c < 0.0 ? 0 : (c >= (double)g.nc[d] ? g.nc[d] - 1 : (int)c);
+}
+
+__global__ void k_agg_keys(int P, AggGeom g, const float *__restrict__ means, const float *__restrict__ radii,
+                           uint32_t *__restrict__ keys, uint32_t *__restrict__ ids) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    uint32_t key = (uint32_t)(g.nc[0] * g.nc[1]);  // not a neighbour of anything: sorts last
+    if (agg_valid(agg_r(radii[i]))) {
+        const int cx = agg_cell_1d(g, 0, means[(int64_t)i * g.D]);
+        const int cy = g.D == 2 ? agg_cell_1d(g, 1, means[(int64_t)i * 2 + 1]) : 0;
+        key = (uint32_t)(cy * g.nc[0] + cx);
+    }
+    keys[i] = key;
+    ids[i] = (uint32_t)i;
+}
+
+// Candidates packed in cell order as {x, y, r, id}.
+__global__ void k_agg_pack(int P, int D, const uint32_t *__restrict__ ids, const float *__restrict__ means,
+                           const float *__restrict__ radii, float4 *__restrict__ cand) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= P) return;
+    const uint32_t j = ids[t];
+    cand[t] = make_float4(means[(int64_t)j * D], D == 2 ? means[(int64_t)j * D + 1] : 0.0f, agg_r(radii[j]),
+                          __uint_as_float(j));
+}
+
+// cstart[c] = first sorted position whose key is >= c, for c in [0, ncells].
+__global__ void k_agg_cell_start(int ncells, int P, const uint32_t *__restrict__ keys, int32_t *__restrict__ cstart) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c > ncells) return;
+    int lo = 0, hi = P;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (keys[mid] < (uint32_t)c) lo = mid + 1;
+        else hi = mid;
+    }
+    cstart[c] = lo;
+}
+
+// min(dx, |2 - fmod(|dx|, 2)|) of the reference (aggregate_neighbors.cu:43-46), evaluated there
+// in double and rounded to float.  fmod is exact, 2 - r rounds once, and rounding is monotonic
+// (so min commutes with it): this float evaluation is bit-identical.
+__device__ __forceinline__ float torus_dx(float dx) {
+    const float ax = fabsf(dx);
+    const float r = ax < 2.0f ? ax : fmodf(ax, 2.0f);
+    return fminf(dx, fabsf(2.0f - r));
+}
+
+// findCollisions' predicate (aggregate_neighbors.cu:36-53): float, no contraction.
+__device__ __forceinline__ bool agg_collides(int D, float mix, float miy, float ri, float4 cj) {
+    DGS_NO_CONTRACT
+    if (!agg_valid(cj.z)) return false;
+    const float dx = torus_dx(cj.x - mix);
+    float dist = dx * dx;
+    if (D == 2) {
+        const float dy = torus_dx(cj.y - miy);
+        dist = dist + dy * dy;
+    }
+    const float radius = ri + cj.z;
+    return !(dist > radius * radius);
+}
+
+// Per-axis candidate cell ranges of a row: the direct window [m - R, m + R] and the images
+// [m + 2k - R, m + 2k] (k >= 1) that a positive dx can wrap onto, widened by a rounding
+// tolerance and merged into disjoint ranges.
+struct AxisRanges {
+    int n;
+    int lo[8], hi[8];
+};
+
+__device__ inline void agg_axis_ranges(const AggGeom &g, int d, float m, float R, AxisRanges &out) {
+    out.n = 0;
+    for (int k = 0;; ++k) {
+        const double tol = 1e-5 * (1.0 + fabs((double)m) + 2.0 * k);
+        const double a = (double)m + 2.0 * k - R - tol;
+        const double b = (double)m + (k == 0 ? (double)R : 2.0 * k) + tol;
+        if (a > g.hi[d]) break;
+        if (b < g.lo[d]) continue;
+        const int c0 = agg_cell_1d(g, d, a), c1 = agg_cell_1d(g, d, b);
+        if (out.n > 0 && c0 <= out.hi[out.n - 1] + 1) {
+            out.hi[out.n - 1] = max(out.hi[out.n - 1], c1);
+        } else if (out.n == 8) {  // pathological spread: the whole axis
+            out.n = 1;
+            out.lo[0] = 0;
+            out.hi[0] = g.nc[d] - 1;
+            return;
+        } else {
+            out.lo[out.n] = c0;
+            out.hi[out.n] = c1;
+            ++out.n;
+        }
+    }
+}
+
+// Visit every candidate of row i: wave-uniform loops over cell ranges, lanes over members;
+// f(j, ok) is called by every lane (ok = the lane holds a neighbour j).
+template <class Fn>
+__device__ inline void agg_for_candidates(const AggGeom &g, float mix, float miy, float ri,
+                                          const float4 *__restrict__ cand, const int32_t *__restrict__ cstart,
+                                          int lane, Fn f) {
+    const float R = ri + g.rmax;
+    AxisRanges ax, ay;
+    agg_axis_ranges(g, 0, mix, R, ax);
+    if (g.D == 2) {
+        agg_axis_ranges(g, 1, miy, R, ay);
+    } else {
+        ay.n = 1;
+        ay.lo[0] = ay.hi[0] = 0;
+    }
+    for (int ry = 0; ry < ay.n; ++ry)
+        for (int cy = ay.lo[ry]; cy <= ay.hi[ry]; ++cy)
+            for (int rx = 0; rx < ax.n; ++rx) {
+                // the cells of one x range are contiguous in the sorted order
+                const int row = cy * g.nc[0];
+                const int b = cstart[row + ax.lo[rx]], e = cstart[row + ax.hi[rx] + 1];
+                for (int t0 = b; t0 < e; t0 += kWave) {
+                    const int t = t0 + lane;
+                    bool ok = false;
+                    uint32_t j = 0;
+                    if (t < e) {
+                        const float4 c = cand[t];
+                        j = __float_as_uint(c.w);
+                        ok = agg_collides(g.D, mix, miy, ri, c);
+                    }
+                    f(j, ok);
+                }
+            }
+}
+
+__global__ __launch_bounds__(kBlock) void k_agg_count(int P, AggGeom g, const float *__restrict__ means,
+                                                      const float *__restrict__ radii,
+                                                      const float4 *__restrict__ cand,
+                                                      const int32_t *__restrict__ cstart,
+                                                      int64_t *__restrict__ counts) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int stride = gridDim.x * kWavesPerBlock;
+    for (int i = wave_unit_index(); i < P; i += stride) {
+        int64_t n = 0;
+        const float ri = agg_r(radii[i]);
+        if (agg_valid(ri)) {
+            const float mix = means[(int64_t)i * g.D], miy = g.D == 2 ? means[(int64_t)i * 2 + 1] : 0.0f;
+            agg_for_candidates(g, mix, miy, ri, cand, cstart, lane,
+                               [&](uint32_t, bool ok) { n += __popcll(__ballot(ok)); });
+        }
+        if (lane == 0) counts[i] = n;
+    }
+}
+
+// X[d] of aggregate_neighbors.cu:91-101 (fmod(X, 2.0) -+ 2.0 in double: exact as in torus_dx).
+__device__ __forceinline__ float agg_wrap(float x) {
+    if (fabsf(x) > 1.0f) return x >= 0.0f ? fmodf(x, 2.0f) - 2.0f : fmodf(x, 2.0f) + 2.0f;
+    return x;
+}
+
+// One slot of aggregate_neighbors.cu:84-119: X, power with the neighbour's conic, scaled X,
+// density; index -1 and density 0 when power > 0.  Returns the density added to the total.
+__device__ __forceinline__ float agg_slot(int D, float mix, float miy, float inv_r, const float *mj,
+                                          const float *con, int64_t j, int64_t *idx_out, float *X_out,
+                                          float *dens_out) {
+    DGS_NO_CONTRACT
+    const float X0 = agg_wrap(mj[0] - mix);
+    const float X1 = D == 2 ? agg_wrap(mj[1] - miy) : 0.0f;
+    float power;
+    if (D == 1) {
+        power = (float)(-0.5 * (double)con[0] * (double)X0 * (double)X0);
+    } else {
+        const float a = con[0] * X0 * X0 + con[2] * X1 * X1;
+        const float b = con[1] * X0 * X1;
+        power = (float)(-0.5 * (double)a - (double)b);
+    }
+    X_out[0] = X0 * inv_r;
+    if (D == 2) X_out[1] = X1 * inv_r;
+    if (power > 0.0f) {
+        *idx_out = -1;
+        *dens_out = 0.0f;
+        return 0.0f;
+    }
+    const float dn = expf(power);
+    *idx_out = j;
+    *dens_out = dn;
+    return dn;
+}
+
+// LDS hand-off between the lanes of one wave.
+__device__ __forceinline__ void wave_sync_lds() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Ascending bitonic sort of n (a power of two) keys in this wave's LDS region.
+__device__ inline void wave_bitonic(uint32_t *s, int n, int lane) {
+    for (int k = 2; k <= n; k <<= 1)
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int t = lane; t < (n >> 1); t += kWave) {
+                const int i = 2 * jj * (t / jj) + (t % jj), l = i + jj;
+                const uint32_t a = s[i], b = s[l];
+                const bool up = (i & k) == 0;
+                if ((a > b) == up) {
+                    s[i] = b;
+                    s[l] = a;
+                }
+            }
+            wave_sync_lds();
+        }
+}
+
+__device__ __forceinline__ float wave_sum(float v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+__global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const float *__restrict__ means,
+                                                     const float *__restrict__ conics,
+                                                     const float *__restrict__ radii,
+                                                     const float4 *__restrict__ cand,
+                                                     const int32_t *__restrict__ cstart,
+                                                     const int64_t *__restrict__ ranges,
+                                                     int64_t *__restrict__ indices, float *__restrict__ dists,
+                                                     float *__restrict__ densities,
+                                                     float *__restrict__ inv_total) {
+    __shared__ uint32_t buf[kWavesPerBlock][kAggNMax];
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t *s = buf[threadIdx.x >> 6];
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int D = g.D, S = D * (D + 1) / 2;
+    for (int i = wave_unit_index(); i < P; i += stride) {
+        const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
+        // aggregate_neighbors.cu:73-74 (0.333 and 1.0 / (r + 1e-6) in double)
+        const float my_radius = (float)((double)radii[i] * 0.333);
+        const float inv_r = (float)(1.0 / ((double)my_radius + 1e-6));
+        const float ri = agg_r(radii[i]);
+        const float mix = means[(int64_t)i * D], miy = D == 2 ? means[(int64_t)i * 2 + 1] : 0.0f;
+        float total = 0.0f;
+        int64_t slot = start;
+        uint32_t lo = 0;
+        while (slot < end) {
+            // collect the neighbours with id in [lo, hi), halving the window until they fit
+            uint32_t hi = (uint32_t)P;
+            int n;
+            for (;;) {
+                n = 0;
+                agg_for_candidates(g, mix, miy, ri, cand, cstart, lane, [&](uint32_t j, bool ok) {
+                    const bool take = ok && j >= lo && j < hi;
+                    const uint64_t bal = __ballot(take);
+                    const int pos = n + (int)__popcll(bal & ((1ull << lane) - 1ull));
+                    if (take && pos < kAggNMax) s[pos] = j;
+                    n += (int)__popcll(bal);
+                });
+                if (n <= kAggNMax) break;
+                hi = lo + (hi - lo) / 2;
+            }
+            int np2 = 1;
+            while (np2 < n) np2 <<= 1;
+            for (int t = n + lane; t < np2; t += kWave) s[t] = 0xffffffffu;
+            wave_sync_lds();
+            wave_bitonic(s, np2, lane);
+            for (int t0 = 0; t0 < n; t0 += kWave) {
+                const int t = t0 + lane;
+                float dv = 0.0f;
+                if (t < n) {
+                    const int64_t j = s[t], o = slot + t;
+                    dv = agg_slot(D, mix, miy, inv_r, means + j * D, conics + j * S, j, &indices[o], &dists[o * D],
+                                  &densities[o]);
+                }
+                total += wave_sum(dv);  // 64 slots at a time, in slot order
+            }
+            slot += n;
+            lo = hi;
+            wave_sync_lds();
+        }
+        if (lane == 0) inv_total[i] = (float)(1.0 / ((double)total + 1e-6));
+    }
+}
+
+// --------------------------------------------------------------------- forward / backward
+struct AggArgs {
+    int P, D, L, K, E;
+    const float *features, *transform, *queries, *keys, *freq, *dt;
+    const int64_t *indices, *ranges;
+    const float *dists, *densities, *inv_total;
+    float *weights, *embeddings, *factors;  // forward: written; backward: read
+    float *out;                             // forward
+    const float *dL;                        // backward
+    float *arows;                           // backward scratch: a of every row [P][L]
+    float *dfeat, *dq, *dkeys, *dfreq, *ddt;
+};
+
+// sin / cos of the reference's double argument frequencies * M_PI * X (aggregate_neighbors.cu
+// :181-182 evaluate sin/cos in double and round to float): quadrant reduction in double, then
+// float sin/cos of the reduced argument (|r| <= pi/4).
+__device__ __forceinline__ void ref_sincos(float f, float X, float *s, float *c) {
+    const double arg = (double)f * M_PI * (double)X;
+    if (!(fabs(arg) < 1e6)) {
+        *s = (float)sin(arg);
+        *c = (float)cos(arg);
+        return;
+    }
+    const double n = rint(arg * M_2_PI);
+    double r = fma(-n, 1.5707963267948966, arg);
+    r = fma(-n, 6.123233995736766e-17, r);
+    float sr, cr;
+    sincosf((float)r, &sr, &cr);
+    switch ((int)n & 3) {
+    case 0: *s = sr; *c = cr; break;
+    case 1: *s = cr; *c = -sr; break;
+    case 2: *s = -sr; *c = -cr; break;
+    default: *s = -cr; *c = sr; break;
+    }
+}
+
+// embedding / factor of one slot (aggregate_neighbors.cu:176-193).
+__device__ __forceinline__ void agg_embed(int D, int F, int E, const float *__restrict__ freq,
+                                          const float *__restrict__ dt, const float *X, float *emb, float *fac) {
+    const int stride = (E - 1) / D;
+    float e0 = 0.0f, f0 = 0.0f;
+    for (int d = 0; d < D; ++d)
+        for (int e = 0; e < F; ++e) {
+            float sn, cs;
+            ref_sincos(freq[e], X[d], &sn, &cs);
+            const int a = d * stride + e * 2;
+            e0 += dt[a] * sn;
+            e0 += dt[a + 1] * cs;
+            f0 += dt[E + a] * sn;
+            f0 += dt[E + a + 1] * cs;
+        }
+    *emb = e0 + dt[E - 1];
+    *fac = f0 + dt[2 * E - 1];
+}
+
+// per-lane partial sums -> lane l holds the wave total of value l (l < NB)
+template <int NB>
+__device__ __forceinline__ float reduce_row(const float (&acc)[NB], int lane) {
+    float x[64];
+#pragma unroll
+    for (int t = 0; t < 64; ++t) x[t] = t < NB ? acc[t] : 0.0f;
+    return reduce_scatter64(x, lane);
+}
+
+// NB (16, 32 or 64): features per pass; L > 64 takes several passes over the row.
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_agg_forward(AggArgs A) {
+    __shared__ float arow[kWavesPerBlock][256];
+    const int lane = threadIdx.x & (kWave - 1);
+    float *ar = arow[threadIdx.x >> 6];
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2;
+    for (int i = wave_unit_index(); i < A.P; i += stride) {
+        const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
+        const float inv = A.inv_total[i];
+        const float *q = A.queries + (int64_t)i * K;
+        for (int fb = 0; fb == 0 || fb < L; fb += NB) {  // one pass even without features
+            float acc[NB];
+#pragma unroll
+            for (int t = 0; t < NB; ++t) acc[t] = 0.0f;
+            for (int64_t s = start + lane; s < end; s += kWave) {
+                const int64_t idx = A.indices[s];
+                if (idx < 0) {
+                    if (fb == 0) A.weights[s] = A.embeddings[s] = A.factors[s] = 0.0f;
+                    continue;
+                }
+                const float *key = A.keys + idx * K;
+                float weight = 0.0f;
+                for (int k = 0; k < K; ++k) weight += q[k] * key[k];
+                const float X[2] = {A.dists[s * D], D == 2 ? A.dists[s * D + 1] : 0.0f};
+                float emb, fac;
+                agg_embed(D, F, E, A.freq, A.dt, X, &emb, &fac);
+                if (fb == 0) {
+                    A.weights[s] = weight;
+                    A.embeddings[s] = emb;
+                    A.factors[s] = fac;
+                }
+                const float dw = inv * A.densities[s] * weight;
+                const float dwf = dw * fac, dwe = dw * emb;
+                const float *feat = A.features + idx * L + fb;
+                if (fb + NB <= L) {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) acc[t] += dwe + dwf * feat[t];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t)
+                        if (fb + t < L) acc[t] += dwe + dwf * feat[t];
+                }
+            }
+            const float r = reduce_row<NB>(acc, lane);
+            if (lane < NB && fb + lane < L) ar[fb + lane] = r;
+        }
+        wave_sync_lds();
+        for (int k = lane; k < L; k += kWave) {
+            float o = 0.0f;
+            for (int j = 0; j < L; ++j) o += A.transform[j * L + k] * ar[j];
+            A.out[(int64_t)i * L + k] = o;
+        }
+        wave_sync_lds();
+    }
+}
+
+// Dynamic LDS per wave: NV x 64 per-lane partials of the shared arrays (ddt[2E], dfreq[F]),
+// then st[256].
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = threadIdx.x >> 6;
+    const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2, dstride = (E - 1) / D;
+    const int NV = 2 * E + F;
+    float *part = lds + w * (NV * kWave + 256) + lane;  // value v of this lane: part[v * 64]
+    float *st = lds + w * (NV * kWave + 256) + NV * kWave;
+    for (int v = 0; v < NV; ++v) part[v * kWave] = 0.0f;
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int LK = max(L, K);
+    for (int i = wave_unit_index(); i < A.P; i += stride) {
+        const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
+        const float inv = A.inv_total[i];
+        const float *q = A.queries + (int64_t)i * K, *g = A.dL + (int64_t)i * L;
+        // summed_transform (aggregate_neighbors.cu:257-262)
+        for (int j = lane; j < L; j += kWave) {
+            float v = 0.0f;
+            for (int k = 0; k < L; ++k) v += A.transform[j * L + k] * g[k];
+            st[j] = v;
+        }
+        wave_sync_lds();
+        float S1 = 0.0f;
+        for (int j = 0; j < L; ++j) S1 += st[j];
+        for (int fb = 0; fb == 0 || fb < LK; fb += NB) {
+            float acc_a[NB], acc_q[NB];
+#pragma unroll
+            for (int t = 0; t < NB; ++t) acc_a[t] = acc_q[t] = 0.0f;
+            for (int64_t s = start + lane; s < end; s += kWave) {
+                const int64_t idx = A.indices[s];
+                if (idx < 0) continue;
+                const float *feat = A.features + idx * L, *key = A.keys + idx * K;
+                const float dc = A.densities[s] * inv;
+                const float dcw = dc * A.weights[s];
+                const float emb = A.embeddings[s], fac = A.factors[s];
+                float S2 = 0.0f;
+                for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
+                const float te = (dc * emb) * S1 + (dc * fac) * S2;  // sum_j te_j
+                const float dwe = dcw * emb, dwf = dcw * fac;
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    if (fb + t < L) {
+                        acc_a[t] += dwe + dwf * feat[fb + t];
+                        atomicAdd(&A.dfeat[idx * L + fb + t], dcw * st[fb + t] * fac);
+                    }
+                    if (fb + t < K) {
+                        acc_q[t] += key[fb + t] * te;
+                        atomicAdd(&A.dkeys[idx * K + fb + t], q[fb + t] * te);
+                    }
+                }
+                if (fb != 0) continue;
+                // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
+                const float t1 = dcw * S1, t2 = dcw * S2;
+                for (int d = 0; d < D; ++d) {
+                    const float Xd = A.dists[s * D + d];
+                    const double px = M_PI * (double)Xd;
+                    for (int e = 0; e < F; ++e) {
+                        float sn, cs;
+                        ref_sincos(A.freq[e], Xd, &sn, &cs);
+                        const int a = d * dstride + e * 2;
+                        part[a * kWave] += t1 * sn;
+                        part[(a + 1) * kWave] += t1 * cs;
+                        part[(E + a) * kWave] += t2 * sn;
+                        part[(E + a + 1) * kWave] += t2 * cs;
+                        const float f0 = (float)((double)cs * px * ((double)A.dt[a] * t1 + (double)A.dt[E + a] * t2));
+                        const float f1 =
+                            (float)((double)-sn * px * ((double)A.dt[a + 1] * t1 + (double)A.dt[E + a + 1] * t2));
+                        part[(2 * E + e) * kWave] += f0 + f1;
+                    }
+                }
+                part[(E - 1) * kWave] += t1;
+                part[(2 * E - 1) * kWave] += t2;
+            }
+            const float ra = reduce_row<NB>(acc_a, lane);
+            if (lane < NB && fb + lane < L) A.arows[(int64_t)i * L + fb + lane] = ra;
+            const float rq = reduce_row<NB>(acc_q, lane);
+            if (lane < NB && fb + lane < K) A.dq[(int64_t)i * K + fb + lane] = rq;
+        }
+        wave_sync_lds();
+    }
+    for (int v = 0; v < NV; ++v) {
+        const float x = wave_sum(part[v * kWave]);
+        if (lane == 0) atomicAdd(v < 2 * E ? &A.ddt[v] : &A.dfreq[v - 2 * E], x);
+    }
+}
+
+// dL_dtransform = A^T dL over the rows' a (aggregate_neighbors.cu:301-304, summed over slots).
+__global__ __launch_bounds__(kBlock) void k_agg_dtrans(int P, int L, const float *__restrict__ arows,
+                                                       const float *__restrict__ dL, float *__restrict__ dtrans) {
+    const int64_t per = ((int64_t)P + gridDim.x - 1) / gridDim.x;
+    const int64_t r0 = (int64_t)blockIdx.x * per, r1 = min<int64_t>(P, r0 + per);
+    if (r0 >= r1) return;
+    for (int e = threadIdx.x; e < L * L; e += blockDim.x) {
+        const int j = e / L, k = e - j * L;
+        float acc = 0.0f;
+        for (int64_t i = r0; i < r1; ++i) acc += arows[i * L + j] * dL[i * L + k];
+        atomicAdd(&dtrans[e], acc);
+    }
+}
+
+}  // namespace dgs
+
+using namespace dgs;
+
+static unsigned agg_elem_blocks(int64_t n) { return (unsigned)std::max<int64_t>(1, (n + kBlock - 1) / kBlock); }
+static unsigned agg_row_blocks(int P) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((P + kWavesPerBlock - 1) / kWavesPerBlock, 1 << 20));
+}
+
+extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float *conics, const float *radii,
+                                  int64_t *ranges, float *inv_total, dgs_alloc_fn alloc, void *alloc_ctx,
+                                  int64_t *length, dgs_stream_t stream, int debug) {
+    if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "aggregate: only D = 1 or D = 2 is supported");
+    if (P < 0 || !alloc || !length) return fail(DGS_ERR_ARG, "dgs_agg_preprocess: bad arguments");
+    *length = 0;
+    if (P == 0) return DGS_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    auto scratch = [&](size_t n) { return alloc(alloc_ctx, DGS_BUF_SCRATCH, std::max<size_t>(n, 16)); };
+    uint32_t *stats = static_cast<uint32_t *>(scratch(64));
+    if (!stats) return fail(DGS_ERR_ALLOC, "aggregate: scratch allocation failed");
+    static const uint32_t init[5] = {0u, 0xffffffffu, 0xffffffffu, 0u, 0u};
+    DGS_TRY_HIP(hipMemcpyAsync(stats, init, sizeof(init), hipMemcpyHostToDevice, s));
+    k_agg_prep<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, D, means, radii, stats);
+    DGS_LAUNCH_CHECK(s, debug);
+    uint32_t h[5];
+    DGS_TRY_HIP(hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+
+    AggGeom g;
+    g.D = D;
+    const bool any = h[0] != 0;
+    g.rmax = any ? o2f(h[0]) : 0.0f;
+    for (int d = 0; d < 2; ++d) {
+        g.lo[d] = (any && d < D) ? (double)o2f(h[1 + d]) : 0.0;
+        g.hi[d] = (any && d < D) ? (double)o2f(h[3 + d]) : 0.0;
+    }
+    // cell >= 2 rmax (a row's direct window spans at most three cells); at most kAggMaxCells
+    double cell = std::max(2.0 * (double)g.rmax, 1e-6);
+    for (;;) {
+        int64_t tot = 1;
+        for (int d = 0; d < 2; ++d) {
+            g.nc[d] = d < D ? (int)std::min<double>((g.hi[d] - g.lo[d]) / cell + 1.0, 1 << 24) : 1;
+            tot *= g.nc[d];
+        }
+        if (tot <= kAggMaxCells) break;
+        cell *= 2.0;
+    }
+    g.cs = cell;
+    const int ncells = g.nc[0] * g.nc[1];
+
+    uint32_t *keys = static_cast<uint32_t *>(scratch(4 * (size_t)P));
+    uint32_t *keys_s = static_cast<uint32_t *>(scratch(4 * (size_t)P));
+    uint32_t *ids = static_cast<uint32_t *>(scratch(4 * (size_t)P));
+    uint32_t *ids_s = static_cast<uint32_t *>(scratch(4 * (size_t)P));
+    float4 *cand = static_cast<float4 *>(scratch(16 * (size_t)P));
+    int32_t *cstart = static_cast<int32_t *>(scratch(4 * ((size_t)ncells + 1)));
+    int64_t *counts = static_cast<int64_t *>(scratch(8 * (size_t)P));
+    if (!keys || !keys_s || !ids || !ids_s || !cand || !cstart || !counts)
+        return fail(DGS_ERR_ALLOC, "aggregate: scratch allocation failed");
+    size_t tsort = 0, tscan = 0;
+    int bits = 1;
+    while (bits < 32 && (1u << bits) <= (uint32_t)ncells) ++bits;
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, keys, keys_s, ids, ids_s, P, 0, bits, s));
+    DGS_TRY_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tscan, counts, ranges, P, s));
+    size_t tb = std::max(tsort, tscan);
+    void *tmp = scratch(tb);
+    if (!tmp) return fail(DGS_ERR_ALLOC, "aggregate: scratch allocation failed");
+
+    k_agg_keys<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, g, means, radii, keys, ids);
+    DGS_LAUNCH_CHECK(s, debug);
+    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_s, ids, ids_s, P, 0, bits, s));
+    k_agg_pack<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, D, ids_s, means, radii, cand);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_agg_cell_start<<<agg_elem_blocks((int64_t)ncells + 1), kBlock, 0, s>>>(ncells, P, keys_s, cstart);
+    DGS_LAUNCH_CHECK(s, debug);
+    const unsigned wblocks = agg_row_blocks(P);
+    k_agg_count<<<wblocks, kBlock, 0, s>>>(P, g, means, radii, cand, cstart, counts);
+    DGS_LAUNCH_CHECK(s, debug);
+    tb = std::max(tsort, tscan);
+    DGS_TRY_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tb, counts, ranges, P, s));
+    int64_t len = 0;
+    DGS_TRY_HIP(hipMemcpyAsync(&len, ranges + (P - 1), sizeof(len), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    *length = len;
+    int64_t *indices =
+        static_cast<int64_t *>(alloc(alloc_ctx, DGS_BUF_AGG_INDICES, std::max<size_t>(8 * (size_t)len, 16)));
+    float *dists = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_AGG_DISTS, std::max<size_t>(4 * (size_t)len * D, 16)));
+    float *dens = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_AGG_DENSITIES, std::max<size_t>(4 * (size_t)len, 16)));
+    if (!indices || !dists || !dens) return fail(DGS_ERR_ALLOC, "aggregate: output allocation failed");
+    k_agg_fill<<<wblocks, kBlock, 0, s>>>(P, g, means, conics, radii, cand, cstart, ranges, indices, dists, dens,
+                                          inv_total);
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+static int agg_check(int P, int D, int L, int K, int E) {
+    if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "aggregate: only D = 1 or D = 2 is supported");
+    if (P < 0 || L < 0 || K < 0) return fail(DGS_ERR_ARG, "aggregate: negative size");
+    if (E < 1) return fail(DGS_ERR_ARG, "aggregate: distance_transform needs at least 2 entries");
+    if (L > 256) return fail(DGS_ERR_ARG, "aggregate: at most 256 features are supported");
+    return DGS_OK;
+}
+
+static int agg_nb(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : 64); }
+
+extern "C" size_t dgs_agg_workspace_size(int P, int L) { return 4 * (size_t)std::max(P, 0) * std::max(L, 0) + 256; }
+
+extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                               const float *queries, const float *keys, const float *frequencies,
+                               const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                               const float *dists, const float *densities, const float *inv_total, float *weights,
+                               float *embeddings, float *factors, float *out, dgs_stream_t stream, int debug) {
+    int rc = agg_check(P, D, L, K, E);
+    if (rc) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0) return DGS_OK;
+    AggArgs A{};
+    A.P = P, A.D = D, A.L = L, A.K = K, A.E = E;
+    A.features = features, A.transform = transform, A.queries = queries, A.keys = keys;
+    A.freq = frequencies, A.dt = distance_transform, A.indices = indices, A.ranges = ranges;
+    A.dists = dists, A.densities = densities, A.inv_total = inv_total;
+    A.weights = weights, A.embeddings = embeddings, A.factors = factors, A.out = out;
+    const unsigned nb = agg_row_blocks(P);
+    switch (agg_nb(std::min(std::max(L, 1), 64))) {
+    case 16: k_agg_forward<16><<<nb, kBlock, 0, s>>>(A); break;
+    case 32: k_agg_forward<32><<<nb, kBlock, 0, s>>>(A); break;
+    default: k_agg_forward<64><<<nb, kBlock, 0, s>>>(A); break;
+    }
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                                const float *queries, const float *keys, const float *frequencies,
+                                const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                                const float *dists, const float *densities, const float *weights,
+                                const float *embeddings, const float *factors, const float *inv_total,
+                                const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                                float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
+                                void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
+    int rc = agg_check(P, D, L, K, E);
+    if (rc) return rc;
+    if (workspace_bytes < dgs_agg_workspace_size(P, L) || (!workspace && P > 0))
+        return fail(DGS_ERR_ARG, "dgs_agg_backward: workspace smaller than dgs_agg_workspace_size");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int F = (E - 1) / D / 2;
+    const int NV = 2 * E + F;
+    const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * ((size_t)NV * kWave + 256);
+    if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
+    auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
+    DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
+    DGS_TRY_HIP(zero(dL_dtransform, (size_t)L * L));
+    DGS_TRY_HIP(zero(dL_dqueries, (size_t)P * K));
+    DGS_TRY_HIP(zero(dL_dkeys, (size_t)P * K));
+    DGS_TRY_HIP(zero(dL_dfrequencies, (size_t)F));
+    DGS_TRY_HIP(zero(dL_ddistance_transform, 2 * (size_t)E));
+    if (P == 0) return DGS_OK;
+    AggArgs A{};
+    A.P = P, A.D = D, A.L = L, A.K = K, A.E = E;
+    A.features = features, A.transform = transform, A.queries = queries, A.keys = keys;
+    A.freq = frequencies, A.dt = distance_transform, A.indices = indices, A.ranges = ranges;
+    A.dists = dists, A.densities = densities, A.inv_total = inv_total;
+    A.weights = const_cast<float *>(weights), A.embeddings = const_cast<float *>(embeddings);
+    A.factors = const_cast<float *>(factors);
+    A.dL = dL_dout, A.arows = static_cast<float *>(workspace);
+    A.dfeat = dL_dfeatures, A.dq = dL_dqueries, A.dkeys = dL_dkeys, A.dfreq = dL_dfrequencies;
+    A.ddt = dL_ddistance_transform;
+    // few enough waves that each flushes its shared-array partials after many rows
+    const unsigned nb = std::min(agg_row_blocks(P), 2048u);
+    switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {
+    case 16: k_agg_backward<16><<<nb, kBlock, lds, s>>>(A); break;
+    case 32: k_agg_backward<32><<<nb, kBlock, lds, s>>>(A); break;
+    default: k_agg_backward<64><<<nb, kBlock, lds, s>>>(A); break;
+    }
+    DGS_LAUNCH_CHECK(s, debug);
+    if (L > 0) {
+        const unsigned tb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, ((int64_t)P + 255) / 256));
+        k_agg_dtrans<<<tb, kBlock, 0, s>>>(P, L, A.arows, dL_dout, dL_dtransform);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
+    return DGS_OK;
+}

@@ -43,7 +43,7 @@ Tensor u8(const Tensor &t, const char *name) {
 
 struct AllocCtx {
     torch::Device device;
-    Tensor bufs[4];
+    Tensor bufs[8];
     std::vector<Tensor> scratch;
 };
 
@@ -52,7 +52,7 @@ void *alloc_cb(void *vctx, int which, size_t bytes) {
     try {
         Tensor t = torch::empty({(int64_t)bytes}, torch::TensorOptions().dtype(torch::kUInt8).device(ctx->device));
         void *p = t.data_ptr();
-        if (which >= 0 && which < 4) ctx->bufs[which] = t;
+        if (which >= 0 && which < 8 && which != DGS_BUF_SCRATCH) ctx->bufs[which] = t;
         else ctx->scratch.push_back(t);
         return p;
     } catch (...) {
@@ -245,6 +245,123 @@ std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_
     return std::make_tuple(grid, off);
 }
 
+// ---- neighbour aggregation (aggregate_neighbors.h:11-47) --------------------------------
+
+Tensor i64(const Tensor &t, const char *name) {
+    TORCH_CHECK(t.scalar_type() == torch::kInt64, name, " must be an int64 tensor (got ", t.scalar_type(), ")");
+    TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
+    return t.contiguous();
+}
+
+// AggregateNeighborsPreprocessCUDA (aggregate_neighbors.cu:323-367)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessCUDA(
+    const Tensor &means_in, const Tensor &conics_in, const Tensor &radii_in, const bool debug) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const Tensor radii = f32(radii_in, "radii");
+    const int P = (int)means.size(0), D = (int)means.size(-1);
+    const auto lopt = means.options().dtype(torch::kInt64);
+    Tensor ranges = torch::zeros({P}, lopt);
+    Tensor inv_total = torch::zeros({P}, means.options());
+    AllocCtx ctx{means.device()};
+    int64_t length = 0;
+    if (P != 0) {
+        TORCH_CHECK(D == 1 || D == 2, "only D = 1 or D = 2 is supported");
+        TORCH_CHECK(radii.numel() == P && conics.size(0) == P, "means, conics and radii must have P rows");
+        check(dgs_agg_preprocess(P, D, means.data_ptr<float>(), conics.data_ptr<float>(), radii.data_ptr<float>(),
+                                 ranges.data_ptr<int64_t>(), inv_total.data_ptr<float>(), alloc_cb, &ctx, &length,
+                                 as_dgs(cur_stream()), debug ? 1 : 0),
+              "preprocess_aggregate");
+    }
+    auto view = [&](int which, torch::ScalarType st, std::vector<int64_t> shape) {
+        if (length == 0) return torch::empty(shape, means.options().dtype(st));
+        return ctx.bufs[which].view(st).narrow(0, 0, length * (shape.size() > 1 ? shape[1] : 1)).view(shape);
+    };
+    return std::make_tuple(view(DGS_BUF_AGG_INDICES, torch::kInt64, {length}), ranges,
+                           view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
+                           view(DGS_BUF_AGG_DENSITIES, torch::kFloat32, {length}), inv_total);
+}
+
+struct AggIn {
+    Tensor features, transform, queries, keys, freq, dt, indices, ranges, dists, densities, inv_total;
+    int P, D, L, K, E;
+};
+
+AggIn agg_inputs(const Tensor &features, const Tensor &transform, const Tensor &queries, const Tensor &keys,
+                 const Tensor &frequencies, const Tensor &distance_transform, const Tensor &indices,
+                 const Tensor &ranges, const Tensor &dists, const Tensor &densities, const Tensor &inv_total) {
+    AggIn a;
+    a.features = f32(features, "features"), a.transform = f32(transform, "transform");
+    a.queries = f32(queries, "queries"), a.keys = f32(keys, "keys");
+    a.freq = f32(frequencies, "frequencies"), a.dt = f32(distance_transform, "distance_transform");
+    a.indices = i64(indices, "indices"), a.ranges = i64(ranges, "ranges");
+    a.dists = f32(dists, "dists"), a.densities = f32(densities, "densities");
+    a.inv_total = f32(inv_total, "inv_total_densities");
+    // aggregate_neighbors.cu:383-387
+    a.P = (int)a.features.size(0), a.D = (int)a.dists.size(-1), a.L = (int)a.features.size(-1);
+    a.K = (int)a.queries.size(-1), a.E = (int)(a.dt.size(-1) / 2);
+    TORCH_CHECK(a.ranges.numel() == a.P && a.inv_total.numel() == a.P, "ranges / inv_total must have P entries");
+    TORCH_CHECK(a.transform.numel() == (int64_t)a.L * a.L, "transform must be L x L");
+    TORCH_CHECK(a.keys.numel() == (int64_t)a.P * a.K && a.queries.numel() == (int64_t)a.P * a.K,
+                "queries / keys must be P x K");
+    const int F = a.E >= 1 ? (a.E - 1) / a.D / 2 : 0;
+    TORCH_CHECK(a.freq.numel() >= F, "frequencies must hold (E-1)/D/2 entries");
+    TORCH_CHECK(a.indices.numel() == a.densities.numel() && a.dists.numel() == a.indices.numel() * a.D,
+                "indices / dists / densities must come from preprocess_aggregate");
+    return a;
+}
+
+// AggregateNeighborsCUDA (aggregate_neighbors.cu:369-415)
+std::tuple<Tensor, Tensor, Tensor, Tensor> AggregateNeighborsCUDA(
+    const Tensor &features, const Tensor &transform, const Tensor &queries, const Tensor &keys,
+    const Tensor &frequencies, const Tensor &distance_transform, const Tensor &indices, const Tensor &ranges,
+    const Tensor &dists, const Tensor &densities, const Tensor &inv_total_densities, const bool debug) {
+    const AggIn a = agg_inputs(features, transform, queries, keys, frequencies, distance_transform, indices,
+                               ranges, dists, densities, inv_total_densities);
+    Tensor weights = torch::zeros(a.densities.sizes(), a.features.options());
+    Tensor embeddings = torch::zeros(a.densities.sizes(), a.features.options());
+    Tensor factors = torch::zeros(a.densities.sizes(), a.features.options());
+    Tensor out = torch::zeros({a.P, a.L}, a.features.options());
+    check(dgs_agg_forward(a.P, a.D, a.L, a.K, a.E, a.features.data_ptr<float>(), a.transform.data_ptr<float>(),
+                          a.queries.data_ptr<float>(), a.keys.data_ptr<float>(), a.freq.data_ptr<float>(),
+                          a.dt.data_ptr<float>(), a.indices.data_ptr<int64_t>(), a.ranges.data_ptr<int64_t>(),
+                          a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), a.inv_total.data_ptr<float>(),
+                          weights.data_ptr<float>(), embeddings.data_ptr<float>(), factors.data_ptr<float>(),
+                          out.data_ptr<float>(), as_dgs(cur_stream()), debug ? 1 : 0),
+          "aggregate_neighbors");
+    return std::make_tuple(weights, embeddings, factors, out);
+}
+
+// AggregateNeighborsBackwardCUDA (aggregate_neighbors.cu:417-475)
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBackwardCUDA(
+    const Tensor &features, const Tensor &transform, const Tensor &queries, const Tensor &keys,
+    const Tensor &frequencies, const Tensor &distance_transform, const Tensor &indices, const Tensor &ranges,
+    const Tensor &dists, const Tensor &densities, const Tensor &weights_in, const Tensor &embeddings_in,
+    const Tensor &factors_in, const Tensor &inv_total_densities, const Tensor &dL_in, const bool debug) {
+    const AggIn a = agg_inputs(features, transform, queries, keys, frequencies, distance_transform, indices,
+                               ranges, dists, densities, inv_total_densities);
+    const Tensor weights = f32(weights_in, "weights"), embeddings = f32(embeddings_in, "embeddings");
+    const Tensor factors = f32(factors_in, "factors"), dL = f32(dL_in, "dL_dneighbor_features");
+    TORCH_CHECK(dL.numel() == (int64_t)a.P * a.L, "dL_dneighbor_features must be P x L");
+    Tensor dfeat = torch::zeros(a.features.sizes(), a.features.options());
+    Tensor dtrans = torch::zeros(a.transform.sizes(), a.features.options());
+    Tensor dq = torch::zeros(a.queries.sizes(), a.features.options());
+    Tensor dkeys = torch::zeros(a.keys.sizes(), a.features.options());
+    Tensor dfreq = torch::zeros(a.freq.sizes(), a.features.options());
+    Tensor ddt = torch::zeros(a.dt.sizes(), a.features.options());
+    const size_t ws = dgs_agg_workspace_size(a.P, a.L);
+    Tensor work = torch::empty({(int64_t)ws}, a.features.options().dtype(torch::kUInt8));
+    check(dgs_agg_backward(a.P, a.D, a.L, a.K, a.E, a.features.data_ptr<float>(), a.transform.data_ptr<float>(),
+                           a.queries.data_ptr<float>(), a.keys.data_ptr<float>(), a.freq.data_ptr<float>(),
+                           a.dt.data_ptr<float>(), a.indices.data_ptr<int64_t>(), a.ranges.data_ptr<int64_t>(),
+                           a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), weights.data_ptr<float>(),
+                           embeddings.data_ptr<float>(), factors.data_ptr<float>(), a.inv_total.data_ptr<float>(),
+                           dL.data_ptr<float>(), dfeat.data_ptr<float>(), dtrans.data_ptr<float>(),
+                           dq.data_ptr<float>(), dkeys.data_ptr<float>(), dfreq.data_ptr<float>(),
+                           ddt.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),
+          "aggregate_neighbors_backward");
+    return std::make_tuple(dfeat, dtrans, dq, dkeys, dfreq, ddt);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -259,6 +376,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sample_gaussians_laplacian_backward", &SampleGaussiansLaplacianBackwardCUDA);
     m.def("sample_gaussians_third_derivative", &SampleGaussiansThirdCUDA);
     m.def("sample_gaussians_third_derivative_backward", &SampleGaussiansThirdBackwardCUDA);
+    m.def("aggregate_neighbors", &AggregateNeighborsCUDA);
+    m.def("aggregate_neighbors_backward", &AggregateNeighborsBackwardCUDA);
+    m.def("preprocess_aggregate", &AggregateNeighborsPreprocessCUDA);
     // extensions (not on the reference surface)
     m.def("preprocess_gaussians_bounded", &PreprocessBoundedCUDA);
     m.def("count_pairs", &CountPairs);

@@ -45,7 +45,10 @@ enum dgs_buffer {
     DGS_BUF_SAMPLE_BINNING = 1, /* opaque sample-side binning state (returned to Python)   */
     DGS_BUF_RANGES = 2,         /* uint2[T] + 8 B, reference layout (sample_points.cu:76)  */
     DGS_BUF_SAMPLE_RANGES = 3,  /* uint2[T] + 8 B, reference layout (sample_points.cu:77)  */
-    DGS_BUF_SCRATCH = 4         /* temporary, released by the caller after the call        */
+    DGS_BUF_SCRATCH = 4,        /* temporary, released by the caller after the call        */
+    DGS_BUF_AGG_INDICES = 5,    /* int64[length] neighbour ids (dgs_agg_preprocess)        */
+    DGS_BUF_AGG_DISTS = 6,      /* float[length][D] scaled displacements                   */
+    DGS_BUF_AGG_DENSITIES = 7   /* float[length] densities                                 */
 };
 
 /* Returns device memory of at least `bytes` bytes (16-byte aligned), or NULL on failure.
@@ -107,6 +110,48 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
                     const void *sample_binning, size_t sample_binning_bytes, float thr,
                     int64_t *counts, void *workspace, size_t workspace_bytes,
                     dgs_stream_t stream);
+
+/* ---- neighbour aggregation (aggregate_neighbors.{h,cu}) ------------------------------- */
+
+/* Neighbour lists: replaces AggregateNeighborsPreprocessCUDA (aggregate_neighbors.cu:323-367)
+ * with its kernels findCollisions (18-55) and preprocess (57-127), without the P x P matrix.
+ *   means[P][D], conics[P][S], radii[P]   (D in {1,2})
+ *   ranges[P]: out, int64 inclusive cumsum of the per-row neighbour counts
+ *   inv_total[P]: out, 1 / (sum of the row's densities + 1e-6)
+ *   length: out (host), ranges[P-1] (0 when P == 0)
+ * indices (int64, -1 where the exponent is positive), dists [length][D] and densities [length]
+ * are requested through `alloc` (DGS_BUF_AGG_*), slots in ascending neighbour id per row;
+ * every slot is written.  Synchronises `stream` twice (grid bounds, list length). */
+int dgs_agg_preprocess(int P, int D, const float *means, const float *conics, const float *radii,
+                       int64_t *ranges, float *inv_total, dgs_alloc_fn alloc, void *alloc_ctx,
+                       int64_t *length, dgs_stream_t stream, int debug);
+
+/* Forward: replaces AggregateNeighborsCUDA (aggregate_neighbors.cu:369-415) and its kernel
+ * aggregateNeighbors (129-208).  E = len(distance_transform) / 2, F = (E-1)/D/2 frequencies.
+ *   features[P][L] (L <= 256), transform[L][L], queries/keys[P][K]
+ *   weights/embeddings/factors[length]: out (0 at index -1); out[P][L]: out (overwritten) */
+int dgs_agg_forward(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                    const float *queries, const float *keys, const float *frequencies,
+                    const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                    const float *dists, const float *densities, const float *inv_total,
+                    float *weights, float *embeddings, float *factors, float *out,
+                    dgs_stream_t stream, int debug);
+
+/* Workspace bytes needed by dgs_agg_backward. */
+size_t dgs_agg_workspace_size(int P, int L);
+
+/* Backward: replaces AggregateNeighborsBackwardCUDA (aggregate_neighbors.cu:417-475) and its
+ * kernel aggregateNeighborsBackward (210-321).  Writes (overwrites) the six gradients, shaped as
+ * features, transform, queries, keys, frequencies[F], distance_transform[2E]. */
+int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features,
+                     const float *transform, const float *queries, const float *keys,
+                     const float *frequencies, const float *distance_transform,
+                     const int64_t *indices, const int64_t *ranges, const float *dists,
+                     const float *densities, const float *weights, const float *embeddings,
+                     const float *factors, const float *inv_total, const float *dL_dout,
+                     float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                     float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
+                     void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug);
 
 /* Benchmark support: bracket every forward (which = 0) / backward (which = 1) render-kernel
  * launch with HIP events on its stream.  dgs_timing_read waits for the recorded events, adds

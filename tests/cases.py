@@ -107,3 +107,28 @@ def seam_case(D=2, P=400, n=4000, C=1, seed=131):
         conics = torch.stack([covs[:, 2] / det, -covs[:, 1] / det, covs[:, 0] / det], 1).float()
     values = torch.randn(P, C, generator=g).float()
     return means, values, covs, conics, syn.samples(n, D, seed=seed + 1)
+
+
+def agg_problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0, radius=(0.3, 1.2), centre=0.0):
+    """aggregate_neighbors inputs (aggregate_neighbors.cu:323-475): means, conics, radii and the
+    feature tensors.  Gaussians 0-2 have radius 0 (absent from every list); Gaussian 5 has a
+    non-PD conic when D == 2 (power > 0 slots, index -1).  E = 2 D F + 1."""
+    r = np.random.default_rng(seed)
+    means = (centre + r.uniform(-1, 1, (P, D)) * spread).astype(np.float32)
+    radii = r.uniform(radius[0], radius[1], P).astype(np.float32)
+    radii[:min(3, P)] = 0.0
+    if D == 2:
+        sx, sy = r.uniform(0.05, 0.2, P), r.uniform(0.05, 0.2, P)
+        conics = np.stack([1 / sx ** 2, r.uniform(-0.3, 0.3, P) / (sx * sy), 1 / sy ** 2], 1)
+        if P > 5:
+            conics[5] = [-3.0, 0.0, 4.0]
+    else:
+        conics = 1 / r.uniform(0.05, 0.2, (P, 1)) ** 2
+    E = 2 * D * F + 1
+    feats = dict(features=r.normal(size=(P, L)), transform=r.normal(size=(L, L)) / max(L, 1),
+                 queries=r.normal(size=(P, K)), keys=r.normal(size=(P, K)),
+                 frequencies=r.uniform(0.5, 3.0, F), distance_transform=r.normal(size=2 * E))
+    return means, conics.astype(np.float32), radii, {k: v.astype(np.float32) for k, v in feats.items()}
+
+
+AGG_FEATURES = ("features", "transform", "queries", "keys", "frequencies", "distance_transform")

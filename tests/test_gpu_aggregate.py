@@ -1,0 +1,138 @@
+"""GPU parity of neighbour aggregation: preprocess_aggregate / aggregate_neighbors /
+aggregate_neighbors_backward through diff_gaussian_sampling._C (libdgs.so, dgs_aggregate.hip)
+against the CPU oracle (oracle/oracle_agg.c, the restatement of aggregate_neighbors.cu).
+
+Bit-exact: ranges, indices (slot order = ascending neighbour id, -1 where power > 0) and dists
+(the wrapped, scaled displacement is a fixed sequence of float operations).
+Tolerances (|gpu - ref| <= RTOL |ref| + ATOL max|ref|):
+    densities    RTOL 1e-6             (GPU expf vs libm expf, <= 1 ulp apart)
+    inv_total    RTOL 1e-5             (the density total is summed 64 slots at a time)
+    weights, embeddings, factors  RTOL 1e-5, ATOL 1e-6 (FMA contraction on the GPU)
+    neighbor_features             RTOL 1e-4, ATOL 1e-5 (out = T^T sum_slots, not sum_slots T^T)
+    gradients                     RTOL 1e-4, ATOL 2e-5 (reference order is atomic)
+"""
+import numpy as np
+import pytest
+import torch
+
+import cases
+from cases import AGG_FEATURES, agg_problem
+from helpers import close
+
+pytestmark = pytest.mark.gpu
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).cuda()
+
+
+def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True):
+    idx_r, rg_r, X_r, dn_r, inv_r = oracle.agg_preprocess(means, conics, radii)
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    torch.cuda.synchronize()
+    assert idx.dtype == torch.int64 and rg.dtype == torch.int64
+    assert np.array_equal(rg.cpu().numpy(), rg_r), "ranges"
+    assert np.array_equal(idx.cpu().numpy(), idx_r), "indices"
+    assert np.array_equal(X.cpu().numpy().reshape(X_r.shape), X_r), "dists"
+    close(dn.cpu().numpy(), dn_r, 1e-6, 0.0, "densities")
+    close(inv.cpu().numpy(), inv_r, 1e-5, 0.0, "inv_total")
+    args = [fe[k] for k in AGG_FEATURES]
+    w_r, e_r, f_r, out_r = oracle.agg_forward(*args, idx_r, rg_r, X_r, dn_r, inv_r)
+    targs = [_cuda(a) for a in args]
+    w, e, f, out = dgs._C.aggregate_neighbors(*targs, idx, rg, X, dn, inv, False)
+    close(w.cpu().numpy(), w_r, 1e-5, 1e-6, "weights")
+    close(e.cpu().numpy(), e_r, 1e-5, 1e-6, "embeddings")
+    close(f.cpu().numpy(), f_r, 1e-5, 1e-6, "factors")
+    close(out.cpu().numpy(), out_r, 1e-4, 1e-5, "neighbor_features")
+    if not check_grads:
+        return
+    g = np.random.default_rng(seed).normal(size=out_r.shape).astype(np.float32)
+    ref = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
+    got = dgs._C.aggregate_neighbors_backward(*targs, idx, rg, X, dn, w, e, f, inv, _cuda(g), False)
+    for name, a, b in zip(AGG_FEATURES, got, ref):
+        close(a.cpu().numpy().reshape(b.shape), b, 1e-4, 2e-5, f"d/d{name}")
+
+
+@pytest.mark.parametrize("D", [1, 2])
+def test_aggregate_config5_shape(dgs, oracle, D):
+    """K = L = 16, F = 4 (SURVEY config 5), at a size the oracle finishes in a second."""
+    means, conics, radii, fe = agg_problem(P=1500, D=D, L=16, K=16, F=4, seed=20 + D)
+    _run(dgs, oracle, means, conics, radii, fe)
+
+
+@pytest.mark.parametrize("D", [1, 2])
+def test_aggregate_wrapped_images(dgs, oracle, D):
+    """Means far outside [-1, 1]: positive displacements wrap onto images at +2k (k >= 1) and
+    fmod(|dx|, 2) takes its general branch."""
+    means, conics, radii, fe = agg_problem(P=1200, D=D, L=8, K=4, F=2, seed=30 + D, spread=3.1,
+                                           radius=(0.5, 3.0))
+    _run(dgs, oracle, means, conics, radii, fe)
+
+
+def test_aggregate_row_overflow_windows(dgs, oracle):
+    """Every row has ~5000 neighbours (> the 4096 ids a wave sorts at once): rows are emitted in
+    id windows; slot order must still be ascending j."""
+    means, conics, radii, fe = agg_problem(P=5000, D=2, L=4, K=2, F=1, seed=40, spread=0.04,
+                                           radius=(1.0, 1.5))
+    _run(dgs, oracle, means, conics, radii, fe, check_grads=False)
+
+
+def test_aggregate_odd_sizes(dgs, oracle):
+    """L = 70 (> 64: several feature passes), K = 3, no frequencies (E = 1), D = 1."""
+    means, conics, radii, fe = agg_problem(P=400, D=1, L=70, K=3, F=0, seed=50)
+    _run(dgs, oracle, means, conics, radii, fe)
+
+
+def test_aggregate_large_k(dgs, oracle):
+    """K = 80 > L = 12: query/key passes beyond the feature passes."""
+    means, conics, radii, fe = agg_problem(P=600, D=2, L=12, K=80, F=3, seed=60)
+    _run(dgs, oracle, means, conics, radii, fe)
+
+
+def test_aggregate_known_answers(dgs, oracle):
+    """The asymmetric torus predicate and the skips (tests/test_oracle_agg.py known answers)."""
+    means = np.array([[-0.99, 0.0], [0.99, 0.0], [0.0, 0.5], [0.0, 0.52]], np.float32)
+    radii = np.array([0.5, 0.5, 0.0, 0.5], np.float32)
+    conics = np.tile(np.array([100.0, 0.0, 100.0], np.float32), (4, 1))
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    rg = rg.cpu().numpy()
+    idx = idx.cpu().numpy()
+    rows = [idx[(0 if i == 0 else rg[i - 1]):rg[i]].tolist() for i in range(4)]
+    assert rows == [[0, 1], [1], [], [3]]
+    assert inv.cpu().numpy()[2] == np.float32(1.0 / 1e-6)
+
+
+def test_aggregate_empty(dgs):
+    z = torch.zeros(0, 2, device="cuda")
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(z, torch.zeros(0, 3, device="cuda"),
+                                                      torch.zeros(0, device="cuda"), False)
+    assert idx.numel() == 0 and rg.numel() == 0 and X.shape == (0, 2) and inv.numel() == 0
+
+
+def test_aggregate_all_radius_zero(dgs, oracle):
+    means, conics, radii, fe = agg_problem(P=64, D=2, L=4, K=4, F=1, seed=70)
+    radii[:] = 0
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    assert idx.numel() == 0 and int(rg.max()) == 0
+    assert np.all(inv.cpu().numpy() == np.float32(1.0 / 1e-6))
+    out = dgs._C.aggregate_neighbors(*[_cuda(fe[k]) for k in AGG_FEATURES], idx, rg, X, dn, inv, False)[3]
+    assert float(out.abs().max()) == 0.0
+
+
+def test_aggregate_autograd_through_sampler(dgs, oracle):
+    """GaussianSampler.preprocess_aggregate + aggregate_neighbors + backward (py:291-317)."""
+    means, conics, radii, fe = agg_problem(P=700, D=2, L=16, K=16, F=4, seed=80)
+    s = dgs.GaussianSampler(False)
+    s.means, s.conics, s.radii = _cuda(means), _cuda(conics), _cuda(radii)
+    s.preprocess_aggregate()
+    t = [_cuda(fe[k]).requires_grad_(True) for k in AGG_FEATURES]
+    out = s.aggregate_neighbors(*t)
+    g = np.random.default_rng(3).normal(size=tuple(out.shape)).astype(np.float32)
+    out.backward(_cuda(g))
+    args = [fe[k] for k in AGG_FEATURES]
+    idx_r, rg_r, X_r, dn_r, inv_r = oracle.agg_preprocess(means, conics, radii)
+    w_r, e_r, f_r, out_r = oracle.agg_forward(*args, idx_r, rg_r, X_r, dn_r, inv_r)
+    close(out.detach().cpu().numpy(), out_r, 1e-4, 1e-5, "neighbor_features")
+    ref = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
+    for name, a, b in zip(AGG_FEATURES, t, ref):
+        close(a.grad.cpu().numpy().reshape(b.shape), b, 1e-4, 2e-5, f"d/d{name}")

@@ -13,25 +13,12 @@ import numpy as np
 import pytest
 import torch
 
+from cases import agg_problem
 from helpers import close
 
 
-def _problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0):
-    r = np.random.default_rng(seed)
-    means = (r.uniform(-1, 1, (P, D)) * spread).astype(np.float32)
-    radii = r.uniform(0.3, 1.2, P).astype(np.float32)
-    radii[:3] = 0.0  # radius-0 Gaussians (absent from every list)
-    if D == 2:
-        sx, sy = r.uniform(0.05, 0.2, P), r.uniform(0.05, 0.2, P)
-        conics = np.stack([1 / sx ** 2, r.uniform(-0.3, 0.3, P) / (sx * sy), 1 / sy ** 2], 1)
-        conics[5] = [-3.0, 0.0, 4.0]  # non-PD: power > 0 slots
-    else:
-        conics = (1 / r.uniform(0.05, 0.2, (P, 1)) ** 2)
-    E = 2 * D * F + 1
-    feats = dict(features=r.normal(size=(P, L)), transform=r.normal(size=(L, L)) / L,
-                 queries=r.normal(size=(P, K)), keys=r.normal(size=(P, K)),
-                 frequencies=r.uniform(0.5, 3.0, F), distance_transform=r.normal(size=2 * E))
-    return means, conics.astype(np.float32), radii, {k: v.astype(np.float32) for k, v in feats.items()}
+def _problem(**kw):
+    return agg_problem(**kw)
 
 
 def np_neighbours(means, radii):
