@@ -38,7 +38,7 @@
 
 namespace dgs {
 
-constexpr int kAggNMax = 4096;  // neighbour ids a wave sorts in LDS at once
+constexpr int kAggNMax = 2048;  // neighbour ids a wave sorts in LDS at once
 constexpr int kAggMaxCells = 1 << 24;
 
 struct AggGeom {
@@ -217,10 +217,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_count(int P, AggGeom g, const fl
                                                       const float *__restrict__ radii,
                                                       const float4 *__restrict__ cand,
                                                       const int32_t *__restrict__ cstart,
+                                                      const uint32_t *__restrict__ order,
                                                       int64_t *__restrict__ counts) {
     const int lane = threadIdx.x & (kWave - 1);
     const int stride = gridDim.x * kWavesPerBlock;
-    for (int i = wave_unit_index(); i < P; i += stride) {
+    for (int w = wave_unit_index(); w < P; w += stride) {
+        const int i = (int)order[w];  // rows in cell order: concurrent waves share neighbours in L2
         int64_t n = 0;
         const float ri = agg_r(radii[i]);
         if (agg_valid(ri)) {
@@ -278,8 +280,9 @@ __device__ __forceinline__ void wave_sync_lds() {
 __device__ inline void wave_bitonic(uint32_t *s, int n, int lane) {
     for (int k = 2; k <= n; k <<= 1)
         for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            const int lj = __builtin_ctz(jj);
             for (int t = lane; t < (n >> 1); t += kWave) {
-                const int i = 2 * jj * (t / jj) + (t % jj), l = i + jj;
+                const int i = ((t >> lj) << (lj + 1)) | (t & (jj - 1)), l = i + jj;
                 const uint32_t a = s[i], b = s[l];
                 const bool up = (i & k) == 0;
                 if ((a > b) == up) {
@@ -301,6 +304,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const flo
                                                      const float *__restrict__ radii,
                                                      const float4 *__restrict__ cand,
                                                      const int32_t *__restrict__ cstart,
+                                                     const uint32_t *__restrict__ order,
                                                      const int64_t *__restrict__ ranges,
                                                      int64_t *__restrict__ indices, float *__restrict__ dists,
                                                      float *__restrict__ densities,
@@ -310,7 +314,8 @@ __global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const flo
     uint32_t *s = buf[threadIdx.x >> 6];
     const int stride = gridDim.x * kWavesPerBlock;
     const int D = g.D, S = D * (D + 1) / 2;
-    for (int i = wave_unit_index(); i < P; i += stride) {
+    for (int w = wave_unit_index(); w < P; w += stride) {
+        const int i = (int)order[w];
         const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
         // aggregate_neighbors.cu:73-74 (0.333 and 1.0 / (r + 1e-6) in double)
         const float my_radius = (float)((double)radii[i] * 0.333);
@@ -370,7 +375,10 @@ struct AggArgs {
     const float *dL;                        // backward
     float *arows;                           // backward scratch: a of every row [P][L]
     float *dfeat, *dq, *dkeys, *dfreq, *ddt;
+    const int32_t *order;  // optional row order (spatial, from dgs_agg_preprocess); NULL = 0..P-1
 };
+
+__device__ __forceinline__ int agg_row(const AggArgs &A, int w) { return A.order ? A.order[w] : w; }
 
 // sin / cos of the reference's double argument frequencies * M_PI * X (aggregate_neighbors.cu
 // :181-182 evaluate sin/cos in double and round to float): quadrant reduction in double, then
@@ -431,7 +439,8 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward(AggArgs A) {
     float *ar = arow[threadIdx.x >> 6];
     const int stride = gridDim.x * kWavesPerBlock;
     const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2;
-    for (int i = wave_unit_index(); i < A.P; i += stride) {
+    for (int w = wave_unit_index(); w < A.P; w += stride) {
+        const int i = agg_row(A, w);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];
         const float *q = A.queries + (int64_t)i * K;
@@ -481,8 +490,11 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward(AggArgs A) {
     }
 }
 
-// Dynamic LDS per wave: NV x 64 per-lane partials of the shared arrays (ddt[2E], dfreq[F]),
-// then st[256].
+// Dynamic LDS per wave (kAggBwdLds): NV x 64 per-lane partials of the shared arrays (ddt[2E],
+// dfreq[F]), st[256], and the batch's (neighbour, dcw * fac, te) for the scatter.
+constexpr int kAggStash = 256 + 3 * kWave;
+__host__ __device__ constexpr int agg_bwd_lds_floats(int NV) { return NV * kWave + kAggStash; }
+
 template <int NB>
 __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
     extern __shared__ float lds[];
@@ -490,12 +502,20 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
     const int w = threadIdx.x >> 6;
     const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2, dstride = (E - 1) / D;
     const int NV = 2 * E + F;
-    float *part = lds + w * (NV * kWave + 256) + lane;  // value v of this lane: part[v * 64]
-    float *st = lds + w * (NV * kWave + 256) + NV * kWave;
+    float *base = lds + w * agg_bwd_lds_floats(NV);
+    float *part = base + lane;  // value v of this lane: part[v * 64]
+    float *st = base + NV * kWave;
+    int *sm = reinterpret_cast<int *>(st + 256);
+    float *sc = st + 256 + kWave, *ste = st + 256 + 2 * kWave;
     for (int v = 0; v < NV; ++v) part[v * kWave] = 0.0f;
     const int stride = gridDim.x * kWavesPerBlock;
     const int LK = max(L, K);
-    for (int i = wave_unit_index(); i < A.P; i += stride) {
+    // scatter layout: G = L + K lanes per neighbour row (dfeat row, then dkeys row), spp rows
+    // per atomic instruction, so one instruction covers whole rows instead of 64 scattered words
+    const int G = L + K, spp = G <= kWave ? kWave / max(G, 1) : 1;
+    const int sub = G <= kWave ? lane / max(G, 1) : 0;
+    for (int wr = wave_unit_index(); wr < A.P; wr += stride) {
+        const int i = agg_row(A, wr);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];
         const float *q = A.queries + (int64_t)i * K, *g = A.dL + (int64_t)i * L;
@@ -512,50 +532,69 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
             float acc_a[NB], acc_q[NB];
 #pragma unroll
             for (int t = 0; t < NB; ++t) acc_a[t] = acc_q[t] = 0.0f;
-            for (int64_t s = start + lane; s < end; s += kWave) {
-                const int64_t idx = A.indices[s];
-                if (idx < 0) continue;
-                const float *feat = A.features + idx * L, *key = A.keys + idx * K;
-                const float dc = A.densities[s] * inv;
-                const float dcw = dc * A.weights[s];
-                const float emb = A.embeddings[s], fac = A.factors[s];
-                float S2 = 0.0f;
-                for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
-                const float te = (dc * emb) * S1 + (dc * fac) * S2;  // sum_j te_j
-                const float dwe = dcw * emb, dwf = dcw * fac;
+            for (int64_t s0 = start; s0 < end; s0 += kWave) {
+                const int64_t s = s0 + lane;
+                const int64_t idx = s < end ? A.indices[s] : -1;
+                float c = 0.0f, te = 0.0f;
+                if (idx >= 0) {
+                    const float *feat = A.features + idx * L, *key = A.keys + idx * K;
+                    const float dc = A.densities[s] * inv;
+                    const float dcw = dc * A.weights[s];
+                    const float emb = A.embeddings[s], fac = A.factors[s];
+                    float S2 = 0.0f;
+                    for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
+                    te = (dc * emb) * S1 + (dc * fac) * S2;  // sum_j te_j
+                    c = dcw * fac;
+                    const float dwe = dcw * emb, dwf = dcw * fac;
 #pragma unroll
-                for (int t = 0; t < NB; ++t) {
-                    if (fb + t < L) {
-                        acc_a[t] += dwe + dwf * feat[fb + t];
-                        atomicAdd(&A.dfeat[idx * L + fb + t], dcw * st[fb + t] * fac);
+                    for (int t = 0; t < NB; ++t) {
+                        if (fb + t < L) acc_a[t] += dwe + dwf * feat[fb + t];
+                        if (fb + t < K) acc_q[t] += key[fb + t] * te;
                     }
-                    if (fb + t < K) {
-                        acc_q[t] += key[fb + t] * te;
-                        atomicAdd(&A.dkeys[idx * K + fb + t], q[fb + t] * te);
+                    if (fb == 0) {
+                        // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
+                        const float t1 = dcw * S1, t2 = dcw * S2;
+                        for (int d = 0; d < D; ++d) {
+                            const float Xd = A.dists[s * D + d];
+                            const double px = M_PI * (double)Xd;
+                            for (int e = 0; e < F; ++e) {
+                                float sn, cs;
+                                ref_sincos(A.freq[e], Xd, &sn, &cs);
+                                const int a = d * dstride + e * 2;
+                                part[a * kWave] += t1 * sn;
+                                part[(a + 1) * kWave] += t1 * cs;
+                                part[(E + a) * kWave] += t2 * sn;
+                                part[(E + a + 1) * kWave] += t2 * cs;
+                                const float f0 =
+                                    (float)((double)cs * px * ((double)A.dt[a] * t1 + (double)A.dt[E + a] * t2));
+                                const float f1 = (float)((double)-sn * px *
+                                                         ((double)A.dt[a + 1] * t1 + (double)A.dt[E + a + 1] * t2));
+                                part[(2 * E + e) * kWave] += f0 + f1;
+                            }
+                        }
+                        part[(E - 1) * kWave] += t1;
+                        part[(2 * E - 1) * kWave] += t2;
                     }
                 }
                 if (fb != 0) continue;
-                // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
-                const float t1 = dcw * S1, t2 = dcw * S2;
-                for (int d = 0; d < D; ++d) {
-                    const float Xd = A.dists[s * D + d];
-                    const double px = M_PI * (double)Xd;
-                    for (int e = 0; e < F; ++e) {
-                        float sn, cs;
-                        ref_sincos(A.freq[e], Xd, &sn, &cs);
-                        const int a = d * dstride + e * 2;
-                        part[a * kWave] += t1 * sn;
-                        part[(a + 1) * kWave] += t1 * cs;
-                        part[(E + a) * kWave] += t2 * sn;
-                        part[(E + a + 1) * kWave] += t2 * cs;
-                        const float f0 = (float)((double)cs * px * ((double)A.dt[a] * t1 + (double)A.dt[E + a] * t2));
-                        const float f1 =
-                            (float)((double)-sn * px * ((double)A.dt[a + 1] * t1 + (double)A.dt[E + a + 1] * t2));
-                        part[(2 * E + e) * kWave] += f0 + f1;
+                // neighbour gradients (aggregate_neighbors.cu:296-319):
+                //   dfeat[idx][j] += dcw fac st[j],  dkeys[idx][k] += q[k] te
+                sm[lane] = (int)idx;
+                sc[lane] = c;
+                ste[lane] = te;
+                wave_sync_lds();
+                const int nb = (int)min<int64_t>(kWave, end - s0);
+                for (int b = 0; b < nb; b += spp) {
+                    const int sl = b + sub;
+                    const int m = (sub < spp && sl < nb) ? sm[sl] : -1;
+                    if (m >= 0) {
+                        for (int t = G <= kWave ? lane - sub * G : lane; t < G; t += kWave) {
+                            if (t < L) atomicAdd(&A.dfeat[(int64_t)m * L + t], sc[sl] * st[t]);
+                            else atomicAdd(&A.dkeys[(int64_t)m * K + (t - L)], ste[sl] * q[t - L]);
+                        }
                     }
                 }
-                part[(E - 1) * kWave] += t1;
-                part[(2 * E - 1) * kWave] += t2;
+                wave_sync_lds();
             }
             const float ra = reduce_row<NB>(acc_a, lane);
             if (lane < NB && fb + lane < L) A.arows[(int64_t)i * L + fb + lane] = ra;
@@ -594,8 +633,8 @@ static unsigned agg_row_blocks(int P) {
 }
 
 extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float *conics, const float *radii,
-                                  int64_t *ranges, float *inv_total, dgs_alloc_fn alloc, void *alloc_ctx,
-                                  int64_t *length, dgs_stream_t stream, int debug) {
+                                  int64_t *ranges, float *inv_total, int32_t *row_order, dgs_alloc_fn alloc,
+                                  void *alloc_ctx, int64_t *length, dgs_stream_t stream, int debug) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "aggregate: only D = 1 or D = 2 is supported");
     if (P < 0 || !alloc || !length) return fail(DGS_ERR_ARG, "dgs_agg_preprocess: bad arguments");
     *length = 0;
@@ -660,7 +699,7 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     k_agg_cell_start<<<agg_elem_blocks((int64_t)ncells + 1), kBlock, 0, s>>>(ncells, P, keys_s, cstart);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned wblocks = agg_row_blocks(P);
-    k_agg_count<<<wblocks, kBlock, 0, s>>>(P, g, means, radii, cand, cstart, counts);
+    k_agg_count<<<wblocks, kBlock, 0, s>>>(P, g, means, radii, cand, cstart, ids_s, counts);
     DGS_LAUNCH_CHECK(s, debug);
     tb = std::max(tsort, tscan);
     DGS_TRY_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tb, counts, ranges, P, s));
@@ -673,9 +712,10 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     float *dists = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_AGG_DISTS, std::max<size_t>(4 * (size_t)len * D, 16)));
     float *dens = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_AGG_DENSITIES, std::max<size_t>(4 * (size_t)len, 16)));
     if (!indices || !dists || !dens) return fail(DGS_ERR_ALLOC, "aggregate: output allocation failed");
-    k_agg_fill<<<wblocks, kBlock, 0, s>>>(P, g, means, conics, radii, cand, cstart, ranges, indices, dists, dens,
-                                          inv_total);
+    k_agg_fill<<<wblocks, kBlock, 0, s>>>(P, g, means, conics, radii, cand, cstart, ids_s, ranges, indices, dists,
+                                          dens, inv_total);
     DGS_LAUNCH_CHECK(s, debug);
+    if (row_order) DGS_TRY_HIP(hipMemcpyAsync(row_order, ids_s, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
     return DGS_OK;
 }
 
@@ -694,8 +734,9 @@ extern "C" size_t dgs_agg_workspace_size(int P, int L) { return 4 * (size_t)std:
 extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *features, const float *transform,
                                const float *queries, const float *keys, const float *frequencies,
                                const float *distance_transform, const int64_t *indices, const int64_t *ranges,
-                               const float *dists, const float *densities, const float *inv_total, float *weights,
-                               float *embeddings, float *factors, float *out, dgs_stream_t stream, int debug) {
+                               const float *dists, const float *densities, const float *inv_total,
+                               const int32_t *row_order, float *weights, float *embeddings, float *factors, float *out,
+                               dgs_stream_t stream, int debug) {
     int rc = agg_check(P, D, L, K, E);
     if (rc) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
@@ -705,7 +746,7 @@ extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *f
     A.features = features, A.transform = transform, A.queries = queries, A.keys = keys;
     A.freq = frequencies, A.dt = distance_transform, A.indices = indices, A.ranges = ranges;
     A.dists = dists, A.densities = densities, A.inv_total = inv_total;
-    A.weights = weights, A.embeddings = embeddings, A.factors = factors, A.out = out;
+    A.weights = weights, A.embeddings = embeddings, A.factors = factors, A.out = out, A.order = row_order;
     const unsigned nb = agg_row_blocks(P);
     switch (agg_nb(std::min(std::max(L, 1), 64))) {
     case 16: k_agg_forward<16><<<nb, kBlock, 0, s>>>(A); break;
@@ -721,7 +762,7 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
                                 const float *distance_transform, const int64_t *indices, const int64_t *ranges,
                                 const float *dists, const float *densities, const float *weights,
                                 const float *embeddings, const float *factors, const float *inv_total,
-                                const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                                const int32_t *row_order, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
                                 float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
                                 void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
     int rc = agg_check(P, D, L, K, E);
@@ -731,7 +772,7 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int F = (E - 1) / D / 2;
     const int NV = 2 * E + F;
-    const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * ((size_t)NV * kWave + 256);
+    const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * agg_bwd_lds_floats(NV);
     if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
     auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
     DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
@@ -750,7 +791,7 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     A.factors = const_cast<float *>(factors);
     A.dL = dL_dout, A.arows = static_cast<float *>(workspace);
     A.dfeat = dL_dfeatures, A.dq = dL_dqueries, A.dkeys = dL_dkeys, A.dfreq = dL_dfrequencies;
-    A.ddt = dL_ddistance_transform;
+    A.ddt = dL_ddistance_transform, A.order = row_order;
     // few enough waves that each flushes its shared-array partials after many rows
     const unsigned nb = std::min(agg_row_blocks(P), 2048u);
     switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {

@@ -12,6 +12,7 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <mutex>
 #include <stdexcept>
 #include <tuple>
 #include <vector>
@@ -247,6 +248,37 @@ std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_
 
 // ---- neighbour aggregation (aggregate_neighbors.h:11-47) --------------------------------
 
+// Spatial row order of the last few preprocess_aggregate calls, keyed by the indices buffer
+// they returned.  Only a scheduling hint (any permutation of 0..P-1 gives identical results),
+// so a stale entry whose key was reused by another tensor of the same P costs speed at most.
+struct OrderEntry {
+    const void *indices;
+    int64_t P, length;
+    Tensor order;
+};
+std::mutex g_order_mu;
+std::vector<OrderEntry> g_orders;
+
+void order_put(const Tensor &indices, int64_t P, const Tensor &order) {
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    for (auto it = g_orders.begin(); it != g_orders.end(); ++it)
+        if (it->indices == indices.data_ptr()) {
+            g_orders.erase(it);
+            break;
+        }
+    g_orders.push_back({indices.data_ptr(), P, indices.numel(), order});
+    if (g_orders.size() > 4) g_orders.erase(g_orders.begin());
+}
+
+const int32_t *order_get(const Tensor &indices, int64_t P) {
+    std::lock_guard<std::mutex> lk(g_order_mu);
+    for (const auto &e : g_orders)
+        if (e.indices == indices.data_ptr() && e.P == P && e.length == indices.numel() &&
+            e.order.device() == indices.device())
+            return e.order.data_ptr<int32_t>();
+    return nullptr;
+}
+
 Tensor i64(const Tensor &t, const char *name) {
     TORCH_CHECK(t.scalar_type() == torch::kInt64, name, " must be an int64 tensor (got ", t.scalar_type(), ")");
     TORCH_CHECK(t.is_cuda(), name, " must be a GPU tensor");
@@ -264,11 +296,13 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessC
     Tensor inv_total = torch::zeros({P}, means.options());
     AllocCtx ctx{means.device()};
     int64_t length = 0;
+    Tensor order = torch::empty({P}, means.options().dtype(torch::kInt32));
     if (P != 0) {
         TORCH_CHECK(D == 1 || D == 2, "only D = 1 or D = 2 is supported");
         TORCH_CHECK(radii.numel() == P && conics.size(0) == P, "means, conics and radii must have P rows");
         check(dgs_agg_preprocess(P, D, means.data_ptr<float>(), conics.data_ptr<float>(), radii.data_ptr<float>(),
-                                 ranges.data_ptr<int64_t>(), inv_total.data_ptr<float>(), alloc_cb, &ctx, &length,
+                                 ranges.data_ptr<int64_t>(), inv_total.data_ptr<float>(), order.data_ptr<int32_t>(),
+                                 alloc_cb, &ctx, &length,
                                  as_dgs(cur_stream()), debug ? 1 : 0),
               "preprocess_aggregate");
     }
@@ -276,8 +310,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessC
         if (length == 0) return torch::empty(shape, means.options().dtype(st));
         return ctx.bufs[which].view(st).narrow(0, 0, length * (shape.size() > 1 ? shape[1] : 1)).view(shape);
     };
-    return std::make_tuple(view(DGS_BUF_AGG_INDICES, torch::kInt64, {length}), ranges,
-                           view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
+    Tensor indices = view(DGS_BUF_AGG_INDICES, torch::kInt64, {length});
+    if (length > 0) order_put(indices, P, order);
+    return std::make_tuple(indices, ranges, view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
                            view(DGS_BUF_AGG_DENSITIES, torch::kFloat32, {length}), inv_total);
 }
 
@@ -325,7 +360,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor> AggregateNeighborsCUDA(
                           a.queries.data_ptr<float>(), a.keys.data_ptr<float>(), a.freq.data_ptr<float>(),
                           a.dt.data_ptr<float>(), a.indices.data_ptr<int64_t>(), a.ranges.data_ptr<int64_t>(),
                           a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), a.inv_total.data_ptr<float>(),
-                          weights.data_ptr<float>(), embeddings.data_ptr<float>(), factors.data_ptr<float>(),
+                          order_get(a.indices, a.P), weights.data_ptr<float>(), embeddings.data_ptr<float>(), factors.data_ptr<float>(),
                           out.data_ptr<float>(), as_dgs(cur_stream()), debug ? 1 : 0),
           "aggregate_neighbors");
     return std::make_tuple(weights, embeddings, factors, out);
@@ -355,7 +390,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
                            a.dt.data_ptr<float>(), a.indices.data_ptr<int64_t>(), a.ranges.data_ptr<int64_t>(),
                            a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), weights.data_ptr<float>(),
                            embeddings.data_ptr<float>(), factors.data_ptr<float>(), a.inv_total.data_ptr<float>(),
-                           dL.data_ptr<float>(), dfeat.data_ptr<float>(), dtrans.data_ptr<float>(),
+                           order_get(a.indices, a.P), dL.data_ptr<float>(), dfeat.data_ptr<float>(), dtrans.data_ptr<float>(),
                            dq.data_ptr<float>(), dkeys.data_ptr<float>(), dfreq.data_ptr<float>(),
                            ddt.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),
           "aggregate_neighbors_backward");

@@ -118,24 +118,29 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
  *   means[P][D], conics[P][S], radii[P]   (D in {1,2})
  *   ranges[P]: out, int64 inclusive cumsum of the per-row neighbour counts
  *   inv_total[P]: out, 1 / (sum of the row's densities + 1e-6)
+ *   row_order[P]: optional out (NULL = not wanted), a permutation of the rows in spatial (grid
+ *     cell) order.  Passed to dgs_agg_forward / dgs_agg_backward it only changes the order in
+ *     which rows are scheduled -- concurrent rows then share their neighbours in L2 -- never a
+ *     result; any permutation of 0..P-1 is valid there.
  *   length: out (host), ranges[P-1] (0 when P == 0)
  * indices (int64, -1 where the exponent is positive), dists [length][D] and densities [length]
  * are requested through `alloc` (DGS_BUF_AGG_*), slots in ascending neighbour id per row;
  * every slot is written.  Synchronises `stream` twice (grid bounds, list length). */
 int dgs_agg_preprocess(int P, int D, const float *means, const float *conics, const float *radii,
-                       int64_t *ranges, float *inv_total, dgs_alloc_fn alloc, void *alloc_ctx,
-                       int64_t *length, dgs_stream_t stream, int debug);
+                       int64_t *ranges, float *inv_total, int32_t *row_order, dgs_alloc_fn alloc,
+                       void *alloc_ctx, int64_t *length, dgs_stream_t stream, int debug);
 
 /* Forward: replaces AggregateNeighborsCUDA (aggregate_neighbors.cu:369-415) and its kernel
  * aggregateNeighbors (129-208).  E = len(distance_transform) / 2, F = (E-1)/D/2 frequencies.
  *   features[P][L] (L <= 256), transform[L][L], queries/keys[P][K]
+ *   row_order[P]: optional (NULL = 0..P-1), see dgs_agg_preprocess
  *   weights/embeddings/factors[length]: out (0 at index -1); out[P][L]: out (overwritten) */
 int dgs_agg_forward(int P, int D, int L, int K, int E, const float *features, const float *transform,
                     const float *queries, const float *keys, const float *frequencies,
                     const float *distance_transform, const int64_t *indices, const int64_t *ranges,
                     const float *dists, const float *densities, const float *inv_total,
-                    float *weights, float *embeddings, float *factors, float *out,
-                    dgs_stream_t stream, int debug);
+                    const int32_t *row_order, float *weights, float *embeddings, float *factors,
+                    float *out, dgs_stream_t stream, int debug);
 
 /* Workspace bytes needed by dgs_agg_backward. */
 size_t dgs_agg_workspace_size(int P, int L);
@@ -148,7 +153,8 @@ int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features,
                      const float *frequencies, const float *distance_transform,
                      const int64_t *indices, const int64_t *ranges, const float *dists,
                      const float *densities, const float *weights, const float *embeddings,
-                     const float *factors, const float *inv_total, const float *dL_dout,
+                     const float *factors, const float *inv_total, const int32_t *row_order,
+                     const float *dL_dout,
                      float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
                      float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
                      void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug);

@@ -70,7 +70,7 @@ def test_aggregate_wrapped_images(dgs, oracle, D):
 
 
 def test_aggregate_row_overflow_windows(dgs, oracle):
-    """Every row has ~5000 neighbours (> the 4096 ids a wave sorts at once): rows are emitted in
+    """Every row has ~5000 neighbours (> the 2048 ids a wave sorts at once): rows are emitted in
     id windows; slot order must still be ascending j."""
     means, conics, radii, fe = agg_problem(P=5000, D=2, L=4, K=2, F=1, seed=40, spread=0.04,
                                            radius=(1.0, 1.5))
@@ -136,3 +136,21 @@ def test_aggregate_autograd_through_sampler(dgs, oracle):
     ref = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
     for name, a, b in zip(AGG_FEATURES, t, ref):
         close(a.grad.cpu().numpy().reshape(b.shape), b, 1e-4, 2e-5, f"d/d{name}")
+
+
+def test_aggregate_row_order_is_only_a_schedule(dgs, oracle):
+    """preprocess_aggregate caches a spatial row order keyed by its indices buffer; a clone of
+    indices misses the cache and runs rows in id order.  The forward must be bit-identical
+    either way (one wave per row), the backward equal up to atomic ordering."""
+    means, conics, radii, fe = agg_problem(P=900, D=2, L=16, K=16, F=4, seed=90)
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    t = [_cuda(fe[k]) for k in AGG_FEATURES]
+    a = dgs._C.aggregate_neighbors(*t, idx, rg, X, dn, inv, False)
+    b = dgs._C.aggregate_neighbors(*t, idx.clone(), rg, X, dn, inv, False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    g = _cuda(np.random.default_rng(1).normal(size=(900, 16)).astype(np.float32))
+    ga = dgs._C.aggregate_neighbors_backward(*t, idx, rg, X, dn, *a[:3], inv, g, False)
+    gb = dgs._C.aggregate_neighbors_backward(*t, idx.clone(), rg, X, dn, *b[:3], inv, g, False)
+    for name, x, y in zip(AGG_FEATURES, ga, gb):
+        close(x.cpu().numpy(), y.cpu().numpy(), 1e-5, 1e-6, name)
