@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "dgs_internal.h"
@@ -376,13 +377,16 @@ struct AggArgs {
     float *arows;                           // backward scratch: a of every row [P][L]
     float *dfeat, *dq, *dkeys, *dfreq, *ddt;
     const int32_t *order;  // optional row order (spatial, from dgs_agg_preprocess); NULL = 0..P-1
+    int expt;              // profiling experiments (DGS_AGG_EXPT): bit 0 skips the scatter, bit 1 the
+                           // distance-transform terms -- results are then wrong; 0 in production
 };
 
 __device__ __forceinline__ int agg_row(const AggArgs &A, int w) { return A.order ? A.order[w] : w; }
 
 // sin / cos of the reference's double argument frequencies * M_PI * X (aggregate_neighbors.cu
 // :181-182 evaluate sin/cos in double and round to float): quadrant reduction in double, then
-// float sin/cos of the reduced argument (|r| <= pi/4).
+// float minimax polynomials on |r| <= pi/4 (Cephes sinf/cosf coefficients; < 1 ulp there, so
+// within ~2 ulp of the correctly rounded double result).
 __device__ __forceinline__ void ref_sincos(float f, float X, float *s, float *c) {
     const double arg = (double)f * M_PI * (double)X;
     if (!(fabs(arg) < 1e6)) {
@@ -391,16 +395,16 @@ __device__ __forceinline__ void ref_sincos(float f, float X, float *s, float *c)
         return;
     }
     const double n = rint(arg * M_2_PI);
-    double r = fma(-n, 1.5707963267948966, arg);
-    r = fma(-n, 6.123233995736766e-17, r);
-    float sr, cr;
-    sincosf((float)r, &sr, &cr);
-    switch ((int)n & 3) {
-    case 0: *s = sr; *c = cr; break;
-    case 1: *s = cr; *c = -sr; break;
-    case 2: *s = -sr; *c = -cr; break;
-    default: *s = -cr; *c = sr; break;
-    }
+    double rd = fma(-n, 1.5707963267948966, arg);
+    rd = fma(-n, 6.123233995736766e-17, rd);
+    const float r = (float)rd, z = r * r;
+    const float sr = fmaf(fmaf(fmaf(-1.9515295891e-4f, z, 8.3321608736e-3f), z, -1.6666654611e-1f) * z, r, r);
+    const float cp = fmaf(fmaf(2.443315711809948e-5f, z, -1.388731625493765e-3f), z, 4.166664568298827e-2f);
+    const float cr = fmaf(cp * z, z, -0.5f * z) + 1.0f;
+    const int q = (int)n & 3;
+    const float a = (q & 1) ? cr : sr, b = (q & 1) ? sr : cr;
+    *s = (q & 2) ? -a : a;
+    *c = ((q + 1) & 2) ? -b : b;
 }
 
 // embedding / factor of one slot (aggregate_neighbors.cu:176-193).
@@ -422,13 +426,54 @@ __device__ __forceinline__ void agg_embed(int D, int F, int E, const float *__re
     *fac = f0 + dt[2 * E - 1];
 }
 
-// per-lane partial sums -> lane l holds the wave total of value l (l < NB)
-template <int NB>
-__device__ __forceinline__ float reduce_row(const float (&acc)[NB], int lane) {
-    float x[64];
+// Wave sum of y over the lane pairs (l, l ^ 32) / 16-lane row pairs, every lane keeping the sum.
+__device__ __forceinline__ float swap_add32(float y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+__device__ __forceinline__ float swap_add16(float y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(y), __float_as_uint(y), false, false);
+    return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+
+template <int N>
+__device__ __forceinline__ void rs_stage(float (&x)[16], int lane, int bit, int ctrl) {
+    const bool hi = (lane & bit) != 0;
 #pragma unroll
-    for (int t = 0; t < 64; ++t) x[t] = t < NB ? acc[t] : 0.0f;
-    return reduce_scatter64(x, lane);
+    for (int i = 0; i < N; ++i) {
+        const float keep = hi ? x[i + N] : x[i];
+        const float send = hi ? x[i] : x[i + N];
+        x[i] = keep + rs_partner(send, ctrl);
+    }
+}
+
+// NB per-lane partial sums (consumed) -> lane l holds the wave total of value l % NB.  NB = 64
+// is reduce_scatter64; NB = 32 / 16 fold the lane halves (and quarters) first and keep only NB
+// registers live.
+template <int NB>
+__device__ __forceinline__ float reduce_row(float (&acc)[NB], int lane) {
+    if constexpr (NB == 64) {
+        return reduce_scatter64(acc, lane);
+    } else {
+        float x[16];
+        if constexpr (NB == 32) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float a = swap_add32(acc[i]), b = swap_add32(acc[i + 16]);
+                const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(a), __float_as_uint(b), false, false);
+                x[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+            }
+        } else {
+            static_assert(NB == 16, "NB is 16, 32 or 64");
+#pragma unroll
+            for (int i = 0; i < 16; ++i) x[i] = swap_add16(swap_add32(acc[i]));
+        }
+        rs_stage<8>(x, lane, 8, 0x140);
+        rs_stage<4>(x, lane, 4, 0x141);
+        rs_stage<2>(x, lane, 2, 0x4e);
+        rs_stage<1>(x, lane, 1, 0xb1);
+        return x[0];
+    }
 }
 
 // NB (16, 32 or 64): features per pass; L > 64 takes several passes over the row.
@@ -551,7 +596,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
                         if (fb + t < L) acc_a[t] += dwe + dwf * feat[fb + t];
                         if (fb + t < K) acc_q[t] += key[fb + t] * te;
                     }
-                    if (fb == 0) {
+                    if (fb == 0 && !(A.expt & 2)) {
                         // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
                         const float t1 = dcw * S1, t2 = dcw * S2;
                         for (int d = 0; d < D; ++d) {
@@ -576,7 +621,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
                         part[(2 * E - 1) * kWave] += t2;
                     }
                 }
-                if (fb != 0) continue;
+                if (fb != 0 || (A.expt & 1)) continue;
                 // neighbour gradients (aggregate_neighbors.cu:296-319):
                 //   dfeat[idx][j] += dcw fac st[j],  dkeys[idx][k] += q[k] te
                 sm[lane] = (int)idx;
@@ -606,6 +651,252 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
     for (int v = 0; v < NV; ++v) {
         const float x = wave_sum(part[v * kWave]);
         if (lane == 0) atomicAdd(v < 2 * E ? &A.ddt[v] : &A.dfreq[v - 2 * E], x);
+    }
+}
+
+// ---------------------------------------------------------- staged fast path (L, K <= 64)
+// In the lane-per-slot form every lane gathers its own neighbour row, so one load instruction
+// touches 64 cache lines and the vector memory pipe (not HBM, not the ALUs) bounds the kernels.
+// Here a batch's 64 neighbour rows are first copied into LDS with coalesced 16-byte pieces
+// (consecutive lanes take consecutive pieces of one row: 4 lanes per 64-byte row at L = 16),
+// then each slot lane reads its row from LDS.
+struct AggStage {
+    int SL, SK;      // LDS row strides (floats) of the staged feature / key rows
+    int vf, vk;      // rows may be moved in 16-byte pieces (width % 4 == 0, base 16-byte aligned)
+    int per_wave;    // LDS floats per wave
+};
+
+__device__ __forceinline__ void stage_rows(const float *__restrict__ src, int W, int vec, const int *sm, int nb,
+                                           float *dst, int SW, int lane) {
+    if (vec) {
+        const int PW = W >> 2;
+        const float inv = 1.0f / (float)max(PW, 1);
+        for (int p = lane; p < nb * PW; p += kWave) {
+            const int r = (int)(((float)p + 0.5f) * inv), q = p - r * PW;
+            const int m = sm[r];
+            if (m >= 0)
+                *reinterpret_cast<float4 *>(dst + r * SW + 4 * q) =
+                    *reinterpret_cast<const float4 *>(src + (int64_t)m * W + 4 * q);
+        }
+    } else {
+        const float inv = 1.0f / (float)max(W, 1);
+        for (int p = lane; p < nb * W; p += kWave) {
+            const int r = (int)(((float)p + 0.5f) * inv), q = p - r * W;
+            const int m = sm[r];
+            if (m >= 0) dst[r * SW + q] = src[(int64_t)m * W + q];
+        }
+    }
+}
+
+__device__ __forceinline__ float dot_row(const float *__restrict__ q, const float *row, int K) {
+    float v = 0.0f;
+    for (int k = 0; k < K; ++k) v += q[k] * row[k];
+    return v;
+}
+
+// NB = L rounded up to 16 / 32 / 64; K <= 64.
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x & (kWave - 1);
+    float *base = lds + (threadIdx.x >> 6) * G.per_wave;
+    int *sm = reinterpret_cast<int *>(base);
+    float *sf = base + kWave, *sk = sf + kWave * G.SL, *ar = sk + kWave * G.SK;
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2;
+    for (int w = wave_unit_index(); w < A.P; w += stride) {
+        const int i = agg_row(A, w);
+        const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
+        const float inv = A.inv_total[i];
+        const float *q = A.queries + (int64_t)i * K;
+        float acc[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc[t] = 0.0f;
+        for (int64_t s0 = start; s0 < end; s0 += kWave) {
+            const int64_t s = s0 + lane;
+            const int nb = (int)min<int64_t>(kWave, end - s0);
+            const int64_t idx = s < end ? A.indices[s] : -1;
+            float X[2] = {0.0f, 0.0f}, dn = 0.0f;
+            if (idx >= 0) {
+                X[0] = A.dists[s * D];
+                if (D == 2) X[1] = A.dists[s * D + 1];
+                dn = A.densities[s];
+            }
+            sm[lane] = (int)idx;
+            wave_sync_lds();
+            stage_rows(A.features, L, G.vf, sm, nb, sf, G.SL, lane);
+            stage_rows(A.keys, K, G.vk, sm, nb, sk, G.SK, lane);
+            wave_sync_lds();
+            if (idx >= 0) {
+                const float weight = dot_row(q, sk + lane * G.SK, K);
+                float emb, fac;
+                agg_embed(D, F, E, A.freq, A.dt, X, &emb, &fac);
+                A.weights[s] = weight;
+                A.embeddings[s] = emb;
+                A.factors[s] = fac;
+                const float dw = inv * dn * weight;
+                const float dwf = dw * fac, dwe = dw * emb;
+                const float *feat = sf + lane * G.SL;
+                if (L == NB) {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t) acc[t] += dwe + dwf * feat[t];
+                } else {
+#pragma unroll
+                    for (int t = 0; t < NB; ++t)
+                        if (t < L) acc[t] += dwe + dwf * feat[t];
+                }
+            } else if (s < end) {
+                A.weights[s] = A.embeddings[s] = A.factors[s] = 0.0f;
+            }
+            wave_sync_lds();
+        }
+        const float r = reduce_row<NB>(acc, lane);
+        if (lane < L) ar[lane] = r;
+        wave_sync_lds();
+        for (int k = lane; k < L; k += kWave) {
+            float o = 0.0f;
+            for (int j = 0; j < L; ++j) o += A.transform[j * L + k] * ar[j];
+            A.out[(int64_t)i * L + k] = o;
+        }
+        wave_sync_lds();
+    }
+}
+
+// Backward, L and K <= 64 (NB = max(L, K) rounded up).  Per-wave LDS: the staged rows, the
+// batch's (neighbour, dcw * fac, te), st[64], and the shared-array partials: every value is
+// first summed over the lane quartet (l, l^16, l^32, l^48) and kept by lanes 0..15 (NV x 16).
+template <int NB>
+__global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G) {
+    extern __shared__ float lds[];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2, dstride = (E - 1) / D;
+    const int NV = 2 * E + F;
+    float *base = lds + (threadIdx.x >> 6) * G.per_wave;
+    int *sm = reinterpret_cast<int *>(base);
+    float *sc = base + kWave, *ste = sc + kWave, *st = ste + kWave;
+    float *sf = st + kWave, *sk = sf + kWave * G.SL, *part = sk + kWave * G.SK + (lane & 15);
+    for (int v = lane; v < NV * 16; v += kWave) part[v - (lane & 15)] = 0.0f;
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int G2 = L + K, spp = kWave / max(G2, 1), sub = lane / max(G2, 1), tl = lane - sub * G2;
+    const bool keep = lane < 16;
+    auto put = [&](int v, float x) {  // part[v] += x summed over the lane quartet
+        x = swap_add16(swap_add32(x));
+        if (keep) part[v * 16] += x;
+    };
+    for (int wr = wave_unit_index(); wr < A.P; wr += stride) {
+        const int i = agg_row(A, wr);
+        const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
+        const float inv = A.inv_total[i];
+        const float *q = A.queries + (int64_t)i * K, *g = A.dL + (int64_t)i * L;
+        // summed_transform (aggregate_neighbors.cu:257-262)
+        if (lane < L) {
+            float v = 0.0f;
+            for (int k = 0; k < L; ++k) v += A.transform[lane * L + k] * g[k];
+            st[lane] = v;
+        }
+        // this lane's factor in the scatter: st[t] for a feature lane, q[t - L] for a key lane
+        wave_sync_lds();
+        const float coef = (sub < spp && tl < G2) ? (tl < L ? st[tl] : q[tl - L]) : 0.0f;
+        float S1 = 0.0f;
+        for (int j = 0; j < L; ++j) S1 += st[j];
+        float acc_a[NB], acc_q[NB];
+#pragma unroll
+        for (int t = 0; t < NB; ++t) acc_a[t] = acc_q[t] = 0.0f;
+        for (int64_t s0 = start; s0 < end; s0 += kWave) {
+            const int64_t s = s0 + lane;
+            const int nb = (int)min<int64_t>(kWave, end - s0);
+            const int64_t idx = s < end ? A.indices[s] : -1;
+            float dn = 0.0f, wt = 0.0f, emb = 0.0f, fac = 0.0f;
+            if (idx >= 0) {
+                dn = A.densities[s];
+                wt = A.weights[s];
+                emb = A.embeddings[s];
+                fac = A.factors[s];
+            }
+            sm[lane] = (int)idx;
+            wave_sync_lds();
+            stage_rows(A.features, L, G.vf, sm, nb, sf, G.SL, lane);
+            stage_rows(A.keys, K, G.vk, sm, nb, sk, G.SK, lane);
+            wave_sync_lds();
+            float c = 0.0f, te = 0.0f, t1 = 0.0f, t2 = 0.0f;
+            if (idx >= 0) {
+                const float *feat = sf + lane * G.SL, *key = sk + lane * G.SK;
+                const float dc = dn * inv;
+                const float dcw = dc * wt;
+                float S2 = 0.0f;
+                for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
+                te = (dc * emb) * S1 + (dc * fac) * S2;  // sum_j te_j
+                c = dcw * fac;
+                const float dwe = dcw * emb, dwf = dcw * fac;
+#pragma unroll
+                for (int t = 0; t < NB; ++t) {
+                    if (t < L) acc_a[t] += dwe + dwf * feat[t];
+                    if (t < K) acc_q[t] += key[t] * te;
+                }
+                t1 = dcw * S1;
+                t2 = dcw * S2;
+            }
+            // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
+            if (!(A.expt & 2)) {
+                for (int d = 0; d < D; ++d) {
+                    const float Xd = idx >= 0 ? A.dists[s * D + d] : 0.0f;
+                    const double px = M_PI * (double)Xd;
+                    for (int e = 0; e < F; ++e) {
+                        float sn = 0.0f, cs = 0.0f;
+                        if (idx >= 0) ref_sincos(A.freq[e], Xd, &sn, &cs);
+                        const int a = d * dstride + e * 2;
+                        put(a, t1 * sn);
+                        put(a + 1, t1 * cs);
+                        put(E + a, t2 * sn);
+                        put(E + a + 1, t2 * cs);
+                        const float f0 = (float)((double)cs * px * ((double)A.dt[a] * t1 + (double)A.dt[E + a] * t2));
+                        const float f1 =
+                            (float)((double)-sn * px * ((double)A.dt[a + 1] * t1 + (double)A.dt[E + a + 1] * t2));
+                        put(2 * E + e, f0 + f1);
+                    }
+                }
+                put(E - 1, t1);
+                put(2 * E - 1, t2);
+            }
+            // neighbour gradients (aggregate_neighbors.cu:296-319), a whole neighbour row
+            // (dfeat row, then dkeys row) per G2 lanes of one atomic instruction
+            if (!(A.expt & 1)) {
+                sc[lane] = c;
+                ste[lane] = te;
+                wave_sync_lds();
+                if (spp > 0) {
+                    for (int b = 0; b < nb; b += spp) {
+                        const int sl = b + sub;
+                        const int m = (sub < spp && sl < nb) ? sm[sl] : -1;
+                        if (m >= 0) {
+                            if (tl < L) atomicAdd(&A.dfeat[(int64_t)m * L + tl], sc[sl] * coef);
+                            else atomicAdd(&A.dkeys[(int64_t)m * K + (tl - L)], ste[sl] * coef);
+                        }
+                    }
+                } else {  // L + K > 64: one neighbour row per pass
+                    for (int sl = 0; sl < nb; ++sl) {
+                        const int m = sm[sl];
+                        if (m < 0) continue;
+                        for (int t = lane; t < G2; t += kWave) {
+                            if (t < L) atomicAdd(&A.dfeat[(int64_t)m * L + t], sc[sl] * st[t]);
+                            else atomicAdd(&A.dkeys[(int64_t)m * K + (t - L)], ste[sl] * q[t - L]);
+                        }
+                    }
+                }
+            }
+            wave_sync_lds();
+        }
+        const float ra = reduce_row<NB>(acc_a, lane);
+        if (lane < L) A.arows[(int64_t)i * L + lane] = ra;
+        const float rq = reduce_row<NB>(acc_q, lane);
+        if (lane < K) A.dq[(int64_t)i * K + lane] = rq;
+        wave_sync_lds();
+    }
+    wave_sync_lds();
+    for (int v = lane; v < NV; v += kWave) {
+        float x = 0.0f;
+        for (int l = 0; l < 16; ++l) x += part[v * 16 + l - (lane & 15)];
+        atomicAdd(v < 2 * E ? &A.ddt[v] : &A.dfreq[v - 2 * E], x);
     }
 }
 
@@ -729,6 +1020,18 @@ static int agg_check(int P, int D, int L, int K, int E) {
 
 static int agg_nb(int m) { return m <= 16 ? 16 : (m <= 32 ? 32 : 64); }
 
+// Staged-row LDS layout: strides padded to a multiple of 4 floats plus 4 (16-byte aligned rows,
+// staggered banks).
+static AggStage agg_stage(int L, int K, const float *features, const float *keys, int extra) {
+    AggStage G;
+    G.SL = ((L + 3) & ~3) + 4;
+    G.SK = ((K + 3) & ~3) + 4;
+    G.vf = (L % 4 == 0) && (reinterpret_cast<uintptr_t>(features) % 16 == 0);
+    G.vk = (K % 4 == 0) && (reinterpret_cast<uintptr_t>(keys) % 16 == 0);
+    G.per_wave = kWave * (G.SL + G.SK) + extra;
+    return G;
+}
+
 extern "C" size_t dgs_agg_workspace_size(int P, int L) { return 4 * (size_t)std::max(P, 0) * std::max(L, 0) + 256; }
 
 extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *features, const float *transform,
@@ -748,10 +1051,20 @@ extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *f
     A.dists = dists, A.densities = densities, A.inv_total = inv_total;
     A.weights = weights, A.embeddings = embeddings, A.factors = factors, A.out = out, A.order = row_order;
     const unsigned nb = agg_row_blocks(P);
-    switch (agg_nb(std::min(std::max(L, 1), 64))) {
-    case 16: k_agg_forward<16><<<nb, kBlock, 0, s>>>(A); break;
-    case 32: k_agg_forward<32><<<nb, kBlock, 0, s>>>(A); break;
-    default: k_agg_forward<64><<<nb, kBlock, 0, s>>>(A); break;
+    if (L <= 64 && K <= 64) {
+        const AggStage G = agg_stage(L, K, features, keys, 2 * kWave + 64 /* sm, ar */);
+        const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * G.per_wave;
+        switch (agg_nb(std::max(L, 1))) {
+        case 16: k_agg_forward_s<16><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 32: k_agg_forward_s<32><<<nb, kBlock, lds, s>>>(A, G); break;
+        default: k_agg_forward_s<64><<<nb, kBlock, lds, s>>>(A, G); break;
+        }
+    } else {
+        switch (agg_nb(std::min(std::max(L, 1), 64))) {
+        case 16: k_agg_forward<16><<<nb, kBlock, 0, s>>>(A); break;
+        case 32: k_agg_forward<32><<<nb, kBlock, 0, s>>>(A); break;
+        default: k_agg_forward<64><<<nb, kBlock, 0, s>>>(A); break;
+        }
     }
     DGS_LAUNCH_CHECK(s, debug);
     return DGS_OK;
@@ -772,7 +1085,9 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int F = (E - 1) / D / 2;
     const int NV = 2 * E + F;
-    const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * agg_bwd_lds_floats(NV);
+    const bool staged = L <= 64 && K <= 64;
+    const AggStage G = agg_stage(L, K, features, keys, 4 * kWave + NV * 16 /* sm, sc, ste, st, partials */);
+    const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * (staged ? G.per_wave : agg_bwd_lds_floats(NV));
     if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
     auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
     DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
@@ -792,12 +1107,21 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     A.dL = dL_dout, A.arows = static_cast<float *>(workspace);
     A.dfeat = dL_dfeatures, A.dq = dL_dqueries, A.dkeys = dL_dkeys, A.dfreq = dL_dfrequencies;
     A.ddt = dL_ddistance_transform, A.order = row_order;
+    if (const char *e = getenv("DGS_AGG_EXPT")) A.expt = atoi(e);
     // few enough waves that each flushes its shared-array partials after many rows
     const unsigned nb = std::min(agg_row_blocks(P), 2048u);
-    switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {
-    case 16: k_agg_backward<16><<<nb, kBlock, lds, s>>>(A); break;
-    case 32: k_agg_backward<32><<<nb, kBlock, lds, s>>>(A); break;
-    default: k_agg_backward<64><<<nb, kBlock, lds, s>>>(A); break;
+    if (staged) {
+        switch (agg_nb(std::max(std::max(L, K), 1))) {
+        case 16: k_agg_backward_s<16><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 32: k_agg_backward_s<32><<<nb, kBlock, lds, s>>>(A, G); break;
+        default: k_agg_backward_s<64><<<nb, kBlock, lds, s>>>(A, G); break;
+        }
+    } else {
+        switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {
+        case 16: k_agg_backward<16><<<nb, kBlock, lds, s>>>(A); break;
+        case 32: k_agg_backward<32><<<nb, kBlock, lds, s>>>(A); break;
+        default: k_agg_backward<64><<<nb, kBlock, lds, s>>>(A); break;
+        }
     }
     DGS_LAUNCH_CHECK(s, debug);
     if (L > 0) {

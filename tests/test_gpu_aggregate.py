@@ -154,3 +154,15 @@ def test_aggregate_row_order_is_only_a_schedule(dgs, oracle):
     gb = dgs._C.aggregate_neighbors_backward(*t, idx.clone(), rg, X, dn, *b[:3], inv, g, False)
     for name, x, y in zip(AGG_FEATURES, ga, gb):
         close(x.cpu().numpy(), y.cpu().numpy(), 1e-5, 1e-6, name)
+
+
+def test_aggregate_wide_staged(dgs, oracle):
+    """L = K = 64: the staged path at its limit (L + K > 64 lanes per scatter row), D = 2."""
+    means, conics, radii, fe = agg_problem(P=500, D=2, L=64, K=64, F=2, seed=95)
+    _run(dgs, oracle, means, conics, radii, fe)
+
+
+def test_aggregate_unaligned_rows(dgs, oracle):
+    """L = 6, K = 5 (rows not 16-byte multiples: word-wise staging)."""
+    means, conics, radii, fe = agg_problem(P=700, D=2, L=6, K=5, F=3, seed=97)
+    _run(dgs, oracle, means, conics, radii, fe)
