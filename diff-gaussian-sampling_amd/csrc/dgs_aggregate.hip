@@ -666,25 +666,65 @@ struct AggStage {
     int per_wave;    // LDS floats per wave
 };
 
-__device__ __forceinline__ void stage_rows(const float *__restrict__ src, int W, int vec, const int *sm, int nb,
-                                           float *dst, int SW, int lane) {
+// Up to U pieces of a row array per lane per round: all U loads are issued before the first LDS
+// write, so a round costs one memory latency (the loop form waited on every load).
+template <int U>
+__device__ __forceinline__ void stage_round(const float *__restrict__ src, int W, int vec, const int *sm, int npieces,
+                                            float *dst, int SW, int lane, int p0) {
     if (vec) {
         const int PW = W >> 2;
         const float inv = 1.0f / (float)max(PW, 1);
-        for (int p = lane; p < nb * PW; p += kWave) {
-            const int r = (int)(((float)p + 0.5f) * inv), q = p - r * PW;
-            const int m = sm[r];
-            if (m >= 0)
-                *reinterpret_cast<float4 *>(dst + r * SW + 4 * q) =
-                    *reinterpret_cast<const float4 *>(src + (int64_t)m * W + 4 * q);
+        float4 v[U];
+        int off[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int p = p0 + u * kWave + lane;
+            off[u] = -1;
+            v[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (p < npieces) {
+                const int r = (int)(((float)p + 0.5f) * inv), q = p - r * PW;
+                const int m = sm[r];
+                if (m >= 0) {
+                    v[u] = *reinterpret_cast<const float4 *>(src + (int64_t)m * W + 4 * q);
+                    off[u] = r * SW + 4 * q;
+                }
+            }
         }
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (off[u] >= 0) *reinterpret_cast<float4 *>(dst + off[u]) = v[u];
     } else {
         const float inv = 1.0f / (float)max(W, 1);
-        for (int p = lane; p < nb * W; p += kWave) {
-            const int r = (int)(((float)p + 0.5f) * inv), q = p - r * W;
-            const int m = sm[r];
-            if (m >= 0) dst[r * SW + q] = src[(int64_t)m * W + q];
+        float v[4 * U];
+        int off[4 * U];
+#pragma unroll
+        for (int u = 0; u < 4 * U; ++u) {
+            const int p = p0 + u * kWave + lane;
+            off[u] = -1;
+            v[u] = 0.0f;
+            if (p < npieces) {
+                const int r = (int)(((float)p + 0.5f) * inv), q = p - r * W;
+                const int m = sm[r];
+                if (m >= 0) {
+                    v[u] = src[(int64_t)m * W + q];
+                    off[u] = r * SW + q;
+                }
+            }
         }
+#pragma unroll
+        for (int u = 0; u < 4 * U; ++u)
+            if (off[u] >= 0) dst[off[u]] = v[u];
+    }
+}
+
+// Stage the batch's neighbour rows of features and keys (nb rows, sm[r] < 0 skipped).
+__device__ __forceinline__ void stage_rows2(const AggArgs &A, const AggStage &G, const int *sm, int nb, float *sf,
+                                            float *sk, int lane) {
+    const int nf = nb * (G.vf ? A.L >> 2 : A.L), nk = nb * (G.vk ? A.K >> 2 : A.K);
+    const int sf_step = (G.vf ? 4 : 16) * kWave, sk_step = (G.vk ? 4 : 16) * kWave;
+    for (int pf = 0, pk = 0; pf < nf || pk < nk; pf += sf_step, pk += sk_step) {
+        if (pf < nf) stage_round<4>(A.features, A.L, G.vf, sm, nf, sf, G.SL, lane, pf);
+        if (pk < nk) stage_round<4>(A.keys, A.K, G.vk, sm, nk, sk, G.SK, lane, pk);
     }
 }
 
@@ -712,20 +752,30 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
         float acc[NB];
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc[t] = 0.0f;
+        // the streamed per-slot inputs are loaded one batch ahead (their HBM latency then
+        // overlaps the current batch's row staging and arithmetic)
+        int64_t idx_n = -1;
+        float X0_n = 0.0f, X1_n = 0.0f, dn_n = 0.0f;
+        auto fetch = [&](int64_t sp) {
+            idx_n = -1;
+            if (sp < end) {
+                idx_n = A.indices[sp];
+                X0_n = A.dists[sp * D];
+                X1_n = D == 2 ? A.dists[sp * D + 1] : 0.0f;
+                dn_n = A.densities[sp];
+            }
+        };
+        fetch(start + lane);
         for (int64_t s0 = start; s0 < end; s0 += kWave) {
             const int64_t s = s0 + lane;
             const int nb = (int)min<int64_t>(kWave, end - s0);
-            const int64_t idx = s < end ? A.indices[s] : -1;
-            float X[2] = {0.0f, 0.0f}, dn = 0.0f;
-            if (idx >= 0) {
-                X[0] = A.dists[s * D];
-                if (D == 2) X[1] = A.dists[s * D + 1];
-                dn = A.densities[s];
-            }
+            const int64_t idx = idx_n;
+            float X[2] = {X0_n, X1_n};
+            const float dn = dn_n;
+            fetch(s + kWave);
             sm[lane] = (int)idx;
             wave_sync_lds();
-            stage_rows(A.features, L, G.vf, sm, nb, sf, G.SL, lane);
-            stage_rows(A.keys, K, G.vk, sm, nb, sk, G.SK, lane);
+            stage_rows2(A, G, sm, nb, sf, sk, lane);
             wave_sync_lds();
             if (idx >= 0) {
                 const float weight = dot_row(q, sk + lane * G.SK, K);
@@ -802,21 +852,31 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
         float acc_a[NB], acc_q[NB];
 #pragma unroll
         for (int t = 0; t < NB; ++t) acc_a[t] = acc_q[t] = 0.0f;
+        int64_t idx_n = -1;  // streamed per-slot inputs, one batch ahead (see the forward)
+        float dn_n = 0.0f, wt_n = 0.0f, emb_n = 0.0f, fac_n = 0.0f, X0_n = 0.0f, X1_n = 0.0f;
+        auto fetch = [&](int64_t sp) {
+            idx_n = -1;
+            if (sp < end) {
+                idx_n = A.indices[sp];
+                dn_n = A.densities[sp];
+                wt_n = A.weights[sp];
+                emb_n = A.embeddings[sp];
+                fac_n = A.factors[sp];
+                X0_n = A.dists[sp * D];
+                X1_n = D == 2 ? A.dists[sp * D + 1] : 0.0f;
+            }
+        };
+        fetch(start + lane);
         for (int64_t s0 = start; s0 < end; s0 += kWave) {
             const int64_t s = s0 + lane;
             const int nb = (int)min<int64_t>(kWave, end - s0);
-            const int64_t idx = s < end ? A.indices[s] : -1;
-            float dn = 0.0f, wt = 0.0f, emb = 0.0f, fac = 0.0f;
-            if (idx >= 0) {
-                dn = A.densities[s];
-                wt = A.weights[s];
-                emb = A.embeddings[s];
-                fac = A.factors[s];
-            }
+            const int64_t idx = idx_n;
+            const float dn = dn_n, wt = wt_n, emb = emb_n, fac = fac_n;
+            const float Xs[2] = {X0_n, X1_n};
+            fetch(s + kWave);
             sm[lane] = (int)idx;
             wave_sync_lds();
-            stage_rows(A.features, L, G.vf, sm, nb, sf, G.SL, lane);
-            stage_rows(A.keys, K, G.vk, sm, nb, sk, G.SK, lane);
+            stage_rows2(A, G, sm, nb, sf, sk, lane);
             wave_sync_lds();
             float c = 0.0f, te = 0.0f, t1 = 0.0f, t2 = 0.0f;
             if (idx >= 0) {
@@ -839,7 +899,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
             if (!(A.expt & 2)) {
                 for (int d = 0; d < D; ++d) {
-                    const float Xd = idx >= 0 ? A.dists[s * D + d] : 0.0f;
+                    const float Xd = idx >= 0 ? Xs[d] : 0.0f;
                     const double px = M_PI * (double)Xd;
                     for (int e = 0; e < F; ++e) {
                         float sn = 0.0f, cs = 0.0f;
