@@ -815,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
 // Backward, L and K <= 64 (NB = max(L, K) rounded up).  Per-wave LDS: the staged rows, the
 // batch's (neighbour, dcw * fac, te), st[64], and the shared-array partials: every value is
 // first summed over the lane quartet (l, l^16, l^32, l^48) and kept by lanes 0..15 (NV x 16).
-template <int NB>
+template <int NB, bool COMBO>
 __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G) {
     extern __shared__ float lds[];
     const int lane = threadIdx.x & (kWave - 1);
@@ -824,8 +824,26 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
     float *base = lds + (threadIdx.x >> 6) * G.per_wave;
     int *sm = reinterpret_cast<int *>(base);
     float *sc = base + kWave, *ste = sc + kWave, *st = ste + kWave;
-    float *sf = st + kWave, *sk = sf + kWave * G.SL, *part = sk + kWave * G.SK + (lane & 15);
-    for (int v = lane; v < NV * 16; v += kWave) part[v - (lane & 15)] = 0.0f;
+    float *sf = st + kWave, *sk = sf + kWave * G.SL, *s1 = sk + kWave * G.SK, *s2 = s1 + kWave;
+    float *sx0 = s2 + kWave, *sx1 = sx0 + kWave, *pbase = sx1 + kWave, *part = pbase + (lane & 15);
+    for (int v = lane; v < NV * 16; v += kWave) pbase[v] = 0.0f;
+    // distance-transform / frequency terms: lane = (slot group cg, combination cc = (d, e)); each
+    // lane keeps its five sums in registers for the wave's lifetime (DF <= 64; otherwise the
+    // per-slot `put` reduction below)
+    const int DF = D * F, DFe = max(DF, 1);
+    constexpr bool combo_path = COMBO;  // host: COMBO == (D * F <= 64)
+    const int GR = kWave / DFe, cg = lane / DFe, cc = lane - cg * DFe;
+    const bool cact = combo_path && cg < GR;
+    const int cd = DF > 0 ? cc / F : 0, ce = DF > 0 ? cc - cd * F : 0, ca = cd * dstride + 2 * ce;
+    float cfr = 0.0f, c_a0 = 0.0f, c_a1 = 0.0f, c_b0 = 0.0f, c_b1 = 0.0f;
+    if (cact && DF > 0) {
+        cfr = A.freq[ce];
+        c_a0 = A.dt[ca];
+        c_a1 = A.dt[ca + 1];
+        c_b0 = A.dt[E + ca];
+        c_b1 = A.dt[E + ca + 1];
+    }
+    float a_ts = 0.0f, a_tc = 0.0f, a_us = 0.0f, a_uc = 0.0f, a_fr = 0.0f, a_t1 = 0.0f, a_t2 = 0.0f;
     const int stride = gridDim.x * kWavesPerBlock;
     const int G2 = L + K, spp = kWave / max(G2, 1), sub = lane / max(G2, 1), tl = lane - sub * G2;
     const bool keep = lane < 16;
@@ -897,7 +915,37 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
                 t2 = dcw * S2;
             }
             // distance-transform and frequency terms (aggregate_neighbors.cu:270-295)
-            if (!(A.expt & 2)) {
+            if constexpr (COMBO) {
+              if (!(A.expt & 2)) {
+                s1[lane] = t1;
+                s2[lane] = t2;
+                sx0[lane] = Xs[0];
+                sx1[lane] = Xs[1];
+                wave_sync_lds();
+                if (cact) {
+                    for (int sl = cg; sl < nb; sl += GR) {
+                        const float u1 = s1[sl], u2 = s2[sl];
+                        if (cc == 0) {
+                            a_t1 += u1;
+                            a_t2 += u2;
+                        }
+                        if (DF > 0) {
+                            const float Xd = cd ? sx1[sl] : sx0[sl];
+                            float sn, cs;
+                            ref_sincos(cfr, Xd, &sn, &cs);
+                            a_ts += u1 * sn;
+                            a_tc += u1 * cs;
+                            a_us += u2 * sn;
+                            a_uc += u2 * cs;
+                            const double px = M_PI * (double)Xd;
+                            const float f0 = (float)((double)cs * px * ((double)c_a0 * u1 + (double)c_b0 * u2));
+                            const float f1 = (float)((double)-sn * px * ((double)c_a1 * u1 + (double)c_b1 * u2));
+                            a_fr += f0 + f1;
+                        }
+                    }
+                }
+              }
+            } else if (!(A.expt & 2)) {
                 for (int d = 0; d < D; ++d) {
                     const float Xd = idx >= 0 ? Xs[d] : 0.0f;
                     const double px = M_PI * (double)Xd;
@@ -953,10 +1001,37 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
         wave_sync_lds();
     }
     wave_sync_lds();
-    for (int v = lane; v < NV; v += kWave) {
-        float x = 0.0f;
-        for (int l = 0; l < 16; ++l) x += part[v * 16 + l - (lane & 15)];
-        atomicAdd(v < 2 * E ? &A.ddt[v] : &A.dfreq[v - 2 * E], x);
+    if constexpr (COMBO) {
+        float *cp = pbase;  // 7 x 64 per-lane sums (the put area is unused on this path)
+        const float vals[7] = {a_ts, a_tc, a_us, a_uc, a_fr, a_t1, a_t2};
+#pragma unroll
+        for (int v = 0; v < 7; ++v) cp[v * kWave + lane] = vals[v];
+        wave_sync_lds();
+        if (lane < DFe) {
+            float sum[7];
+#pragma unroll
+            for (int v = 0; v < 7; ++v) {
+                sum[v] = 0.0f;
+                for (int g2 = 0; g2 < GR; ++g2) sum[v] += cp[v * kWave + g2 * DFe + lane];
+            }
+            if (DF > 0) {
+                atomicAdd(&A.ddt[ca], sum[0]);
+                atomicAdd(&A.ddt[ca + 1], sum[1]);
+                atomicAdd(&A.ddt[E + ca], sum[2]);
+                atomicAdd(&A.ddt[E + ca + 1], sum[3]);
+                atomicAdd(&A.dfreq[ce], sum[4]);
+            }
+            if (lane == 0) {
+                atomicAdd(&A.ddt[E - 1], sum[5]);
+                atomicAdd(&A.ddt[2 * E - 1], sum[6]);
+            }
+        }
+    } else {
+        for (int v = lane; v < NV; v += kWave) {
+            float x = 0.0f;
+            for (int l = 0; l < 16; ++l) x += part[v * 16 + l - (lane & 15)];
+            atomicAdd(v < 2 * E ? &A.ddt[v] : &A.dfreq[v - 2 * E], x);
+        }
     }
 }
 
@@ -1146,7 +1221,8 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     const int F = (E - 1) / D / 2;
     const int NV = 2 * E + F;
     const bool staged = L <= 64 && K <= 64;
-    const AggStage G = agg_stage(L, K, features, keys, 4 * kWave + NV * 16 /* sm, sc, ste, st, partials */);
+    const AggStage G = agg_stage(L, K, features, keys,
+                                 8 * kWave + std::max(NV * 16, 7 * kWave) /* sm sc ste st s1 s2 sx0 sx1, sums */);
     const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * (staged ? G.per_wave : agg_bwd_lds_floats(NV));
     if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
     auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
@@ -1171,10 +1247,14 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     // few enough waves that each flushes its shared-array partials after many rows
     const unsigned nb = std::min(agg_row_blocks(P), 2048u);
     if (staged) {
-        switch (agg_nb(std::max(std::max(L, K), 1))) {
-        case 16: k_agg_backward_s<16><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 32: k_agg_backward_s<32><<<nb, kBlock, lds, s>>>(A, G); break;
-        default: k_agg_backward_s<64><<<nb, kBlock, lds, s>>>(A, G); break;
+        const bool combo = D * F <= kWave;
+        switch (agg_nb(std::max(std::max(L, K), 1)) * 2 + (combo ? 1 : 0)) {
+        case 33: k_agg_backward_s<16, true><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 32: k_agg_backward_s<16, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 65: k_agg_backward_s<32, true><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 64: k_agg_backward_s<32, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 129: k_agg_backward_s<64, true><<<nb, kBlock, lds, s>>>(A, G); break;
+        default: k_agg_backward_s<64, false><<<nb, kBlock, lds, s>>>(A, G); break;
         }
     } else {
         switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {

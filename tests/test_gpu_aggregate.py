@@ -166,3 +166,10 @@ def test_aggregate_unaligned_rows(dgs, oracle):
     """L = 6, K = 5 (rows not 16-byte multiples: word-wise staging)."""
     means, conics, radii, fe = agg_problem(P=700, D=2, L=6, K=5, F=3, seed=97)
     _run(dgs, oracle, means, conics, radii, fe)
+
+
+def test_aggregate_many_frequencies(dgs, oracle):
+    """D F = 66 > 64 frequency/dimension combinations: the per-slot reduction path of the
+    distance-transform gradients."""
+    means, conics, radii, fe = agg_problem(P=300, D=2, L=8, K=8, F=33, seed=99)
+    _run(dgs, oracle, means, conics, radii, fe)
