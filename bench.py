@@ -51,6 +51,10 @@ def main():
     ap.add_argument("--C", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-samples", type=int, default=3072)
+    ap.add_argument("--op", default="sample", choices=["sample", "aggregate"],
+                    help="sample: the headline (default); aggregate: aggregate_neighbors at SURVEY "
+                         "config 5 (P = 1M, K = L = 16, F = 4), one GPU or N replicas")
+    ap.add_argument("--cpu-rows", type=int, default=20000, help="aggregate CPU-baseline rows")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -60,6 +64,8 @@ def main():
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
+    if args.op == "aggregate":
+        return bench_aggregate(args, world, rank, dev)
 
     import diff_gaussian_sampling as dgs
     from diff_gaussian_sampling import synthetic as syn
@@ -172,6 +178,121 @@ def main():
         result["cpu_baseline"] = cpu_baseline(means.detach().cpu(), values.detach().cpu(),
                                               covs.cpu(), conics.detach().cpu(), samples.cpu(),
                                               dL.cpu(), fn, args.cpu_samples)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+PEAK_HBM_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E peak
+PEAK_ATOMIC_GBS = 1300.0     # MI355X_MICROARCH.md "Global float atomics": chip-wide added-byte rate
+
+
+def bench_aggregate(args, world, rank, dev):
+    """aggregate_neighbors: P = 1M Gaussians (the headline's, radii from
+    preprocess_gaussians), K = L = 16, F = 4.  A step = forward + backward through the autograd
+    Function on resident neighbour lists; preprocess_aggregate is timed separately.  N > 1 runs
+    N independent replicas (the rows shard, but nothing in a step is exchanged)."""
+    import diff_gaussian_sampling as dgs
+    from diff_gaussian_sampling import synthetic as syn
+    P, L, K, F, D = args.P, 16, 16, 4, 2
+    E = 2 * D * F + 1
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, D, 1, seed=0))
+    samples = syn.samples(args.N, D, seed=4).to(dev)
+    radii = dgs.preprocess_gaussians(means, values, covs, conics, samples, False)[5]
+    del samples
+    g = torch.Generator().manual_seed(7)
+    feats = [torch.randn(P, L, generator=g), torch.randn(L, L, generator=g) / L,
+             torch.randn(P, K, generator=g), torch.randn(P, K, generator=g),
+             torch.rand(F, generator=g) * 2.5 + 0.5, torch.randn(2 * E, generator=g)]
+    feats_d = [t.to(dev).requires_grad_(True) for t in feats]
+    dL = torch.randn(P, L, generator=torch.Generator().manual_seed(5)).to(dev)
+    sampler = dgs.GaussianSampler(False)
+    sampler.means, sampler.conics, sampler.radii = means, conics, radii
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    sampler.preprocess_aggregate()
+    torch.cuda.synchronize()
+    pre_ms = (time.perf_counter() - t0) * 1e3
+    Lnb = int(sampler.indices.numel())
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fwd_ms, bwd_ms = [], []
+
+    def step(timed):
+        for t in feats_d:
+            t.grad = None
+        if timed:
+            ev[0].record()
+        out = sampler.aggregate_neighbors(*feats_d)
+        if timed:
+            ev[1].record()
+        out.backward(dL)
+        if timed:
+            ev[2].record()
+            torch.cuda.synchronize()
+            fwd_ms.append(ev[0].elapsed_time(ev[1]))
+            bwd_ms.append(ev[1].elapsed_time(ev[2]))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    for _ in range(3):  # per-phase event times, outside the timed region
+        step(True)
+    ms_per_step = elapsed * 1e3 / args.steps
+    f_ms, b_ms = sorted(fwd_ms)[1], sorted(bwd_ms)[1]
+    # algorithmic bytes: per slot the backward streams indices (8), dists (8), densities (4),
+    # weights / embeddings / factors (12) and adds L + K floats into neighbour rows
+    stream_b = 32.0 * Lnb + 4.0 * P * (3 * L + 3 * K)
+    atomic_b = 4.0 * (L + K) * Lnb
+    result = {
+        "metric": "aggregated neighbour slots/sec (aggregate_neighbors fwd+bwd), 1M Gaussians",
+        "value": Lnb * world / (ms_per_step / 1e3),
+        "unit": "slots/s",
+        "n_gpus": world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (the headline Gaussians; N(0,1) features, queries, keys, transform/L)",
+        "config": {"workload": f"aggregate_neighbors, P={P}, K={K}, L={L}, F={F}, D=2, fwd+bwd",
+                   "neighbour_slots": Lnb, "parallelism": f"replicas x{world}"},
+        "preprocess_aggregate_ms": pre_ms,
+        "phases_ms": {"forward": f_ms, "backward": b_ms},
+        "roofline": {"bound": "hbm", "kernel": "k_agg_backward_s", "achieved": stream_b / (b_ms * 1e-3) / 1e9,
+                     "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": stream_b / (b_ms * 1e-3) / 1e9 / PEAK_HBM_GBS, "traffic": None,
+                     "atomic_added_GBs": atomic_b / (b_ms * 1e-3) / 1e9, "atomic_peak_GBs": PEAK_ATOMIC_GBS,
+                     "atomic_frac": atomic_b / (b_ms * 1e-3) / 1e9 / PEAK_ATOMIC_GBS},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu:
+        import numpy as np
+        from oracle import oracle as orc
+        orc.build()
+        host = lambda t: t.detach().cpu().numpy()  # noqa: E731
+        args_np = [host(t) for t in feats_d]
+        idx, rg, X, dn, inv = (host(t) for t in (sampler.indices, sampler.ranges, sampler.dists,
+                                                sampler.densities, sampler.inv_total_densities))
+        rows = min(args.cpu_rows, P)
+        t0 = time.perf_counter()
+        w, e_, f_, _ = orc.agg_forward(*args_np, idx, rg, X, dn, inv, rows=rows)
+        orc.agg_backward(*args_np, idx, rg, X, dn, w, e_, f_, inv, host(dL), rows=rows)
+        dt = time.perf_counter() - t0
+        nslots = int(rg[rows - 1])
+        result["cpu_baseline"] = {"value": nslots / dt, "unit": "slots/s", "cores": 1, "kind": "port",
+                                  "sample": f"first {rows} rows ({nslots} slots) of the same lists, "
+                                            f"fwd+bwd, neighbour search excluded ({dt:.1f} s)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -199,8 +199,9 @@ def agg_preprocess(means, conics, radii):
 
 
 def agg_forward(features, transform, queries, keys, frequencies, distance_transform, indices,
-                ranges, dists, densities, inv_total):
-    """aggregate_neighbors forward: (weights, embeddings, factors, neighbor_features)."""
+                ranges, dists, densities, inv_total, rows=None):
+    """aggregate_neighbors forward: (weights, embeddings, factors, neighbor_features).
+    rows: evaluate only the first `rows` rows (a bounded CPU-baseline sample)."""
     lib = _load()
     f, T, q, k = _f32(features), _f32(transform), _f32(queries), _f32(keys)
     fr, dt = _f32(frequencies), _f32(distance_transform)
@@ -212,14 +213,14 @@ def agg_forward(features, transform, queries, keys, frequencies, distance_transf
     n = idx.size
     w, emb, fac = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
     out = np.zeros((P, L), np.float32)
-    lib.orc_agg_forward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    lib.orc_agg_forward(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                         _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(w), _ptr(emb),
                         _ptr(fac), _ptr(out))
     return w, emb, fac, out
 
 
 def agg_backward(features, transform, queries, keys, frequencies, distance_transform, indices,
-                 ranges, dists, densities, weights, embeddings, factors, inv_total, dL):
+                 ranges, dists, densities, weights, embeddings, factors, inv_total, dL, rows=None):
     """aggregate_neighbors backward: the six gradients (features, transform, queries, keys,
     frequencies, distance_transform)."""
     lib = _load()
@@ -233,7 +234,7 @@ def agg_backward(features, transform, queries, keys, frequencies, distance_trans
     E = dt.size // 2
     outs = [np.zeros_like(f), np.zeros_like(T), np.zeros_like(q), np.zeros_like(k),
             np.zeros_like(fr), np.zeros_like(dt)]
-    lib.orc_agg_backward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    lib.orc_agg_backward(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                          _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
                          _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
     return tuple(outs)
