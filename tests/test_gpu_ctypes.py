@@ -34,3 +34,24 @@ def test_ctypes_binding_matches_extension(dgs, function):
     for x, y in zip(ga, gb):  # atomics: order-dependent in the last bits
         np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5,
                                    atol=1e-6 * float(x.abs().max()))
+
+
+def test_ctypes_aggregate_matches_extension(dgs):
+    import dgs_ctypes
+    from cases import AGG_FEATURES, agg_problem
+    means, conics, radii, fe = agg_problem(P=800, D=2, L=16, K=16, F=4, seed=150)
+    cu = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    a = dgs._C.preprocess_aggregate(cu(means), cu(conics), cu(radii), False)
+    b = dgs_ctypes.preprocess_aggregate(cu(means), cu(conics), cu(radii), False)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    t = [cu(fe[k]) for k in AGG_FEATURES]
+    fa = dgs._C.aggregate_neighbors(*t, *a, False)
+    fb = dgs_ctypes.aggregate_neighbors(*t, *b, False)
+    for x, y in zip(fa, fb):
+        assert torch.equal(x, y)
+    g = torch.randn_like(fa[3])
+    ga = dgs._C.aggregate_neighbors_backward(*t, *a[:4], *fa[:3], a[4], g, False)
+    gb = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False)
+    for x, y in zip(ga, gb):
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))

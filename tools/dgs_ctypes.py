@@ -131,3 +131,92 @@ sample_gaussians_derivative, sample_gaussians_derivative_backward = _make("sampl
 sample_gaussians_laplacian, sample_gaussians_laplacian_backward = _make("sample_gaussians_laplacian")
 sample_gaussians_third_derivative, sample_gaussians_third_derivative_backward = _make(
     "sample_gaussians_third_derivative")
+
+
+# ---- neighbour aggregation (aggregate_neighbors.h:11-47) ---------------------------------
+_lib.dgs_agg_preprocess.argtypes = [_I, _I, _P, _P, _P, _P, _P, _P, ALLOC_FN, _P, ctypes.POINTER(_I64), _P, _I]
+_lib.dgs_agg_forward.argtypes = [_I] * 5 + [_P] * 11 + [_P] + [_P] * 4 + [_P, _I]
+_lib.dgs_agg_backward.argtypes = [_I] * 5 + [_P] * 14 + [_P] + [_P] * 7 + [_P, _SZ, _P, _I]
+_lib.dgs_agg_workspace_size.restype = _SZ
+_lib.dgs_agg_workspace_size.argtypes = [_I, _I]
+_orders = {}  # indices data_ptr -> (P, row order tensor): the scheduling hint of dgs_agg_preprocess
+
+
+def _i64(t):
+    if t.dtype != torch.int64:
+        raise RuntimeError("expected int64 tensors")
+    return t.contiguous()
+
+
+def preprocess_aggregate(means, conics, radii, debug):
+    """aggregate_neighbors.h:11-15 -> (indices, ranges, dists, densities, inv_total_densities)."""
+    means, conics, radii = map(_f32, (means, conics, radii))
+    P, D = means.shape
+    dev = means.device
+    ranges = torch.zeros(P, dtype=torch.int64, device=dev)
+    inv = torch.zeros(P, device=dev)
+    order = torch.empty(P, dtype=torch.int32, device=dev)
+    buffers = {}
+
+    def alloc(ctx, which, nbytes):
+        t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=dev)
+        buffers.setdefault(which, []).append(t)
+        return t.data_ptr()
+
+    length = ctypes.c_int64(0)
+    if P > 0:
+        _check(_lib.dgs_agg_preprocess(P, D, _ptr(means), _ptr(conics), _ptr(radii), _ptr(ranges), _ptr(inv),
+                                       _ptr(order), ALLOC_FN(alloc), None, ctypes.byref(length), _stream(),
+                                       int(bool(debug))))
+    n = length.value
+    if n == 0:
+        return (torch.empty(0, dtype=torch.int64, device=dev), ranges, torch.empty(0, D, device=dev),
+                torch.empty(0, device=dev), inv)
+    indices = buffers[5][-1].view(torch.int64)[:n]
+    _orders.clear()
+    _orders[indices.data_ptr()] = (P, order)
+    return (indices, ranges, buffers[6][-1].view(torch.float32)[:n * D].view(n, D),
+            buffers[7][-1].view(torch.float32)[:n], inv)
+
+
+def _agg_sizes(features, queries, distance_transform, dists):
+    return (features.shape[0], dists.shape[-1] if dists.dim() == 2 else 1, features.shape[-1],
+            queries.shape[-1], distance_transform.shape[-1] // 2)
+
+
+def _order(indices, P):
+    e = _orders.get(indices.data_ptr())
+    return e[1] if e is not None and e[0] == P else None
+
+
+def aggregate_neighbors(features, transform, queries, keys, frequencies, distance_transform, indices, ranges,
+                        dists, densities, inv_total_densities, debug):
+    """aggregate_neighbors.h:17-29 -> (weights, embeddings, factors, neighbor_features)."""
+    f, T, q, k, fr, dt, X, dn, inv = map(_f32, (features, transform, queries, keys, frequencies,
+                                               distance_transform, dists, densities, inv_total_densities))
+    idx, rg = _i64(indices), _i64(ranges)
+    P, D, L, K, E = _agg_sizes(f, q, dt, X)
+    w, e, fa = (torch.zeros_like(dn) for _ in range(3))
+    out = torch.zeros(P, L, device=f.device)
+    _check(_lib.dgs_agg_forward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt), _ptr(idx),
+                                _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(_order(idx, P)), _ptr(w), _ptr(e),
+                                _ptr(fa), _ptr(out), _stream(), int(bool(debug))))
+    return w, e, fa, out
+
+
+def aggregate_neighbors_backward(features, transform, queries, keys, frequencies, distance_transform, indices,
+                                 ranges, dists, densities, weights, embeddings, factors, inv_total_densities,
+                                 dL_dneighbor_features, debug):
+    """aggregate_neighbors.h:31-47 -> the six gradients."""
+    f, T, q, k, fr, dt, X, dn, w, e, fa, inv, g = map(
+        _f32, (features, transform, queries, keys, frequencies, distance_transform, dists, densities, weights,
+               embeddings, factors, inv_total_densities, dL_dneighbor_features))
+    idx, rg = _i64(indices), _i64(ranges)
+    P, D, L, K, E = _agg_sizes(f, q, dt, X)
+    outs = [torch.zeros_like(t) for t in (f, T, q, k, fr, dt)]
+    ws = torch.empty(_lib.dgs_agg_workspace_size(P, L), dtype=torch.uint8, device=f.device)
+    _check(_lib.dgs_agg_backward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt), _ptr(idx),
+                                 _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(e), _ptr(fa), _ptr(inv),
+                                 _ptr(_order(idx, P)), _ptr(g), *[_ptr(o) for o in outs], _ptr(ws), ws.numel(),
+                                 _stream(), int(bool(debug))))
+    return tuple(outs)
