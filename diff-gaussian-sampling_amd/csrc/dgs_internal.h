@@ -19,7 +19,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 1;
+constexpr uint32_t kVersion = 2;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -45,10 +45,13 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // Opaque buffer layout.  Gaussian-side buffer (DGS_BUF_BINNING):
 //   [header 256 B][counts int32[4]][perm int32[P]][cell_gbeg int32[ncells]]
 //   [cell_gmid int32[ncells]][cell_gend int32[ncells]][entries uint32[E]][bwd_units uint2[bwd_cap]]
+//   [gmean float2[P]][gcon float4[P]]  (means / conics in internal order, packed at binning:
+//                                       forward/backward must pass the binned means/conics)
 // A cell's list is [gbeg, gend); its flag-free entries come first, [gbeg, gmid).
 // Sample-side buffer (DGS_BUF_SAMPLE_BINNING):
 //   [header copy 256 B][sorted_sid int32[N]][cell_sbeg int32[ncells]][cell_send int32[ncells]]
-//   [fwd_units uint2[fwd_cap]]
+//   [fwd_units uint2[fwd_cap]][cell_box float4[ncells]]
+//   [fsrows: sample pair rows [s0(2p) s0(2p+1) (s1(2p) s1(2p+1))] in sorted order, + slack]
 // ---------------------------------------------------------------------------------------
 struct Header {
     uint32_t magic, version;
@@ -67,6 +70,7 @@ struct Header {
     uint64_t stamp;  // identical in both buffers of one preprocess call
     uint64_t o_cell_gmid;
     uint64_t o_cell_box;  // sample buffer: per-cell bounding box of the cell's samples
+    uint64_t o_gmean, o_gcon, o_fsrows;
 };
 static_assert(sizeof(Header) <= 256, "header too large");
 constexpr size_t kHeaderBytes = 256;
@@ -77,8 +81,13 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
-    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, s_bytes;
+    uint64_t o_gmean, o_gcon;
+    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, s_bytes;
 };
+
+// Forward sample pair rows: N rounded up to a pair, plus slack for a pass's wide scalar loads
+// (up to 32 pairs + one x16 load past the last pair).
+inline size_t fsrows_bytes(int64_t N, int D) { return ((size_t)N + 1) * D * 4 + 36 * 16; }
 
 inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64_t fwd_cap,
                           int64_t bwd_cap) {
@@ -91,6 +100,8 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_cell_gend = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_entries = o;   o = align_up(o + 4 * (size_t)E + 64, 256);  // slack: 8-entry scalar loads
     L.o_bwd_units = o; o = align_up(o + 8 * (size_t)bwd_cap, 256);
+    L.o_gmean = o;     o = align_up(o + 8 * (size_t)P, 256);
+    L.o_gcon = o;      o = align_up(o + 16 * (size_t)P, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
     L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);
@@ -98,6 +109,7 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_cell_send = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_fwd_units = o; o = align_up(o + 8 * (size_t)fwd_cap, 256);
     L.o_cell_box = o;  o = align_up(o + 16 * (size_t)ncells, 256);
+    L.o_fsrows = o;    o = align_up(o + fsrows_bytes(N, 2), 256);
     L.s_bytes = o;
     return L;
 }
@@ -114,6 +126,9 @@ struct Bins {
     const int32_t *cell_sbeg, *cell_send;
     const uint2 *fwd_units;
     const float4 *cell_box;  // [min0 min1 max0 max1] of each cell's samples
+    const float2 *gmean;     // means in internal order ({m, 0} at D = 1)
+    const float4 *gcon;      // conics in internal order ({c0, c1, c2, 0}; {c0, 0, 0, 0} at D = 1)
+    const float *fsrows;     // sample pair rows in sorted order
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -143,6 +158,8 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     const uint64_t o_sorted = sload(&B.h->o_sorted), o_sbeg = sload(&B.h->o_cell_sbeg);
     const uint64_t o_send = sload(&B.h->o_cell_send), o_fu = sload(&B.h->o_fwd_units);
     const uint64_t o_box = sload(&B.h->o_cell_box);
+    const uint64_t o_gmean = sload(&B.h->o_gmean), o_gcon = sload(&B.h->o_gcon);
+    const uint64_t o_fsrows = sload(&B.h->o_fsrows);
     B.counts = reinterpret_cast<const int32_t *>(gb + o_counts);
     B.perm = reinterpret_cast<const int32_t *>(gb + o_perm);
     B.cell_gbeg = reinterpret_cast<const int32_t *>(gb + o_gbeg);
@@ -155,6 +172,9 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.cell_send = reinterpret_cast<const int32_t *>(sb + o_send);
     B.fwd_units = reinterpret_cast<const uint2 *>(sb + o_fu);
     B.cell_box = reinterpret_cast<const float4 *>(sb + o_box);
+    B.gmean = reinterpret_cast<const float2 *>(gb + o_gmean);
+    B.gcon = reinterpret_cast<const float4 *>(gb + o_gcon);
+    B.fsrows = reinterpret_cast<const float *>(sb + o_fsrows);
     return B;
 }
 

@@ -482,6 +482,38 @@ __global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
     }
 }
 
+// Means and conics in internal order (the forward/backward read them coalesced from here).
+__global__ void k_geo_pack(int P, int D, const uint32_t *__restrict__ perm, const float *__restrict__ means,
+                           const float *__restrict__ conics, float2 *__restrict__ gmean,
+                           float4 *__restrict__ gcon) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int64_t g = perm[i];
+    if (D == 2) {
+        gmean[i] = make_float2(means[g * 2], means[g * 2 + 1]);
+        gcon[i] = make_float4(conics[g * 3], conics[g * 3 + 1], conics[g * 3 + 2], 0.0f);
+    } else {
+        gmean[i] = make_float2(means[g], 0.0f);
+        gcon[i] = make_float4(conics[g], 0.0f, 0.0f, 0.0f);
+    }
+}
+
+// Forward sample pair rows in sorted order: pair p = samples 2p, 2p+1, field-interleaved
+// [s0 s0' (s1 s1')]; a missing second sample (odd N) is 0.
+__global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, const float *__restrict__ samples,
+                          float *__restrict__ rows) {
+    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= (int64_t)(N + 1) / 2 * 2) return;
+    float s[2] = {0.0f, 0.0f};
+    if (j < N) {
+        const int64_t sid = sorted[j];
+        s[0] = samples[sid * D];
+        if (D == 2) s[1] = samples[sid * D + 1];
+    }
+    float *row = rows + (j >> 1) * (2 * D) + (j & 1);
+    for (int f = 0; f < D; ++f) row[2 * f] = s[f];
+}
+
 __global__ void k_copy_u32(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) b[i] = (int32_t)a[i];
@@ -649,6 +681,10 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     k_cell_box<<<grid_for(ncells), kBlock, 0, s>>>(ncells, D, cell_sbeg, cell_send, sorted_sid,
                                                   samples, cell_box);
     DGS_LAUNCH_CHECK(s, debug);
+    float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
+    DGS_TRY_HIP(hipMemsetAsync(fsrows, 0, fsrows_bytes(N, D), s));
+    k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
+    DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
     k_gauss_prep<<<grid_for(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
@@ -706,6 +742,10 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipMemsetAsync(hend, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
     k_copy_u32<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
     DGS_LAUNCH_CHECK(s, debug);
+    k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
+                                              reinterpret_cast<float2 *>(gbuf + L.o_gmean),
+                                              reinterpret_cast<float4 *>(gbuf + L.o_gcon));
+    DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
         k_fine_fill<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
                                                    cell_send, cell_box, foffs, ekeys, evals, counters);
@@ -755,6 +795,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     h.g_bytes = L.g_bytes;
     h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
     h.o_fwd_units = L0.o_fwd_units; h.o_cell_box = L0.o_cell_box; h.s_bytes = L0.s_bytes;
+    h.o_gmean = L.o_gmean; h.o_gcon = L.o_gcon; h.o_fsrows = L0.o_fsrows;
     h.stamp = ++stamp_counter;
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);

@@ -32,41 +32,45 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 
 // --------------------------------------------------------------------------- packing
 template <int FN, int D, int CB>
-__global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *__restrict__ means,
-                             const float *__restrict__ conics, const float *__restrict__ values,
-                             int C, int cbase, float *__restrict__ rows, float4 *__restrict__ crows) {
+__global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *__restrict__ values, int C,
+                             int cbase, float *__restrict__ rows) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
+    // means / conics were packed in internal order at binning (coalesced here); only the
+    // values are gathered through perm
     const Header *h = reinterpret_cast<const Header *>(gbuf);
     const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
-    const int64_t g = perm[i];
-    constexpr int S = D * (D + 1) / 2, RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
-    const float c[3] = {conics[g * S], D == 2 ? conics[g * S + 1] : 0.0f, D == 2 ? conics[g * S + 2] : 0.0f};
+    const float2 mm = reinterpret_cast<const float2 *>(gbuf + h->o_gmean)[i];
+    const float4 cc = reinterpret_cast<const float4 *>(gbuf + h->o_gcon)[i];
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    const float c[3] = {cc.x, cc.y, cc.z};
     float out[RS];
 #pragma unroll
     for (int k = 0; k < RS; ++k) out[k] = 0.0f;
     if constexpr (D == 2) {
-        out[0] = means[g * 2];
-        out[1] = means[g * 2 + 1];
+        out[0] = mm.x;
+        out[1] = mm.y;
         out[2] = -0.5f * kLog2e * c[0];
         out[3] = -kLog2e * c[1];
         out[4] = -0.5f * kLog2e * c[2];
         if constexpr (FN != 0) { out[5] = c[0]; out[6] = c[1]; out[7] = c[2]; }
     } else {
-        out[0] = means[g];
+        out[0] = mm.x;
         out[1] = -0.5f * kLog2e * c[0];
         if constexpr (FN != 0) out[2] = c[0];
     }
+    if (CB > 0 && cbase < C) {
+        const int64_t g = perm[i];
 #pragma unroll
-    for (int ch = 0; ch < CB; ++ch) {
-        const int gc = cbase + ch;
-        out[B + ch] = gc < C ? values[g * C + gc] : 0.0f;
+        for (int ch = 0; ch < CB; ++ch) {
+            const int gc = cbase + ch;
+            out[B + ch] = gc < C ? values[g * C + gc] : 0.0f;
+        }
     }
     float *row = rows + i * RS;
 #pragma unroll
     for (int k = 0; k < RS; k += 4)
         *reinterpret_cast<float4 *>(row + k) = make_float4(out[k], out[k + 1], out[k + 2], out[k + 3]);
-    crows[i] = make_float4(c[0], c[1], c[2], 0.0f);
 }
 
 // Sample rows of the backward.  Packed layout (kPairRows): samples j = 2p, 2p+1 share the
@@ -90,8 +94,10 @@ __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char 
         const Header *h = reinterpret_cast<const Header *>(gbuf);
         const int32_t *sorted = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted);
         const int64_t sid = sorted[j];
-        out[0] = samples[sid * D];
-        if constexpr (D == 2) out[1] = samples[sid * D + 1];
+        // coordinates from the binning's sorted pair rows (coalesced); only dL is gathered
+        const float *fr = reinterpret_cast<const float *>(sbuf + h->o_fsrows) + (j >> 1) * (2 * D) + (j & 1);
+        out[0] = fr[0];
+        if constexpr (D == 2) out[1] = fr[2];
         const float *d = dL + sid * K * C;
 #pragma unroll
         for (int k = 0; k < K; ++k) {
@@ -272,13 +278,13 @@ template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
                                                       const float *__restrict__ grows,
-                                                      const float *__restrict__ fsrows,
                                                       float *__restrict__ out, int C, int cbase) {
     using Tr = Traits<FN, D>;
     constexpr int U = Tr::U, K = Tr::K, UC = U * CB, RS = grow_stride<FN, D, CB>(), B = Tr::GBASE;
     constexpr int NP = 32 / UC, NS = 2 * NP;  // sample pairs / samples per pass
     static_assert(NP >= 1 && NS * UC <= 64, "accumulator does not fit the reduce-scatter");
     const Bins bins = resolve(gbuf, sbuf);
+    const float *__restrict__ fsrows = bins.fsrows;
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
@@ -390,7 +396,6 @@ template <int FN, int D, int CB, bool TAIL>
 __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbuf,
                                                     const char *__restrict__ sbuf,
                                                     const float *__restrict__ grows,
-                                                    const float4 *__restrict__ crows,
                                                     const float *__restrict__ samples,
                                                     float *__restrict__ out, int C, int cbase) {
     constexpr int U = Traits<FN, D>::U, K = Traits<FN, D>::K;
@@ -413,7 +418,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
         for (int a = 0; a < U; ++a)
 #pragma unroll
             for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
-        fwd_accumulate<FN, D, CB, TAIL>(bins, grows, crows, TAIL ? gm : gb, ge, gm, s0, s1, acc);
+        fwd_accumulate<FN, D, CB, TAIL>(bins, grows, bins.gcon, TAIL ? gm : gb, ge, gm, s0, s1, acc);
         if (active) {
             float *o = out + sid * K * C;
 #pragma unroll
@@ -429,25 +434,6 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
             }
         }
     }
-}
-
-// Forward sample pair rows (transposed form): pair p = sorted samples (2p, 2p+1), fields
-// interleaved [s0 s0' (s1 s1')]; a missing second sample (odd N) is 0.
-template <int D>
-__global__ void k_pack_fsamples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
-                                const float *__restrict__ samples, float *__restrict__ rows) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (int64_t)(N + 1) / 2 * 2) return;
-    float s[2] = {0.0f, 0.0f};
-    if (j < N) {
-        const Header *h = reinterpret_cast<const Header *>(gbuf);
-        const int64_t sid = reinterpret_cast<const int32_t *>(sbuf + h->o_sorted)[j];
-        s[0] = samples[sid * D];
-        if constexpr (D == 2) s[1] = samples[sid * D + 1];
-    }
-    float *row = rows + (j >> 1) * (2 * D) + (j & 1);
-#pragma unroll
-    for (int f = 0; f < D; ++f) row[2 * f] = s[f];
 }
 
 // ------------------------------------------------------------------ backward kernel
@@ -548,7 +534,6 @@ template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gbuf,
                                                      const char *__restrict__ sbuf,
                                                      const float *__restrict__ grows,
-                                                     const float4 *__restrict__ crows,
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0) {
     using Tr = Traits<FN, D>;
@@ -572,7 +557,7 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
             const float4 q = *reinterpret_cast<const float4 *>(grow + k);
             r[k] = q.x; r[k + 1] = q.y; r[k + 2] = q.z; r[k + 3] = q.w;
         }
-        const float4 cr = crows[id];
+        const float4 cr = bins.gcon[id];
         const bool wrap = (ent & kGeneral) != 0;
         const bool unsafe = (ent & kUnsafe) != 0;
         const float c[3] = {cr.x, cr.y, cr.z};
@@ -628,7 +613,6 @@ template <int D>
 __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
                                                   const char *__restrict__ sbuf,
                                                   const float *__restrict__ grows,
-                                                  const float4 *__restrict__ crows,
                                                   const float *__restrict__ samples, float thr,
                                                   unsigned long long *__restrict__ counts) {
     constexpr int RS = grow_stride<0, D, 1>();
@@ -646,7 +630,7 @@ __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
         for (int e = gb; e < ge; ++e) {
             const int64_t id = sload(&bins.entries[e]) & kIdMask;
             const float *row = grows + id * RS;
-            const float4 cr = sload(&crows[id]);
+            const float4 cr = sload(&bins.gcon[id]);
             const float c[3] = {cr.x, cr.y, cr.z};
             float X[2] = {ref_wrap(sload(row) - s0), D == 2 ? ref_wrap(sload(row + 1) - s1) : 0.0f};
             const float p = ref_power<0, D>(X, c);
@@ -695,18 +679,15 @@ static int srow_stride_rt(int FN, int D, int CB) { return (D + unique_rt(FN, D) 
 static size_t a256(size_t x) { return align_up(x, 256); }
 
 struct WsLayout {
-    size_t grows, crows, fsrows, srows, acc, total;
+    size_t grows, srows, acc, total;
 };
 static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
     WsLayout w;
     w.grows = a256((size_t)P * grow_stride_rt(FN, D, CB) * 4 + 64);
-    w.crows = a256((size_t)P * 16 + 64);
-    // forward pair rows; a pass reads up to 32 pairs (+ one x16 load) past the last pair
-    w.fsrows = backward ? 0 : a256(((size_t)N + 1) * D * 4 + 36 * 16);
     w.srows = backward ? a256(((size_t)N + 1) * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;  // pair rows: N rounded up to even
     w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
-    w.total = w.grows + w.crows + w.fsrows + w.srows + w.acc;
+    w.total = w.grows + w.srows + w.acc;
     return w;
 }
 
@@ -747,33 +728,25 @@ template <int FN, int D, int CB>
 static int run_forward(const Call &a) {
     const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, false);
     float *grows = reinterpret_cast<float *>(a.ws);
-    float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
-    float *fsrows = reinterpret_cast<float *>(a.ws + w.grows + w.crows);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
     constexpr bool T = fwd_transposed<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
     const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
-    if constexpr (T) {
-        k_pack_fsamples<D><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples, fsrows);
-        DGS_LAUNCH_CHECK(a.s, a.debug);
-    }
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
-                                                                 a.values, a.C, cbase, grows, crows);
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         {
             KernelTimer t(0, a.s);
             if constexpr (T)
-                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, fsrows, a.out,
-                                                                     a.C, cbase);
+                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.out, a.C, cbase);
             else
-                k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows,
+                k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                           a.samples, a.out, a.C, cbase);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if constexpr (T) {
             if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
-                k_forward<FN, D, CB, true><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows,
+                k_forward<FN, D, CB, true><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                          a.samples, a.out, a.C, cbase);
                 DGS_LAUNCH_CHECK(a.s, a.debug);
             }
@@ -786,15 +759,13 @@ template <int FN, int D, int CB>
 static int run_backward(const Call &a) {
     const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, true);
     float *grows = reinterpret_cast<float *>(a.ws);
-    float4 *crows = reinterpret_cast<float4 *>(a.ws + w.grows);
-    float *srows = reinterpret_cast<float *>(a.ws + w.grows + w.crows);
-    float *acc = reinterpret_cast<float *>(a.ws + w.grows + w.crows + w.srows);
+    float *srows = reinterpret_cast<float *>(a.ws + w.grows);
+    float *acc = reinterpret_cast<float *>(a.ws + w.grows + w.srows);
     constexpr int S = D * (D + 1) / 2;
     DGS_TRY_HIP(hipMemsetAsync(acc, 0, w.acc, a.s));
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.means, a.conics,
-                                                                 a.values, a.C, cbase, grows, crows);
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
                                                                       a.dL, a.C, cbase, srows);
@@ -802,7 +773,7 @@ static int run_backward(const Call &a) {
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s);
-            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, crows, srows, acc,
+            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc,
                                                                 a.P, D + S + cbase);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
@@ -920,17 +891,16 @@ extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const fl
     const char *gb = static_cast<const char *>(binning), *sb = static_cast<const char *>(sample_binning);
     const WsLayout w = ws_layout(0, P, D, N, 1, false);
     float *grows = static_cast<float *>(workspace);
-    float4 *crows = reinterpret_cast<float4 *>(static_cast<char *>(workspace) + w.grows);
     unsigned long long *dcnt = reinterpret_cast<unsigned long long *>(
         static_cast<char *>(workspace) + need - 256);
     DGS_TRY_HIP(hipMemsetAsync(dcnt, 0, 16, s));
     const unsigned blocks = unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false);
     if (D == 2) {
-        k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
-        k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
+        k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows);
+        k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
     } else {
-        k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, means, conics, conics, 0, 0, grows, crows);
-        k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, crows, samples, thr, dcnt);
+        k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows);
+        k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
     }
     DGS_TRY_HIP(hipGetLastError());
     unsigned long long h[2];
