@@ -17,9 +17,9 @@ import sysconfig
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-PKG = os.path.join(HERE, "diff_gaussian_sampling")
+PKG = os.environ.get("DGS_PKG_OUT", os.path.join(HERE, "diff_gaussian_sampling"))  # variants: tools/variant.sh
 INCLUDE = os.path.join(REPO, "include")
-OBJ = os.path.join(HERE, "build")
+OBJ = os.environ.get("DGS_OBJ_OUT", os.path.join(HERE, "build"))
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("DGS_OFFLOAD_ARCH", "gfx950")
 LIB = os.path.join(PKG, "libdgs.so")

@@ -531,7 +531,7 @@ static double cell_target() {
     static const double t = [] {
         const char *e = std::getenv("DGS_CELL_TARGET");
         const double v = e ? std::atof(e) : 0.0;
-        return v > 0.0 ? v : 100.0;
+        return v > 0.0 ? v : 150.0;
     }();
     return t;
 }

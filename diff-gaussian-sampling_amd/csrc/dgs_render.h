@@ -16,6 +16,10 @@ namespace dgs {
 
 constexpr float kLog2e = 1.4426950408889634f;
 
+#ifndef DGS_VFACTOR
+#define DGS_VFACTOR 1  // backward, gaussian, C = 1: moments of G dL, scaled by v per unit
+#endif
+
 template <int FN, int D>
 struct Traits {
     static constexpr int K = FN == 0 ? 1 : FN == 1 ? D : FN == 2 ? D * D : D * D * D;  // out comps
@@ -266,10 +270,18 @@ __device__ __forceinline__ void bwd_terms(const V *X, const float *c, V G, const
         Gu[u] = s;  // dL_dG (per unique component), reference's dL_dG* sums
     }
     if constexpr (FN == 0) {
-        // moments: gm = -[A (sum t X)], gc = -1/2 sum t X X^T (off-diagonal -sum t X0 X1)
+        // moments: gm = -[A (sum t X)], gc = -1/2 sum t X X^T (off-diagonal -sum t X0 X1).
+        // CB = 1: t = v * (G dL) -- the moments accumulate w = G dL (also the values gradient)
+        // and k_backward scales them by v once per unit (one op per pair fewer).
+        V t;
+        if constexpr (CB == 1 && DGS_VFACTOR) {
+            t = G * dl[0][0];
+            gv[0] += t;
+        } else {
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = vfma(G, dl[0][ch], gv[ch]);
-        const V t = G * Gu[0];
+            for (int ch = 0; ch < CB; ++ch) gv[ch] = vfma(G, dl[0][ch], gv[ch]);
+            t = G * Gu[0];
+        }
         const V tx = t * X[0];
         gm[0] += tx;                              // sum t X0
         gc[0] = vfma(tx, X[0], gc[0]);            // sum t X0^2

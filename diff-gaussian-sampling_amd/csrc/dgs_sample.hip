@@ -203,6 +203,7 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // whole cell list; one cross-lane reduce-scatter per pass then leaves sum (sample, comp) =
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
+
 template <int FN, int D, int CB>
 __host__ __device__ constexpr bool fwd_transposed() { return Traits<FN, D>::U * CB <= 4; }
 
@@ -215,11 +216,12 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
                                             const float *m, const float *sh, const float *c,
                                             const float *kk, const float *v,
                                             f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
-    constexpr int PRF = 2 * D, PPL = 16 / PRF;  // floats per pair row, pairs per s_load_dwordx16
+    constexpr int LW = 16;  // (x8 loads measured 6x slower: the unrolled pass stopped interleaving)
+    constexpr int PRF = 2 * D, PPL = LW / PRF;  // floats per pair row, pairs per s_load_dwordx16
 #pragma unroll
     for (int q = 0; q < NP; q += PPL) {
         if (q >= np) break;
-        const F32s<16> sr = sload_f<16>(fsrows + (int64_t)(p0 + q) * PRF);
+        const F32s<LW> sr = sload_f<LW>(fsrows + (int64_t)(p0 + q) * PRF);
 #pragma unroll
         for (int j = 0; j < PPL; ++j) {
             if (q + j < NP) {
@@ -237,40 +239,65 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
 }
 
 // Cell-list entries [eb, ee) against the pass's sample pairs, 64 Gaussians (lanes) at a time.
+template <int RS>
+__device__ __forceinline__ void load_grow(const float *__restrict__ grows, uint32_t ent, float (&r)[RS]) {
+    const float *grow = grows + (int64_t)(ent & kIdMask) * RS;
+#pragma unroll
+    for (int k = 0; k < RS; k += 4) {
+        const float4 qv = *reinterpret_cast<const float4 *>(grow + k);
+        r[k] = qv.x; r[k + 1] = qv.y; r[k + 2] = qv.z; r[k + 3] = qv.w;
+    }
+}
+
+// One group: the lane's row r (entry ent; `active` = a real entry) against the pass's pairs.
+template <int FN, int D, int CB, int NP, bool FLAGGED>
+__device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, float (&r)[grow_stride<FN, D, CB>()],
+                                            uint32_t ent, bool active, int p0, int np, const float *ctr,
+                                            f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0: its row
+    // is zeroed (finite, zero values)
+    if (!active || (FLAGGED && (ent & kUnsafe))) {
+#pragma unroll
+        for (int k = 0; k < RS; ++k) r[k] = 0.0f;
+    }
+    float c[3];
+    row_conic<FN, D, RS>(r, c);
+    const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
+    float sh[2] = {0.0f, 0.0f};  // the lane's constant wrap shift (kGeneral entries)
+    if constexpr (FLAGGED) {
+        if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+        }
+    }
+    fwd_t_pairs<FN, D, CB, NP, FLAGGED>(fsrows, p0, np, m, sh, c, &r[D], &r[B], acc);
+}
+
+// Software-pipelined over the groups: group g + 1's rows and group g + 2's entries are in
+// flight while group g is evaluated (each group otherwise starts with two dependent memory
+// round trips, entry then row).
 template <int FN, int D, int CB, int NP, bool FLAGGED>
 __device__ __forceinline__ void fwd_t_groups(const Bins &bins, const float *__restrict__ grows,
                                              const float *__restrict__ fsrows, int eb, int ee,
                                              int p0, int np, int lane, const float *ctr,
                                              f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
-    constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    constexpr int RS = grow_stride<FN, D, CB>();
+    if (eb >= ee) return;
+    const int last = ee - 1;
+    uint32_t e_cur = bins.entries[min(eb + lane, last)];
+    uint32_t e_nxt = bins.entries[min(eb + kWave + lane, last)];
+    float r_cur[RS];
+    load_grow<RS>(grows, e_cur, r_cur);
     for (int g0 = eb; g0 < ee; g0 += kWave) {
-        const bool active = g0 + lane < ee;
-        const uint32_t ent = bins.entries[active ? g0 + lane : eb];
-        const int64_t id = ent & kIdMask;
-        const float *grow = grows + id * RS;
-        float r[RS];
+        float r_nxt[RS];
+        load_grow<RS>(grows, e_nxt, r_nxt);  // (a clamped, valid row past the list's end)
+        const uint32_t e_nn = bins.entries[min(g0 + 2 * kWave + lane, last)];
+        fwd_t_group<FN, D, CB, NP, FLAGGED>(fsrows, r_cur, e_cur, g0 + lane < ee, p0, np, ctr, acc);
 #pragma unroll
-        for (int k = 0; k < RS; k += 4) {
-            const float4 qv = *reinterpret_cast<const float4 *>(grow + k);
-            r[k] = qv.x; r[k + 1] = qv.y; r[k + 2] = qv.z; r[k + 3] = qv.w;
-        }
-        // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0: its row
-        // is zeroed (finite, zero values)
-        if (!active || (FLAGGED && (ent & kUnsafe))) {
-#pragma unroll
-            for (int k = 0; k < RS; ++k) r[k] = 0.0f;
-        }
-        float c[3];
-        row_conic<FN, D, RS>(r, c);
-        const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
-        float sh[2] = {0.0f, 0.0f};  // the lane's constant wrap shift (kGeneral entries)
-        if constexpr (FLAGGED) {
-            if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
-#pragma unroll
-                for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
-            }
-        }
-        fwd_t_pairs<FN, D, CB, NP, FLAGGED>(fsrows, p0, np, m, sh, c, &r[D], &r[B], acc);
+        for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
+        e_cur = e_nxt;
+        e_nxt = e_nn;
     }
 }
 
@@ -530,66 +557,86 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
     }
 }
 
+// One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
+// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane.
+template <int FN, int D, int CB>
+__device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows,
+                                         float *__restrict__ acc, int P, int vrow0, uint2 u,
+                                         uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
+                                         float4 cr, int lane) {
+    using Tr = Traits<FN, D>;
+    using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
+    constexpr int B = Tr::GBASE, S = Tr::S;
+    const int cell = (int)u.x, eb = (int)u.y;
+    const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
+    const bool active = eb + lane < ee;
+    const int64_t id = ent & kIdMask;
+    const bool wrap = (ent & kGeneral) != 0;
+    const bool unsafe = (ent & kUnsafe) != 0;
+    const float c[3] = {cr.x, cr.y, cr.z};
+    const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
+    const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+    V gm[2] = {bc<V>(0.0f), bc<V>(0.0f)}, gc[3] = {bc<V>(0.0f), bc<V>(0.0f), bc<V>(0.0f)}, gv[CB];
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) gv[ch] = bc<V>(0.0f);
+    float sh[2] = {0.0f, 0.0f};
+    if (__any(active && unsafe)) {
+        bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
+    } else if (__any(active && wrap)) {
+        if (active && wrap) {
+            float ctr[2];
+            cell_center<D>(bins, cell, ctr);
+#pragma unroll
+            for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+        }
+        bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+    } else {
+        bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+    }
+    if (active) {
+        float sm[2] = {hsum(gm[0]), hsum(gm[1])}, sc[3] = {hsum(gc[0]), hsum(gc[1]), hsum(gc[2])};
+        if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) sm[d] *= r[B];
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sc[k] *= r[B];
+        }
+        bwd_finish<FN, D>(c, sm, sc);
+#pragma unroll
+        for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
+#pragma unroll
+        for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, hsum(gv[ch]));
+    }
+}
+
+// The lane's entry of unit u (clamped to the unit's last entry for padding lanes).
+__device__ __forceinline__ uint32_t bwd_entry(const Bins &bins, uint2 u, int lane) {
+    const int ee = min((int)u.y + kWave, sload(&bins.cell_gend[u.x]));
+    return bins.entries[min((int)u.y + lane, ee - 1)];
+}
+
+// One wave per unit (exact grid from the preprocess hint; grid-strided otherwise).  A
+// persistent, software-pipelined form (rows of unit k + 1 in flight during unit k) measured
+// 5-15 % slower: the hardware's dynamic wave dispatch balances the uneven units better.
 template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gbuf,
                                                      const char *__restrict__ sbuf,
                                                      const float *__restrict__ grows,
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0) {
-    using Tr = Traits<FN, D>;
-    using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
-    constexpr int RS = grow_stride<FN, D, CB>(), B = Tr::GBASE, S = Tr::S;
+    constexpr int RS = grow_stride<FN, D, CB>();
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumBwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
     for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
         const uint2 u = sload(&bins.bwd_units[unit]);
-        const int cell = (int)u.x, eb = (int)u.y;
-        const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
-        const bool active = eb + lane < ee;
-        const uint32_t ent = bins.entries[active ? eb + lane : eb];
-        const int64_t id = ent & kIdMask;
-        const float *grow = grows + id * RS;
+        const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
-#pragma unroll
-        for (int k = 0; k < RS; k += 4) {
-            const float4 q = *reinterpret_cast<const float4 *>(grow + k);
-            r[k] = q.x; r[k + 1] = q.y; r[k + 2] = q.z; r[k + 3] = q.w;
-        }
-        const float4 cr = bins.gcon[id];
-        const bool wrap = (ent & kGeneral) != 0;
-        const bool unsafe = (ent & kUnsafe) != 0;
-        const float c[3] = {cr.x, cr.y, cr.z};
-        const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
-        const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
-        V gm[2] = {bc<V>(0.0f), bc<V>(0.0f)}, gc[3] = {bc<V>(0.0f), bc<V>(0.0f), bc<V>(0.0f)}, gv[CB];
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch) gv[ch] = bc<V>(0.0f);
-        float sh[2] = {0.0f, 0.0f};
-        if (__any(active && unsafe)) {
-            bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
-        } else if (__any(active && wrap)) {
-            if (active && wrap) {
-                float ctr[2];
-                cell_center<D>(bins, cell, ctr);
-#pragma unroll
-                for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
-            }
-            bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
-        } else {
-            bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
-        }
-        if (active) {
-            float sm[2] = {hsum(gm[0]), hsum(gm[1])}, sc[3] = {hsum(gc[0]), hsum(gc[1]), hsum(gc[2])};
-            bwd_finish<FN, D>(c, sm, sc);
-#pragma unroll
-            for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
-#pragma unroll
-            for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
-#pragma unroll
-            for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, hsum(gv[ch]));
-        }
+        load_grow<RS>(grows, ent, r);
+        bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane);
     }
 }
 
@@ -603,6 +650,15 @@ __global__ void k_finalize(int P, int D, int C, const char *__restrict__ gbuf,
     const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
     const int64_t g = perm[i];
     const int S = D * (D + 1) / 2;
+    if (D == 2 && C == 1 && (reinterpret_cast<uintptr_t>(dmeans) & 7) == 0) {  // 4 stores, not 6
+        *reinterpret_cast<float2 *>(dmeans + g * 2) = make_float2(acc[i], acc[P + i]);
+        float *o = dconics + g * 3;
+        o[0] = acc[2 * (int64_t)P + i];
+        o[1] = acc[3 * (int64_t)P + i];
+        o[2] = acc[4 * (int64_t)P + i];
+        dvalues[g] = acc[5 * (int64_t)P + i];
+        return;
+    }
     for (int d = 0; d < D; ++d) dmeans[g * D + d] = acc[(int64_t)d * P + i];
     for (int k = 0; k < S; ++k) dconics[g * S + k] = acc[(int64_t)(D + k) * P + i];
     for (int ch = 0; ch < C; ++ch) dvalues[g * C + ch] = acc[(int64_t)(D + S + ch) * P + i];
