@@ -19,7 +19,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 2;
+constexpr uint32_t kVersion = 3;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -94,7 +94,7 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     Layout L;
     size_t o = kHeaderBytes;
     L.o_counts = o;    o = align_up(o + 16, 256);
-    L.o_perm = o;      o = align_up(o + 4 * (size_t)P, 256);
+    L.o_perm = o;      o = align_up(o + 8 * (size_t)P, 256);  // perm[P], then its inverse[P]
     L.o_cell_gbeg = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_cell_gmid = o; o = align_up(o + 4 * (size_t)ncells, 256);
     L.o_cell_gend = o; o = align_up(o + 4 * (size_t)ncells, 256);

@@ -514,9 +514,13 @@ __global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, cons
     for (int f = 0; f < D; ++f) row[2 * f] = s[f];
 }
 
-__global__ void k_copy_u32(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
+// perm (internal -> caller id) and its inverse, stored back to back.
+__global__ void k_perm_pair(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) b[i] = (int32_t)a[i];
+    if (i >= n) return;
+    const uint32_t g = a[i];
+    b[i] = (int32_t)g;
+    b[n + g] = (int32_t)i;
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -740,7 +744,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipMemsetAsync(counters, 0, 16, s));
     DGS_TRY_HIP(hipMemsetAsync(hbeg, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
     DGS_TRY_HIP(hipMemsetAsync(hend, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
-    k_copy_u32<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
+    k_perm_pair<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
     DGS_LAUNCH_CHECK(s, debug);
     k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
                                               reinterpret_cast<float2 *>(gbuf + L.o_gmean),

@@ -640,28 +640,46 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
     }
 }
 
-// Internal (spatial) order -> caller order.
+// Internal (spatial) order -> caller order: thread = caller id g gathers its six sums from
+// internal index inv[g] (the stores are coalesced; scattered 4-byte stores were 2-3x slower).
 __global__ void k_finalize(int P, int D, int C, const char *__restrict__ gbuf,
                            const float *__restrict__ acc, float *__restrict__ dmeans,
                            float *__restrict__ dvalues, float *__restrict__ dconics) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P) return;
     const Header *h = reinterpret_cast<const Header *>(gbuf);
-    const int32_t *perm = reinterpret_cast<const int32_t *>(gbuf + h->o_perm);
-    const int64_t g = perm[i];
+    const int32_t *inv = reinterpret_cast<const int32_t *>(gbuf + h->o_perm) + P;
+    const int64_t i = inv[g];
     const int S = D * (D + 1) / 2;
-    if (D == 2 && C == 1 && (reinterpret_cast<uintptr_t>(dmeans) & 7) == 0) {  // 4 stores, not 6
-        *reinterpret_cast<float2 *>(dmeans + g * 2) = make_float2(acc[i], acc[P + i]);
-        float *o = dconics + g * 3;
-        o[0] = acc[2 * (int64_t)P + i];
-        o[1] = acc[3 * (int64_t)P + i];
-        o[2] = acc[4 * (int64_t)P + i];
-        dvalues[g] = acc[5 * (int64_t)P + i];
-        return;
-    }
     for (int d = 0; d < D; ++d) dmeans[g * D + d] = acc[(int64_t)d * P + i];
     for (int k = 0; k < S; ++k) dconics[g * S + k] = acc[(int64_t)(D + k) * P + i];
     for (int ch = 0; ch < C; ++ch) dvalues[g * C + ch] = acc[(int64_t)(D + S + ch) * P + i];
+}
+
+// D = 2, C = 1: the six sums go through an AoS row per Gaussian (internal order, coalesced
+// transpose), then each caller id gathers one 32-byte row: 1 random sector per Gaussian
+// instead of 6 (k_finalize, 75 us at 1M Gaussians, was bound by those random sectors).
+__global__ void k_soa_to_rows(int P, const float *__restrict__ acc, float4 *__restrict__ rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    rows[2 * i] = make_float4(acc[i], acc[P + i], acc[2 * (int64_t)P + i], acc[3 * (int64_t)P + i]);
+    rows[2 * i + 1] = make_float4(acc[4 * (int64_t)P + i], acc[5 * (int64_t)P + i], 0.0f, 0.0f);
+}
+
+__global__ void k_finalize_rows(int P, const char *__restrict__ gbuf, const float4 *__restrict__ rows,
+                                float *__restrict__ dmeans, float *__restrict__ dvalues,
+                                float *__restrict__ dconics) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P) return;
+    const Header *h = reinterpret_cast<const Header *>(gbuf);
+    const int64_t i = (reinterpret_cast<const int32_t *>(gbuf + h->o_perm) + P)[g];
+    const float4 a = rows[2 * i], b = rows[2 * i + 1];
+    dmeans[2 * g] = a.x;
+    dmeans[2 * g + 1] = a.y;
+    dconics[3 * g] = a.z;
+    dconics[3 * g + 1] = a.w;
+    dconics[3 * g + 2] = b.x;
+    dvalues[g] = b.y;
 }
 
 // ------------------------------------------------------------- diagnostic pair count
@@ -833,6 +851,16 @@ static int run_backward(const Call &a) {
                                                                 a.P, D + S + cbase);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
+    }
+    if constexpr (D == 2 && CB == 1 && grow_stride<FN, D, CB>() >= 8) {
+        if (a.C == 1) {  // the Gaussian-row region is free again: AoS rows there
+            float4 *rows = reinterpret_cast<float4 *>(a.ws);
+            k_soa_to_rows<<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, acc, rows);
+            DGS_LAUNCH_CHECK(a.s, a.debug);
+            k_finalize_rows<<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, rows, a.dm, a.dv, a.dc);
+            DGS_LAUNCH_CHECK(a.s, a.debug);
+            return DGS_OK;
+        }
     }
     k_finalize<<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, D, a.C, a.gb, acc, a.dm, a.dv, a.dc);
     DGS_LAUNCH_CHECK(a.s, a.debug);

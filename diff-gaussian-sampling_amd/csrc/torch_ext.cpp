@@ -163,9 +163,11 @@ Grads sample_backward_generic(int fn, const Tensor &means_in, const Tensor &valu
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
     const int C = (int)values.size(-1);
-    Tensor dmeans = torch::zeros({P, D}, means.options());
-    Tensor dvalues = torch::zeros({P, C}, means.options());
-    Tensor dconics = torch::zeros({P, D * (D + 1) / 2}, means.options());
+    // dgs_sample_backward overwrites every gradient element; nothing to do -> zeros
+    const auto alloc = [&](int64_t cols) {
+        return N != 0 ? torch::empty({P, cols}, means.options()) : torch::zeros({P, cols}, means.options());
+    };
+    Tensor dmeans = alloc(D), dvalues = alloc(C), dconics = alloc(D * (D + 1) / 2);
     if (P != 0 && N != 0) {
         const Tensor dL = f32(dL_in, "dL_dout_values");
         int64_t K = 1;
