@@ -293,47 +293,71 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                 fhi[d] = hi > G.n - 1 ? G.n - 1 : hi;
                 if (flo[d] > fhi[d]) { any = false; break; }
             }
+            const bool local = cull && ks[0] == 0 && ks[1] == 0 && e[0] + 3.0 * G.fs < 0.9 &&
+                               (D == 1 || e[1] + 3.0 * G.fs < 0.9);
             if (any) {
                 const int ylo = D == 2 ? flo[1] : 0, yhi = D == 2 ? fhi[1] : 0;
-                for (int fy = ylo; fy <= yhi; ++fy)
-                    for (int fx = flo[0]; fx <= fhi[0]; ++fx) {
+                for (int fy = ylo; fy <= yhi; ++fy) {
+                    int fxl = flo[0], fxh = fhi[0];
+                    if (cull && D == 2) {
+                        // The row's cells that meet the ellipse X^T A X <= q: project the
+                        // ellipse's slice over the row's X1 band onto X0 (a slice of a convex
+                        // set is convex, so "box meets ellipse" <=> the cell's X0 range meets
+                        // that interval).  Same margins as box_hits_ellipse, widened slightly:
+                        // an extra candidate only evaluates exact zeros.
+                        const double o1 = tc[1] * BS, o0 = tc[0] * BS;
+                        const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
+                        double ya = md[1] - (o1 + (fy + 1) * G.fs + slack) - epsx[1] - 2.0 * ks[1];
+                        double yb = md[1] - (o1 + fy * G.fs - slack) + epsx[1] - 2.0 * ks[1];
+                        ya = fmax(ya, -e[1]);
+                        yb = fmin(yb, e[1]);
+                        if (ya > yb) continue;
+                        const double det = c0 * c2 - c1 * c1;
+                        const double e0 = sqrt(qc * c2 / det);
+                        const double yu = fmin(fmax(-c1 * e0 / c2, ya), yb);  // argmax of the upper root
+                        const double yl = fmin(fmax(c1 * e0 / c2, ya), yb);   // argmin of the lower root
+                        const double xu = (-c1 * yu + sqrt(fmax(qc * c0 - det * yu * yu, 0.0))) / c0;
+                        const double xl = (-c1 * yl - sqrt(fmax(qc * c0 - det * yl * yl, 0.0))) / c0;
+                        const double tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
+                        const double A = md[0] - o0 - slack - epsx[0] - 2.0 * ks[0];
+                        const double B = md[0] - o0 + slack + epsx[0] - 2.0 * ks[0];
+                        const double fa = ceil((A - (xu + tol)) / G.fs - 1.0 - 1e-9);
+                        const double fb2 = floor((B - (xl - tol)) / G.fs + 1e-9);
+                        if (fa > (double)fxl) fxl = fa > (double)G.n ? G.n : (int)fa;
+                        if (fb2 < (double)fxh) fxh = fb2 < -1.0 ? -1 : (int)fb2;
+                    }
+                    for (int fx = fxl; fx <= fxh; ++fx) {
                         const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
                         if (send[cell] <= sbeg[cell]) continue;
-                        const int f[2] = {fx, fy};
-                        double xa[2] = {0, 0}, xb[2] = {0, 0};
-                        for (int d = 0; d < D; ++d) {
-                            const double o = tc[d] * BS;
-                            const double dlo = o + f[d] * G.fs - slack, dhi = o + (f[d] + 1) * G.fs + slack;
-                            xa[d] = md[d] - dhi - epsx[d];
-                            xb[d] = md[d] - dlo + epsx[d];
-                        }
-                        if (cull) {
-                            bool hit;
-                            if (D == 1) {
-                                hit = xa[0] - 2.0 * ks[0] <= e[0] && xb[0] - 2.0 * ks[0] >= -e[0];
-                            } else {
-                                hit = box_hits_ellipse(xa[0] - 2.0 * ks[0], xb[0] - 2.0 * ks[0],
-                                                       xa[1] - 2.0 * ks[1], xb[1] - 2.0 * ks[1],
-                                                       c0, c1, c2, kQCut);
-                            }
-                            if (!hit) continue;
+                        if (cull && D == 1) {
+                            const double o = tc[0] * BS;
+                            const double dlo = o + fx * G.fs - slack, dhi = o + (fx + 1) * G.fs + slack;
+                            const double xa = md[0] - dhi - epsx[0], xb = md[0] - dlo + epsx[0];
+                            if (!(xa - 2.0 * ks[0] <= e[0] && xb - 2.0 * ks[0] >= -e[0])) continue;
                         }
                         // Wrap class from the cell's actual samples (box = their bounding box;
                         // the nominal cell may reach past the last sample): kGeneral when some
                         // |X| may exceed 1 (torus wrap) -- a constant shift over the cell unless
                         // the X range crosses a wrap breakpoint, which takes the fully general
                         // per-pair path (kUnsafe).  eps covers the float rounding of m - s.
-                        const float4 bx = box[cell];
-                        const double blo[2] = {bx.x, bx.y}, bhi[2] = {bx.z, bx.w};
-                        bool inside = true, constant = true;
-                        for (int d = 0; d < D; ++d) {
-                            const double eps = 1e-6 * (1.0 + fabs((double)m[d]) + fmax(fabs(blo[d]), fabs(bhi[d])));
-                            const double wa = (double)m[d] - bhi[d] - eps, wb = (double)m[d] - blo[d] + eps;
-                            inside = inside && wa >= -1.0 && wb <= 1.0;
-                            constant = constant && wrap_shift(wa) == wrap_shift(wb);
+                        // Unshifted (k = 0) cells of a culled Gaussian lie within e + fs of its
+                        // mean, so |X| < 1 there whenever e + fs stays well below 1.
+                        uint32_t cls = 0u;
+                        if (!local) {
+                            const float4 bx = box[cell];
+                            const double blo[2] = {bx.x, bx.y}, bhi[2] = {bx.z, bx.w};
+                            bool inside = true, constant = true;
+                            for (int d = 0; d < D; ++d) {
+                                const double eps = 1e-6 * (1.0 + fabs((double)m[d]) + fmax(fabs(blo[d]), fabs(bhi[d])));
+                                const double wa = (double)m[d] - bhi[d] - eps, wb = (double)m[d] - blo[d] + eps;
+                                inside = inside && wa >= -1.0 && wb <= 1.0;
+                                constant = constant && wrap_shift(wa) == wrap_shift(wb);
+                            }
+                            cls = inside ? 0u : (constant ? kGeneral : kGeneral | kUnsafe);
                         }
-                        emit(cell, id | uflag | (inside ? 0u : (constant ? kGeneral : kGeneral | kUnsafe)));
+                        emit(cell, id | uflag | cls);
                     }
+                }
             }
             const uint32_t fb = base + (uint32_t)(G.CT - 1);
             if (send[fb] > sbeg[fb]) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
@@ -350,25 +374,37 @@ __device__ inline void load_gauss(int D, const float *__restrict__ means,
     c[2] = D == 2 ? conics[g * S + 2] : 0.0f;
 }
 
-// Bounding box of each cell's samples [min0 min1 max0 max1] (empty cells: unused).
-__global__ void k_cell_box(int ncells, int D, const int32_t *__restrict__ sbeg,
-                           const int32_t *__restrict__ send, const int32_t *__restrict__ sorted,
-                           const float *__restrict__ samples, float4 *__restrict__ box) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+// Bounding box of each cell's samples [min0 min1 max0 max1] (empty cells: unused).  One wave
+// per cell, lanes striding over the cell's samples in the packed sorted rows (k_fs_pack).
+__global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const int32_t *__restrict__ sbeg,
+                                                     const int32_t *__restrict__ send,
+                                                     const float *__restrict__ rows,
+                                                     float4 *__restrict__ box) {
+    const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
     float lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
-    for (int j = sbeg[c]; j < send[c]; ++j) {
-        const int64_t sid = sorted[j];
+    const int e = send[c];
+    for (int j = sbeg[c] + lane; j < e; j += kWave) {
+        const float *row = rows + (int64_t)(j >> 1) * (2 * D) + (j & 1);
         for (int d = 0; d < D; ++d) {
-            const float v = samples[sid * D + d];
+            const float v = row[2 * d];
             lo[d] = fminf(lo[d], v);
             hi[d] = fmaxf(hi[d], v);
         }
     }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int d = 0; d < 2; ++d) {
+            lo[d] = fminf(lo[d], __shfl_xor(lo[d], off));
+            hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off));
+        }
     if (D == 1) { lo[1] = hi[1] = 0.0f; }
-    box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
+    if (lane == 0) box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
 }
 
+// Number of fine entries of each Gaussian (k_fine_fill writes them).
 __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
                              const float *__restrict__ means, const float *__restrict__ conics,
                              const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
@@ -387,28 +423,54 @@ __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
     counts[i] = n;
 }
 
-__global__ void k_fine_fill(int P, Geom G, const uint32_t *__restrict__ perm,
-                            const float *__restrict__ means, const float *__restrict__ conics,
-                            const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
-                            const int32_t *__restrict__ send, const float4 *__restrict__ box,
-                            const uint64_t *__restrict__ offs, uint32_t *__restrict__ ekeys,
-                            uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const int64_t g = perm[i];
-    const float r = radii[g];
-    if (!(r > 0.0f)) return;
-    float m[2], c[3];
-    load_gauss(G.D, means, conics, g, m, c);
-    uint64_t o = offs[i];
+// The block's Gaussians own one contiguous output range (offs is an exclusive scan in i
+// order); it is staged in LDS and written out coalesced when it fits (per-lane runs of ~15
+// entries at 64 different addresses per store were most of this kernel's time).
+constexpr int kFillBlock = 128, kFillCap = 3072;
+
+__global__ __launch_bounds__(kFillBlock) void k_fine_fill(
+    int P, Geom G, const uint32_t *__restrict__ perm, const float *__restrict__ means,
+    const float *__restrict__ conics, const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+    const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
+    const uint64_t *__restrict__ cnts, uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals,
+    int32_t *__restrict__ counters) {
+    __shared__ uint32_t skey[kFillCap], sval[kFillCap];
+    const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
+    const int64_t i = i0 + threadIdx.x;
+    const int64_t ilast = min((int64_t)P, i0 + kFillBlock) - 1;
+    const uint64_t base = offs[i0], end = offs[ilast] + cnts[ilast];
+    const bool stage = end - base <= (uint64_t)kFillCap;
     uint32_t nunsafe = 0;
-    enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
-        ekeys[o] = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
-        evals[o] = val;
-        nunsafe += (val & kUnsafe) ? 1u : 0u;
-        ++o;
-    });
+    if (i < P) {
+        const int64_t g = perm[i];
+        const float r = radii[g];
+        if (r > 0.0f) {
+            float m[2], c[3];
+            load_gauss(G.D, means, conics, g, m, c);
+            uint64_t o = offs[i];
+            enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
+                const uint32_t key = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
+                if (stage) {
+                    skey[o - base] = key;
+                    sval[o - base] = val;
+                } else {
+                    ekeys[o] = key;
+                    evals[o] = val;
+                }
+                nunsafe += (val & kUnsafe) ? 1u : 0u;
+                ++o;
+            });
+        }
+    }
     if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
+    if (stage) {
+        __syncthreads();
+        const int n = (int)(end - base);
+        for (int k = threadIdx.x; k < n; k += kFillBlock) {
+            ekeys[base + k] = skey[k];
+            evals[base + k] = sval[k];
+        }
+    }
 }
 
 // Half-cell ranges (key = cell << 1 | flagged) -> per-cell [gbeg, gmid, gend).
@@ -682,12 +744,12 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
-    k_cell_box<<<grid_for(ncells), kBlock, 0, s>>>(ncells, D, cell_sbeg, cell_send, sorted_sid,
-                                                  samples, cell_box);
-    DGS_LAUNCH_CHECK(s, debug);
     float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
     DGS_TRY_HIP(hipMemsetAsync(fsrows, 0, fsrows_bytes(N, D), s));
     k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
+        ncells, D, cell_sbeg, cell_send, fsrows, cell_box);
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
@@ -751,8 +813,9 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
                                               reinterpret_cast<float4 *>(gbuf + L.o_gcon));
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
-        k_fine_fill<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                   cell_send, cell_box, foffs, ekeys, evals, counters);
+        k_fine_fill<<<(unsigned)((P + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
+            P, G, perm, means, conics, radii, cell_sbeg, cell_send, cell_box, foffs, fcount, ekeys,
+            evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = std::max(t_esort, t_cscan);
         DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,

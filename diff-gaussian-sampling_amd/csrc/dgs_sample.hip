@@ -255,11 +255,19 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
                                             uint32_t ent, bool active, int p0, int np, const float *ctr,
                                             f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
     constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
-    // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0: its row
-    // is zeroed (finite, zero values)
-    if (!active || (FLAGGED && (ent & kUnsafe))) {
+    // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0.  Flagged
+    // groups zero the whole row (an unsafe conic may overflow); a padding lane of a flag-free
+    // group holds a copy of a well-conditioned row (finite terms), so zero values suffice.
+    if constexpr (FLAGGED) {
+        if (!active || (ent & kUnsafe)) {
 #pragma unroll
-        for (int k = 0; k < RS; ++k) r[k] = 0.0f;
+            for (int k = 0; k < RS; ++k) r[k] = 0.0f;
+        }
+    } else {
+        if (!active) {
+#pragma unroll
+            for (int k = B; k < RS; ++k) r[k] = 0.0f;
+        }
     }
     float c[3];
     row_conic<FN, D, RS>(r, c);
