@@ -108,6 +108,12 @@ __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char 
                 if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
             }
         }
+        if constexpr (bwd_mom<FN, D, CB>()) {  // moment form: pre-scaled coefficients
+            float h[Traits<FN, D>::U];
+#pragma unroll
+            for (int u = 0; u < Traits<FN, D>::U; ++u) h[u] = out[D + u];
+            mom_coef<FN>(h, &out[D]);
+        }
     }
     if constexpr (PK) {
         float *row = rows + (j >> 1) * (2 * RSS) + (j & 1);
@@ -477,7 +483,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
 template <int FN, int D, int CB, int MODE, typename V>
 __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *sh,
                                            const float *c, const float *kk, const float *v,
-                                           bool wrap, bool unsafe, V *gm, V *gv, V *gc) {
+                                           bool wrap, bool unsafe, V *acc) {
     constexpr int U = Traits<FN, D>::U;
     V dl[U][CB];
 #pragma unroll
@@ -492,7 +498,8 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
     V G;
     if constexpr (MODE == 2) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
     else G = fast_prob<D, V>(X, kk);
-    bwd_terms<FN, D, CB, V>(X, c, G, v, dl, gm, gv, gc);
+    if constexpr (bwd_mom<FN, D, CB>()) bwd_mom_terms<FN, V>(X, c, G, &srow[D], acc);
+    else bwd_terms<FN, D, CB, V>(X, c, G, v, dl, acc, acc + 2, acc + 2 + CB);
 }
 
 // One sample pair (packed layout) as RSS f2 fields; `drop` = 1 / 2 zeroes the dL fields of the
@@ -516,8 +523,7 @@ __device__ __forceinline__ void pair_fields(const float *p, f2 (&f)[RSS], int dr
 template <int FN, int D, int CB, int MODE, typename V>
 __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict__ srows,
                                          const float *m, const float *sh, const float *c, const float *kk,
-                                         const float *v, bool wrap, bool unsafe, V *gm, V *gv,
-                                         V *gc) {
+                                         const float *v, bool wrap, bool unsafe, V *acc) {
     constexpr int RSS = srow_stride<FN, D, CB>();
     if constexpr (sizeof(V) == 4) {
         constexpr int NB = bwd_batch<RSS>();
@@ -526,11 +532,11 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
             const F32s<NB * RSS> sr = sload_f<NB * RSS>(srows + (int64_t)j0 * RSS);
 #pragma unroll
             for (int q = 0; q < NB; ++q)
-                bwd_sample<FN, D, CB, MODE, V>(&sr.v[q * RSS], m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+                bwd_sample<FN, D, CB, MODE, V>(&sr.v[q * RSS], m, sh, c, kk, v, wrap, unsafe, acc);
         }
         for (; j0 < se; ++j0) {
             const F32s<RSS> sr = sload_f<RSS>(srows + (int64_t)j0 * RSS);
-            bwd_sample<FN, D, CB, MODE, V>(sr.v, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(sr.v, m, sh, c, kk, v, wrap, unsafe, acc);
         }
     } else {
         constexpr int PR = 2 * RSS, NB = bwd_batch<PR>();
@@ -541,7 +547,7 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
         if (sb & 1) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
             pair_fields<RSS, D>(sr.v, f, 1);
-            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
             ++p;
         }
         for (; p + NB <= pf; p += NB) {
@@ -549,18 +555,18 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
 #pragma unroll
             for (int q = 0; q < NB; ++q) {
                 pair_fields<RSS, D>(&sr.v[q * PR], f, 0);
-                bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+                bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
             }
         }
         for (; p < pf; ++p) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)p * PR);
             pair_fields<RSS, D>(sr.v, f, 0);
-            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
         }
         if (se & 1) {
             const F32s<PR> sr = sload_f<PR>(srows + (int64_t)(pe - 1) * PR);
             pair_fields<RSS, D>(sr.v, f, 2);
-            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, gm, gv, gc);
+            bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
         }
     }
 }
@@ -584,12 +590,14 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
     const float c[3] = {cr.x, cr.y, cr.z};
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
-    V gm[2] = {bc<V>(0.0f), bc<V>(0.0f)}, gc[3] = {bc<V>(0.0f), bc<V>(0.0f), bc<V>(0.0f)}, gv[CB];
+    // register accumulators: [gm(2) gv(CB) gc(3)], or the kMomAcc sums of the moment form
+    constexpr int NA = bwd_mom<FN, D, CB>() ? kMomAcc : 2 + CB + 3;
+    V ra[NA];
 #pragma unroll
-    for (int ch = 0; ch < CB; ++ch) gv[ch] = bc<V>(0.0f);
+    for (int k = 0; k < NA; ++k) ra[k] = bc<V>(0.0f);
     float sh[2] = {0.0f, 0.0f};
     if (__any(active && unsafe)) {
-        bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, gm, gv, gc);
+        bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, ra);
     } else if (__any(active && wrap)) {
         if (active && wrap) {
             float ctr[2];
@@ -597,25 +605,38 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
 #pragma unroll
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
-        bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+        bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     } else {
-        bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, gm, gv, gc);
+        bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     }
     if (active) {
-        float sm[2] = {hsum(gm[0]), hsum(gm[1])}, sc[3] = {hsum(gc[0]), hsum(gc[1]), hsum(gc[2])};
-        if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
+        float sm[2], sc[3], sv[CB];
+        if constexpr (bwd_mom<FN, D, CB>()) {
+            float s[kMomAcc];
 #pragma unroll
-            for (int d = 0; d < 2; ++d) sm[d] *= r[B];
+            for (int k = 0; k < kMomAcc; ++k) s[k] = hsum(ra[k]);
+            bwd_mom_finish<FN>(c, r[B], s, sm, sc, sv[0]);
+        } else {
+            const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
+            sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) sc[k] *= r[B];
+            for (int k = 0; k < 3; ++k) sc[k] = hsum(gc[k]);
+#pragma unroll
+            for (int ch = 0; ch < CB; ++ch) sv[ch] = hsum(gv[ch]);
+            if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
+#pragma unroll
+                for (int d = 0; d < 2; ++d) sm[d] *= r[B];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) sc[k] *= r[B];
+            }
+            bwd_finish<FN, D>(c, sm, sc);
         }
-        bwd_finish<FN, D>(c, sm, sc);
 #pragma unroll
         for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
 #pragma unroll
         for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, hsum(gv[ch]));
+        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
     }
 }
 
