@@ -20,26 +20,51 @@ constexpr float kLog2e = 1.4426950408889634f;
 #define DGS_VFACTOR 1  // backward, gaussian, C = 1: moments of G dL, scaled by v per unit
 #endif
 
+// Function codes: 0..3 = gaussian, derivative, laplacian, third (dgs_function); kMulti + mask
+// = the fused form that evaluates every function of `mask` (bit f = function f) in one
+// traversal of the pairs (D = 2, C = 1; dgs_sample_forward_multi).
+constexpr int kMulti = 16;
+__host__ __device__ constexpr bool is_multi(int FN) { return FN >= kMulti; }
+__host__ __device__ constexpr int fn_mask(int FN) { return FN >= kMulti ? FN - kMulti : 1 << FN; }
+__host__ __device__ constexpr int fn_k(int f, int D) { return f == 0 ? 1 : f == 1 ? D : f == 2 ? D * D : D * D * D; }
+__host__ __device__ constexpr int fn_u(int f, int D) { return D == 1 ? 1 : f + 1; }
+// sample-row coefficient fields of the moment-form backward (mom_coef)
+__host__ __device__ constexpr int fn_mfields(int f) { return f == 0 ? 1 : f == 1 ? 2 : f == 2 ? 5 : 6; }
+__host__ __device__ constexpr int mask_sum(int M, int D, int what) {  // 0: K, 1: U, 2: fields
+    int s = 0;
+    for (int f = 0; f < 4; ++f)
+        if (M & (1 << f)) s += what == 0 ? fn_k(f, D) : what == 1 ? fn_u(f, D) : fn_mfields(f);
+    return s;
+}
+// first unique component / coefficient field of function f in a mask's block
+__host__ __device__ constexpr int mask_uoff(int M, int D, int f) { return mask_sum(M & ((1 << f) - 1), D, 1); }
+__host__ __device__ constexpr int mask_foff(int M, int f) { return mask_sum(M & ((1 << f) - 1), 2, 2); }
+
 template <int FN, int D>
 struct Traits {
-    static constexpr int K = FN == 0 ? 1 : FN == 1 ? D : FN == 2 ? D * D : D * D * D;  // out comps
-    static constexpr int U = D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4);  // unique
+    static constexpr int M = fn_mask(FN);
+    static constexpr int K = mask_sum(M, D, 0);  // output components (summed over the mask)
+    static constexpr int U = mask_sum(M, D, 1);  // unique components
     static constexpr int S = D * (D + 1) / 2;
-    static constexpr int GBASE = D == 2 ? (FN == 0 ? 5 : 8) : (FN == 0 ? 2 : 3);  // first value slot
+    static constexpr bool CONIC = (M & ~1) != 0;  // a function other than gaussian: raw conic in the row
+    static constexpr int GBASE = D == 2 ? (CONIC ? 8 : 5) : (CONIC ? 3 : 2);  // first value slot
 };
 
-// expanded component -> unique term (forward.cu:288-291, 322-329)
-template <int FN, int D>
-__host__ __device__ constexpr int unique_of(int k) {
-    if (D == 1 || FN <= 1) return k;
-    if constexpr (FN == 2) return k == 0 ? 0 : (k == 3 ? 2 : 1);
+// expanded component k of function f -> its unique term (forward.cu:288-291, 322-329)
+__host__ __device__ constexpr int unique_fk(int f, int D, int k) {
+    if (D == 1 || f <= 1) return k;
+    if (f == 2) return k == 0 ? 0 : (k == 3 ? 2 : 1);
     return k == 0 ? 0 : (k == 7 ? 3 : ((k == 1 || k == 2 || k == 4) ? 1 : 2));
 }
+template <int FN, int D>
+__host__ __device__ constexpr int unique_of(int k) { return unique_fk(FN, D, k); }
 
 template <int FN, int D, int CB>
 __host__ __device__ constexpr int grow_stride() { return (Traits<FN, D>::GBASE + CB + 3) / 4 * 4; }
 template <int FN, int D, int CB>
-__host__ __device__ constexpr int srow_stride() { return (D + Traits<FN, D>::U * CB + 3) / 4 * 4; }
+__host__ __device__ constexpr int srow_stride() {
+    return is_multi(FN) ? (D + mask_sum(fn_mask(FN), D, 2) + 3) / 4 * 4 : (D + Traits<FN, D>::U * CB + 3) / 4 * 4;
+}
 
 __device__ __forceinline__ float fast_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -213,11 +238,13 @@ __device__ __forceinline__ float ref_power(const float *X, const float *c) {
 template <int FN, int D, int CB, typename V>
 __device__ __forceinline__ void fwd_terms(const V *X, const float *c, V G, const float *v,
                                           V (&acc)[Traits<FN, D>::U][CB]) {
-    if constexpr (FN == 0) {
+    constexpr int M = fn_mask(FN), UT = Traits<FN, D>::U;
+    static_assert(!is_multi(FN) || D == 2, "the fused form is D = 2 only");
+    if constexpr (M == 1) {
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) acc[0][ch] = vfma(bc<V>(v[ch]), G, acc[0][ch]);
     } else {
-    V t[4];
+    V t[UT];
     if constexpr (D == 1) {
         const V x1 = c[0] * X[0];
         if constexpr (FN == 1) t[0] = x1;
@@ -226,25 +253,31 @@ __device__ __forceinline__ void fwd_terms(const V *X, const float *c, V G, const
     } else {
         const V a1 = vfma(bc<V>(c[1]), X[1], c[0] * X[0]);
         const V a2 = vfma(bc<V>(c[1]), X[0], c[2] * X[1]);
-        if constexpr (FN == 1) {
-            t[0] = a1; t[1] = a2;
-        } else if constexpr (FN == 2) {
-            t[0] = vfma(a1, a1, bc<V>(-c[0]));
-            t[1] = vfma(a1, a2, bc<V>(-c[1]));
-            t[2] = vfma(a2, a2, bc<V>(-c[2]));
-        } else {
+        if constexpr ((M & 1) != 0) t[mask_uoff(M, D, 0)] = bc<V>(1.0f);
+        if constexpr ((M & 2) != 0) {
+            constexpr int o = mask_uoff(M, D, 1);
+            t[o] = a1; t[o + 1] = a2;
+        }
+        if constexpr ((M & 4) != 0) {
+            constexpr int o = mask_uoff(M, D, 2);
+            t[o] = vfma(a1, a1, bc<V>(-c[0]));
+            t[o + 1] = vfma(a1, a2, bc<V>(-c[1]));
+            t[o + 2] = vfma(a2, a2, bc<V>(-c[2]));
+        }
+        if constexpr ((M & 8) != 0) {
+            constexpr int o = mask_uoff(M, D, 3);
             const V a11 = a1 * a1, a22 = a2 * a2;
-            t[0] = a1 * (3.0f * c[0] - a11);
-            t[1] = vfma(bc<V>(2.0f * c[1]), a1, a2 * (c[0] - a11));
-            t[2] = vfma(bc<V>(2.0f * c[1]), a2, a1 * (c[2] - a22));
-            t[3] = a2 * (3.0f * c[2] - a22);
+            t[o] = a1 * (3.0f * c[0] - a11);
+            t[o + 1] = vfma(bc<V>(2.0f * c[1]), a1, a2 * (c[0] - a11));
+            t[o + 2] = vfma(bc<V>(2.0f * c[1]), a2, a1 * (c[2] - a22));
+            t[o + 3] = a2 * (3.0f * c[2] - a22);
         }
     }
 #pragma unroll
     for (int ch = 0; ch < CB; ++ch) {
         const V vg = v[ch] * G;
 #pragma unroll
-        for (int u = 0; u < Traits<FN, D>::U; ++u) acc[u][ch] = vfma(vg, t[u], acc[u][ch]);
+        for (int u = 0; u < UT; ++u) acc[u][ch] = vfma(vg, t[u], acc[u][ch]);
     }
     }
 }
@@ -417,10 +450,12 @@ __device__ __forceinline__ void bwd_terms(const V *X, const float *c, V G, const
 //    S G (g0 X0 + e0) | S G (g0 X1 + g1 X0 + e1) | S G (g1 X1 + e2)]
 // and bwd_mom_finish contracts them once per unit.  The sample row carries pre-scaled h
 // coefficients (k_pack_samples, mom_coef): derivative [h0 h1], laplacian [h0 h1 h2 2h0 2h2],
-// third [3h0 h1 2h1 h2 2h2 3h3].  For the third, phi is evaluated as 3 phi = a.g + 2 c.e
+// third [3h0 h1 2h1 h2 2h2 3h3].  For the third, phi is evaluated as (a.g + 2 c.e) / 3
 // (Euler's identity on the cubic and linear parts of phi: a.g = 3 cubic + linear, and the
-// linear part is c.e), and the 1/3 is applied in the epilogue.
-// Per pair: 34 / 43 / 53 VALU ops against 46 / 103 / 140 for the reference-literal terms.
+// linear part is c.e).
+// Per pair: 34 / 43 / 54 VALU ops against 46 / 103 / 140 for the reference-literal terms.
+// The fused form (FN = kMulti + mask) sums phi, g and e over the mask's functions: all four
+// cost ~75 ops per pair against 34 + 43 + 54 + 16 in four separate passes.
 // ---------------------------------------------------------------------------------------
 #ifndef DGS_HMOM
 #define DGS_HMOM 1
@@ -428,42 +463,66 @@ __device__ __forceinline__ void bwd_terms(const V *X, const float *c, V G, const
 constexpr int kMomAcc = 11;
 
 template <int FN, int D, int CB>
-__host__ __device__ constexpr bool bwd_mom() { return DGS_HMOM && D == 2 && CB == 1 && FN >= 1; }
+__host__ __device__ constexpr bool bwd_mom() {
+    return is_multi(FN) || (DGS_HMOM && D == 2 && CB == 1 && FN >= 1);
+}
 
-// Sample-row coefficients (after s0, s1) from h[U] (dL summed over symmetric components).
-template <int FN>
-__host__ __device__ inline void mom_coef(const float *h, float *o) {
-    if constexpr (FN == 1) { o[0] = h[0]; o[1] = h[1]; }
-    else if constexpr (FN == 2) { o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = 2.0f * h[0]; o[4] = 2.0f * h[2]; }
+// Sample-row coefficients of function f (after s0, s1) from its h (dL summed over symmetric
+// components): gaussian [h], derivative [h0 h1], laplacian [h0 h1 h2 2h0 2h2],
+// third [3h0 h1 2h1 h2 2h2 3h3].
+__host__ __device__ inline void mom_coef(int f, const float *h, float *o) {
+    if (f == 0) { o[0] = h[0]; }
+    else if (f == 1) { o[0] = h[0]; o[1] = h[1]; }
+    else if (f == 2) { o[0] = h[0]; o[1] = h[1]; o[2] = h[2]; o[3] = 2.0f * h[0]; o[4] = 2.0f * h[2]; }
     else { o[0] = 3.0f * h[0]; o[1] = h[1]; o[2] = 2.0f * h[1]; o[3] = h[2]; o[4] = 2.0f * h[2]; o[5] = 3.0f * h[3]; }
 }
 
+// One pair of the moment form for the functions of mask M (the fused form sums phi, g and e
+// over them: the loss of a fused call is the sum of the functions' losses).
 template <int FN, typename V>
 __device__ __forceinline__ void bwd_mom_terms(const V *X, const float *c, V G, const V *f, V *acc) {
+    constexpr int M = fn_mask(FN);
     const V X0 = X[0], X1 = X[1];
     const V a1 = vfma(bc<V>(c[1]), X1, c[0] * X0);
     const V a2 = vfma(bc<V>(c[1]), X0, c[2] * X1);
-    V phi, g0, g1, e0, e1, e2;
-    if constexpr (FN == 1) {
-        phi = vfma(f[0], a1, f[1] * a2);
-        g0 = f[0];
-        g1 = f[1];
-    } else if constexpr (FN == 2) {
+    V phi = bc<V>(0.0f), g0 = bc<V>(0.0f), g1 = bc<V>(0.0f);
+    V e0 = bc<V>(0.0f), e1 = bc<V>(0.0f), e2 = bc<V>(0.0f);
+    constexpr bool HAS_E = (M & 12) != 0;
+    if constexpr ((M & 1) != 0) phi = f[mask_foff(M, 0)];
+    if constexpr ((M & 2) != 0) {
+        const V *h = f + mask_foff(M, 1);
+        phi = vfma(h[0], a1, vfma(h[1], a2, phi));
+        g0 = h[0];
+        g1 = h[1];
+    }
+    if constexpr ((M & 4) != 0) {
+        const V *h = f + mask_foff(M, 2);
         const V t0 = vfma(a1, a1, bc<V>(-c[0])), t1 = vfma(a1, a2, bc<V>(-c[1])),
                 t2 = vfma(a2, a2, bc<V>(-c[2]));
-        phi = vfma(f[2], t2, vfma(f[1], t1, f[0] * t0));
-        g0 = vfma(f[3], a1, f[1] * a2);
-        g1 = vfma(f[4], a2, f[1] * a1);
-    } else {
+        phi = vfma(h[2], t2, vfma(h[1], t1, vfma(h[0], t0, phi)));
+        g0 = vfma(h[3], a1, vfma(h[1], a2, g0));
+        g1 = vfma(h[4], a2, vfma(h[1], a1, g1));
+        e0 = -h[0];
+        e1 = -h[1];
+        e2 = -h[2];
+    }
+    if constexpr ((M & 8) != 0) {
+        const V *h = f + mask_foff(M, 3);
         const V p = vfma(-a1, a1, bc<V>(c[0])), r = vfma(-a1, a2, bc<V>(c[1])),
                 s = vfma(-a2, a2, bc<V>(c[2]));
-        g0 = vfma(f[3], s, vfma(f[2], r, f[0] * p));
-        g1 = vfma(f[5], s, vfma(f[4], r, f[1] * p));
-        e0 = vfma(f[0], a1, f[1] * a2);
-        e1 = vfma(f[2], a1, f[4] * a2);
-        e2 = vfma(f[3], a1, f[5] * a2);
-        const V l = vfma(bc<V>(c[2]), e2, vfma(bc<V>(c[1]), e1, c[0] * e0));
-        phi = vfma(bc<V>(2.0f), l, vfma(a2, g1, a1 * g0));  // 3 phi
+        const V q0 = vfma(h[3], s, vfma(h[2], r, h[0] * p));
+        const V q1 = vfma(h[5], s, vfma(h[4], r, h[1] * p));
+        const V E0 = vfma(h[0], a1, h[1] * a2);
+        const V E1 = vfma(h[2], a1, h[4] * a2);
+        const V E2 = vfma(h[3], a1, h[5] * a2);
+        const V l = vfma(bc<V>(c[2]), E2, vfma(bc<V>(c[1]), E1, c[0] * E0));
+        // 3 phi_third = a.g + 2 c.e (Euler's identity, see above)
+        phi = vfma(vfma(bc<V>(2.0f), l, vfma(a2, q1, a1 * q0)), bc<V>(1.0f / 3.0f), phi);
+        g0 += q0;
+        g1 += q1;
+        e0 += E0;
+        e1 += E1;
+        e2 += E2;
     }
     const V t = G * phi, u0 = G * g0, u1 = G * g1;
     const V tx = t * X0, ty = t * X1;
@@ -478,11 +537,7 @@ __device__ __forceinline__ void bwd_mom_terms(const V *X, const float *c, V G, c
     acc[8] = vfma(u0, X0, acc[8]);
     acc[9] = vfma(u1, X0, vfma(u0, X1, acc[9]));
     acc[10] = vfma(u1, X1, acc[10]);
-    if constexpr (FN == 2) {  // e = -h
-        acc[8] = vfma(-G, f[0], acc[8]);
-        acc[9] = vfma(-G, f[1], acc[9]);
-        acc[10] = vfma(-G, f[2], acc[10]);
-    } else if constexpr (FN == 3) {
+    if constexpr (HAS_E) {
         acc[8] = vfma(G, e0, acc[8]);
         acc[9] = vfma(G, e1, acc[9]);
         acc[10] = vfma(G, e2, acc[10]);
@@ -490,17 +545,15 @@ __device__ __forceinline__ void bwd_mom_terms(const V *X, const float *c, V G, c
 }
 
 // Sums -> (dmeans, dconics, dvalues) of one Gaussian (c: conic, v: value).
-template <int FN>
 __device__ __forceinline__ void bwd_mom_finish(const float *c, float v, const float *s, float *gm,
                                                float *gc, float &gv) {
-    const float k = FN == 3 ? (1.0f / 3.0f) : 1.0f;  // the third accumulated 3 phi
-    gv = k * s[0];
-    const float M0 = fmaf(-k, s[3], s[1]), M1 = fmaf(-k, s[4], s[2]);
+    gv = s[0];
+    const float M0 = s[1] - s[3], M1 = s[2] - s[4];
     gm[0] = v * fmaf(c[0], M0, c[1] * M1);
     gm[1] = v * fmaf(c[1], M0, c[2] * M1);
-    gc[0] = v * fmaf(-0.5f * k, s[5], s[8]);
-    gc[1] = v * fmaf(-k, s[6], s[9]);
-    gc[2] = v * fmaf(-0.5f * k, s[7], s[10]);
+    gc[0] = v * fmaf(-0.5f, s[5], s[8]);
+    gc[1] = v * (s[9] - s[6]);
+    gc[2] = v * fmaf(-0.5f, s[7], s[10]);
 }
 
 // Epilogue of the gaussian moment form: convert moments to gradients.

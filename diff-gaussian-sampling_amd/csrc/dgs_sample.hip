@@ -53,11 +53,11 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
         out[2] = -0.5f * kLog2e * c[0];
         out[3] = -kLog2e * c[1];
         out[4] = -0.5f * kLog2e * c[2];
-        if constexpr (FN != 0) { out[5] = c[0]; out[6] = c[1]; out[7] = c[2]; }
+        if constexpr (Traits<FN, D>::CONIC) { out[5] = c[0]; out[6] = c[1]; out[7] = c[2]; }
     } else {
         out[0] = mm.x;
         out[1] = -0.5f * kLog2e * c[0];
-        if constexpr (FN != 0) out[2] = c[0];
+        if constexpr (Traits<FN, D>::CONIC) out[2] = c[0];
     }
     if (CB > 0 && cbase < C) {
         const int64_t g = perm[i];
@@ -79,14 +79,22 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
 template <int FN, int D, int CB>
 __host__ __device__ constexpr bool pair_rows() { return srow_stride<FN, D, CB>() <= 16; }
 
+// dL of each function (indexed by function code; the fused form reads those of its mask)
+struct DLs {
+    const float *p[4];
+};
+// Output of each function (indexed by function code)
+struct Outs {
+    float *p[4];
+};
+
 template <int FN, int D, int CB>
 __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
-                               const float *__restrict__ samples, const float *__restrict__ dL,
-                               int C, int cbase, float *__restrict__ rows) {
+                               const DLs dls, int C, int cbase, float *__restrict__ rows) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     constexpr bool PK = pair_rows<FN, D, CB>();
     if (j >= (PK ? (int64_t)(N + 1) / 2 * 2 : (int64_t)N)) return;
-    constexpr int K = Traits<FN, D>::K, RSS = srow_stride<FN, D, CB>();
+    constexpr int M = fn_mask(FN), RSS = srow_stride<FN, D, CB>();
     float out[RSS];
 #pragma unroll
     for (int k = 0; k < RSS; ++k) out[k] = 0.0f;
@@ -98,21 +106,27 @@ __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char 
         const float *fr = reinterpret_cast<const float *>(sbuf + h->o_fsrows) + (j >> 1) * (2 * D) + (j & 1);
         out[0] = fr[0];
         if constexpr (D == 2) out[1] = fr[2];
-        const float *d = dL + sid * K * C;
 #pragma unroll
-        for (int k = 0; k < K; ++k) {
-            const int u = unique_of<FN, D>(k);
+        for (int f = 0; f < 4; ++f) {
+            if (!(M & (1 << f))) continue;
+            const int K = fn_k(f, D);
+            const float *d = dls.p[f] + sid * K * C;
+            if constexpr (bwd_mom<FN, D, CB>()) {  // moment form (C = 1): pre-scaled coefficients
+                float hs[4] = {0.0f, 0.0f, 0.0f, 0.0f};
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) {
-                const int gc = cbase + ch;
-                if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
+                for (int k = 0; k < K; ++k) hs[unique_fk(f, D, k)] += d[k];
+                mom_coef(f, hs, &out[D + mask_foff(M, f)]);
+            } else {  // dL summed over symmetric components, [U][CB]
+#pragma unroll
+                for (int k = 0; k < K; ++k) {
+                    const int u = unique_fk(f, D, k);
+#pragma unroll
+                    for (int ch = 0; ch < CB; ++ch) {
+                        const int gc = cbase + ch;
+                        if (gc < C) out[D + u * CB + ch] += d[k * C + gc];
+                    }
+                }
             }
-        }
-        if constexpr (bwd_mom<FN, D, CB>()) {  // moment form: pre-scaled coefficients
-            float h[Traits<FN, D>::U];
-#pragma unroll
-            for (int u = 0; u < Traits<FN, D>::U; ++u) h[u] = out[D + u];
-            mom_coef<FN>(h, &out[D]);
         }
     }
     if constexpr (PK) {
@@ -166,7 +180,7 @@ __device__ __forceinline__ f2 general_prob(f2 *X, const float *c, const float *k
 // Raw conic of a Gaussian row (FN != gaussian keeps it in the row).
 template <int FN, int D, int RS>
 __device__ __forceinline__ void row_conic(const float (&r)[RS], float *c) {
-    if constexpr (FN != 0) {
+    if constexpr (Traits<FN, D>::CONIC) {
         if constexpr (D == 2) { c[0] = r[5]; c[1] = r[6]; c[2] = r[7]; }
         else { c[0] = r[2]; c[1] = c[2] = 0.0f; }
     } else {
@@ -202,6 +216,28 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
     ctr[1] = 0.5f * (b.y + b.w);
 }
 
+// Stores (ADD: adds) the sum x of unique component ui (over the mask's functions), channel
+// ch, of sample sid into every output component of its function that maps to it.
+template <int FN, int D, bool ADD>
+__device__ __forceinline__ void store_unique(const Outs &outs, int64_t sid, int ui, int C, int ch,
+                                             float x) {
+    constexpr int M = fn_mask(FN);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        if (!(M & (1 << f))) continue;
+        const int o = mask_uoff(M, D, f), K = fn_k(f, D);
+        if (ui < o || ui >= o + fn_u(f, D)) continue;
+        float *p = outs.p[f] + sid * K * C + ch;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (unique_fk(f, D, k) == ui - o) {
+                if (ADD) p[k * C] += x;
+                else p[k * C] = x;
+            }
+        }
+    }
+}
+
 // (a) Transposed form (small accumulators, U * CB <= 4).  Lane = Gaussian of the cell list,
 // 64 at a time (rows by vector gather); the block's samples are wave-uniform, read in order
 // as packed pair rows [s0(2p) s0(2p+1) s1(2p) s1(2p+1)] through the scalar cache, and the
@@ -210,8 +246,13 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
+#ifndef DGS_MULTI_T
+#define DGS_MULTI_T 1  // fused form: transposed forward (else lane-per-sample)
+#endif
 template <int FN, int D, int CB>
-__host__ __device__ constexpr bool fwd_transposed() { return Traits<FN, D>::U * CB <= 4; }
+__host__ __device__ constexpr bool fwd_transposed() {
+    return Traits<FN, D>::U * CB <= 4 || (is_multi(FN) && DGS_MULTI_T);
+}
 
 // The pass's first `np` (<= NP, wave-uniform) sample pairs against the lane's Gaussian.
 // WRAP: some lane's entry crosses the torus seam.  Its wrap (forward.cu:149-157) is a
@@ -319,7 +360,7 @@ template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
                                                       const float *__restrict__ grows,
-                                                      float *__restrict__ out, int C, int cbase) {
+                                                      const Outs outs, int C, int cbase) {
     using Tr = Traits<FN, D>;
     constexpr int U = Tr::U, K = Tr::K, UC = U * CB, RS = grow_stride<FN, D, CB>(), B = Tr::GBASE;
     constexpr int NP = 32 / UC, NS = 2 * NP;  // sample pairs / samples per pass
@@ -368,10 +409,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
             const int slot = lane / UC, comp = lane - slot * UC;
             const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
             if (lane < NS * UC && j >= fu.lo && j < fu.hi && ch < nch) {
-                float *o = out + (int64_t)bins.sorted_sid[j] * K * C + cbase + ch;
-#pragma unroll
-                for (int k = 0; k < K; ++k)
-                    if (unique_of<FN, D>(k) == ui) o[k * C] = sum;
+                store_unique<FN, D, false>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
             }
         }
     }
@@ -438,7 +476,7 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
                                                     const char *__restrict__ sbuf,
                                                     const float *__restrict__ grows,
                                                     const float *__restrict__ samples,
-                                                    float *__restrict__ out, int C, int cbase) {
+                                                    const Outs outs, int C, int cbase) {
     constexpr int U = Traits<FN, D>::U, K = Traits<FN, D>::K;
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
@@ -461,18 +499,11 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
             for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
         fwd_accumulate<FN, D, CB, TAIL>(bins, grows, bins.gcon, TAIL ? gm : gb, ge, gm, s0, s1, acc);
         if (active) {
-            float *o = out + sid * K * C;
 #pragma unroll
-            for (int k = 0; k < K; ++k) {
-                const int ui = unique_of<FN, D>(k);
+            for (int ui = 0; ui < U; ++ui)
 #pragma unroll
-                for (int ch = 0; ch < CB; ++ch) {
-                    if (ch < nch) {
-                        if constexpr (TAIL) o[k * C + cbase + ch] += acc[ui][ch];
-                        else o[k * C + cbase + ch] = acc[ui][ch];
-                    }
-                }
-            }
+                for (int ch = 0; ch < CB; ++ch)
+                    if (ch < nch) store_unique<FN, D, TAIL>(outs, sid, ui, C, cbase + ch, acc[ui][ch]);
         }
     }
 }
@@ -615,7 +646,7 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
             float s[kMomAcc];
 #pragma unroll
             for (int k = 0; k < kMomAcc; ++k) s[k] = hsum(ra[k]);
-            bwd_mom_finish<FN>(c, r[B], s, sm, sc, sv[0]);
+            bwd_mom_finish(c, r[B], s, sm, sc, sv[0]);
         } else {
             const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
             sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
@@ -774,11 +805,14 @@ struct KernelTimer {
 // ------------------------------------------------------------------ host dispatch
 static int channel_block(int C) { return C <= 1 ? 1 : C <= 2 ? 2 : C <= 4 ? 4 : C <= 8 ? 8 : 16; }
 static int grow_stride_rt(int FN, int D, int CB) {
-    const int base = D == 2 ? (FN == 0 ? 5 : 8) : (FN == 0 ? 2 : 3);
+    const bool conic = (fn_mask(FN) & ~1) != 0;
+    const int base = D == 2 ? (conic ? 8 : 5) : (conic ? 3 : 2);
     return (base + CB + 3) / 4 * 4;
 }
-static int unique_rt(int FN, int D) { return D == 1 ? 1 : (FN == 0 ? 1 : FN == 1 ? 2 : FN == 2 ? 3 : 4); }
-static int srow_stride_rt(int FN, int D, int CB) { return (D + unique_rt(FN, D) * CB + 3) / 4 * 4; }
+static int srow_stride_rt(int FN, int D, int CB) {
+    const int M = fn_mask(FN);
+    return is_multi(FN) ? (D + mask_sum(M, D, 2) + 3) / 4 * 4 : (D + mask_sum(M, D, 1) * CB + 3) / 4 * 4;
+}
 static size_t a256(size_t x) { return align_up(x, 256); }
 
 struct WsLayout {
@@ -818,10 +852,12 @@ static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_
 
 struct Call {
     int FN, P, D, N, C;
-    const float *means, *values, *conics, *samples, *dL;
+    const float *means, *values, *conics, *samples;
+    DLs dls;
     const char *gb, *sb;
     size_t gbytes, sbytes;
-    float *out, *dm, *dv, *dc;
+    Outs outs;
+    float *dm, *dv, *dc;
     char *ws;
     hipStream_t s;
     int debug;
@@ -841,16 +877,16 @@ static int run_forward(const Call &a) {
         {
             KernelTimer t(0, a.s);
             if constexpr (T)
-                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.out, a.C, cbase);
+                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase);
             else
                 k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
-                                                                          a.samples, a.out, a.C, cbase);
+                                                                          a.samples, a.outs, a.C, cbase);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if constexpr (T) {
             if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
                 k_forward<FN, D, CB, true><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
-                                                                         a.samples, a.out, a.C, cbase);
+                                                                         a.samples, a.outs, a.C, cbase);
                 DGS_LAUNCH_CHECK(a.s, a.debug);
             }
         }
@@ -870,8 +906,8 @@ static int run_backward(const Call &a) {
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.samples,
-                                                                      a.dL, a.C, cbase, srows);
+        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.dls, a.C,
+                                                                      cbase, srows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
@@ -912,7 +948,29 @@ static int dispatch_d(const Call &a, bool bwd) {
     return a.D == 1 ? dispatch_cb<FN, 1>(a, bwd) : dispatch_cb<FN, 2>(a, bwd);
 }
 
+// Fused masks (two or more functions; D = 2, C = 1): one instantiation per mask.
+template <int M>
+static int run_multi(const Call &a, bool bwd) {
+    return bwd ? run_backward<kMulti + M, 2, 1>(a) : run_forward<kMulti + M, 2, 1>(a);
+}
+static int dispatch_multi(const Call &a, bool bwd) {
+    switch (fn_mask(a.FN)) {
+    case 3: return run_multi<3>(a, bwd);
+    case 5: return run_multi<5>(a, bwd);
+    case 6: return run_multi<6>(a, bwd);
+    case 7: return run_multi<7>(a, bwd);
+    case 9: return run_multi<9>(a, bwd);
+    case 10: return run_multi<10>(a, bwd);
+    case 11: return run_multi<11>(a, bwd);
+    case 12: return run_multi<12>(a, bwd);
+    case 13: return run_multi<13>(a, bwd);
+    case 14: return run_multi<14>(a, bwd);
+    default: return run_multi<15>(a, bwd);
+    }
+}
+
 static int dispatch(const Call &a, bool bwd) {
+    if (is_multi(a.FN)) return dispatch_multi(a, bwd);
     switch (a.FN) {
     case DGS_GAUSSIAN: return dispatch_d<0>(a, bwd);
     case DGS_DERIVATIVE: return dispatch_d<1>(a, bwd);
@@ -923,7 +981,10 @@ static int dispatch(const Call &a, bool bwd) {
 
 static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t gbytes,
                     const void *sb, size_t sbytes, size_t need, size_t have) {
-    if (FN < 0 || FN > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
+    if (FN < 0 || (FN > 3 && !is_multi(FN))) return fail(DGS_ERR_ARG, "unknown sampling function");
+    if (is_multi(FN) && (fn_mask(FN) < 1 || fn_mask(FN) > 15)) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
+    if (is_multi(FN) && (D != 2 || C != 1))
+        return fail(DGS_ERR_ARG, "the fused form supports D = 2, C = 1 (call the per-function entry points)");
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported");
     if (P < 0 || N < 0 || C < 0) return fail(DGS_ERR_ARG, "negative size");
     if (P == 0 || N == 0 || C == 0) return DGS_OK;
@@ -940,6 +1001,7 @@ static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t g
 using namespace dgs;
 
 extern "C" size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward) {
+    if (function < 0 || (function > 3 && !is_multi(function))) return 256;
     if (P <= 0 || N <= 0 || C <= 0 || (D != 1 && D != 2)) return 256;
     return ws_layout(function, P, D, N, C, backward != 0).total;
 }
@@ -950,13 +1012,16 @@ extern "C" int dgs_sample_forward(int function, int P, int D, int N, int C, cons
                                   const void *sample_binning, size_t sample_binning_bytes,
                                   float *out, void *workspace, size_t workspace_bytes,
                                   dgs_stream_t stream, int debug) {
+    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
     const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 0);
     int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
                       sample_binning_bytes, need, workspace_bytes);
     if (rc || P == 0 || N == 0 || C == 0) return rc;
-    Call a{function, P, D, N, C, means, values, conics, samples, nullptr,
+    Outs outs{{nullptr, nullptr, nullptr, nullptr}};
+    outs.p[function] = out;
+    Call a{function, P, D, N, C, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
-           binning_bytes, sample_binning_bytes, out, nullptr, nullptr, nullptr,
+           binning_bytes, sample_binning_bytes, outs, nullptr, nullptr, nullptr,
            static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
     return dispatch(a, false);
 }
@@ -968,6 +1033,7 @@ extern "C" int dgs_sample_backward(int function, int P, int D, int N, int C, con
                                    float *dL_dmeans, float *dL_dvalues, float *dL_dconics,
                                    void *workspace, size_t workspace_bytes, dgs_stream_t stream,
                                    int debug) {
+    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
     const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 1);
     int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
                       sample_binning_bytes, need, workspace_bytes);
@@ -983,10 +1049,96 @@ extern "C" int dgs_sample_backward(int function, int P, int D, int N, int C, con
         }
         return DGS_OK;
     }
-    Call a{function, P, D, N, C, means, values, conics, samples, dL_dout,
+    DLs dls{{nullptr, nullptr, nullptr, nullptr}};
+    dls.p[function] = dL_dout;
+    Call a{function, P, D, N, C, means, values, conics, samples, dls,
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
-           binning_bytes, sample_binning_bytes, nullptr, dL_dmeans, dL_dvalues, dL_dconics,
-           static_cast<char *>(workspace), s, debug};
+           binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
+           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
+    return dispatch(a, true);
+}
+
+// ------------------------------------------------------------------ fused functions
+// One traversal of the pairs for every function of `mask` (bit f = dgs_function f): the
+// forward writes each function's output, the backward takes each function's dL and returns
+// the gradients of the summed loss.  A single-bit mask is the per-function path.
+static int mask_code(int mask) {
+    if (mask < 1 || mask > 15) return -1;
+    for (int f = 0; f < 4; ++f)
+        if (mask == (1 << f)) return f;
+    return kMulti + mask;
+}
+
+extern "C" size_t dgs_sample_workspace_size_multi(int mask, int P, int D, int N, int C, int backward) {
+    const int FN = mask_code(mask);
+    return FN < 0 ? 256 : dgs_sample_workspace_size(FN, P, D, N, C, backward);
+}
+
+extern "C" int dgs_sample_forward_multi(int mask, int P, int D, int N, int C, const float *means,
+                                        const float *values, const float *conics, const float *samples,
+                                        const void *binning, size_t binning_bytes,
+                                        const void *sample_binning, size_t sample_binning_bytes,
+                                        float *const *outs, void *workspace, size_t workspace_bytes,
+                                        dgs_stream_t stream, int debug) {
+    const int FN = mask_code(mask);
+    if (FN < 0) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
+    Outs o{{nullptr, nullptr, nullptr, nullptr}};
+    for (int f = 0; f < 4; ++f) {
+        if (!(mask & (1 << f))) continue;
+        if (!outs || !outs[f]) return fail(DGS_ERR_ARG, "missing output pointer for a function of the mask");
+        o.p[f] = outs[f];
+    }
+    if (!is_multi(FN))
+        return dgs_sample_forward(FN, P, D, N, C, means, values, conics, samples, binning, binning_bytes,
+                                  sample_binning, sample_binning_bytes, o.p[FN], workspace,
+                                  workspace_bytes, stream, debug);
+    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 0);
+    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
+                      need, workspace_bytes);
+    if (rc || P == 0 || N == 0 || C == 0) return rc;
+    Call a{FN, P, D, N, C, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
+           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
+           binning_bytes, sample_binning_bytes, o, nullptr, nullptr, nullptr,
+           static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
+    return dispatch(a, false);
+}
+
+extern "C" int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float *means,
+                                         const float *values, const float *conics, const float *samples,
+                                         const float *const *dL_douts, const void *binning,
+                                         size_t binning_bytes, const void *sample_binning,
+                                         size_t sample_binning_bytes, float *dL_dmeans,
+                                         float *dL_dvalues, float *dL_dconics, void *workspace,
+                                         size_t workspace_bytes, dgs_stream_t stream, int debug) {
+    const int FN = mask_code(mask);
+    if (FN < 0) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
+    DLs d{{nullptr, nullptr, nullptr, nullptr}};
+    for (int f = 0; f < 4; ++f) {
+        if (!(mask & (1 << f))) continue;
+        if (!dL_douts || !dL_douts[f]) return fail(DGS_ERR_ARG, "missing dL_dout for a function of the mask");
+        d.p[f] = dL_douts[f];
+    }
+    if (!is_multi(FN))
+        return dgs_sample_backward(FN, P, D, N, C, means, values, conics, samples, d.p[FN], binning,
+                                   binning_bytes, sample_binning, sample_binning_bytes, dL_dmeans,
+                                   dL_dvalues, dL_dconics, workspace, workspace_bytes, stream, debug);
+    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 1);
+    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
+                      need, workspace_bytes);
+    if (rc) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0 || N == 0) {  // zero gradients (sample_points.cu:165-167)
+        if (P > 0) {
+            DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, sizeof(float) * (size_t)P * 2, s));
+            DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, sizeof(float) * (size_t)P * 3, s));
+            DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, sizeof(float) * (size_t)P, s));
+        }
+        return DGS_OK;
+    }
+    Call a{FN, P, D, N, C, means, values, conics, samples, d,
+           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
+           binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
+           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
     return dispatch(a, true);
 }
 

@@ -216,6 +216,106 @@ DGS_BWD(SampleGaussiansDerivativeBackwardCUDA, DGS_DERIVATIVE)
 DGS_BWD(SampleGaussiansLaplacianBackwardCUDA, DGS_LAPLACIAN)
 DGS_BWD(SampleGaussiansThirdBackwardCUDA, DGS_THIRD)
 
+// Fused functions (dgs_sample_{forward,backward}_multi): `functions` holds
+// distinct codes 0..3; the outputs come back in that order.  Several functions at D = 2,
+// C = 1 share one traversal of the pairs; otherwise the per-function kernels run in turn (on
+// the GPU) and the backward adds their gradients.
+static int function_mask(const std::vector<int64_t> &functions) {
+    int mask = 0;
+    for (int64_t f : functions) {
+        TORCH_CHECK(f >= 0 && f <= 3, "sampling function codes are 0..3");
+        TORCH_CHECK(!(mask & (1 << f)), "each sampling function may appear once");
+        mask |= 1 << f;
+    }
+    TORCH_CHECK(mask != 0, "no sampling function given");
+    return mask;
+}
+
+std::vector<Tensor> SampleGaussiansMulti(const std::vector<int64_t> &functions, const Tensor &means_in,
+                                         const Tensor &values_in, const Tensor &conics_in,
+                                         const Tensor &samples_in, const Tensor &binning_in,
+                                         const Tensor &sbinning_in, const bool debug) {
+    const int mask = function_mask(functions);
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    const int C = (int)values.size(-1);
+    std::vector<Tensor> outs;
+    if (functions.size() == 1 || D != 2 || C != 1) {
+        for (int64_t f : functions)
+            outs.push_back(sample_generic((int)f, means, values, conics, samples, binning_in, sbinning_in, debug));
+        return outs;
+    }
+    float *ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int64_t f : functions) {
+        std::vector<int64_t> shape{N};
+        for (int k = 0; k < f; ++k) shape.push_back(D);
+        shape.push_back(C);
+        outs.push_back(torch::full(shape, 0.0, means.options()));
+        ptr[f] = outs.back().data_ptr<float>();
+    }
+    if (P != 0 && N != 0) {
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 0);
+        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_sample_forward_multi(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                       conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(),
+                                       (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), ptr,
+                                       work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),
+              "sample_gaussians_multi");
+    }
+    return outs;
+}
+
+Grads SampleGaussiansMultiBackward(const std::vector<int64_t> &functions, const Tensor &means_in,
+                                   const Tensor &values_in, const Tensor &conics_in,
+                                   const Tensor &samples_in, const std::vector<Tensor> &dLs_in,
+                                   const Tensor &binning_in, const Tensor &sbinning_in, const bool debug) {
+    const int mask = function_mask(functions);
+    TORCH_CHECK(dLs_in.size() == functions.size(), "one dL_dout per sampling function");
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    const int C = (int)values.size(-1);
+    if (functions.size() == 1 || D != 2 || C != 1) {
+        Grads g = sample_backward_generic((int)functions[0], means, values, conics, samples, dLs_in[0],
+                                          binning_in, sbinning_in, debug);
+        for (size_t i = 1; i < functions.size(); ++i) {
+            Grads h = sample_backward_generic((int)functions[i], means, values, conics, samples, dLs_in[i],
+                                              binning_in, sbinning_in, debug);
+            std::get<0>(g).add_(std::get<0>(h));
+            std::get<1>(g).add_(std::get<1>(h));
+            std::get<2>(g).add_(std::get<2>(h));
+        }
+        return g;
+    }
+    const auto alloc = [&](int64_t cols) {
+        return N != 0 ? torch::empty({P, cols}, means.options()) : torch::zeros({P, cols}, means.options());
+    };
+    Tensor dmeans = alloc(2), dvalues = alloc(1), dconics = alloc(3);
+    if (P != 0 && N != 0) {
+        std::vector<Tensor> dLs;
+        const float *ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+        for (size_t i = 0; i < functions.size(); ++i) {
+            const int f = (int)functions[i];
+            dLs.push_back(f32(dLs_in[i], "dL_dout_values"));
+            TORCH_CHECK(dLs.back().numel() == (int64_t)N * (1 << f), "dL_dout has the wrong number of elements");
+            ptr[f] = dLs.back().data_ptr<float>();
+        }
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 1);
+        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_sample_backward_multi(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                        conics.data_ptr<float>(), samples.data_ptr<float>(), ptr,
+                                        gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
+                                        dmeans.data_ptr<float>(), dvalues.data_ptr<float>(),
+                                        dconics.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
+                                        debug ? 1 : 0),
+              "sample_gaussians_multi_backward");
+    }
+    return std::make_tuple(dmeans, dvalues, dconics);
+}
+
 // Diagnostics: (W_cand, W_live) over the pairs the forward evaluates.
 std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &conics_in,
                                         const Tensor &samples_in, const Tensor &binning_in,
@@ -419,6 +519,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     // extensions (not on the reference surface)
     m.def("preprocess_gaussians_bounded", &PreprocessBoundedCUDA);
     m.def("count_pairs", &CountPairs);
+    m.def("sample_gaussians_multi", &SampleGaussiansMulti);
+    m.def("sample_gaussians_multi_backward", &SampleGaussiansMultiBackward);
     m.def("tile_grid", &TileGrid);
     m.def("library_version", []() { return dgs_version(); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });

@@ -19,7 +19,11 @@ __all__ = [
     "sample_gaussians", "sample_gaussians_derivative", "sample_gaussians_laplacian",
     "sample_gaussians_third_derivative", "aggregate_neighbors", "preprocess_gaussians",
     "preprocess_aggregate", "call_debug", "cpu_deep_copy_tuple", "GaussianSampler",
+    "sample_gaussians_multi", "FUNCTIONS",
 ]
+
+# Function names of the fused entry point (codes of dgs_function, include/dgs.h).
+FUNCTIONS = {"gaussian": 0, "derivative": 1, "laplacian": 2, "third": 3}
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -49,6 +53,21 @@ def aggregate_neighbors(features, transform, queries, keys, frequencies, distanc
     return _AggregateNeighbors.apply(features, transform, queries, keys, frequencies,
                                      distance_transform, indices, ranges, dists, densities,
                                      inv_total_densities, debug)
+
+
+def sample_gaussians_multi(functions, means, values, conics, samples, num_rendered,
+                           binning_buffer, sample_binning_buffer, ranges, sample_ranges, debug):
+    """Several sampling functions over one binning in one traversal of the pairs (not on the
+    reference API).  `functions` is a sequence of names from FUNCTIONS
+    ("gaussian", "derivative", "laplacian", "third"), each at most once; returns their
+    outputs in that order, equal to the per-function calls within the parity tolerance.
+    Gradients flow to (means, values, conics) as the sum over the returned outputs' losses.
+    Several functions at D = 2, C = 1 share the traversal; otherwise the per-function kernels
+    run in turn."""
+    codes = tuple(FUNCTIONS[f] if isinstance(f, str) else int(f) for f in functions)
+    return _SampleGaussiansMulti.apply(codes, means, values, conics, samples, num_rendered,
+                                       binning_buffer, sample_binning_buffer, ranges,
+                                       sample_ranges, debug)
 
 
 def call_debug(func, debug, name, *args):
@@ -129,6 +148,28 @@ class _SampleGaussiansLaplacian(torch.autograd.Function):
         return call_backward(ctx, _C.sample_gaussians_laplacian_backward, grad_out, "lap_bw")
 
 
+class _SampleGaussiansMulti(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, codes, means, values, conics, samples, num_rendered, binning_buffer,
+                sample_binning_buffer, ranges, sample_ranges, debug):
+        outs = call_debug(_C.sample_gaussians_multi, debug, "multi_fw", list(codes), means, values,
+                          conics, samples, binning_buffer, sample_binning_buffer, debug)
+        ctx.codes, ctx.debug = codes, debug
+        ctx.save_for_backward(means, values, conics, samples, binning_buffer, sample_binning_buffer)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grads):
+        means, values, conics, samples, binning_buffer, sample_binning_buffer = ctx.saved_tensors
+        live = [(c, g.contiguous()) for c, g in zip(ctx.codes, grads) if g is not None]
+        if not live:
+            return (None,) * 11
+        gm, gv, gc = call_debug(_C.sample_gaussians_multi_backward, ctx.debug, "multi_bw",
+                                [c for c, _ in live], means, values, conics, samples,
+                                [g for _, g in live], binning_buffer, sample_binning_buffer, ctx.debug)
+        return (None, gm, gv, gc) + (None,) * 7
+
+
 class _SampleGaussiansThirdDerivative(torch.autograd.Function):
     @staticmethod
     def forward(ctx, *args):
@@ -200,6 +241,11 @@ class GaussianSampler:
 
     def sample_gaussians_third_derivative(self):
         return sample_gaussians_third_derivative(*self._args())
+
+    def sample_gaussians_multi(self, *functions):
+        """Outputs of several functions ("gaussian", "derivative", "laplacian", "third") in
+        one traversal of the binned pairs (see sample_gaussians_multi)."""
+        return sample_gaussians_multi(functions, *self._args())
 
     def preprocess_aggregate(self):
         (self.indices, self.ranges_agg, self.dists, self.densities,

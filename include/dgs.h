@@ -102,6 +102,30 @@ int dgs_sample_backward(int function, int P, int D, int N, int C, const float *m
                         float *dL_dmeans, float *dL_dvalues, float *dL_dconics, void *workspace,
                         size_t workspace_bytes, dgs_stream_t stream, int debug);
 
+/* Fused functions (not on the reference API): one traversal of the
+ * binned pairs for every function of `mask` (bit f set = dgs_function f, mask in 1..15), as
+ * the Physics-Informed-GS loss calls several of the four per step.  Each result equals the
+ * per-function entry point's within the parity tolerance.
+ *   forward : outs[f] = out of function f (as dgs_sample_forward; zero-filled by the caller),
+ *             for every f in mask (the other entries are ignored and may be NULL)
+ *   backward: dL_douts[f] = dL/d out of function f for every f in mask; writes the gradients
+ *             of the summed loss, sum_f <dL_douts[f], out_f>
+ * Two or more functions need D = 2 and C = 1 (DGS_ERR_ARG otherwise: call the per-function
+ * entry points and add their gradients); a single-bit mask is the per-function path. */
+size_t dgs_sample_workspace_size_multi(int mask, int P, int D, int N, int C, int backward);
+int dgs_sample_forward_multi(int mask, int P, int D, int N, int C, const float *means,
+                             const float *values, const float *conics, const float *samples,
+                             const void *binning, size_t binning_bytes, const void *sample_binning,
+                             size_t sample_binning_bytes, float *const *outs, void *workspace,
+                             size_t workspace_bytes, dgs_stream_t stream, int debug);
+int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float *means,
+                              const float *values, const float *conics, const float *samples,
+                              const float *const *dL_douts, const void *binning,
+                              size_t binning_bytes, const void *sample_binning,
+                              size_t sample_binning_bytes, float *dL_dmeans, float *dL_dvalues,
+                              float *dL_dconics, void *workspace, size_t workspace_bytes,
+                              dgs_stream_t stream, int debug);
+
 /* Diagnostics (not on the reference API): counts, over the pairs the forward evaluates,
  * W_cand (candidate pairs after culling) and W_live (pairs with power >= thr, the survey's
  * live-pair count for thr = -104).  counts[0] = W_cand, counts[1] = W_live (host, syncs). */
