@@ -14,6 +14,7 @@
 //   * Gaussians renumbered by spatial home cell (perm), per-cell Gaussian lists in ascending
 //     internal id, backward work units (cell, 64 list entries)
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -115,17 +116,23 @@ __global__ void k_bounds_final(int nparts, int D, const float *part, int *grid, 
 // Per-block tile histograms in LDS (a [-1,1)^2 domain has 16 tiles: global atomics on 16
 // words serialise), flushed with one atomic per non-empty bin.
 constexpr int kHistBins = 4096;
+constexpr int64_t kHistGrid = 1024;  // blocks of the histogram kernels (4 per CU)
+static inline unsigned hist_grid(int64_t n) {
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kHistGrid));
+}
 
 __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids,
                                uint32_t *__restrict__ tile_count) {
+    // grid-strided over a capped grid (kHistGrid blocks): the per-block LDS tile histogram is
+    // flushed once, so the global same-address atomics on the few tile counters stay few
     __shared__ uint32_t hist[kHistBins];
     const bool lds = G.T <= kHistBins;
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < N) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
+         i += (int64_t)gridDim.x * blockDim.x) {
         float s[2] = {samples[i * G.D], G.D == 2 ? samples[i * G.D + 1] : 0.0f};
         const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
         if (key < (uint32_t)G.T) {
@@ -166,52 +173,47 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
                              uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
                              uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
                              int home_w, int home_h) {
-    __shared__ uint32_t hist[kHistBins];
+    __shared__ uint32_t hist[kHistBins];  // grid-strided, capped grid: see k_sample_cells
     const bool lds = G.T <= kHistBins;
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
     __syncthreads();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const int D = G.D, S = D * (D + 1) / 2;
-    float r = 0.0f;
-    float m[2] = {0.0f, 0.0f};
-    if (i < P) {
-        m[0] = means[i * D];
-        m[1] = D == 2 ? means[i * D + 1] : 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        float r = 0.0f;
+        float m[2] = {means[i * D], D == 2 ? means[i * D + 1] : 0.0f};
         float cv[3] = {covs[i * S], D == 2 ? covs[i * S + 1] : 0.0f, D == 2 ? covs[i * S + 2] : 0.0f};
         const uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
         radii[i] = r;
         touched[i] = t;
         ids[i] = (uint32_t)i;
-        if (r > 0.0f) {
-            const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
-            for (int y = kr.y0; y < kr.y1; ++y)
-                for (int x = kr.x0; x < kr.x1; ++x) {
-                    const uint32_t key = key_of(D, x, y, G.grid);
-                    if (key < (uint32_t)G.T) {
-                        if (lds) atomicAdd(&hist[key], 1u);
-                        else atomicAdd(&tile_count[key], 1u);
-                    }
-                }
+        if (!(r > 0.0f)) {
+            home[i] = (uint32_t)home_w * (uint32_t)home_h;  // absent: after every home cell
+            continue;
         }
+        const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
+        for (int y = kr.y0; y < kr.y1; ++y)
+            for (int x = kr.x0; x < kr.x1; ++x) {
+                const uint32_t key = key_of(D, x, y, G.grid);
+                if (key < (uint32_t)G.T) {
+                    if (lds) atomicAdd(&hist[key], 1u);
+                    else atomicAdd(&tile_count[key], 1u);
+                }
+            }
+        int h[2] = {0, 0};
+        const int lim[2] = {home_w, home_h};
+        for (int d = 0; d < D; ++d) {
+            const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
+            int v = (u == u) ? (int)floor(fmin(fmax(u, -1.0), (double)lim[d])) : 0;
+            h[d] = v < 0 ? 0 : (v >= lim[d] ? lim[d] - 1 : v);
+        }
+        home[i] = (uint32_t)(h[1] * home_w + h[0]);
     }
     __syncthreads();
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x)
             if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
-    if (i >= P) return;
-    if (!(r > 0.0f)) {
-        home[i] = 0xffffffffu;
-        return;
-    }
-    int h[2] = {0, 0};
-    const int lim[2] = {home_w, home_h};
-    for (int d = 0; d < D; ++d) {
-        const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
-        int v = (u == u) ? (int)floor(fmin(fmax(u, -1.0), (double)lim[d])) : 0;
-        h[d] = v < 0 ? 0 : (v >= lim[d] ? lim[d] - 1 : v);
-    }
-    home[i] = (uint32_t)(h[1] * home_w + h[0]);
 }
 
 // Does [xa, xb] x [ya, yb] contain an X with X^T A X <= qcut?  (convex quadratic: the
@@ -587,6 +589,18 @@ __global__ void k_perm_pair(int64_t n, const uint32_t *__restrict__ a, int32_t *
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
+// Stable LSD radix sort of (u32 key, u32 value) pairs, always the onesweep algorithm: rocprim's
+// default switches to block sort + merge passes below 2^20 items (24 launches, ~170 us for the
+// 1M home keys against ~25 us here).
+static hipError_t sort_pairs_onesweep(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
+                                      const uint32_t *vin, uint32_t *vout, int n, int b0, int b1,
+                                      hipStream_t s) {
+    using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                           rocprim::default_config, 0>;
+    return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n,
+                                          (unsigned)b0, (unsigned)b1, s);
+}
+
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
 // waves per cell), capped so that cells stay reasonably large for sparse sample sets.
 // Fine cells per tile axis.  A forward unit holds up to kFwdUnit = 128 samples of one cell and
@@ -719,10 +733,10 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     // hipcub temp storage: one allocation sized for the largest phase-A primitive
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0, t_red = 0;
     const int sbits = bit_length((uint64_t)ncells);
-    const int hbits = 32;  // home keys may be 0xffffffff for absent Gaussians
+    const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_ssort, skeys, skeys_sorted, sids,
                                                    (uint32_t *)sorted_sid, N, 0, sbits, s));
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_hsort, home, home_sorted, gids,
+    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
                                                    perm, P, 0, hbits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, fcount, foffs, P, s));
     DGS_TRY_HIP(hipcub::DeviceReduce::Sum(nullptr, t_red, touched, rsum, P, s));
@@ -736,7 +750,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipMemsetAsync(cell_send, 0, sizeof(int32_t) * ncells, s));
 
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
-    k_sample_cells<<<grid_for(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
+    k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
     DGS_LAUNCH_CHECK(s, debug);
     size_t tb = t_a;
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, skeys, skeys_sorted, sids,
@@ -753,11 +767,11 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
-    k_gauss_prep<<<grid_for(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
+    k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
                                                 home, gids, home_w, home_h);
     DGS_LAUNCH_CHECK(s, debug);
     tb = t_a;
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
+    DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
