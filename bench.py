@@ -46,6 +46,9 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--function", default="gaussian", choices=list(FUNCS))
+    ap.add_argument("--functions", default=None,
+                    help="comma-separated functions evaluated by ONE fused call per step "
+                         "(sample_gaussians_multi, SURVEY 8f f2), e.g. gaussian,derivative,laplacian,third")
     ap.add_argument("--P", type=int, default=1_000_000)
     ap.add_argument("--N", type=int, default=2_000_000, help="query points per GPU")
     ap.add_argument("--C", type=int, default=1)
@@ -101,12 +104,20 @@ def main():
            "third": dgs.sample_gaussians_third_derivative}[fn]
     dLv = dL.reshape((N,) + (D,) * FUNCS[fn] + (C,))
     flat = torch.empty(P * (D + C + D * (D + 1) // 2), device=dev)
+    multi = args.functions.split(",") if args.functions else None
+    if multi:  # one dL per function of the fused call
+        dLm = [syn.grad_out(N, D ** FUNCS[f], C, seed=5 + 1000 * rank + 17 * i).to(dev).reshape(
+            (N,) + (D,) * FUNCS[f] + (C,)) for i, f in enumerate(multi)]
 
     def step():
         for t in (means, values, conics):
             t.grad = None
-        out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
-        out.backward(dLv)
+        if multi:
+            outs = dgs.sample_gaussians_multi(multi, means, values, conics, samples, R, gb, sb, rg, srg, False)
+            torch.autograd.backward(list(outs), dLm)
+        else:
+            out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
+            out.backward(dLv)
         if world > 1:
             torch.cat([means.grad.reshape(-1), values.grad.reshape(-1), conics.grad.reshape(-1)], out=flat)
             dist.all_reduce(flat)
@@ -154,8 +165,11 @@ def main():
         except Exception:
             traffic = None
 
+    if multi:  # per-pair FLOPs of the fused functions are not in SURVEY 8d: no roofline line
+        fn = "+".join(multi)
     result = {
-        "metric": "sampled points/sec (fwd+bwd), 1M Gaussians x 2M queries per GPU",
+        "metric": "sampled points/sec (fwd+bwd), 1M Gaussians x 2M queries per GPU"
+                  + (f", fused functions {fn}" if multi else ""),
         "value": value,
         "unit": "points/s",
         "n_gpus": world,
@@ -172,6 +186,8 @@ def main():
                    "gaussians": P, "query_points_per_gpu": N, "channels": C, "function": fn,
                    "parallelism": f"query-point shards x{world}, Gaussians replicated"},
         "preprocess_ms": pre_ms,
+        # the Physics-Informed-GS loop re-bins every step (means move): its step time
+        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms,
         "preprocess_first_call_ms": pre_first_ms,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
@@ -182,7 +198,9 @@ def main():
         "cpu_baseline": None,
     }
 
-    if rank == 0 and world == 1 and not args.no_cpu:
+    if multi:
+        result["roofline"] = None
+    if rank == 0 and world == 1 and not args.no_cpu and not multi:
         result["cpu_baseline"] = cpu_baseline(means.detach().cpu(), values.detach().cpu(),
                                               covs.cpu(), conics.detach().cpu(), samples.cpu(),
                                               dL.cpu(), fn, args.cpu_samples)

@@ -55,3 +55,23 @@ def test_ctypes_aggregate_matches_extension(dgs):
     gb = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False)
     for x, y in zip(ga, gb):
         np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))
+
+
+def test_ctypes_multi_matches_extension(dgs):
+    """dgs_sample_{forward,backward}_multi through ctypes against the extension's fused call."""
+    import dgs_ctypes
+    dev = "cuda:0"
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(2000, 2, 1, seed=151))
+    samples = syn.samples(8000, 2, seed=152).to(dev)
+    a = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
+    codes = [3, 0, 2]
+    fa = dgs._C.sample_gaussians_multi(codes, means, values, conics, samples, a[1], a[2], False)
+    fb = dgs_ctypes.sample_gaussians_multi(codes, means, values, conics, samples, a[1], a[2], False)
+    for x, y in zip(fa, fb):
+        assert torch.equal(x, y)
+    dLs = [torch.randn_like(x) for x in fa]
+    ga = dgs._C.sample_gaussians_multi_backward(codes, means, values, conics, samples, dLs, a[1], a[2], False)
+    gb = dgs_ctypes.sample_gaussians_multi_backward(codes, means, values, conics, samples, dLs, a[1], a[2], False)
+    for x, y in zip(ga, gb):
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5,
+                                   atol=1e-6 * float(x.abs().max()))

@@ -133,6 +133,54 @@ sample_gaussians_third_derivative, sample_gaussians_third_derivative_backward = 
     "sample_gaussians_third_derivative")
 
 
+
+# ---- fused functions (dgs_sample_{forward,backward}_multi; not on the reference API) --------
+_lib.dgs_sample_workspace_size_multi.restype = _SZ
+_lib.dgs_sample_workspace_size_multi.argtypes = [_I] * 6
+_PP = ctypes.c_void_p * 4
+_lib.dgs_sample_forward_multi.argtypes = [_I] * 5 + [_P] * 4 + [_P, _SZ, _P, _SZ, _PP, _P, _SZ, _P, _I]
+_lib.dgs_sample_backward_multi.argtypes = [_I] * 5 + [_P] * 4 + [_PP, _P, _SZ, _P, _SZ, _P, _P, _P, _P, _SZ, _P, _I]
+
+
+def sample_gaussians_multi(codes, means, values, conics, samples, binning, sample_binning, debug):
+    """Outputs of the functions `codes` (0..3, each once; D = 2, C = 1 for two or more) in one
+    traversal of the pairs, in the order given."""
+    means, values, conics, samples = map(_f32, (means, values, conics, samples))
+    P, D = means.shape
+    N, C = samples.shape[0], values.shape[1]
+    mask = sum(1 << c for c in codes)
+    outs = {c: torch.zeros((N,) + (D,) * c + (C,), device=means.device) for c in codes}
+    ptrs = _PP(*[outs[c].data_ptr() if c in outs else None for c in range(4)])
+    ws = torch.empty(_lib.dgs_sample_workspace_size_multi(mask, P, D, N, C, 0), dtype=torch.uint8,
+                     device=means.device)
+    _check(_lib.dgs_sample_forward_multi(mask, P, D, N, C, _ptr(means), _ptr(values), _ptr(conics),
+                                         _ptr(samples), _ptr(binning), binning.numel(),
+                                         _ptr(sample_binning), sample_binning.numel(), ptrs,
+                                         _ptr(ws), ws.numel(), _stream(), int(bool(debug))))
+    return [outs[c] for c in codes]
+
+
+def sample_gaussians_multi_backward(codes, means, values, conics, samples, dLs, binning,
+                                    sample_binning, debug):
+    """Gradients of sum_f <dLs[f], out_f> for the functions `codes`."""
+    means, values, conics, samples = map(_f32, (means, values, conics, samples))
+    dLs = {c: _f32(d) for c, d in zip(codes, dLs)}
+    P, D = means.shape
+    N, C = samples.shape[0], values.shape[1]
+    mask = sum(1 << c for c in codes)
+    dm = torch.zeros(P, D, device=means.device)
+    dv = torch.zeros(P, C, device=means.device)
+    dc = torch.zeros(P, D * (D + 1) // 2, device=means.device)
+    ptrs = _PP(*[dLs[c].data_ptr() if c in dLs else None for c in range(4)])
+    ws = torch.empty(_lib.dgs_sample_workspace_size_multi(mask, P, D, N, C, 1), dtype=torch.uint8,
+                     device=means.device)
+    _check(_lib.dgs_sample_backward_multi(mask, P, D, N, C, _ptr(means), _ptr(values), _ptr(conics),
+                                          _ptr(samples), ptrs, _ptr(binning), binning.numel(),
+                                          _ptr(sample_binning), sample_binning.numel(), _ptr(dm),
+                                          _ptr(dv), _ptr(dc), _ptr(ws), ws.numel(), _stream(),
+                                          int(bool(debug))))
+    return dm, dv, dc
+
 # ---- neighbour aggregation (aggregate_neighbors.h:11-47) ---------------------------------
 _lib.dgs_agg_preprocess.argtypes = [_I, _I, _P, _P, _P, _P, _P, _P, ALLOC_FN, _P, ctypes.POINTER(_I64), _P, _I]
 _lib.dgs_agg_forward.argtypes = [_I] * 5 + [_P] * 11 + [_P] + [_P] * 4 + [_P, _I]
