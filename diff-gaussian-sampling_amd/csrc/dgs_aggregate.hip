@@ -222,7 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_count(int P, AggGeom g, const fl
                                                       int64_t *__restrict__ counts) {
     const int lane = threadIdx.x & (kWave - 1);
     const int stride = gridDim.x * kWavesPerBlock;
-    for (int w = wave_unit_index(); w < P; w += stride) {
+    for (int w = wave_unit_index(P); w < P; w += stride) {
         const int i = (int)order[w];  // rows in cell order: concurrent waves share neighbours in L2
         int64_t n = 0;
         const float ri = agg_r(radii[i]);
@@ -315,7 +315,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const flo
     uint32_t *s = buf[threadIdx.x >> 6];
     const int stride = gridDim.x * kWavesPerBlock;
     const int D = g.D, S = D * (D + 1) / 2;
-    for (int w = wave_unit_index(); w < P; w += stride) {
+    for (int w = wave_unit_index(P); w < P; w += stride) {
         const int i = (int)order[w];
         const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
         // aggregate_neighbors.cu:73-74 (0.333 and 1.0 / (r + 1e-6) in double)
@@ -484,7 +484,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward(AggArgs A) {
     float *ar = arow[threadIdx.x >> 6];
     const int stride = gridDim.x * kWavesPerBlock;
     const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2;
-    for (int w = wave_unit_index(); w < A.P; w += stride) {
+    for (int w = wave_unit_index(A.P); w < A.P; w += stride) {
         const int i = agg_row(A, w);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];
@@ -559,7 +559,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward(AggArgs A) {
     // per atomic instruction, so one instruction covers whole rows instead of 64 scattered words
     const int G = L + K, spp = G <= kWave ? kWave / max(G, 1) : 1;
     const int sub = G <= kWave ? lane / max(G, 1) : 0;
-    for (int wr = wave_unit_index(); wr < A.P; wr += stride) {
+    for (int wr = wave_unit_index(A.P); wr < A.P; wr += stride) {
         const int i = agg_row(A, wr);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];
@@ -744,7 +744,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
     float *sf = base + kWave, *sk = sf + kWave * G.SL, *ar = sk + kWave * G.SK;
     const int stride = gridDim.x * kWavesPerBlock;
     const int D = A.D, L = A.L, K = A.K, E = A.E, F = (E - 1) / D / 2;
-    for (int w = wave_unit_index(); w < A.P; w += stride) {
+    for (int w = wave_unit_index(A.P); w < A.P; w += stride) {
         const int i = agg_row(A, w);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];
@@ -851,7 +851,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
         x = swap_add16(swap_add32(x));
         if (keep) part[v * 16] += x;
     };
-    for (int wr = wave_unit_index(); wr < A.P; wr += stride) {
+    for (int wr = wave_unit_index(A.P); wr < A.P; wr += stride) {
         const int i = agg_row(A, wr);
         const int64_t start = i == 0 ? 0 : A.ranges[i - 1], end = A.ranges[i];
         const float inv = A.inv_total[i];

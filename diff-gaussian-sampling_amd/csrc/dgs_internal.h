@@ -182,11 +182,17 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
 // block remap (cdna_hip_programming.md T1): consecutive units -- neighbouring cells that
 // share Gaussians -- run on one XCD and share its L2.  Kernels grid-stride by
 // gridDim.x * kWavesPerBlock from here.
-__device__ __forceinline__ int wave_unit_index() {
-    const int nb = gridDim.x, b = blockIdx.x;
+__device__ __forceinline__ int wave_unit_index(int nunits) {
+    // The remap is a bijection on the first nb blocks, nb = the blocks the device-side unit
+    // count needs (the launch may be larger: preprocess hands the host only capacities), so
+    // the working blocks stay spread over all 8 XCDs; surplus blocks map to themselves and
+    // exit.  With nunits > the grid's waves (grid-strided use) every block is remapped.
+    const int need = (nunits + kWavesPerBlock - 1) / kWavesPerBlock;
+    const int nb = min((int)gridDim.x, need), b = blockIdx.x;
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (b >= nb) return b * kWavesPerBlock + w;
     const int xcd = b & 7, q = nb >> 3, r = nb & 7;
     const int bb = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     return bb * kWavesPerBlock + w;
 }
 

@@ -881,13 +881,12 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);
 
-    // exact unit counts for the launch-size hint (second and last host sync)
-    int32_t hc[3] = {0, 0, 0};
-    DGS_TRY_HIP(hipMemcpyAsync(hc, counters, sizeof(hc), hipMemcpyDeviceToHost, s));
-    DGS_TRY_HIP(hipStreamSynchronize(s));
+    // launch-size hint: the unit capacities (the exact counts stay on the device and the render
+    // kernels grid-stride over them; surplus waves exit at once), so the binning needs no second
+    // host sync.  nunsafe = -1: unknown on the host (the tail pass checks the device counter).
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
-    uh.nfwd = hc[kNumFwdUnits]; uh.nbwd = hc[kNumBwdUnits]; uh.nunsafe = hc[kNumUnsafe];
+    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = -1;
     hint_put(uh);
     return DGS_OK;
 }

@@ -371,7 +371,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
     const int nch = min(CB, C - cbase);
-    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         const FwdUnit fu = fwd_unit_at(bins, unit);
         // every entry but the kUnsafe ones (added by k_forward<..., TAIL = true>)
         const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
@@ -483,7 +483,8 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
     const int nch = min(CB, C - cbase);
-    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+    if (TAIL && sload(&bins.counts[kNumUnsafe]) == 0) return;  // no unsafe entry anywhere
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         const FwdUnit fu = fwd_unit_at(bins, unit);
         if (TAIL && sload(&bins.cell_gmid[fu.cell]) == sload(&bins.cell_gend[fu.cell])) continue;
         const int j = fu.sb + lane;
@@ -691,7 +692,7 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
     const int nunits = sload(&bins.counts[kNumBwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
-    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         const uint2 u = sload(&bins.bwd_units[unit]);
         const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
@@ -753,7 +754,7 @@ __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
     const int stride = gridDim.x * kWavesPerBlock;
-    for (int unit = wave_unit_index(); unit < nunits; unit += stride) {
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         const FwdUnit fu = fwd_unit_at(bins, unit);
         const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
         const int j = fu.sb + (threadIdx.x & (kWave - 1));
@@ -870,6 +871,7 @@ static int run_forward(const Call &a) {
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
     constexpr bool T = fwd_transposed<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
+    hint.nunsafe = -1;
     const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
@@ -885,7 +887,10 @@ static int run_forward(const Call &a) {
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if constexpr (T) {
             if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
-                k_forward<FN, D, CB, true><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
+                // (grid-strided over a capped grid: it exits at once when the device-side
+                // unsafe count is 0, which the host does not know without a sync)
+                const unsigned tb = hint.nunsafe > 0 ? blocks : std::min(blocks, 1024u);
+                k_forward<FN, D, CB, true><<<tb, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                          a.samples, a.outs, a.C, cbase);
                 DGS_LAUNCH_CHECK(a.s, a.debug);
             }
