@@ -734,8 +734,57 @@ __device__ __forceinline__ float dot_row(const float *__restrict__ q, const floa
     return v;
 }
 
+// Pipelined staging (L, K <= 16, 16-byte rows: at most 4 pieces of each row array per lane):
+// the next batch's pieces are loaded into registers before the current batch's arithmetic
+// and written to LDS after it, so the gather latency overlaps the arithmetic (the
+// synchronous form left the waves parked on s_waitcnt for ~70 % of their cycles, PMC
+// SQ_WAIT_ANY).
+struct Pieces {
+    float4 f[4], k[4];
+};
+
+__device__ __forceinline__ void piece_rq(int p, int PW, int &r, int &q) {
+    r = (int)(((float)p + 0.5f) / (float)PW);
+    q = p - r * PW;
+}
+
+__device__ __forceinline__ void pieces_load(const AggArgs &A, const int *sm, int nb, int lane, Pieces &pc) {
+    const int PF = A.L >> 2, PK = A.K >> 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int p = u * kWave + lane;
+        int r, q;
+        pc.f[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        piece_rq(p, PF, r, q);
+        if (r < nb) {
+            const int m = sm[r];
+            if (m >= 0) pc.f[u] = *reinterpret_cast<const float4 *>(A.features + (int64_t)m * A.L + 4 * q);
+        }
+        pc.k[u] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        piece_rq(p, PK, r, q);
+        if (r < nb) {
+            const int m = sm[r];
+            if (m >= 0) pc.k[u] = *reinterpret_cast<const float4 *>(A.keys + (int64_t)m * A.K + 4 * q);
+        }
+    }
+}
+
+__device__ __forceinline__ void pieces_store(const AggArgs &A, const AggStage &G, const Pieces &pc, float *sf,
+                                             float *sk, int lane) {
+    const int PF = A.L >> 2, PK = A.K >> 2;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int p = u * kWave + lane;
+        int r, q;
+        piece_rq(p, PF, r, q);
+        if (r < kWave) *reinterpret_cast<float4 *>(sf + r * G.SL + 4 * q) = pc.f[u];
+        piece_rq(p, PK, r, q);
+        if (r < kWave) *reinterpret_cast<float4 *>(sk + r * G.SK + 4 * q) = pc.k[u];
+    }
+}
+
 // NB = L rounded up to 16 / 32 / 64; K <= 64.
-template <int NB>
+template <int NB, bool PIPE>
 __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G) {
     extern __shared__ float lds[];
     const int lane = threadIdx.x & (kWave - 1);
@@ -765,18 +814,8 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
                 dn_n = A.densities[sp];
             }
         };
-        fetch(start + lane);
-        for (int64_t s0 = start; s0 < end; s0 += kWave) {
-            const int64_t s = s0 + lane;
-            const int nb = (int)min<int64_t>(kWave, end - s0);
-            const int64_t idx = idx_n;
-            float X[2] = {X0_n, X1_n};
-            const float dn = dn_n;
-            fetch(s + kWave);
-            sm[lane] = (int)idx;
-            wave_sync_lds();
-            stage_rows2(A, G, sm, nb, sf, sk, lane);
-            wave_sync_lds();
+        // one slot of the batch: weight, embedding, factor and the lane's share of a
+        auto slot = [&](int64_t s, int64_t idx, const float *X, float dn) {
             if (idx >= 0) {
                 const float weight = dot_row(q, sk + lane * G.SK, K);
                 float emb, fac;
@@ -798,7 +837,56 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
             } else if (s < end) {
                 A.weights[s] = A.embeddings[s] = A.factors[s] = 0.0f;
             }
+        };
+        fetch(start + lane);
+        if constexpr (PIPE) {
+            Pieces pc;
+            int64_t idx = idx_n;
+            float X[2] = {X0_n, X1_n}, dn = dn_n;
+            sm[lane] = (int)idx;
             wave_sync_lds();
+            pieces_load(A, sm, (int)min<int64_t>(kWave, end - start), lane, pc);
+            fetch(start + kWave + lane);
+            wave_sync_lds();
+            pieces_store(A, G, pc, sf, sk, lane);
+            wave_sync_lds();
+            for (int64_t s0 = start; s0 < end; s0 += kWave) {
+                const int64_t s = s0 + lane;
+                const bool more = s0 + kWave < end;
+                const int64_t idx_x = idx_n;
+                const float Xx[2] = {X0_n, X1_n}, dn_x = dn_n;
+                if (more) {  // the next batch's rows into registers, its successor's streams
+                    sm[lane] = (int)idx_x;
+                    wave_sync_lds();
+                    pieces_load(A, sm, (int)min<int64_t>(kWave, end - s0 - kWave), lane, pc);
+                    fetch(s + 2 * kWave);
+                }
+                slot(s, idx, X, dn);
+                wave_sync_lds();
+                if (more) {
+                    pieces_store(A, G, pc, sf, sk, lane);
+                    wave_sync_lds();
+                }
+                idx = idx_x;
+                X[0] = Xx[0];
+                X[1] = Xx[1];
+                dn = dn_x;
+            }
+        } else {
+        for (int64_t s0 = start; s0 < end; s0 += kWave) {
+            const int64_t s = s0 + lane;
+            const int nb = (int)min<int64_t>(kWave, end - s0);
+            const int64_t idx = idx_n;
+            float X[2] = {X0_n, X1_n};
+            const float dn = dn_n;
+            fetch(s + kWave);
+            sm[lane] = (int)idx;
+            wave_sync_lds();
+            stage_rows2(A, G, sm, nb, sf, sk, lane);
+            wave_sync_lds();
+            slot(s, idx, X, dn);
+            wave_sync_lds();
+        }
         }
         const float r = reduce_row<NB>(acc, lane);
         if (lane < L) ar[lane] = r;
@@ -1189,10 +1277,14 @@ extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *f
     if (L <= 64 && K <= 64) {
         const AggStage G = agg_stage(L, K, features, keys, 2 * kWave + 64 /* sm, ar */);
         const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * G.per_wave;
+        const bool pipe = L <= 16 && K <= 16 && G.vf && G.vk && !std::getenv("DGS_AGG_NOPIPE");
         switch (agg_nb(std::max(L, 1))) {
-        case 16: k_agg_forward_s<16><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 32: k_agg_forward_s<32><<<nb, kBlock, lds, s>>>(A, G); break;
-        default: k_agg_forward_s<64><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 16:
+            if (pipe) k_agg_forward_s<16, true><<<nb, kBlock, lds, s>>>(A, G);
+            else k_agg_forward_s<16, false><<<nb, kBlock, lds, s>>>(A, G);
+            break;
+        case 32: k_agg_forward_s<32, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        default: k_agg_forward_s<64, false><<<nb, kBlock, lds, s>>>(A, G); break;
         }
     } else {
         switch (agg_nb(std::min(std::max(L, 1), 64))) {

@@ -26,7 +26,7 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True):
+def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared_atol=2e-5):
     idx_r, rg_r, X_r, dn_r, inv_r = oracle.agg_preprocess(means, conics, radii)
     idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
     torch.cuda.synchronize()
@@ -50,7 +50,10 @@ def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True):
     ref = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
     got = dgs._C.aggregate_neighbors_backward(*targs, idx, rg, X, dn, w, e, f, inv, _cuda(g), False)
     for name, a, b in zip(AGG_FEATURES, got, ref):
-        close(a.cpu().numpy().reshape(b.shape), b, 1e-4, 2e-5, f"d/d{name}")
+        # frequencies / distance_transform: a handful of values, each a float sum over EVERY
+        # slot (float atomics in the reference too), so its rounding grows with the slot count
+        atol = shared_atol if name in ("frequencies", "distance_transform") else 2e-5
+        close(a.cpu().numpy().reshape(b.shape), b, 1e-4, atol, f"d/d{name}")
 
 
 @pytest.mark.parametrize("D", [1, 2])
@@ -75,6 +78,15 @@ def test_aggregate_row_overflow_windows(dgs, oracle):
     means, conics, radii, fe = agg_problem(P=5000, D=2, L=4, K=2, F=1, seed=40, spread=0.04,
                                            radius=(1.0, 1.5))
     _run(dgs, oracle, means, conics, radii, fe, check_grads=False)
+
+
+def test_aggregate_pipelined_staging_long_rows(dgs, oracle):
+    """L = K = 16 (the pipelined staging of the forward) with rows of several hundred
+    neighbours: many 64-slot batches per row, and a partial last batch."""
+    means, conics, radii, fe = agg_problem(P=2000, D=2, L=16, K=16, F=4, seed=41, spread=0.3,
+                                           radius=(0.6, 1.0))
+    # 2.1M slots: the frequency gradient sums 2.1M terms of both signs (~1e-4 of its scale)
+    _run(dgs, oracle, means, conics, radii, fe, shared_atol=2e-4)
 
 
 def test_aggregate_odd_sizes(dgs, oracle):
