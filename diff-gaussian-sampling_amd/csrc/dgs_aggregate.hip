@@ -903,7 +903,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
 // Backward, L and K <= 64 (NB = max(L, K) rounded up).  Per-wave LDS: the staged rows, the
 // batch's (neighbour, dcw * fac, te), st[64], and the shared-array partials: every value is
 // first summed over the lane quartet (l, l^16, l^32, l^48) and kept by lanes 0..15 (NV x 16).
-template <int NB, bool COMBO>
+template <int NB, bool COMBO, bool PIPE>
 __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G) {
     extern __shared__ float lds[];
     const int lane = threadIdx.x & (kWave - 1);
@@ -973,6 +973,16 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             }
         };
         fetch(start + lane);
+        Pieces pc;  // PIPE: the next batch's row pieces, loaded during this batch's scatter
+        int *snext = reinterpret_cast<int *>(sx0);
+        if constexpr (PIPE) {
+            snext[lane] = (int)idx_n;
+            wave_sync_lds();
+            pieces_load(A, snext, (int)min<int64_t>(kWave, end - start), lane, pc);
+            wave_sync_lds();
+            pieces_store(A, G, pc, sf, sk, lane);
+            wave_sync_lds();
+        }
         for (int64_t s0 = start; s0 < end; s0 += kWave) {
             const int64_t s = s0 + lane;
             const int nb = (int)min<int64_t>(kWave, end - s0);
@@ -982,8 +992,11 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             fetch(s + kWave);
             sm[lane] = (int)idx;
             wave_sync_lds();
-            stage_rows2(A, G, sm, nb, sf, sk, lane);
-            wave_sync_lds();
+            if constexpr (!PIPE) {
+                stage_rows2(A, G, sm, nb, sf, sk, lane);
+                wave_sync_lds();
+            }
+            const bool more = PIPE && s0 + kWave < end;
             float c = 0.0f, te = 0.0f, t1 = 0.0f, t2 = 0.0f;
             if (idx >= 0) {
                 const float *feat = sf + lane * G.SL, *key = sk + lane * G.SK;
@@ -1054,6 +1067,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
                 put(E - 1, t1);
                 put(2 * E - 1, t2);
             }
+            if (more) {  // issue the next batch's row loads; they land during the scatter
+                wave_sync_lds();
+                snext[lane] = (int)idx_n;
+                wave_sync_lds();
+                pieces_load(A, snext, (int)min<int64_t>(kWave, end - s0 - kWave), lane, pc);
+            }
             // neighbour gradients (aggregate_neighbors.cu:296-319), a whole neighbour row
             // (dfeat row, then dkeys row) per G2 lanes of one atomic instruction
             if (!(A.expt & 1)) {
@@ -1081,6 +1100,10 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
                 }
             }
             wave_sync_lds();
+            if (more) {
+                pieces_store(A, G, pc, sf, sk, lane);
+                wave_sync_lds();
+            }
         }
         const float ra = reduce_row<NB>(acc_a, lane);
         if (lane < L) A.arows[(int64_t)i * L + lane] = ra;
@@ -1316,6 +1339,7 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     const AggStage G = agg_stage(L, K, features, keys,
                                  8 * kWave + std::max(NV * 16, 7 * kWave) /* sm sc ste st s1 s2 sx0 sx1, sums */);
     const size_t lds = sizeof(float) * (size_t)kWavesPerBlock * (staged ? G.per_wave : agg_bwd_lds_floats(NV));
+    const bool pipe = staged && L <= 16 && K <= 16 && G.vf && G.vk && !std::getenv("DGS_AGG_NOPIPE");
     if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
     auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
     DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
@@ -1341,12 +1365,15 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     if (staged) {
         const bool combo = D * F <= kWave;
         switch (agg_nb(std::max(std::max(L, K), 1)) * 2 + (combo ? 1 : 0)) {
-        case 33: k_agg_backward_s<16, true><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 32: k_agg_backward_s<16, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 65: k_agg_backward_s<32, true><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 64: k_agg_backward_s<32, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 129: k_agg_backward_s<64, true><<<nb, kBlock, lds, s>>>(A, G); break;
-        default: k_agg_backward_s<64, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 33:
+            if (pipe) k_agg_backward_s<16, true, true><<<nb, kBlock, lds, s>>>(A, G);
+            else k_agg_backward_s<16, true, false><<<nb, kBlock, lds, s>>>(A, G);
+            break;
+        case 32: k_agg_backward_s<16, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 65: k_agg_backward_s<32, true, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 64: k_agg_backward_s<32, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 129: k_agg_backward_s<64, true, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        default: k_agg_backward_s<64, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
         }
     } else {
         switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {
