@@ -39,7 +39,7 @@
 
 namespace dgs {
 
-constexpr int kAggNMax = 2048;  // neighbour ids a wave sorts in LDS at once
+constexpr int kAggNMax = 2048;  // neighbour ids a wave sorts at once (wave_sort_keys: <= 32 per lane)
 constexpr int kAggMaxCells = 1 << 24;
 
 struct AggGeom {
@@ -295,6 +295,67 @@ __device__ inline void wave_bitonic(uint32_t *s, int n, int lane) {
         }
 }
 
+// The same ascending bitonic network with the keys in registers: element e = lane * R + r
+// (R = n / 64 consecutive keys per lane).  Partners closer than R are in the lane's own
+// registers; farther ones are lane ^ (j / R), exchanged with one cross-lane permute per
+// register.  Two thirds of the 66 stages of n = 2048 stay in registers, and no stage waits on
+// LDS banks (the LDS network was ~40 % of k_agg_fill).
+// One stage (K, J compile-time) of the network.
+template <int R, int K, int J>
+__device__ __forceinline__ void reg_bitonic_stage(uint32_t (&v)[R], int lane) {
+    const int e0 = lane * R;
+    if constexpr (J < R) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if (r & J) continue;
+            const bool asc = ((e0 + r) & K) == 0;
+            const uint32_t a = v[r], b = v[r | J];
+            const bool sw = (a > b) == asc;
+            v[r] = sw ? b : a;
+            v[r | J] = sw ? a : b;
+        }
+    } else {
+        constexpr int LX = J / R;
+        const bool keep_min = ((lane & LX) == 0) == ((e0 & K) == 0);
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const uint32_t o = (uint32_t)__shfl_xor((int)v[r], LX);
+            v[r] = keep_min ? min(v[r], o) : max(v[r], o);
+        }
+    }
+    if constexpr (J > 1) reg_bitonic_stage<R, K, J / 2>(v, lane);
+}
+
+template <int R, int K = 2>
+__device__ __forceinline__ void reg_bitonic(uint32_t (&v)[R], int lane) {
+    reg_bitonic_stage<R, K, K / 2>(v, lane);
+    if constexpr (K < R * kWave) reg_bitonic<R, K * 2>(v, lane);
+}
+
+template <int R>
+__device__ __forceinline__ void reg_bitonic_lds(uint32_t *s, int lane) {
+    uint32_t v[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) v[r] = s[lane * R + r];
+    reg_bitonic<R>(v, lane);
+    wave_sync_lds();
+#pragma unroll
+    for (int r = 0; r < R; ++r) s[lane * R + r] = v[r];
+    wave_sync_lds();
+}
+
+// Ascending sort of s[0, np2) (np2 a power of two, 64 <= np2 <= kAggNMax) in registers.
+__device__ inline void wave_sort_keys(uint32_t *s, int np2, int lane) {
+    switch (np2) {
+    case 64: reg_bitonic_lds<1>(s, lane); break;
+    case 128: reg_bitonic_lds<2>(s, lane); break;
+    case 256: reg_bitonic_lds<4>(s, lane); break;
+    case 512: reg_bitonic_lds<8>(s, lane); break;
+    case 1024: reg_bitonic_lds<16>(s, lane); break;
+    default: reg_bitonic_lds<32>(s, lane); break;
+    }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
     return v;
@@ -309,7 +370,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const flo
                                                      const int64_t *__restrict__ ranges,
                                                      int64_t *__restrict__ indices, float *__restrict__ dists,
                                                      float *__restrict__ densities,
-                                                     float *__restrict__ inv_total) {
+                                                     float *__restrict__ inv_total, int regsort) {
     __shared__ uint32_t buf[kWavesPerBlock][kAggNMax];
     const int lane = threadIdx.x & (kWave - 1);
     uint32_t *s = buf[threadIdx.x >> 6];
@@ -342,11 +403,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_fill(int P, AggGeom g, const flo
                 if (n <= kAggNMax) break;
                 hi = lo + (hi - lo) / 2;
             }
-            int np2 = 1;
+            int np2 = kWave;  // register network: at least one key per lane
             while (np2 < n) np2 <<= 1;
             for (int t = n + lane; t < np2; t += kWave) s[t] = 0xffffffffu;
             wave_sync_lds();
-            wave_bitonic(s, np2, lane);
+            if (regsort) wave_sort_keys(s, np2, lane);
+            else wave_bitonic(s, np2, lane);
             for (int t0 = 0; t0 < n; t0 += kWave) {
                 const int t = t0 + lane;
                 float dv = 0.0f;
@@ -1250,7 +1312,8 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     float *dens = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_AGG_DENSITIES, std::max<size_t>(4 * (size_t)len, 16)));
     if (!indices || !dists || !dens) return fail(DGS_ERR_ALLOC, "aggregate: output allocation failed");
     k_agg_fill<<<wblocks, kBlock, 0, s>>>(P, g, means, conics, radii, cand, cstart, ids_s, ranges, indices, dists,
-                                          dens, inv_total);
+                                          dens, inv_total,
+        std::getenv("DGS_AGG_LDSSORT") ? 0 : 1);
     DGS_LAUNCH_CHECK(s, debug);
     if (row_order) DGS_TRY_HIP(hipMemcpyAsync(row_order, ids_s, 4 * (size_t)P, hipMemcpyDeviceToDevice, s));
     return DGS_OK;
