@@ -578,6 +578,26 @@ __global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, cons
     for (int f = 0; f < D; ++f) row[2 * f] = s[f];
 }
 
+// Zero-fills up to 8 word-aligned regions in one launch (each hipMemsetAsync is a launch of its
+// own, ~5 us of GPU time even for a few bytes; the binning needed ten).
+struct ZeroSpec {
+    uint32_t *p[8];
+    int64_t n[8];  // words
+    int count;
+};
+
+__global__ void k_zero_multi(ZeroSpec z) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int r = 0; r < z.count; ++r)
+        for (int64_t i = t; i < z.n[r]; i += st) z.p[r][i] = 0u;
+}
+
+struct ZeroList {
+    ZeroSpec z{};
+    void add(void *p, size_t bytes) { z.p[z.count] = static_cast<uint32_t *>(p); z.n[z.count++] = (int64_t)(bytes / 4); }
+    void launch(hipStream_t s) { k_zero_multi<<<256, 256, 0, s>>>(z); }
+};
+
 // perm (internal -> caller id) and its inverse, stored back to back.
 __global__ void k_perm_pair(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -744,10 +764,20 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     void *tmp_a = S.get<char>(t_a);
     if (S.rc) return S.rc;
 
-    DGS_TRY_HIP(hipMemsetAsync(stile, 0, sizeof(uint32_t) * (G.T + 1), s));
-    DGS_TRY_HIP(hipMemsetAsync(gtile, 0, sizeof(uint32_t) * (G.T + 1), s));
-    DGS_TRY_HIP(hipMemsetAsync(cell_sbeg, 0, sizeof(int32_t) * ncells, s));
-    DGS_TRY_HIP(hipMemsetAsync(cell_send, 0, sizeof(int32_t) * ncells, s));
+    float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
+    {  // one launch for every zero-fill of phase A (k_fs_pack writes all of fsrows but its slack)
+        const size_t fs_written = (size_t)((N + 1) / 2 * 2) * D * 4;
+        ZeroList zl;
+        zl.add(stile, sizeof(uint32_t) * (G.T + 1));
+        zl.add(gtile, sizeof(uint32_t) * (G.T + 1));
+        zl.add(cell_sbeg, sizeof(int32_t) * ncells);
+        zl.add(cell_send, sizeof(int32_t) * ncells);
+        zl.add(reinterpret_cast<char *>(fsrows) + fs_written, fsrows_bytes(N, D) - fs_written);
+        zl.add(rbuf, (size_t)G.T * 8 + 8);
+        zl.add(srbuf, (size_t)G.T * 8 + 8);
+        zl.launch(s);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
 
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
@@ -758,8 +788,6 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
-    float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
-    DGS_TRY_HIP(hipMemsetAsync(fsrows, 0, fsrows_bytes(N, D), s));
     k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
     DGS_LAUNCH_CHECK(s, debug);
     k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
@@ -817,9 +845,14 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     void *tmp_b = S.get<char>(std::max(t_esort, t_cscan));
     if (S.rc) return S.rc;
 
-    DGS_TRY_HIP(hipMemsetAsync(counters, 0, 16, s));
-    DGS_TRY_HIP(hipMemsetAsync(hbeg, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
-    DGS_TRY_HIP(hipMemsetAsync(hend, 0, sizeof(int32_t) * 2 * (size_t)ncells, s));
+    {
+        ZeroList zl;
+        zl.add(counters, 16);
+        zl.add(hbeg, sizeof(int32_t) * 2 * (size_t)ncells);
+        zl.add(hend, sizeof(int32_t) * 2 * (size_t)ncells);
+        zl.launch(s);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     k_perm_pair<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
     DGS_LAUNCH_CHECK(s, debug);
     k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
@@ -852,8 +885,6 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled)
-    DGS_TRY_HIP(hipMemsetAsync(rbuf, 0, (size_t)G.T * 8 + 8, s));
-    DGS_TRY_HIP(hipMemsetAsync(srbuf, 0, (size_t)G.T * 8 + 8, s));
     k_ref_ranges<<<1, 64, 0, s>>>(G.T, gtile, reinterpret_cast<uint2 *>(rbuf));
     k_ref_ranges<<<1, 64, 0, s>>>(G.T, stile, reinterpret_cast<uint2 *>(srbuf));
     DGS_LAUNCH_CHECK(s, debug);
