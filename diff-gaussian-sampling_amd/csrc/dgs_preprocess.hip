@@ -330,7 +330,9 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                     }
                     for (int fx = fxl; fx <= fxh; ++fx) {
                         const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
-                        if (send[cell] <= sbeg[cell]) continue;
+                        // (empty cells get no units, so an entry there is never read: only
+                        // the box-classified cells need the two loads of this test)
+                        if (!local && send[cell] <= sbeg[cell]) continue;
                         if (cull && D == 1) {
                             const double o = tc[0] * BS;
                             const double dlo = o + fx * G.fs - slack, dhi = o + (fx + 1) * G.fs + slack;
