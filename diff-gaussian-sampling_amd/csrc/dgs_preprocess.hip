@@ -149,15 +149,16 @@ __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
 }
 
 // identifyTileRanges (sampler_impl.cu:134-151) over sorted cell keys; keys >= limit ignored.
-__global__ void k_identify(int64_t L, const uint32_t *__restrict__ keys, uint32_t limit,
+template <typename KT>
+__global__ void k_identify(int64_t L, const KT *__restrict__ keys, uint32_t limit,
                            int32_t *__restrict__ beg, int32_t *__restrict__ end, int shift) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L) return;
-    const uint32_t k = keys[i] >> shift;
+    const uint32_t k = (uint32_t)keys[i] >> shift;
     if (i == 0) {
         if (k < limit) beg[k] = 0;
     } else {
-        const uint32_t p = keys[i - 1] >> shift;
+        const uint32_t p = (uint32_t)keys[i - 1] >> shift;
         if (k != p) {
             if (p < limit) end[p] = (int32_t)i;
             if (k < limit) beg[k] = (int32_t)i;
@@ -432,11 +433,14 @@ __global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
 // entries at 64 different addresses per store were most of this kernel's time).
 constexpr int kFillBlock = 128, kFillCap = 3072;
 
+// KT: the entry key type -- uint16_t when every (cell, flag) key fits 16 bits (the radix sort
+// then moves 6 instead of 8 bytes per entry and pass).
+template <typename KT>
 __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     int P, Geom G, const uint32_t *__restrict__ perm, const float *__restrict__ means,
     const float *__restrict__ conics, const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
-    const uint64_t *__restrict__ cnts, uint32_t *__restrict__ ekeys, uint32_t *__restrict__ evals,
+    const uint64_t *__restrict__ cnts, KT *__restrict__ ekeys, uint32_t *__restrict__ evals,
     int32_t *__restrict__ counters) {
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
                     skey[o - base] = key;
                     sval[o - base] = val;
                 } else {
-                    ekeys[o] = key;
+                    ekeys[o] = (KT)key;
                     evals[o] = val;
                 }
                 nunsafe += (val & kUnsafe) ? 1u : 0u;
@@ -471,7 +475,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
         __syncthreads();
         const int n = (int)(end - base);
         for (int k = threadIdx.x; k < n; k += kFillBlock) {
-            ekeys[base + k] = skey[k];
+            ekeys[base + k] = (KT)skey[k];
             evals[base + k] = sval[k];
         }
     }
@@ -610,6 +614,15 @@ __global__ void k_perm_pair(int64_t n, const uint32_t *__restrict__ a, int32_t *
 }
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
+
+// Entry sort: (key, entry) pairs with keys of type KT (stored in u32 arrays; u16 view when the
+// keys fit 16 bits).
+template <typename KT>
+static hipError_t sort_entries(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
+                               const uint32_t *vin, uint32_t *vout, int64_t n, int bits, hipStream_t s) {
+    return rocprim::radix_sort_pairs(tmp, bytes, reinterpret_cast<const KT *>(kin), reinterpret_cast<KT *>(kout),
+                                     vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+}
 
 // Stable LSD radix sort of (u32 key, u32 value) pairs, always the onesweep algorithm: rocprim's
 // default switches to block sort + merge passes below 2^20 items (24 launches, ~170 us for the
@@ -788,7 +801,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, skeys, skeys_sorted, sids,
                                                    (uint32_t *)sorted_sid, N, 0, sbits, s));
     DGS_LAUNCH_CHECK(s, debug);
-    k_identify<<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
+    k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
     k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
     DGS_LAUNCH_CHECK(s, debug);
@@ -841,8 +854,9 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     if (S.rc) return S.rc;
     size_t t_esort = 0, t_cscan = 0;
     const int ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_esort, ekeys, ekeys_sorted, evals,
-                                                   entries, (int)E, 0, ebits, s));
+    const bool k16 = ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
+    DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(nullptr, t_esort, ekeys, ekeys_sorted, evals, entries, E, ebits, s)
+                    : sort_entries<uint32_t>(nullptr, t_esort, ekeys, ekeys_sorted, evals, entries, E, ebits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_cscan, fcnt, foff, ncells, s));
     void *tmp_b = S.get<char>(std::max(t_esort, t_cscan));
     if (S.rc) return S.rc;
@@ -862,15 +876,24 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
                                               reinterpret_cast<float4 *>(gbuf + L.o_gcon));
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
-        k_fine_fill<<<(unsigned)((P + kFillBlock - 1) / kFillBlock), kFillBlock, 0, s>>>(
-            P, G, perm, means, conics, radii, cell_sbeg, cell_send, cell_box, foffs, fcount, ekeys,
-            evals, counters);
+        const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
+        if (k16)
+            k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
+                                                            cell_box, foffs, fcount,
+                                                            reinterpret_cast<uint16_t *>(ekeys), evals, counters);
+        else
+            k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
+                                                            cell_box, foffs, fcount, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = std::max(t_esort, t_cscan);
-        DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_b, tb, ekeys, ekeys_sorted, evals,
-                                                       entries, (int)E, 0, ebits, s));
+        DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s)
+                        : sort_entries<uint32_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s));
         DGS_LAUNCH_CHECK(s, debug);
-        k_identify<<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
+        if (k16)
+            k_identify<uint16_t><<<grid_for(E), kBlock, 0, s>>>(E, reinterpret_cast<const uint16_t *>(ekeys_sorted),
+                                                                2u * (uint32_t)ncells, hbeg, hend, 0);
+        else
+            k_identify<uint32_t><<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
         DGS_LAUNCH_CHECK(s, debug);
     }
     k_cell_ranges<<<grid_for(ncells), kBlock, 0, s>>>(ncells, hbeg, hend, cell_gbeg, cell_gmid, cell_gend);
