@@ -12,7 +12,7 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [REPO, os.path.join(REPO, "diff-gaussian-sampling_amd")]
+sys.path[:0] = [REPO, os.environ.get("DGS_PKG_ROOT", os.path.join(REPO, "diff-gaussian-sampling_amd"))]  # variants: tools/variant.sh
 
 import torch  # noqa: E402
 
