@@ -12,7 +12,7 @@ import os
 import sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, os.path.join(REPO, "diff-gaussian-sampling_amd"))
+sys.path.insert(0, os.environ.get("DGS_PKG_ROOT", os.path.join(REPO, "diff-gaussian-sampling_amd")))  # variants: tools/variant.sh
 
 import torch  # noqa: E402
 
