@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--C", type=int, default=1)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--cpu-samples", type=int, default=3072)
+    ap.add_argument("--cpu-torch-samples", type=int, default=2048,
+                    help="query points of the PyTorch-eager CPU baseline")
     ap.add_argument("--pre-reps", type=int, default=5, help="warm preprocess repetitions (median)")
     ap.add_argument("--op", default="sample", choices=["sample", "aggregate"],
                     help="sample: the headline (default); aggregate: aggregate_neighbors at SURVEY "
@@ -204,6 +206,10 @@ def main():
         result["cpu_baseline"] = cpu_baseline(means.detach().cpu(), values.detach().cpu(),
                                               covs.cpu(), conics.detach().cpu(), samples.cpu(),
                                               dL.cpu(), fn, args.cpu_samples)
+        if fn == "gaussian":  # BASELINE north_star: PyTorch-eager CPU on the host cores, beside it
+            result["cpu_baseline_torch_eager"] = cpu_baseline_torch(
+                means.detach().cpu(), values.detach().cpu(), covs.cpu(), conics.detach().cpu(),
+                samples.cpu(), dL.cpu(), args.cpu_torch_samples)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
@@ -345,6 +351,24 @@ def cpu_baseline(means, values, covs, conics, samples, dL, fn, nsub):
     return {"value": nsub / dt, "unit": "points/s", "cores": 1, "kind": "port",
             "sample": f"first {nsub} of the 2M query points of the same workload, fwd+bwd, "
                       f"binning excluded ({dt:.1f} s)"}
+
+
+def cpu_baseline_torch(means, values, covs, conics, samples, dL, nsub):
+    """PyTorch eager (float32, all host threads torch uses) on the first `nsub` query points:
+    the same pair set and math, forward + backward by autograd (oracle/torch_eager.py)."""
+    import numpy as np
+    from oracle import oracle as orc
+    from oracle import torch_eager as te
+    orc.build()
+    ob = orc.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+    sub = np.arange(nsub, dtype=np.int32)
+    t0 = time.perf_counter()
+    te.gaussian_fwd_bwd(ob, means.numpy(), values.numpy(), conics.numpy(), samples.numpy(),
+                        dL.numpy(), sub)
+    dt = time.perf_counter() - t0
+    return {"value": nsub / dt, "unit": "points/s", "cores": torch.get_num_threads(), "kind": "port",
+            "sample": f"first {nsub} of the 2M query points, every Gaussian of their tiles, "
+                      f"torch eager fwd + autograd bwd, binning excluded ({dt:.1f} s)"}
 
 
 if __name__ == "__main__":
