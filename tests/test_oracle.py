@@ -188,3 +188,28 @@ def test_known_answer_full_range_and_absent(oracle):
     assert ob.num_rendered == ob.T
     for t in range(ob.T):
         assert list(ob.tile_gaussians(t)) == [1]
+
+
+@pytest.mark.parametrize("case", ["synthetic", "seam"])
+def test_torch_eager_baseline_matches_oracle(oracle, case):
+    """oracle/torch_eager.py (bench.py's PyTorch-eager CPU baseline) computes what the C oracle
+    computes: gaussian forward and its gradients over the reference's tile pair set."""
+    import sys, os
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from oracle import torch_eager as te
+    if case == "synthetic":
+        means, values, covs, conics = syn.gaussians(800, 2, 2, seed=3)
+        samples = syn.samples(3000, 2, seed=4)
+    else:
+        means, values, covs, conics, samples = cases.seam_case(D=2, C=2)
+    N = samples.shape[0]
+    dL = syn.grad_out(N, 1, values.shape[1], seed=6)
+    ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+    sub = np.arange(N, dtype=np.int32)
+    out, grads = te.gaussian_fwd_bwd(ob, means.numpy(), values.numpy(), conics.numpy(), samples.numpy(),
+                                     dL.numpy(), sub)
+    ref = ob.forward("gaussian", values.numpy(), conics.numpy(), subset=sub).reshape(out.shape)
+    close(out.numpy(), ref, 1e-5, 1e-6, "torch eager forward")
+    for g, r, name in zip(grads, ob.backward("gaussian", values.numpy(), conics.numpy(), dL.numpy(), subset=sub),
+                          ("means", "values", "conics")):
+        close(g.numpy(), r, 1e-4, 1e-5, f"torch eager d/d{name}")
