@@ -132,3 +132,17 @@ def agg_problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0, radius=(0.3, 1.2)
 
 
 AGG_FEATURES = ("features", "transform", "queries", "keys", "frequencies", "distance_transform")
+
+
+def wide_domain_case(n=20000, P=3000, half=40.0, seed=141):
+    """Query points over [-half, half)^2: ~157^2 tiles of one fine cell each, so 2 * ncells
+    exceeds 2^16 and the binning sorts 32-bit (cell, flag) keys (the 16-bit path elsewhere)."""
+    g = torch.Generator().manual_seed(seed)
+    means = ((torch.rand(P, 2, generator=g) * 2.0 - 1.0) * half).float()
+    sig = 0.2 + 0.4 * torch.rand(P, 1, generator=g)
+    covs = torch.cat([sig ** 2, 0.1 * sig ** 2, 0.8 * sig ** 2], 1).float()
+    det = covs[:, 0] * covs[:, 2] - covs[:, 1] ** 2
+    conics = torch.stack([covs[:, 2] / det, -covs[:, 1] / det, covs[:, 0] / det], 1).float()
+    values = torch.randn(P, 1, generator=g).float()
+    samples = ((torch.rand(n, 2, generator=g) * 2.0 - 1.0) * half).float()
+    return means, values, covs, conics, samples

@@ -223,3 +223,12 @@ def test_parity_headline_size_subset(dgs, oracle, function):
     dL = torch.zeros(N, K, 1)
     dL[subset] = syn.grad_out(len(subset), K, 1, seed=112)
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=subset)
+
+
+@pytest.mark.parametrize("function", ["gaussian", "laplacian"])
+def test_parity_wide_domain_32bit_entry_keys(dgs, oracle, function):
+    """~25k tiles: the entry sort runs on 32-bit keys (2 * ncells > 2^16)."""
+    means, values, covs, conics, s = cases.wide_domain_case()
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(s.shape[0], K, 1, seed=142)
+    _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
