@@ -553,12 +553,16 @@ __global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
 }
 
 // Means and conics in internal order (the forward/backward read them coalesced from here).
+// Also stores perm (internal -> caller id) and its inverse back to back in gperm (one pass
+// over the permutation instead of two launches).
 __global__ void k_geo_pack(int P, int D, const uint32_t *__restrict__ perm, const float *__restrict__ means,
                            const float *__restrict__ conics, float2 *__restrict__ gmean,
-                           float4 *__restrict__ gcon) {
+                           float4 *__restrict__ gcon, int32_t *__restrict__ gperm) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
+    gperm[i] = (int32_t)g;
+    gperm[P + g] = (int32_t)i;
     if (D == 2) {
         gmean[i] = make_float2(means[g * 2], means[g * 2 + 1]);
         gcon[i] = make_float4(conics[g * 3], conics[g * 3 + 1], conics[g * 3 + 2], 0.0f);
@@ -603,15 +607,6 @@ struct ZeroList {
     void add(void *p, size_t bytes) { z.p[z.count] = static_cast<uint32_t *>(p); z.n[z.count++] = (int64_t)(bytes / 4); }
     void launch(hipStream_t s) { k_zero_multi<<<256, 256, 0, s>>>(z); }
 };
-
-// perm (internal -> caller id) and its inverse, stored back to back.
-__global__ void k_perm_pair(int64_t n, const uint32_t *__restrict__ a, int32_t *__restrict__ b) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t g = a[i];
-    b[i] = (int32_t)g;
-    b[n + g] = (int32_t)i;
-}
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
@@ -869,11 +864,9 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
         zl.launch(s);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    k_perm_pair<<<grid_for(P), kBlock, 0, s>>>(P, perm, gperm);
-    DGS_LAUNCH_CHECK(s, debug);
     k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
                                               reinterpret_cast<float2 *>(gbuf + L.o_gmean),
-                                              reinterpret_cast<float4 *>(gbuf + L.o_gcon));
+                                              reinterpret_cast<float4 *>(gbuf + L.o_gcon), gperm);
     DGS_LAUNCH_CHECK(s, debug);
     if (E > 0) {
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
