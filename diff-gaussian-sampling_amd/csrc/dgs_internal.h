@@ -410,6 +410,7 @@ struct UnitHint {
     size_t gbytes, sbytes;
     int64_t nfwd, nbwd;
     int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
+    int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);

@@ -936,6 +936,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = -1;
+    uh.P = P; uh.D = D; uh.N = N;
     hint_put(uh);
     return DGS_OK;
 }

@@ -998,6 +998,14 @@ static int validate(int FN, int P, int D, int N, int C, const void *gb, size_t g
     if (!gb || !sb || gbytes < kHeaderBytes || sbytes < kHeaderBytes)
         return fail(DGS_ERR_BUFFER, "binning buffers missing or too small (run preprocess first)");
     if (have < need) return fail(DGS_ERR_ARG, "workspace too small");
+    // The kernels index perm / rows / samples by the binned sizes: a call with other sizes than
+    // the buffers were built for is an error (checked on the host against the preprocess record;
+    // buffers from elsewhere have none and are trusted, as in the reference).
+    UnitHint h;
+    if (hint_get(gb, gbytes, sb, sbytes, &h) && (h.P != P || h.D != D || h.N != N))
+        return fail(DGS_ERR_ARG, "P / D / N differ from the ones the binning buffers were built for (P " +
+                                     std::to_string(h.P) + ", D " + std::to_string(h.D) + ", N " +
+                                     std::to_string(h.N) + ")");
     return DGS_OK;
 }
 

@@ -48,6 +48,8 @@ def _load():
     lib.orc_tile_grid.argtypes = [i32, i32, P, P, P]
     lib.orc_agg_counts.argtypes = [i32, i32, P, P, P]
     lib.orc_agg_fill.argtypes = [i32, i32, P, P, P, P, P, P, P, P]
+    lib.orc_agg_counts_rows.argtypes = [i32, i32, P, P, i32, P, P]
+    lib.orc_agg_fill_rows.argtypes = [i32, i32, P, P, P, i32, P, P, P, P, P, P]
     lib.orc_agg_forward.argtypes = [i32] * 5 + [P] * 15
     lib.orc_agg_backward.argtypes = [i32] * 5 + [P] * 21
     _lib = lib
@@ -198,6 +200,27 @@ def agg_preprocess(means, conics, radii):
     return indices, ranges, dists, dens, inv
 
 
+def agg_preprocess_rows(means, conics, radii, rows):
+    """preprocess_aggregate restricted to the rows `rows` (each an O(P) scan): compact lists
+    (indices, ranges [len(rows)] inclusive cumsum, dists, densities, inv_total [len(rows)])
+    equal to those rows' slices of agg_preprocess."""
+    lib = _load()
+    m, c, r = _f32(means), _f32(conics), _f32(radii)
+    rw = np.ascontiguousarray(rows, dtype=np.int32)
+    P, D = m.shape
+    counts = np.zeros(len(rw), np.int64)
+    lib.orc_agg_counts_rows(P, D, _ptr(m), _ptr(r), len(rw), _ptr(rw), _ptr(counts))
+    ranges = np.cumsum(counts).astype(np.int64)
+    n = int(ranges[-1]) if len(rw) else 0
+    indices = np.full(n, -1, np.int64)
+    dists = np.zeros((n, D), np.float32)
+    dens = np.zeros(n, np.float32)
+    inv = np.zeros(len(rw), np.float32)
+    lib.orc_agg_fill_rows(P, D, _ptr(m), _ptr(c), _ptr(r), len(rw), _ptr(rw), _ptr(ranges),
+                          _ptr(indices), _ptr(dists), _ptr(dens), _ptr(inv))
+    return indices, ranges, dists, dens, inv
+
+
 def agg_forward(features, transform, queries, keys, frequencies, distance_transform, indices,
                 ranges, dists, densities, inv_total, rows=None):
     """aggregate_neighbors forward: (weights, embeddings, factors, neighbor_features).
@@ -238,3 +261,48 @@ def agg_backward(features, transform, queries, keys, frequencies, distance_trans
                          _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
                          _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
     return tuple(outs)
+
+
+def agg_forward_rows(features, transform, queries, keys, frequencies, distance_transform, rows,
+                     indices, ranges, dists, densities, inv_total):
+    """agg_forward over the rows `rows` only, on the compact lists of agg_preprocess_rows:
+    (weights, embeddings, factors) of those slots and neighbor_features [len(rows), L]."""
+    lib = _load()
+    f, T, k = _f32(features), _f32(transform), _f32(keys)
+    q = _f32(np.asarray(queries)[np.asarray(rows)])
+    fr, dt = _f32(frequencies), _f32(distance_transform)
+    idx, rg, X, dn, inv = _i64(indices), _i64(ranges), _f32(dists), _f32(densities), _f32(inv_total)
+    L, K, n = f.shape[1], q.shape[1], idx.size
+    D = X.shape[1] if X.ndim == 2 else 1
+    E = dt.size // 2
+    w, emb, fac = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
+    out = np.zeros((len(rows), L), np.float32)
+    lib.orc_agg_forward(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+                        _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(w), _ptr(emb),
+                        _ptr(fac), _ptr(out))
+    return w, emb, fac, out
+
+
+def agg_backward_rows(features, transform, queries, keys, frequencies, distance_transform, rows,
+                      indices, ranges, dists, densities, weights, embeddings, factors, inv_total, dL_rows):
+    """agg_backward with dL/dneighbor_features non-zero on the rows `rows` only (dL_rows
+    [len(rows), L]), on their compact lists: the six gradients (queries' gradient full-size,
+    zero outside `rows`)."""
+    lib = _load()
+    f, T, k = _f32(features), _f32(transform), _f32(keys)
+    qf = _f32(queries)
+    q = _f32(qf[np.asarray(rows)])
+    fr, dt = _f32(frequencies), _f32(distance_transform)
+    idx, rg, X, dn = _i64(indices), _i64(ranges), _f32(dists), _f32(densities)
+    w, emb, fac, inv, g = _f32(weights), _f32(embeddings), _f32(factors), _f32(inv_total), _f32(dL_rows)
+    L, K = f.shape[1], q.shape[1]
+    D = X.shape[1] if X.ndim == 2 else 1
+    E = dt.size // 2
+    dq_rows = np.zeros_like(q)
+    outs = [np.zeros_like(f), np.zeros_like(T), dq_rows, np.zeros_like(k), np.zeros_like(fr), np.zeros_like(dt)]
+    lib.orc_agg_backward(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+                         _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
+                         _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
+    dq = np.zeros_like(qf)
+    dq[np.asarray(rows)] = dq_rows
+    return outs[0], outs[1], dq, outs[3], outs[4], outs[5]

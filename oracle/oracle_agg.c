@@ -46,16 +46,25 @@ void orc_agg_counts(int P, int D, const float *means, const float *radii, int64_
     }
 }
 
+/* The same for the rows rows[0..nrows) only (a bounded check of a large problem). */
+void orc_agg_counts_rows(int P, int D, const float *means, const float *radii, int nrows,
+                         const int32_t *rows, int64_t *counts) {
+    for (int r = 0; r < nrows; ++r) {
+        int64_t n = 0;
+        for (int j = 0; j < P; ++j) n += agg_collides(D, means, radii, rows[r], j);
+        counts[r] = n;
+    }
+}
+
 /* Pass 2: preprocess, aggregate_neighbors.cu:52-127.  ranges = inclusive cumsum of counts;
  * indices pre-filled with -1, dists / densities with 0 (the host glue at 336-341). */
-void orc_agg_fill(int P, int D, const float *means, const float *conics, const float *radii,
-                  const int64_t *ranges, int64_t *indices, float *dists, float *densities,
-                  float *inv_total) {
+static void agg_fill_row(int P, int D, const float *means, const float *conics,
+                         const float *radii, int i, int64_t start, int64_t *indices, float *dists,
+                         float *densities, float *inv_total_i) {
     const int S = D * (D + 1) / 2;
-    for (int i = 0; i < P; ++i) {
+    {
         const float my_radius = (float)((double)radii[i] * 0.333);
         const float my_inv_radius = (float)(1.0 / ((double)my_radius + 1e-6));
-        const int64_t start = i == 0 ? 0 : ranges[i - 1];
         float total = 0.0f;
         int64_t current = -1;
         for (int j = 0; j < P; ++j) {
@@ -83,8 +92,26 @@ void orc_agg_fill(int P, int D, const float *means, const float *conics, const f
             indices[start + current] = j;
             total += densities[start + current];
         }
-        inv_total[i] = (float)(1.0 / ((double)total + 1e-6));
+        *inv_total_i = (float)(1.0 / ((double)total + 1e-6));
     }
+}
+
+void orc_agg_fill(int P, int D, const float *means, const float *conics, const float *radii,
+                  const int64_t *ranges, int64_t *indices, float *dists, float *densities,
+                  float *inv_total) {
+    for (int i = 0; i < P; ++i)
+        agg_fill_row(P, D, means, conics, radii, i, i == 0 ? 0 : ranges[i - 1], indices, dists,
+                     densities, inv_total + i);
+}
+
+/* Rows rows[0..nrows) only, into compact lists: row r's slots start at ranges[r - 1]
+ * (ranges = inclusive cumsum of orc_agg_counts_rows). */
+void orc_agg_fill_rows(int P, int D, const float *means, const float *conics, const float *radii,
+                       int nrows, const int32_t *rows, const int64_t *ranges, int64_t *indices,
+                       float *dists, float *densities, float *inv_total) {
+    for (int r = 0; r < nrows; ++r)
+        agg_fill_row(P, D, means, conics, radii, rows[r], r == 0 ? 0 : ranges[r - 1], indices,
+                     dists, densities, inv_total + r);
 }
 
 /* aggregateNeighbors, aggregate_neighbors.cu:129-208.  E = distance_transform.size / 2. */

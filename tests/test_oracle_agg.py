@@ -120,3 +120,27 @@ def test_forward_and_backward_vs_autograd(oracle, D):
     for name, a, b in zip(("features", "transform", "queries", "keys", "frequencies", "distance_transform"),
                           got, grads):
         close(a, b.numpy(), 1e-4, 2e-5, f"d/d{name}")
+
+
+@pytest.mark.parametrize("D", [1, 2])
+def test_row_restricted_oracle_equals_full(oracle, D):
+    """The row-restricted scan and its forward/backward (the config-5 GPU subset check) equal the
+    full oracle: the same slots, outputs, and the gradients of a loss with dL on those rows only."""
+    m, c, r, fe = _problem(P=150, D=D, seed=31)
+    full = oracle.agg_preprocess(m, c, r)
+    rows = np.array([0, 3, 5, 77, 149], np.int32)
+    sub = oracle.agg_preprocess_rows(m, c, r, rows)
+    rg = full[1]
+    sl = np.concatenate([np.arange(0 if i == 0 else rg[i - 1], rg[i]) for i in rows])
+    assert np.array_equal(full[0][sl], sub[0]) and np.array_equal(full[2][sl], sub[2])
+    assert np.array_equal(full[3][sl], sub[3]) and np.array_equal(full[4][rows], sub[4])
+    args = [fe[k] for k in ("features", "transform", "queries", "keys", "frequencies", "distance_transform")]
+    w, e, f, out = oracle.agg_forward(*args, *full)
+    ws, es, fs, outs = oracle.agg_forward_rows(*args, rows, *sub)
+    assert np.array_equal(w[sl], ws) and np.array_equal(out[rows], outs)
+    g = np.zeros_like(out)
+    g[rows] = np.random.default_rng(32).normal(size=(len(rows), out.shape[1])).astype(np.float32)
+    ref = oracle.agg_backward(*args, *full[:4], w, e, f, full[4], g)
+    got = oracle.agg_backward_rows(*args, rows, *sub[:4], ws, es, fs, sub[4], g[rows])
+    for a, b in zip(got, ref):
+        close(a, b, 1e-6, 1e-7, "row-restricted gradient")
