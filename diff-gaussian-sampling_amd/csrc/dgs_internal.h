@@ -19,7 +19,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 3;
+constexpr uint32_t kVersion = 4;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -45,13 +45,23 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 // Opaque buffer layout.  Gaussian-side buffer (DGS_BUF_BINNING):
 //   [header 256 B][counts int32[4]][perm int32[P]][cell_gbeg int32[ncells]]
 //   [cell_gmid int32[ncells]][cell_gend int32[ncells]][entries uint32[E]][bwd_units uint2[bwd_cap]]
-//   [gmean float2[P]][gcon float4[P]]  (means / conics in internal order, packed at binning:
-//                                       forward/backward must pass the binned means/conics)
+//   [gmean float2[P]][gcon float4[P]]  (means / conics in internal order, packed at binning)
+//   [mcopy float[P*D]][ccopy float[P*S]]  (the binned means / conics as passed, caller order)
+//   [rlist uint32[R]]  the reference's point_list: every tile's Gaussian ids, ascending
+//                      (sampler_impl.cu:265-283), the pair set of the call-time path
+//   [rtab uint32[4][T+1]]  per tile: Gaussian-list start (rlist), sample start (sorted order),
+//                      and the prefix counts of the call-time path's forward / backward units
 // A cell's list is [gbeg, gend); its flag-free entries come first, [gbeg, gmid).
 // Sample-side buffer (DGS_BUF_SAMPLE_BINNING):
-//   [header copy 256 B][sorted_sid int32[N]][cell_sbeg int32[ncells]][cell_send int32[ncells]]
+//   [header copy][sorted_sid int32[N]][cell_sbeg int32[ncells]][cell_send int32[ncells]]
 //   [fwd_units uint2[fwd_cap]][cell_box float4[ncells]]
 //   [fsrows: sample pair rows [s0(2p) s0(2p+1) (s1(2p) s1(2p+1))] in sorted order, + slack]
+//   [scopy float[N*D]]  (the binned samples as passed, caller order)
+// The fine-cell lists are built from the binned means / conics / samples.  The reference reads
+// means / conics / samples at every forward / backward call (forward.cu:136-145,
+// backward.cu:76-85) and only its tile lists from preprocess; each call therefore compares its
+// tensors with the copies (k_verify) and, if any differs, takes the call-time path instead
+// (dgs_reference.hip: the reference's tile pair set, the passed tensors).
 // ---------------------------------------------------------------------------------------
 struct Header {
     uint32_t magic, version;
@@ -71,9 +81,12 @@ struct Header {
     uint64_t o_cell_gmid;
     uint64_t o_cell_box;  // sample buffer: per-cell bounding box of the cell's samples
     uint64_t o_gmean, o_gcon, o_fsrows;
+    uint64_t o_mcopy, o_ccopy, o_rlist, o_rtab, o_scopy;
 };
-static_assert(sizeof(Header) <= 256, "header too large");
-constexpr size_t kHeaderBytes = 256;
+constexpr size_t kHeaderBytes = 512;
+static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
+enum RefTab { kRtGStart = 0, kRtSStart = 1, kRtFwdUnits = 2, kRtBwdUnits = 3 };
+constexpr int kRefUnit = 64;  // call-time path: samples (forward) / list entries (backward) per unit
 
 enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1, kNumUnsafe = 2 };
 
@@ -81,16 +94,17 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
-    uint64_t o_gmean, o_gcon;
-    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, s_bytes;
+    uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab;
+    uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
 };
 
 // Forward sample pair rows: N rounded up to a pair, plus slack for a pass's wide scalar loads
 // (up to 32 pairs + one x16 load past the last pair).
 inline size_t fsrows_bytes(int64_t N, int D) { return ((size_t)N + 1) * D * 4 + 36 * 16; }
 
-inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64_t fwd_cap,
-                          int64_t bwd_cap) {
+inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int64_t ncells, int64_t E,
+                          int64_t fwd_cap, int64_t bwd_cap) {
+    const int S = D * (D + 1) / 2;
     Layout L;
     size_t o = kHeaderBytes;
     L.o_counts = o;    o = align_up(o + 16, 256);
@@ -102,6 +116,10 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_bwd_units = o; o = align_up(o + 8 * (size_t)bwd_cap, 256);
     L.o_gmean = o;     o = align_up(o + 8 * (size_t)P, 256);
     L.o_gcon = o;      o = align_up(o + 16 * (size_t)P, 256);
+    L.o_mcopy = o;     o = align_up(o + 4 * (size_t)P * D, 256);
+    L.o_ccopy = o;     o = align_up(o + 4 * (size_t)P * S, 256);
+    L.o_rlist = o;     o = align_up(o + 4 * (size_t)R + 64, 256);
+    L.o_rtab = o;      o = align_up(o + 16 * ((size_t)T + 1), 256);
     L.g_bytes = o;
     o = kHeaderBytes;
     L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);
@@ -110,6 +128,7 @@ inline Layout make_layout(int64_t P, int64_t N, int64_t ncells, int64_t E, int64
     L.o_fwd_units = o; o = align_up(o + 8 * (size_t)fwd_cap, 256);
     L.o_cell_box = o;  o = align_up(o + 16 * (size_t)ncells, 256);
     L.o_fsrows = o;    o = align_up(o + fsrows_bytes(N, 2), 256);
+    L.o_scopy = o;     o = align_up(o + 4 * (size_t)N * D, 256);
     L.s_bytes = o;
     return L;
 }
@@ -129,6 +148,8 @@ struct Bins {
     const float2 *gmean;     // means in internal order ({m, 0} at D = 1)
     const float4 *gcon;      // conics in internal order ({c0, c1, c2, 0}; {c0, 0, 0, 0} at D = 1)
     const float *fsrows;     // sample pair rows in sorted order
+    const uint32_t *rlist;   // reference tile lists (ascending Gaussian id per tile)
+    const uint32_t *rtab;    // [4][T+1] per-tile tables of the call-time path (RefTab)
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -160,6 +181,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     const uint64_t o_box = sload(&B.h->o_cell_box);
     const uint64_t o_gmean = sload(&B.h->o_gmean), o_gcon = sload(&B.h->o_gcon);
     const uint64_t o_fsrows = sload(&B.h->o_fsrows);
+    const uint64_t o_rlist = sload(&B.h->o_rlist), o_rtab = sload(&B.h->o_rtab);
     B.counts = reinterpret_cast<const int32_t *>(gb + o_counts);
     B.perm = reinterpret_cast<const int32_t *>(gb + o_perm);
     B.cell_gbeg = reinterpret_cast<const int32_t *>(gb + o_gbeg);
@@ -175,6 +197,8 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.gmean = reinterpret_cast<const float2 *>(gb + o_gmean);
     B.gcon = reinterpret_cast<const float4 *>(gb + o_gcon);
     B.fsrows = reinterpret_cast<const float *>(sb + o_fsrows);
+    B.rlist = reinterpret_cast<const uint32_t *>(gb + o_rlist);
+    B.rtab = reinterpret_cast<const uint32_t *>(gb + o_rtab);
     return B;
 }
 
@@ -411,6 +435,7 @@ struct UnitHint {
     int64_t nfwd, nbwd;
     int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
+    int64_t R;        // num_rendered (sizes the call-time path's backward grid)
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);

@@ -496,9 +496,10 @@ __global__ void k_cell_ranges(int ncells, const int32_t *__restrict__ hb, const 
 }
 
 __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
-                         const uint64_t *__restrict__ rsum, int64_t *__restrict__ out) {
+                         const uint64_t *__restrict__ toffs, const uint64_t *__restrict__ touched,
+                         int64_t *__restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    out[0] = (int64_t)rsum[0];
+    out[0] = P > 0 ? (int64_t)(toffs[P - 1] + touched[P - 1]) : 0;  // num_rendered (sampler_impl.cu:253-257)
     out[1] = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;
 }
 
@@ -532,14 +533,93 @@ __global__ void k_unit_fill(int ncells, const int32_t *__restrict__ sbeg,
     }
 }
 
-// Reference-layout ranges (identifyTileRanges semantics: empty tiles stay (0, 0)).
-__global__ void k_ref_ranges(int T, const uint32_t *__restrict__ cnt, uint2 *__restrict__ ranges) {
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    uint32_t acc = 0;
-    for (int t = 0; t < T; ++t) {
-        const uint32_t c = cnt[t];
-        ranges[t] = c ? make_uint2(acc, acc + c) : make_uint2(0u, 0u);
-        acc += c;
+// duplicateWithKeys (sampler_impl.cu:54-129) without the 64-bit key: every Gaussian writes
+// its tiles, in the reference's order, at its scan offset (caller id order); a stable sort by
+// tile then yields the reference's point_list (ascending id per tile) -- the pair set of the
+// call-time path (dgs_reference.hip).
+__global__ void k_ref_keys(int P, Geom G, const float *__restrict__ means, const float *__restrict__ radii,
+                           const uint64_t *__restrict__ offs, uint32_t *__restrict__ keys,
+                           uint32_t *__restrict__ vals) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P) return;
+    const float r = radii[g];
+    if (!(r > 0.0f)) return;
+    const float m[2] = {means[g * G.D], G.D == 2 ? means[g * G.D + 1] : 0.0f};
+    const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
+    uint64_t o = offs[g];
+    for (int y = kr.y0; y < kr.y1; ++y)
+        for (int x = kr.x0; x < kr.x1; ++x) {
+            keys[o] = key_of(G.D, x, y, G.grid);
+            vals[o] = (uint32_t)g;
+            ++o;
+        }
+}
+
+// Reference-layout ranges (identifyTileRanges semantics: empty tiles stay (0, 0)) for the
+// Gaussian and the sample lists, and the call-time path's per-tile tables (RefTab): list
+// starts and unit prefix counts.  One block; each thread scans a contiguous run of tiles.
+__global__ __launch_bounds__(1024) void k_ref_tables(int T, const uint32_t *__restrict__ gcnt,
+                                                     const uint32_t *__restrict__ scnt,
+                                                     uint2 *__restrict__ granges, uint2 *__restrict__ sranges,
+                                                     uint32_t *__restrict__ rtab) {
+    __shared__ uint4 part[1024];
+    const int nt = blockDim.x, t = threadIdx.x;
+    const int per = (T + nt - 1) / nt, a = min(T, t * per), b = min(T, a + per);
+    uint4 sum = make_uint4(0u, 0u, 0u, 0u);
+    for (int k = a; k < b; ++k) {
+        const uint32_t g = gcnt[k], sm = scnt[k];
+        sum.x += g;
+        sum.y += sm;
+        sum.z += g ? (sm + kRefUnit - 1) / kRefUnit : 0u;  // forward units: sample chunks of tiles with Gaussians
+        sum.w += sm ? (g + kRefUnit - 1) / kRefUnit : 0u;  // backward units: list chunks of tiles with samples
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (int d = 1; d < nt; d <<= 1) {  // inclusive Hillis-Steele scan of the thread partials
+        const uint4 o = t >= d ? part[t - d] : make_uint4(0u, 0u, 0u, 0u);
+        __syncthreads();
+        part[t] = make_uint4(part[t].x + o.x, part[t].y + o.y, part[t].z + o.z, part[t].w + o.w);
+        __syncthreads();
+    }
+    const uint4 incl = part[t];
+    uint32_t acc[4] = {incl.x - sum.x, incl.y - sum.y, incl.z - sum.z, incl.w - sum.w};
+    uint32_t *tab[4] = {rtab + kRtGStart * (T + 1), rtab + kRtSStart * (T + 1), rtab + kRtFwdUnits * (T + 1),
+                        rtab + kRtBwdUnits * (T + 1)};
+    for (int k = a; k < b; ++k) {
+        const uint32_t g = gcnt[k], sm = scnt[k];
+        granges[k] = g ? make_uint2(acc[0], acc[0] + g) : make_uint2(0u, 0u);
+        sranges[k] = sm ? make_uint2(acc[1], acc[1] + sm) : make_uint2(0u, 0u);
+        for (int q = 0; q < 4; ++q) tab[q][k] = acc[q];
+        acc[0] += g;
+        acc[1] += sm;
+        acc[2] += g ? (sm + kRefUnit - 1) / kRefUnit : 0u;
+        acc[3] += sm ? (g + kRefUnit - 1) / kRefUnit : 0u;
+    }
+    if (t == nt - 1) {  // the totals
+        tab[0][T] = incl.x; tab[1][T] = incl.y; tab[2][T] = incl.z; tab[3][T] = incl.w;
+    }
+}
+
+// Copies up to 4 word arrays in one launch (the binned tensors, kept for the per-call check).
+struct CopySpec {
+    const uint32_t *src[4];
+    uint32_t *dst[4];
+    int64_t n[4];  // words
+    int count;
+};
+
+__global__ void k_copy_multi(CopySpec c) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int r = 0; r < c.count; ++r) {
+        int64_t done = 0;
+        if (((reinterpret_cast<uintptr_t>(c.src[r]) | reinterpret_cast<uintptr_t>(c.dst[r])) & 15) == 0) {
+            const int64_t n4 = c.n[r] >> 2;  // 16-byte pieces
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(c.src[r]);
+            uint4 *d4 = reinterpret_cast<uint4 *>(c.dst[r]);
+            for (int64_t i = t; i < n4; i += st) d4[i] = s4[i];
+            done = n4 << 2;
+        }
+        for (int64_t i = done + t; i < c.n[r]; i += st) c.dst[r][i] = c.src[r][i];
     }
 }
 
@@ -738,7 +818,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
 
     // ---- sample-side buffer (size known now) and the reference range buffers
     const int64_t fwd_cap = (N + kFwdUnit - 1) / kFwdUnit + 2 * std::min<int64_t>(N, ncells) + 1;
-    Layout L0 = make_layout(P, N, ncells, 0, fwd_cap, 0);
+    Layout L0 = make_layout(D, P, N, G.T, 0, ncells, 0, fwd_cap, 0);
     char *sbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_BINNING, L0.s_bytes));
     char *rbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_RANGES, (size_t)G.T * 8 + 8));
     char *srbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SAMPLE_RANGES, (size_t)G.T * 8 + 8));
@@ -755,13 +835,13 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     uint32_t *home = S.get<uint32_t>(P), *home_sorted = S.get<uint32_t>(P), *gids = S.get<uint32_t>(P);
     uint32_t *perm = S.get<uint32_t>(P);
     uint64_t *touched = S.get<uint64_t>(P), *fcount = S.get<uint64_t>(P), *foffs = S.get<uint64_t>(P);
-    uint64_t *rsum = S.get<uint64_t>(1);
+    uint64_t *toffs = S.get<uint64_t>(P);
 
     int64_t *totals = S.get<int64_t>(2);
     if (S.rc) return S.rc;
 
     // hipcub temp storage: one allocation sized for the largest phase-A primitive
-    size_t t_ssort = 0, t_hsort = 0, t_scan = 0, t_red = 0;
+    size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
     const int sbits = bit_length((uint64_t)ncells);
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
     DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_ssort, skeys, skeys_sorted, sids,
@@ -769,8 +849,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
                                                    perm, P, 0, hbits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, fcount, foffs, P, s));
-    DGS_TRY_HIP(hipcub::DeviceReduce::Sum(nullptr, t_red, touched, rsum, P, s));
-    const size_t t_a = std::max(std::max(t_ssort, t_hsort), std::max(t_scan, t_red));
+    const size_t t_a = std::max(std::max(t_ssort, t_hsort), t_scan);
     void *tmp_a = S.get<char>(t_a);
     if (S.rc) return S.rc;
 
@@ -818,8 +897,8 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     tb = t_a;
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, fcount, foffs, P, s));
     tb = t_a;
-    DGS_TRY_HIP(hipcub::DeviceReduce::Sum(tmp_a, tb, touched, rsum, P, s));
-    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, rsum, totals);
+    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, touched, toffs, P, s));
+    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, totals);
     DGS_LAUNCH_CHECK(s, debug);
     int64_t htot[2] = {0, 0};
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
@@ -827,10 +906,11 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     const int64_t R = htot[0], E = htot[1];
     *num_rendered = R;
     if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries");
+    if (R >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "num_rendered exceeds 2^31 (32-bit tile lists)");
 
     // ---- Gaussian-side buffer
     const int64_t bwd_cap = (E + kWave - 1) / kWave + std::min<int64_t>(E, ncells) + 1;
-    Layout L = make_layout(P, N, ncells, E, fwd_cap, bwd_cap);
+    Layout L = make_layout(D, P, N, G.T, R, ncells, E, fwd_cap, bwd_cap);
     char *gbuf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_BINNING, L.g_bytes));
     if (!gbuf) return fail(DGS_ERR_ALLOC, "binning buffer allocation failed");
     int32_t *counters = reinterpret_cast<int32_t *>(gbuf + L.o_counts);
@@ -846,14 +926,19 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     uint32_t *fcnt = S.get<uint32_t>(ncells), *bcnt = S.get<uint32_t>(ncells);
     int32_t *hbeg = S.get<int32_t>(2 * (size_t)ncells), *hend = S.get<int32_t>(2 * (size_t)ncells);
     uint32_t *foff = S.get<uint32_t>(ncells), *boff = S.get<uint32_t>(ncells);
+    uint32_t *rkeys = S.get<uint32_t>(R + 1), *rkeys_sorted = S.get<uint32_t>(R + 1), *rvals = S.get<uint32_t>(R + 1);
     if (S.rc) return S.rc;
-    size_t t_esort = 0, t_cscan = 0;
+    uint32_t *rlist = reinterpret_cast<uint32_t *>(gbuf + L.o_rlist);
+    size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
+    const int rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
+    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_rsort, rkeys, rkeys_sorted, rvals, rlist, (int)R, 0, rbits, s));
     const int ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
     const bool k16 = ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
     DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(nullptr, t_esort, ekeys, ekeys_sorted, evals, entries, E, ebits, s)
                     : sort_entries<uint32_t>(nullptr, t_esort, ekeys, ekeys_sorted, evals, entries, E, ebits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_cscan, fcnt, foff, ncells, s));
-    void *tmp_b = S.get<char>(std::max(t_esort, t_cscan));
+    const size_t t_b = std::max(std::max(t_esort, t_cscan), t_rsort);
+    void *tmp_b = S.get<char>(t_b);
     if (S.rc) return S.rc;
 
     {
@@ -878,7 +963,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
                                                             cell_box, foffs, fcount, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
-        tb = std::max(t_esort, t_cscan);
+        tb = t_b;
         DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s)
                         : sort_entries<uint32_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s));
         DGS_LAUNCH_CHECK(s, debug);
@@ -894,18 +979,40 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
                                                       cell_gend, fcnt, bcnt);
     DGS_LAUNCH_CHECK(s, debug);
-    tb = std::max(t_esort, t_cscan);
+    tb = t_b;
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, fcnt, foff, ncells, s));
-    tb = std::max(t_esort, t_cscan);
+    tb = t_b;
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, bcnt, boff, ncells, s));
     k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
                                                     boff, fwd_units, bwd_units, counters);
     DGS_LAUNCH_CHECK(s, debug);
 
-    // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled)
-    k_ref_ranges<<<1, 64, 0, s>>>(G.T, gtile, reinterpret_cast<uint2 *>(rbuf));
-    k_ref_ranges<<<1, 64, 0, s>>>(G.T, stile, reinterpret_cast<uint2 *>(srbuf));
+    // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled) and the
+    // call-time path's tables: its tile lists (the reference's point_list) and unit counts
+    k_ref_tables<<<1, 1024, 0, s>>>(G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf),
+                                    reinterpret_cast<uint2 *>(srbuf),
+                                    reinterpret_cast<uint32_t *>(gbuf + L.o_rtab));
     DGS_LAUNCH_CHECK(s, debug);
+    if (R > 0) {
+        k_ref_keys<<<grid_for(P), kBlock, 0, s>>>(P, G, means, radii, toffs, rkeys, rvals);
+        DGS_LAUNCH_CHECK(s, debug);
+        tb = t_b;
+        DGS_TRY_HIP(sort_pairs_onesweep(tmp_b, tb, rkeys, rkeys_sorted, rvals, rlist, (int)R, 0, rbits, s));
+        DGS_LAUNCH_CHECK(s, debug);
+    }
+    {  // the binned tensors as passed (each forward / backward compares its inputs with them)
+        const int S3 = D * (D + 1) / 2;
+        CopySpec c{};
+        c.src[0] = reinterpret_cast<const uint32_t *>(means); c.dst[0] = reinterpret_cast<uint32_t *>(gbuf + L.o_mcopy);
+        c.n[0] = (int64_t)P * D;
+        c.src[1] = reinterpret_cast<const uint32_t *>(conics); c.dst[1] = reinterpret_cast<uint32_t *>(gbuf + L.o_ccopy);
+        c.n[1] = (int64_t)P * S3;
+        c.src[2] = reinterpret_cast<const uint32_t *>(samples); c.dst[2] = reinterpret_cast<uint32_t *>(sbuf + L0.o_scopy);
+        c.n[2] = (int64_t)N * D;
+        c.count = 3;
+        k_copy_multi<<<1024, kBlock, 0, s>>>(c);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
 
     // ---- headers
     static std::atomic<uint64_t> stamp_counter{0x5eed0000ull};
@@ -926,6 +1033,8 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
     h.o_fwd_units = L0.o_fwd_units; h.o_cell_box = L0.o_cell_box; h.s_bytes = L0.s_bytes;
     h.o_gmean = L.o_gmean; h.o_gcon = L.o_gcon; h.o_fsrows = L0.o_fsrows;
+    h.o_mcopy = L.o_mcopy; h.o_ccopy = L.o_ccopy; h.o_rlist = L.o_rlist; h.o_rtab = L.o_rtab;
+    h.o_scopy = L0.o_scopy;
     h.stamp = ++stamp_counter;
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);
@@ -936,7 +1045,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = -1;
-    uh.P = P; uh.D = D; uh.N = N;
+    uh.P = P; uh.D = D; uh.N = N; uh.R = R;
     hint_put(uh);
     return DGS_OK;
 }

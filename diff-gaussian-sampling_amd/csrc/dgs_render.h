@@ -164,6 +164,37 @@ __device__ __forceinline__ U32s<N> sload_u(const uint32_t *p) {
     return r;
 }
 
+// dL of each function (indexed by function code; the fused form reads those of its mask)
+struct DLs {
+    const float *p[4];
+};
+// Output of each function (indexed by function code)
+struct Outs {
+    float *p[4];
+};
+
+// Stores (ADD: adds) the sum x of unique component ui (over the mask's functions), channel
+// ch, of sample sid into every output component of its function that maps to it.
+template <int FN, int D, bool ADD>
+__device__ __forceinline__ void store_unique(const Outs &outs, int64_t sid, int ui, int C, int ch,
+                                             float x) {
+    constexpr int M = fn_mask(FN);
+#pragma unroll
+    for (int f = 0; f < 4; ++f) {
+        if (!(M & (1 << f))) continue;
+        const int o = mask_uoff(M, D, f), K = fn_k(f, D);
+        if (ui < o || ui >= o + fn_u(f, D)) continue;
+        float *p = outs.p[f] + sid * K * C + ch;
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+            if (unique_fk(f, D, k) == ui - o) {
+                if (ADD) p[k * C] += x;
+                else p[k * C] = x;
+            }
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Cross-lane reduce-scatter of a wave: every lane holds 64 partial sums v[0..63]; afterwards
 // lane l holds v[l] summed over all 64 lanes (returned).  Six halving stages, each adding a

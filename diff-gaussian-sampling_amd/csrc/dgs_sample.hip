@@ -24,7 +24,7 @@
 #include <utility>
 #include <vector>
 
-#include "dgs_render.h"
+#include "dgs_reference.h"
 
 namespace dgs {
 
@@ -33,8 +33,9 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 // --------------------------------------------------------------------------- packing
 template <int FN, int D, int CB>
 __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *__restrict__ values, int C,
-                             int cbase, float *__restrict__ rows) {
+                             int cbase, float *__restrict__ rows, uint32_t *__restrict__ flag_zero) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (flag_zero && i == 0) *flag_zero = 0u;  // the call's input check (k_verify) runs next
     if (i >= P) return;
     // means / conics were packed in internal order at binning (coalesced here); only the
     // values are gathered through perm
@@ -78,15 +79,6 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
 // s_load puts each field of both samples into an aligned SGPR pair (a packed-op operand).
 template <int FN, int D, int CB>
 __host__ __device__ constexpr bool pair_rows() { return srow_stride<FN, D, CB>() <= 16; }
-
-// dL of each function (indexed by function code; the fused form reads those of its mask)
-struct DLs {
-    const float *p[4];
-};
-// Output of each function (indexed by function code)
-struct Outs {
-    float *p[4];
-};
 
 template <int FN, int D, int CB>
 __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
@@ -216,28 +208,6 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
     ctr[1] = 0.5f * (b.y + b.w);
 }
 
-// Stores (ADD: adds) the sum x of unique component ui (over the mask's functions), channel
-// ch, of sample sid into every output component of its function that maps to it.
-template <int FN, int D, bool ADD>
-__device__ __forceinline__ void store_unique(const Outs &outs, int64_t sid, int ui, int C, int ch,
-                                             float x) {
-    constexpr int M = fn_mask(FN);
-#pragma unroll
-    for (int f = 0; f < 4; ++f) {
-        if (!(M & (1 << f))) continue;
-        const int o = mask_uoff(M, D, f), K = fn_k(f, D);
-        if (ui < o || ui >= o + fn_u(f, D)) continue;
-        float *p = outs.p[f] + sid * K * C + ch;
-#pragma unroll
-        for (int k = 0; k < K; ++k) {
-            if (unique_fk(f, D, k) == ui - o) {
-                if (ADD) p[k * C] += x;
-                else p[k * C] = x;
-            }
-        }
-    }
-}
-
 // (a) Transposed form (small accumulators, U * CB <= 4).  Lane = Gaussian of the cell list,
 // 64 at a time (rows by vector gather); the block's samples are wave-uniform, read in order
 // as packed pair rows [s0(2p) s0(2p+1) s1(2p) s1(2p+1)] through the scalar cache, and the
@@ -360,7 +330,9 @@ template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
                                                       const float *__restrict__ grows,
-                                                      const Outs outs, int C, int cbase) {
+                                                      const Outs outs, int C, int cbase,
+                                                      const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
     using Tr = Traits<FN, D>;
     constexpr int U = Tr::U, K = Tr::K, UC = U * CB, RS = grow_stride<FN, D, CB>(), B = Tr::GBASE;
     constexpr int NP = 32 / UC, NS = 2 * NP;  // sample pairs / samples per pass
@@ -476,7 +448,9 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
                                                     const char *__restrict__ sbuf,
                                                     const float *__restrict__ grows,
                                                     const float *__restrict__ samples,
-                                                    const Outs outs, int C, int cbase) {
+                                                    const Outs outs, int C, int cbase,
+                                                    const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
     constexpr int U = Traits<FN, D>::U, K = Traits<FN, D>::K;
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumFwdUnits]);
@@ -686,7 +660,9 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
                                                      const char *__restrict__ sbuf,
                                                      const float *__restrict__ grows,
                                                      const float *__restrict__ srows,
-                                                     float *__restrict__ acc, int P, int vrow0) {
+                                                     float *__restrict__ acc, int P, int vrow0,
+                                                     const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
     constexpr int RS = grow_stride<FN, D, CB>();
     const Bins bins = resolve(gbuf, sbuf);
     const int nunits = sload(&bins.counts[kNumBwdUnits]);
@@ -817,7 +793,7 @@ static int srow_stride_rt(int FN, int D, int CB) {
 static size_t a256(size_t x) { return align_up(x, 256); }
 
 struct WsLayout {
-    size_t grows, srows, acc, total;
+    size_t grows, srows, acc, flag, total;  // flag: 256 B after the sums (the call's input check)
 };
 static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
@@ -825,7 +801,8 @@ static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     w.grows = a256((size_t)P * grow_stride_rt(FN, D, CB) * 4 + 64);
     w.srows = backward ? a256(((size_t)N + 1) * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;  // pair rows: N rounded up to even
     w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
-    w.total = w.grows + w.srows + w.acc;
+    w.flag = w.grows + w.srows + w.acc;
+    w.total = w.flag + 256;
     return w;
 }
 
@@ -864,25 +841,39 @@ struct Call {
     int debug;
 };
 
+// The call-time path's arguments (dgs_reference.h).
+static RefCall ref_call(const Call &a, float *acc, const uint32_t *flag, int cbase) {
+    UnitHint h;
+    const int64_t R = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &h) ? h.R : (int64_t)1 << 40;
+    return RefCall{a.gb, a.sb, a.means, a.values, a.conics, a.samples, a.dls, a.outs, acc, flag,
+                   a.P, a.N, a.C, cbase, R, a.s, a.debug};
+}
+
 template <int FN, int D, int CB>
 static int run_forward(const Call &a) {
     const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, false);
     float *grows = reinterpret_cast<float *>(a.ws);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
     constexpr bool T = fwd_transposed<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
     hint.nunsafe = -1;
     const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
+                                                                   cbase == 0 ? flag : nullptr);
         DGS_LAUNCH_CHECK(a.s, a.debug);
+        if (cbase == 0) {  // were the binned means / conics / samples passed? (device-side flag)
+            const int rc = verify_inputs(a.gb, a.sb, a.P, D, a.N, a.means, a.conics, a.samples, flag, a.s, a.debug);
+            if (rc) return rc;
+        }
         {
             KernelTimer t(0, a.s);
             if constexpr (T)
-                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase);
+                k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else
                 k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
-                                                                          a.samples, a.outs, a.C, cbase);
+                                                                          a.samples, a.outs, a.C, cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if constexpr (T) {
@@ -891,10 +882,13 @@ static int run_forward(const Call &a) {
                 // unsafe count is 0, which the host does not know without a sync)
                 const unsigned tb = hint.nunsafe > 0 ? blocks : std::min(blocks, 1024u);
                 k_forward<FN, D, CB, true><<<tb, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
-                                                                         a.samples, a.outs, a.C, cbase);
+                                                                         a.samples, a.outs, a.C, cbase, flag);
                 DGS_LAUNCH_CHECK(a.s, a.debug);
             }
         }
+        // the call-time path (exits at once unless the inputs differ from the binned ones)
+        const int rc = ref_forward<FN, D, CB>(ref_call(a, nullptr, flag, cbase));
+        if (rc) return rc;
     }
     return DGS_OK;
 }
@@ -905,12 +899,18 @@ static int run_backward(const Call &a) {
     float *grows = reinterpret_cast<float *>(a.ws);
     float *srows = reinterpret_cast<float *>(a.ws + w.grows);
     float *acc = reinterpret_cast<float *>(a.ws + w.grows + w.srows);
+    uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
     constexpr int S = D * (D + 1) / 2;
     DGS_TRY_HIP(hipMemsetAsync(acc, 0, w.acc, a.s));
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows);
+        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
+                                                                   cbase == 0 ? flag : nullptr);
         DGS_LAUNCH_CHECK(a.s, a.debug);
+        if (cbase == 0) {
+            const int rc = verify_inputs(a.gb, a.sb, a.P, D, a.N, a.means, a.conics, a.samples, flag, a.s, a.debug);
+            if (rc) return rc;
+        }
         k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.dls, a.C,
                                                                       cbase, srows);
         DGS_LAUNCH_CHECK(a.s, a.debug);
@@ -918,9 +918,11 @@ static int run_backward(const Call &a) {
         {
             KernelTimer t(1, a.s);
             k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc,
-                                                                a.P, D + S + cbase);
+                                                                a.P, D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
+        const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
+        if (rc) return rc;
     }
     if constexpr (D == 2 && CB == 1 && grow_stride<FN, D, CB>() >= 8) {
         if (a.C == 1) {  // the Gaussian-row region is free again: AoS rows there
@@ -1174,10 +1176,10 @@ extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const fl
     DGS_TRY_HIP(hipMemsetAsync(dcnt, 0, 16, s));
     const unsigned blocks = unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false);
     if (D == 2) {
-        k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows);
+        k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows, nullptr);
         k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
     } else {
-        k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows);
+        k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows, nullptr);
         k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
     }
     DGS_TRY_HIP(hipGetLastError());
@@ -1186,6 +1188,29 @@ extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const fl
     DGS_TRY_HIP(hipStreamSynchronize(s));
     counts[0] = (int64_t)h[0];
     counts[1] = (int64_t)h[1];
+    return DGS_OK;
+}
+
+extern "C" int dgs_inputs_match(int P, int D, int N, const float *means, const float *conics,
+                                const float *samples, const void *binning, size_t binning_bytes,
+                                const void *sample_binning, size_t sample_binning_bytes, int *match,
+                                dgs_stream_t stream) {
+    if (!match) return fail(DGS_ERR_ARG, "dgs_inputs_match: match pointer required");
+    *match = 1;
+    int rc = validate(0, P, D, N, 1, binning, binning_bytes, sample_binning, sample_binning_bytes, 0, 0);
+    if (rc || P == 0 || N == 0) return rc;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    uint32_t *flag = nullptr;
+    DGS_TRY_HIP(hipMallocAsync(&flag, 4, s));
+    DGS_TRY_HIP(hipMemsetAsync(flag, 0, 4, s));
+    rc = verify_inputs(static_cast<const char *>(binning), static_cast<const char *>(sample_binning), P, D, N,
+                       means, conics, samples, flag, s, 0);
+    if (rc) return rc;
+    uint32_t h = 0;
+    DGS_TRY_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    DGS_TRY_HIP(hipFreeAsync(flag, s));
+    *match = h ? 0 : 1;
     return DGS_OK;
 }
 

@@ -337,6 +337,23 @@ std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &co
     return std::make_tuple(counts[0], counts[1]);
 }
 
+// Whether forward / backward with these tensors take the binned path (dgs_inputs_match).
+bool InputsMatch(const Tensor &means_in, const Tensor &conics_in, const Tensor &samples_in,
+                 const Tensor &binning_in, const Tensor &sbinning_in) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples");
+    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
+    int match = 1;
+    if (P != 0 && N != 0) {
+        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+        check(dgs_inputs_match(P, D, N, means.data_ptr<float>(), conics.data_ptr<float>(), samples.data_ptr<float>(),
+                               gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), &match,
+                               as_dgs(cur_stream())),
+              "inputs_match");
+    }
+    return match != 0;
+}
+
 // The C-ABI tile grid (device min/max, torch-CUDA arithmetic) -- for tests of dgs_tile_grid.
 std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_in) {
     const Tensor samples = f32(samples_in, "samples");
@@ -522,6 +539,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sample_gaussians_multi", &SampleGaussiansMulti);
     m.def("sample_gaussians_multi_backward", &SampleGaussiansMultiBackward);
     m.def("tile_grid", &TileGrid);
+    m.def("inputs_match", &InputsMatch);
     m.def("library_version", []() { return dgs_version(); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });
     m.def("timing_read", [](int which) {

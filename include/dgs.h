@@ -135,6 +135,15 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
                     int64_t *counts, void *workspace, size_t workspace_bytes,
                     dgs_stream_t stream);
 
+/* Diagnostic: do means / conics / samples equal (bitwise) the tensors the binning was built
+ * from?  *match = 1: forward / backward take the binned fine-cell path; 0: they take the
+ * call-time path (the reference reads these tensors at every call, forward.cu:136-145,
+ * backward.cu:76-85, while its tile lists come from preprocess).  Host, syncs. */
+int dgs_inputs_match(int P, int D, int N, const float *means, const float *conics,
+                     const float *samples, const void *binning, size_t binning_bytes,
+                     const void *sample_binning, size_t sample_binning_bytes, int *match,
+                     dgs_stream_t stream);
+
 /* ---- neighbour aggregation (aggregate_neighbors.{h,cu}) ------------------------------- */
 
 /* Neighbour lists: replaces AggregateNeighborsPreprocessCUDA (aggregate_neighbors.cu:323-367)
