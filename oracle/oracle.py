@@ -52,6 +52,8 @@ def _load():
     lib.orc_agg_fill_rows.argtypes = [i32, i32, P, P, P, i32, P, P, P, P, P, P]
     lib.orc_agg_forward.argtypes = [i32] * 5 + [P] * 15
     lib.orc_agg_backward.argtypes = [i32] * 5 + [P] * 21
+    lib.orc_agg_forward64.argtypes = [i32] * 5 + [P] * 15
+    lib.orc_agg_backward64.argtypes = [i32] * 5 + [P] * 21
     _lib = lib
     return lib
 
@@ -222,9 +224,11 @@ def agg_preprocess_rows(means, conics, radii, rows):
 
 
 def agg_forward(features, transform, queries, keys, frequencies, distance_transform, indices,
-                ranges, dists, densities, inv_total, rows=None):
+                ranges, dists, densities, inv_total, rows=None, exact=False):
     """aggregate_neighbors forward: (weights, embeddings, factors, neighbor_features).
-    rows: evaluate only the first `rows` rows (a bounded CPU-baseline sample)."""
+    rows: evaluate only the first `rows` rows (a bounded CPU-baseline sample).
+    exact: neighbor_features with exact (double) accumulation of the reference's per-slot float
+    terms (float64), instead of the reference's own float summation order."""
     lib = _load()
     f, T, q, k = _f32(features), _f32(transform), _f32(queries), _f32(keys)
     fr, dt = _f32(frequencies), _f32(distance_transform)
@@ -235,17 +239,20 @@ def agg_forward(features, transform, queries, keys, frequencies, distance_transf
     E = dt.size // 2
     n = idx.size
     w, emb, fac = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
-    out = np.zeros((P, L), np.float32)
-    lib.orc_agg_forward(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    out = np.zeros((P, L), np.float64 if exact else np.float32)
+    fn = lib.orc_agg_forward64 if exact else lib.orc_agg_forward
+    fn(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                         _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(w), _ptr(emb),
                         _ptr(fac), _ptr(out))
     return w, emb, fac, out
 
 
 def agg_backward(features, transform, queries, keys, frequencies, distance_transform, indices,
-                 ranges, dists, densities, weights, embeddings, factors, inv_total, dL, rows=None):
+                 ranges, dists, densities, weights, embeddings, factors, inv_total, dL, rows=None,
+                 exact=False):
     """aggregate_neighbors backward: the six gradients (features, transform, queries, keys,
-    frequencies, distance_transform)."""
+    frequencies, distance_transform).  exact: accumulated exactly (float64 results), see
+    agg_forward."""
     lib = _load()
     f, T, q, k = _f32(features), _f32(transform), _f32(queries), _f32(keys)
     fr, dt = _f32(frequencies), _f32(distance_transform)
@@ -255,16 +262,17 @@ def agg_backward(features, transform, queries, keys, frequencies, distance_trans
     K = q.shape[1]
     D = X.shape[1] if X.ndim == 2 else 1
     E = dt.size // 2
-    outs = [np.zeros_like(f), np.zeros_like(T), np.zeros_like(q), np.zeros_like(k),
-            np.zeros_like(fr), np.zeros_like(dt)]
-    lib.orc_agg_backward(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    ot = np.float64 if exact else np.float32
+    outs = [np.zeros(a.shape, ot) for a in (f, T, q, k, fr, dt)]
+    fn = lib.orc_agg_backward64 if exact else lib.orc_agg_backward
+    fn(P if rows is None else min(rows, P), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                          _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
                          _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
     return tuple(outs)
 
 
 def agg_forward_rows(features, transform, queries, keys, frequencies, distance_transform, rows,
-                     indices, ranges, dists, densities, inv_total):
+                     indices, ranges, dists, densities, inv_total, exact=False):
     """agg_forward over the rows `rows` only, on the compact lists of agg_preprocess_rows:
     (weights, embeddings, factors) of those slots and neighbor_features [len(rows), L]."""
     lib = _load()
@@ -276,15 +284,16 @@ def agg_forward_rows(features, transform, queries, keys, frequencies, distance_t
     D = X.shape[1] if X.ndim == 2 else 1
     E = dt.size // 2
     w, emb, fac = np.zeros(n, np.float32), np.zeros(n, np.float32), np.zeros(n, np.float32)
-    out = np.zeros((len(rows), L), np.float32)
-    lib.orc_agg_forward(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    out = np.zeros((len(rows), L), np.float64 if exact else np.float32)
+    (lib.orc_agg_forward64 if exact else lib.orc_agg_forward)(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                         _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(inv), _ptr(w), _ptr(emb),
                         _ptr(fac), _ptr(out))
     return w, emb, fac, out
 
 
 def agg_backward_rows(features, transform, queries, keys, frequencies, distance_transform, rows,
-                      indices, ranges, dists, densities, weights, embeddings, factors, inv_total, dL_rows):
+                      indices, ranges, dists, densities, weights, embeddings, factors, inv_total, dL_rows,
+                      exact=False):
     """agg_backward with dL/dneighbor_features non-zero on the rows `rows` only (dL_rows
     [len(rows), L]), on their compact lists: the six gradients (queries' gradient full-size,
     zero outside `rows`)."""
@@ -298,11 +307,13 @@ def agg_backward_rows(features, transform, queries, keys, frequencies, distance_
     L, K = f.shape[1], q.shape[1]
     D = X.shape[1] if X.ndim == 2 else 1
     E = dt.size // 2
-    dq_rows = np.zeros_like(q)
-    outs = [np.zeros_like(f), np.zeros_like(T), dq_rows, np.zeros_like(k), np.zeros_like(fr), np.zeros_like(dt)]
-    lib.orc_agg_backward(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+    ot = np.float64 if exact else np.float32
+    dq_rows = np.zeros(q.shape, ot)
+    outs = [np.zeros(f.shape, ot), np.zeros(T.shape, ot), dq_rows, np.zeros(k.shape, ot),
+            np.zeros(fr.shape, ot), np.zeros(dt.shape, ot)]
+    (lib.orc_agg_backward64 if exact else lib.orc_agg_backward)(len(rows), D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
                          _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(emb), _ptr(fac),
                          _ptr(inv), _ptr(g), *[_ptr(o) for o in outs])
-    dq = np.zeros_like(qf)
+    dq = np.zeros(qf.shape, ot)
     dq[np.asarray(rows)] = dq_rows
     return outs[0], outs[1], dq, outs[3], outs[4], outs[5]

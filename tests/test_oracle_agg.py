@@ -120,6 +120,15 @@ def test_forward_and_backward_vs_autograd(oracle, D):
     for name, a, b in zip(("features", "transform", "queries", "keys", "frequencies", "distance_transform"),
                           got, grads):
         close(a, b.numpy(), 1e-4, 2e-5, f"d/d{name}")
+    # the exact-accumulation twins (the GPU tests' reference): same formula, only the float
+    # summation rounding removed, so they sit much closer to the fp64 autograd
+    out64 = oracle.agg_forward(*args, idx, ranges, dists, dens, inv, exact=True)[3]
+    assert out64.dtype == np.float64
+    close(out64, ref.detach().numpy(), 1e-5, 1e-6, "aggregate forward (exact accumulation)")
+    got64 = oracle.agg_backward(*args, idx, ranges, dists, dens, w, emb, fac, inv, g, exact=True)
+    for name, a, b in zip(("features", "transform", "queries", "keys", "frequencies", "distance_transform"),
+                          got64, grads):
+        close(a, b.numpy(), 1e-5, 1e-6, f"d/d{name} (exact accumulation)")
 
 
 @pytest.mark.parametrize("D", [1, 2])
