@@ -26,6 +26,7 @@ ap.add_argument("--P", type=int, default=1_000_000)
 ap.add_argument("--N", type=int, default=2_000_000)
 ap.add_argument("--C", type=int, default=1)
 ap.add_argument("--function", default="gaussian", choices=FUNCS)
+ap.add_argument("--prep", type=int, default=0, help="extra (warm) preprocess calls, for profiles")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 D, fi = 2, FUNCS.index(a.function)
@@ -33,6 +34,8 @@ means, values, covs, conics = (t.to(dev) for t in syn.gaussians(a.P, D, a.C, see
 samples = syn.samples(a.N, D, seed=4).to(dev)
 dL = syn.grad_out(a.N, D ** fi, a.C, seed=5).to(dev).reshape((a.N,) + (D,) * fi + (a.C,))
 R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
+for _ in range(a.prep):
+    R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
 name = "sample_gaussians" + ["", "_derivative", "_laplacian", "_third_derivative"][fi]
 fwd, bwd = getattr(dgs._C, name), getattr(dgs._C, name + "_backward")
 
