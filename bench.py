@@ -167,13 +167,19 @@ def bench_sample(args, world, rank, dev, torch, dist):
     # ---- preprocess (binning), reported separately: the first call (cold: code-object load,
     # allocator growth) and the warm median of --pre-reps further calls (the PIGS loop re-bins
     # every step because the means move)
-    grid, off = global_tile_grid(samples)
+    # one GPU: the reference API (grid computed on the device, one host sync per call); N > 1:
+    # every shard bins with the global grid (distributed.global_tile_grid)
+    grid, off = global_tile_grid(samples) if world > 1 else (None, None)
     pre_times = []
     for _ in range(1 + args.pre_reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        binned = dgs._C.preprocess_gaussians_bounded(means.detach(), values.detach(), covs,
-                                                     conics.detach(), samples, grid, off, False)
+        if world > 1:
+            binned = dgs._C.preprocess_gaussians_bounded(means.detach(), values.detach(), covs,
+                                                         conics.detach(), samples, grid, off, False)
+        else:
+            binned = dgs._C.preprocess_gaussians(means.detach(), values.detach(), covs,
+                                                 conics.detach(), samples, False)
         torch.cuda.synchronize()
         pre_times.append((time.perf_counter() - t0) * 1e3)
     pre_first_ms = pre_times[0]

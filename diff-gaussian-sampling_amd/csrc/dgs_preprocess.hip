@@ -497,10 +497,17 @@ __global__ void k_cell_ranges(int ncells, const int32_t *__restrict__ hb, const 
 
 __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
                          const uint64_t *__restrict__ toffs, const uint64_t *__restrict__ touched,
+                         const int *__restrict__ dgrid, const float *__restrict__ doff,
                          int64_t *__restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     out[0] = P > 0 ? (int64_t)(toffs[P - 1] + touched[P - 1]) : 0;  // num_rendered (sampler_impl.cu:253-257)
     out[1] = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;
+    // the device-computed tile grid (dgs_preprocess_auto): read back with the totals
+    int32_t *g = reinterpret_cast<int32_t *>(out + 2);
+    g[0] = dgrid ? dgrid[0] : 0;
+    g[1] = dgrid ? dgrid[1] : 0;
+    g[2] = doff ? __float_as_int(doff[0]) : 0;
+    g[3] = doff ? __float_as_int(doff[1]) : 0;
 }
 
 // ----------------------------------------------------------------------- work units
@@ -784,11 +791,14 @@ extern "C" int dgs_tile_grid(int N, int D, const float *samples, int *grid_out, 
     return DGS_OK;
 }
 
-extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
-                              const float *conics, const float *samples, const int *grid,
-                              const float *grid_offset, float *radii, dgs_alloc_fn alloc,
-                              void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream,
-                              int debug) {
+namespace dgs {
+// The binning with the host-known grid `grid`/`grid_offset`.  dgrid/doff (device, optional): a
+// device-computed grid read back at the one host sync into *dev_grid / *dev_off (D entries).
+static int preprocess_body(int P, int D, int N, const float *means, const float *covariances,
+                           const float *conics, const float *samples, const int *grid,
+                           const float *grid_offset, float *radii, dgs_alloc_fn alloc,
+                           void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream, int debug,
+                           const int *dgrid, const float *doff, int *dev_grid, float *dev_off) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
     if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^30 - 1)");
@@ -837,7 +847,7 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     uint64_t *touched = S.get<uint64_t>(P), *fcount = S.get<uint64_t>(P), *foffs = S.get<uint64_t>(P);
     uint64_t *toffs = S.get<uint64_t>(P);
 
-    int64_t *totals = S.get<int64_t>(2);
+    int64_t *totals = S.get<int64_t>(4);
     if (S.rc) return S.rc;
 
     // hipcub temp storage: one allocation sized for the largest phase-A primitive
@@ -898,13 +908,20 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, fcount, foffs, P, s));
     tb = t_a;
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, touched, toffs, P, s));
-    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, totals);
+    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, dgrid, doff, totals);
     DGS_LAUNCH_CHECK(s, debug);
-    int64_t htot[2] = {0, 0};
+    int64_t htot[4] = {0, 0, 0, 0};
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));  // the one host sync: num_rendered is a Python int
     const int64_t R = htot[0], E = htot[1];
     *num_rendered = R;
+    if (dev_grid) {
+        const int32_t *g = reinterpret_cast<const int32_t *>(htot + 2);
+        for (int d = 0; d < D; ++d) {
+            dev_grid[d] = g[d];
+            std::memcpy(&dev_off[d], &g[2 + d], 4);
+        }
+    }
     if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries");
     if (R >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "num_rendered exceeds 2^31 (32-bit tile lists)");
 
@@ -1049,3 +1066,75 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
     hint_put(uh);
     return DGS_OK;
 }
+}  // namespace dgs
+
+extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
+                              const float *conics, const float *samples, const int *grid,
+                              const float *grid_offset, float *radii, dgs_alloc_fn alloc,
+                              void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream,
+                              int debug) {
+    return preprocess_body(P, D, N, means, covariances, conics, samples, grid, grid_offset, radii, alloc,
+                           alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr);
+}
+
+// The grid of the previous call (per D): the speculation of dgs_preprocess_auto.
+static std::mutex g_grid_mu;
+static bool g_grid_known[3] = {false, false, false};
+static int g_grid_last[3][2];
+static float g_off_last[3][2];
+
+extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *covariances,
+                                   const float *conics, const float *samples, float *radii,
+                                   dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
+                                   int *grid_out, float *offset_out, dgs_stream_t stream, int debug) {
+    if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
+    if (P < 0 || N < 0 || !alloc || !num_rendered || !grid_out || !offset_out)
+        return fail(DGS_ERR_ARG, "dgs_preprocess_auto: bad arguments");
+    *num_rendered = 0;
+    if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // sample_points.cu:70-74 on the device (torch's CUDA arithmetic, k_bounds_final)
+    const int nparts = (int)std::min<int64_t>(1024, grid_for(N));
+    float *part = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, align_up(sizeof(float) * 4 * nparts, 256)));
+    char *gb = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, 256));
+    if (!part || !gb) return fail(DGS_ERR_ALLOC, "scratch allocation failed");
+    int *dgrid = reinterpret_cast<int *>(gb);
+    float *doff = reinterpret_cast<float *>(gb + 16);
+    k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, part);
+    k_bounds_final<<<1, 64, 0, s>>>(nparts, D, part, dgrid, doff);
+    DGS_LAUNCH_CHECK(s, debug);
+    int guess[2] = {1, 1};
+    float goff[2] = {0.0f, 0.0f};
+    bool known;
+    {
+        std::lock_guard<std::mutex> lk(g_grid_mu);
+        known = g_grid_known[D];
+        for (int d = 0; d < D; ++d) { guess[d] = g_grid_last[D][d]; goff[d] = g_off_last[D][d]; }
+    }
+    if (!known) {  // first call: read the grid (the one extra sync of a cold start)
+        DGS_TRY_HIP(hipMemcpyAsync(guess, dgrid, sizeof(int) * D, hipMemcpyDeviceToHost, s));
+        DGS_TRY_HIP(hipMemcpyAsync(goff, doff, sizeof(float) * D, hipMemcpyDeviceToHost, s));
+        DGS_TRY_HIP(hipStreamSynchronize(s));
+    }
+    // Bin with the guess; the device grid comes back with the totals at the body's one sync.  A
+    // wrong guess bins consistently (sample keys clamp, tile ids wrap), so it is only redone.
+    int dg[2] = {0, 0};
+    float dof[2] = {0.0f, 0.0f};
+    int rc = preprocess_body(P, D, N, means, covariances, conics, samples, guess, goff, radii, alloc, alloc_ctx,
+                             num_rendered, stream, debug, dgrid, doff, dg, dof);
+    if (rc) return rc;
+    bool same = true;
+    for (int d = 0; d < D; ++d)
+        same = same && dg[d] == guess[d] && std::memcmp(&dof[d], &goff[d], 4) == 0;
+    {
+        std::lock_guard<std::mutex> lk(g_grid_mu);
+        g_grid_known[D] = true;
+        for (int d = 0; d < D; ++d) { g_grid_last[D][d] = dg[d]; g_off_last[D][d] = dof[d]; }
+    }
+    if (!same)
+        rc = preprocess_body(P, D, N, means, covariances, conics, samples, dg, dof, radii, alloc, alloc_ctx,
+                             num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr);
+    for (int d = 0; d < D; ++d) { grid_out[d] = dg[d]; offset_out[d] = dof[d]; }
+    return rc;
+}
+

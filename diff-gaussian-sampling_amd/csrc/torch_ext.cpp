@@ -5,7 +5,8 @@
 // reference host glue (sample_points.{h,cu}, aggregate_neighbors.{h,cu}):
 //   * inputs are borrowed, made contiguous; wrong dtypes raise RuntimeError (the reference's
 //     data<float>() check); P == 0 or N == 0 returns zero/empty results without launching;
-//   * the tile grid is computed with the reference's own torch ops (sample_points.cu:70-74);
+//   * the tile grid of sample_points.cu:70-74 is computed on the device with torch's CUDA-path
+//     arithmetic and read back at the binning's one host sync (dgs_preprocess_auto);
 //   * opaque u8 buffers come back to Python and are handed back verbatim;
 //   * everything runs on torch's current HIP stream; `debug` synchronises and checks after
 //     every launch (auxiliary.h:33-40).
@@ -65,22 +66,6 @@ Tensor empty_u8(const torch::Device &dev) {
     return torch::empty({0}, torch::TensorOptions().dtype(torch::kUInt8).device(dev));
 }
 
-// sample_points.cu:70-74, literally (torch ops on the device, then to the host).
-std::pair<std::vector<int>, std::vector<float>> tile_grid_torch(const Tensor &samples) {
-    const Tensor min_bound = std::get<0>(samples.min(0));
-    const Tensor max_bound = std::get<0>(samples.max(0));
-    const Tensor tile_grid = torch::ceil((max_bound - min_bound + 1e-6f) / 0.51f).to(torch::kInt32);
-    const Tensor g = tile_grid.cpu(), o = min_bound.cpu();
-    const int D = (int)g.numel();
-    std::vector<int> grid(D);
-    std::vector<float> off(D);
-    for (int d = 0; d < D; ++d) {
-        grid[d] = g.data_ptr<int>()[d];
-        off[d] = o.data_ptr<float>()[d];
-    }
-    return {grid, off};
-}
-
 using PreOut = std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
 PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Tensor &cov_in,
@@ -97,20 +82,22 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
     if (P != 0 && N != 0) {
         TORCH_CHECK(D == 1 || D == 2, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
         TORCH_CHECK(samples.size(-1) == D, "samples must have the same dimension as means");
-        std::vector<int> grid;
-        std::vector<float> off;
         if (grid_in) {
-            grid = *grid_in;
-            off = *off_in;
-        } else {
-            std::tie(grid, off) = tile_grid_torch(samples);
+            TORCH_CHECK((int)grid_in->size() == D && (int)off_in->size() == D, "grid/offset must have D entries");
+            check(dgs_preprocess(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
+                                 conics.data_ptr<float>(), samples.data_ptr<float>(), grid_in->data(),
+                                 off_in->data(), radii.data_ptr<float>(), alloc_cb, &ctx, &rendered,
+                                 as_dgs(cur_stream()), debug ? 1 : 0),
+                  "preprocess_gaussians");
+        } else {  // the grid of sample_points.cu:70-74 on the device: one host sync per call
+            int grid[2];
+            float off[2];
+            check(dgs_preprocess_auto(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
+                                      conics.data_ptr<float>(), samples.data_ptr<float>(),
+                                      radii.data_ptr<float>(), alloc_cb, &ctx, &rendered, grid, off,
+                                      as_dgs(cur_stream()), debug ? 1 : 0),
+                  "preprocess_gaussians");
         }
-        TORCH_CHECK((int)grid.size() == D && (int)off.size() == D, "grid/offset must have D entries");
-        check(dgs_preprocess(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
-                             conics.data_ptr<float>(), samples.data_ptr<float>(), grid.data(),
-                             off.data(), radii.data_ptr<float>(), alloc_cb, &ctx, &rendered,
-                             as_dgs(cur_stream()), debug ? 1 : 0),
-              "preprocess_gaussians");
     }
     return std::make_tuple(rendered, ctx.bufs[DGS_BUF_BINNING], ctx.bufs[DGS_BUF_SAMPLE_BINNING],
                            ctx.bufs[DGS_BUF_RANGES], ctx.bufs[DGS_BUF_SAMPLE_RANGES], radii);

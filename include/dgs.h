@@ -71,12 +71,25 @@ int dgs_tile_grid(int N, int D, const float *samples, int *grid_out, float *offs
  *   radii[P]: out, reference radii (0 for skipped Gaussians)
  *   num_rendered: out (host), the reference's R = sum of tiles touched
  * Buffers are requested through `alloc`.  Synchronises `stream` once (to size the lists).
- * Contract: the forward/backward calls that use these buffers must pass the same means,
- * conics and samples (GaussianSampler guarantees it; values may differ). */
+ * The forward/backward calls read the means, conics and samples they are given, as the
+ * reference does (forward.cu:136-145): inputs that differ from the binned ones are detected on
+ * the device and take the reference's tile pair set (dgs_reference.hip). */
 int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
                    const float *conics, const float *samples, const int *grid,
                    const float *grid_offset, float *radii, dgs_alloc_fn alloc, void *alloc_ctx,
                    int64_t *num_rendered, dgs_stream_t stream, int debug);
+
+/* dgs_preprocess with the tile grid of the reference host glue (sample_points.cu:70-74)
+ * computed on the device (dgs_tile_grid's arithmetic) instead of passed in: the reference's
+ * PreprocessCUDA as a whole, with ONE host sync per call.  The binning starts with the grid of
+ * the previous call (per D) while the device computes this call's grid; both come back at the
+ * binning's single sync, and only a changed grid (the first call, a new domain) re-bins.
+ * grid_out[D] / offset_out[D] (host): the grid used.  Replaces PreprocessCUDA
+ * (sample_points.cu:38-98) + Sampler::preprocess (sampler_impl.cu:216-330). */
+int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *covariances,
+                        const float *conics, const float *samples, float *radii, dgs_alloc_fn alloc,
+                        void *alloc_ctx, int64_t *num_rendered, int *grid_out, float *offset_out,
+                        dgs_stream_t stream, int debug);
 
 /* Workspace bytes needed by dgs_sample_forward (backward == 0) or dgs_sample_backward. */
 size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward);

@@ -232,3 +232,23 @@ def test_parity_wide_domain_32bit_entry_keys(dgs, oracle, function):
     K = syn.out_components(function, 2)
     dL = syn.grad_out(s.shape[0], K, 1, seed=142)
     _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
+
+
+def test_preprocess_grid_changes_between_calls(dgs, oracle):
+    """preprocess_gaussians computes the tile grid on the device and bins with the previous
+    call's grid until the one host sync confirms it (dgs_preprocess_auto): a call whose domain
+    differs from the previous one must re-bin with its own grid (sample_points.cu:70-74).
+    Domains A, B (another grid and offset), A again: each equals the oracle."""
+    cases_ = []
+    for seed, scale, shift in ((61, 1.0, 0.0), (62, 2.3, 0.7), (61, 1.0, 0.0)):
+        means, values, covs, conics = syn.gaussians(600, 2, 1, seed=seed)
+        samples = syn.samples(3000, 2, seed=seed + 4)
+        cases_.append((means * scale + shift, values, covs, conics, samples * scale + shift))
+    for means, values, covs, conics, samples in cases_:
+        res = gpu_run(dgs._C, "gaussian", means, values, covs, conics, samples)
+        ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+        assert res["R"] == ob.num_rendered
+        rg, srg = ref_ranges_bytes(ob)
+        assert np.array_equal(res["ranges"], rg) and np.array_equal(res["sample_ranges"], srg)
+        ref = ob.forward("gaussian", values.numpy(), conics.numpy()).reshape(res["out"].shape)
+        close(res["out"], ref, 1e-5, 1e-6, "forward after a grid change")
