@@ -106,6 +106,11 @@ def main():
     ap.add_argument("--N", type=int, default=None,
                     help="query points per GPU (default: 2M on one GPU, 1M per GPU for N > 1)")
     ap.add_argument("--weak", action="store_true", help="N > 1: 2M query points per GPU")
+    ap.add_argument("--shard", default="spatial", choices=["spatial", "dense"],
+                    help="N > 1: spatial = rank r owns the strip r of the points along y and the "
+                         "gradient sum moves only the Gaussians that reach another strip "
+                         "(distributed.SupportExchange, SURVEY 8f f3); dense = uniform points on "
+                         "every rank and one all-reduce of every gradient")
     ap.add_argument("--C", type=int, default=1)
     ap.add_argument("--grid", type=int, default=0,
                     help="query points on a regular g x g lattice instead of uniform (SURVEY 8d config 5: 4096)")
@@ -145,7 +150,8 @@ def main():
 def bench_sample(args, world, rank, dev, torch, dist):
     import diff_gaussian_sampling as dgs
     from diff_gaussian_sampling import synthetic as syn
-    from diff_gaussian_sampling.distributed import global_tile_grid
+    from diff_gaussian_sampling.distributed import (SupportExchange, global_tile_grid, pack_grads,
+                                                    shard_extents)
 
     P, C, D = args.P, args.C, 2
     N = args.N if args.N is not None else (2_000_000 if (world == 1 or args.weak) else 1_000_000)
@@ -160,6 +166,9 @@ def bench_sample(args, world, rank, dev, torch, dist):
         N = samples.shape[0]
     else:
         samples = syn.samples(N, D, seed=4 + 1000 * rank).to(dev)
+        if world > 1 and args.shard == "spatial":  # strip r of [-1, 1) along y: the union is uniform
+            samples[:, 1] = -1.0 + (2.0 / world) * (rank + 0.5 * (samples[:, 1] + 1.0))
+    spatial = world > 1 and args.shard == "spatial"
     dL = syn.grad_out(N, K, C, seed=5 + 1000 * rank).to(dev)
     for t in (means, values, conics):
         t.requires_grad_(True)
@@ -185,6 +194,13 @@ def bench_sample(args, world, rank, dev, torch, dist):
     pre_first_ms = pre_times[0]
     pre_ms = sorted(pre_times[1:])[len(pre_times[1:]) // 2] if args.pre_reps > 0 else pre_first_ms
     R, gb, sb, rg, srg, radii = binned
+    xchg, xsetup_ms = None, 0.0
+    if spatial:  # the exchange sets: per binning (the PIGS loop re-bins, so it is part of that step)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        xchg = SupportExchange(means, conics, shard_extents(samples), rank)
+        torch.cuda.synchronize()
+        xsetup_ms = (time.perf_counter() - t0) * 1e3
     fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative,
            "laplacian": dgs.sample_gaussians_laplacian,
            "third": dgs.sample_gaussians_third_derivative}[fn]
@@ -206,11 +222,14 @@ def bench_sample(args, world, rank, dev, torch, dist):
             out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
             out.backward(dLv)
         if world > 1:
-            torch.cat([means.grad.reshape(-1), values.grad.reshape(-1), conics.grad.reshape(-1)], out=flat)
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            dist.all_reduce(flat)
+            if spatial:
+                xchg.exchange(pack_grads((means.grad, values.grad, conics.grad)))
+            else:
+                torch.cat([means.grad.reshape(-1), values.grad.reshape(-1), conics.grad.reshape(-1)], out=flat)
+                dist.all_reduce(flat)
             if timed:
                 e1.record()
                 ar_ev.append((e0, e1))
@@ -282,7 +301,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
     workload = (f"{P // 1000}k Gaussians x {N // 1000}k query points per GPU"
                 + (f" ({args.grid}^2 lattice)" if args.grid else "")
                 + f", D=2, C={C}, function={fname}, fwd+bwd"
-                + (", RCCL all-reduce of grads" if world > 1 else ""))
+                + ((", spatial strips + sparse gradient exchange" if spatial else ", RCCL all-reduce of grads")
+                   if world > 1 else ""))
     result = {
         "metric": "sampled points/sec (fwd+bwd), 1M Gaussians x "
                   + (f"{N * world // 1_000_000}M queries over {world} GPUs" if world > 1 else f"{N // 1_000_000}M queries")
@@ -302,10 +322,11 @@ def bench_sample(args, world, rank, dev, torch, dist):
         "config": {"workload": workload, "gaussians": P, "query_points_per_gpu": N,
                    "query_points_total": N * world, "channels": C, "function": fname,
                    "parallelism": f"query-point shards x{world}, Gaussians replicated"
-                                  + (", 1 RCCL all-reduce per step" if world > 1 else "")},
+                                  + ((", spatial strips, sparse gradient exchange (RCCL all-to-all)" if spatial
+                                      else ", 1 RCCL all-reduce per step") if world > 1 else "")},
         "preprocess_ms": pre_ms,
         # the Physics-Informed-GS loop re-bins every step (means move): its step time
-        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms,
+        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms + xsetup_ms,
         "preprocess_first_call_ms": pre_first_ms,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
@@ -314,10 +335,14 @@ def bench_sample(args, world, rank, dev, torch, dist):
         "cpu_baseline": None,
     }
     if world > 1:
-        result["distributed"] = {"backend": dist.get_backend(), "world_size": world,
+        F = D + C + D * (D + 1) // 2
+        result["distributed"] = {"backend": dist.get_backend(), "world_size": world, "shard": args.shard,
                                  "per_rank_ms_per_step": per_rank_ms,
-                                 "allreduce_ms_rank0": ar_ms,
-                                 "allreduce_bytes": int(flat.numel() * 4)}
+                                 "gradient_sum_ms_rank0": ar_ms,
+                                 "gradient_sum_bytes_rank0": (int(xchg.rows_moved() * F * 4 * 2) if spatial
+                                                              else int(flat.numel() * 4)),
+                                 "dense_allreduce_bytes": int(flat.numel() * 4),
+                                 "exchange_setup_ms": xsetup_ms}
 
     if rank == 0 and world == 1 and not args.no_cpu and not multi:
         cpu_baselines(result, means.detach().cpu(), values.detach().cpu(), covs.cpu(),

@@ -7,9 +7,20 @@ therefore its results, would differ from the single-GPU run.  `global_tile_grid`
 with two tiny all-reduces (MIN and MAX of D floats) and then applies the reference formula.
 
 The forward needs no communication (a query point's value depends only on the Gaussians);
-the backward's per-Gaussian gradients are partial sums over each rank's points and are summed
-with ONE all-reduce of the packed [dmeans | dvalues | dconics] buffer.
+the backward's per-Gaussian gradients are partial sums over each rank's points.
+
+* ShardedGaussianSampler: any split of the points; ONE all-reduce of the packed
+  [dmeans | dvalues | dconics] buffer (P (D + C + S) floats: 24 MB at 1M Gaussians, C = 1).
+* SpatialShardedGaussianSampler: ranks own spatial strips of the points.  A
+  Gaussian's partial gradient can be non-zero only on the ranks whose points lie within its
+  exact-zero cut (X^T A X <= 210, the binning's culling bound; with the torus images 2k), so
+  the sum needs only those ranks: SupportExchange sends each such row to the Gaussian's owner
+  (an all-to-all whose splits every rank derives from the replicated means and conics, no
+  count exchange) and returns the sums to the contributing ranks.  With strips, only the
+  Gaussians near a strip boundary travel (~1 MB per rank at config 4 against 24 MB).
 """
+import math
+
 import torch
 import torch.distributed as dist
 
@@ -104,3 +115,163 @@ class ShardedGaussianSampler:
 
     def sample_gaussians_third_derivative(self):
         return self._sample("third")
+
+
+# ------------------------------------------------------------------------ spatial shards (f3)
+Q_CUT = 210.0  # X^T A X above this gives expf(-q / 2) == +0 in fp32 (dgs_internal.h kQCut)
+
+
+def support_halfwidth(means, conics):
+    """Half-width along the sharding axis (y at D = 2, x at D = 1) of every Gaussian's
+    exact-zero cut {X : X^T A X <= Q_CUT}: sqrt(Q_CUT * (A^-1)_axis).  inf for conics that are not
+    positive definite (their pairs are bounded by no ellipse).  float64, widened by 1e-5."""
+    D = means.shape[1]
+    c = conics.detach().double()
+    if D == 2:
+        c0, c1, c2 = c[:, 0], c[:, 1], c[:, 2]
+        det = c0 * c2 - c1 * c1
+        pd = (c0 > 0) & (det > 0) & torch.isfinite(det) & torch.isfinite(c0) & torch.isfinite(c2)
+        e = torch.sqrt(Q_CUT * c0 / torch.where(pd, det, torch.ones_like(det)))
+    else:
+        c0 = c[:, 0]
+        pd = (c0 > 0) & torch.isfinite(c0)
+        e = torch.sqrt(Q_CUT / torch.where(pd, c0, torch.ones_like(c0)))
+    e = e * (1.0 + 1e-5) + 1e-6
+    return torch.where(pd, e, torch.full_like(e, math.inf))
+
+
+class SupportExchange:
+    """Sparse sum of per-Gaussian partial gradients over the ranks that can touch them.
+
+    `extents` [W, 2]: every rank's point range [lo, hi] along the sharding axis (all-gathered).
+    Rank r's partial for Gaussian g can be non-zero only if some point of r lies within the
+    cut of g or of one of its torus images m + 2k (forward.cu:149-157 wraps X with period 2):
+    touch[g, r].  owner[g] = the rank whose range is nearest to the mean (first on ties).
+    The sets are computed identically on every rank from replicated inputs, so the all-to-all
+    splits need no exchange of counts."""
+
+    def __init__(self, means, conics, extents, rank, group=None):
+        D = means.shape[1]
+        dev = means.device
+        y = means.detach()[:, D - 1].double()
+        e = support_halfwidth(means, conics)
+        lo, hi = extents[:, 0].double().to(dev), extents[:, 1].double().to(dev)
+        W = lo.numel()
+        span = float((hi.max() - lo.min()).item()) if W else 0.0
+        kmax = int(math.ceil(span / 2.0)) + 1
+        touch = torch.zeros(y.numel(), W, dtype=torch.bool, device=dev)
+        for k in range(-kmax, kmax + 1):
+            a, b = y + 2.0 * k - e, y + 2.0 * k + e
+            touch |= (a[:, None] <= hi[None, :]) & (b[:, None] >= lo[None, :])
+        dist_r = torch.clamp(torch.maximum(lo[None, :] - y[:, None], y[:, None] - hi[None, :]), min=0.0)
+        owner = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
+        self.rank, self.world, self.group = rank, W, group
+        self.touch, self.owner = touch, owner
+        mine = touch[:, rank]
+        # rows this rank sends to each owner, and the rows it receives from each rank (both
+        # ascending Gaussian id)
+        self.send_idx = [torch.nonzero(mine & (owner == o) & (o != rank)).flatten() for o in range(W)]
+        self.recv_idx = [torch.nonzero(touch[:, r] & (owner == rank)).flatten() if r != rank
+                         else torch.zeros(0, dtype=torch.long, device=dev) for r in range(W)]
+        self.send_splits = [int(i.numel()) for i in self.send_idx]
+        self.recv_splits = [int(i.numel()) for i in self.recv_idx]
+        self.send_cat = torch.cat(self.send_idx)
+        self.recv_cat = torch.cat(self.recv_idx)
+
+    def rows_moved(self):
+        """Gaussian rows this rank sends per step (each way)."""
+        return sum(self.send_splits)
+
+    def exchange(self, G):
+        """G [P, F] float32, this rank's partial sums (modified in place): afterwards every row
+        this rank can touch holds the sum over all ranks."""
+        if self.world == 1:
+            return G
+        F = G.shape[1]
+        # 1. partials to the owners, added in rank order (deterministic: no duplicates per add)
+        send = G.index_select(0, self.send_cat).contiguous()
+        recv = torch.empty((sum(self.recv_splits), F), dtype=G.dtype, device=G.device)
+        dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits, group=self.group)
+        o = 0
+        for r in range(self.world):
+            n = self.recv_splits[r]
+            if n:
+                G.index_add_(0, self.recv_idx[r], recv[o:o + n])
+            o += n
+        # 2. the owners' sums back to every contributing rank
+        back = G.index_select(0, self.recv_cat).contiguous()
+        got = torch.empty((sum(self.send_splits), F), dtype=G.dtype, device=G.device)
+        dist.all_to_all_single(got, back, self.send_splits, self.recv_splits, group=self.group)
+        G.index_copy_(0, self.send_cat, got)
+        return G
+
+
+def shard_extents(samples, group=None):
+    """[W, 2] point range [min, max] of every rank along the sharding axis (all-gather)."""
+    D = samples.shape[1]
+    ax = samples.detach()[:, D - 1]
+    mine = torch.stack([ax.min(), ax.max()]) if ax.numel() else torch.tensor(
+        [math.inf, -math.inf], device=samples.device)
+    W = _world(group)
+    if W == 1:
+        return mine[None, :]
+    out = [torch.empty_like(mine) for _ in range(W)]
+    dist.all_gather(out, mine.contiguous(), group=group)
+    return torch.stack(out)
+
+
+def pack_grads(grads):
+    """(dmeans [P,D], dvalues [P,C], dconics [P,S]) -> one [P, D + C + S] buffer."""
+    return torch.cat([g.reshape(g.shape[0], -1) for g in grads], dim=1)
+
+
+def unpack_grads(G, like):
+    out, o = [], 0
+    for g in like:
+        k = g.reshape(g.shape[0], -1).shape[1]
+        out.append(G[:, o:o + k].reshape(g.shape))
+        o += k
+    return tuple(out)
+
+
+class _SpatialSample(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, function, xchg, means, values, conics, samples, num_rendered, binning,
+                sample_binning, ranges, sample_ranges, debug):
+        fwd = getattr(_C, _FWD[function])
+        out = call_debug(fwd, debug, "spatial_fw", means, values, conics, samples, num_rendered,
+                         binning, sample_binning, ranges, sample_ranges, debug)
+        ctx.function, ctx.xchg, ctx.debug, ctx.num_rendered = function, xchg, debug, num_rendered
+        ctx.save_for_backward(means, values, conics, samples, binning, sample_binning, ranges,
+                              sample_ranges)
+        return out
+
+    @staticmethod
+    def backward(ctx, grad_out):
+        means, values, conics, samples, binning, sample_binning, ranges, sample_ranges = ctx.saved_tensors
+        bwd = getattr(_C, _FWD[ctx.function] + "_backward")
+        grads = call_debug(bwd, ctx.debug, "spatial_bw", means, values, conics, samples,
+                           ctx.num_rendered, grad_out.contiguous(), binning, sample_binning,
+                           ranges, sample_ranges, ctx.debug)
+        G = ctx.xchg.exchange(pack_grads(grads))
+        gm, gv, gc = unpack_grads(G, grads)
+        return (None, None, gm, gv, gc) + (None,) * 7
+
+
+class SpatialShardedGaussianSampler(ShardedGaussianSampler):
+    """ShardedGaussianSampler for ranks that own spatial strips of the query points (SURVEY 8f
+    row f3): the same global grid and per-rank binning, and the gradients summed by
+    SupportExchange instead of a dense all-reduce.  After backward, every Gaussian that can touch
+    this rank's points carries the sum over all ranks; the other rows are this rank's partials,
+    exactly zero (no point of this rank is within their cut)."""
+
+    def preprocess(self, means, values, covariances, conics, samples):
+        super().preprocess(means, values, covariances, conics, samples)
+        rank = dist.get_rank(self.group) if _world(self.group) > 1 else 0
+        self.xchg = SupportExchange(means, conics, shard_extents(samples, self.group), rank, self.group)
+
+    def _sample(self, function):
+        return _SpatialSample.apply(function, self.xchg, self.means, self.values, self.conics,
+                                    self.samples, self.num_rendered, self.binning_buffer,
+                                    self.sample_binning_buffer, self.ranges, self.sample_ranges,
+                                    self.debug)

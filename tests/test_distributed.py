@@ -92,3 +92,84 @@ def test_allreduce_grads_single_process_passthrough():
     from diff_gaussian_sampling.distributed import allreduce_grads
     g = (torch.ones(3, 2), torch.ones(3, 1), torch.ones(3, 3))
     assert allreduce_grads(g) is g
+
+
+def _spatial_problem():
+    """Gaussians small against the strips (h = 2 / sqrt(P) = 0.01, cut half-widths ~0.2), so
+    most of them reach one rank only; the uniform points wrap across y = +-1 (rank 0 <-> W-1)."""
+    from diff_gaussian_sampling import synthetic as syn
+    means, values, covs, conics = syn.gaussians(40000, 2, 2, seed=321)
+    samples = syn.samples(6001, 2, seed=322)
+    w = syn.grad_out(6001, 2, 2, seed=323).reshape(6001, 2, 2)
+    return means, values, covs, conics, samples, w
+
+
+def _spatial_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import diff_gaussian_sampling.distributed as dd
+        from oracle_stub import OracleC
+        dd._C = OracleC()
+        means, values, covs, conics, samples, w = _spatial_problem()
+        order = torch.argsort(samples[:, 1])  # spatial strips along y
+        shard = torch.tensor_split(order, world)[rank].sort().values
+        m, v, c = (t.clone().requires_grad_(True) for t in (means, values, conics))
+        sampler = dd.SpatialShardedGaussianSampler(False)
+        sampler.preprocess(m, v, covs, c, samples[shard])
+        out = sampler.sample_gaussians_derivative()
+        (out * w[shard]).sum().backward()
+        x = sampler.xchg
+        np.savez(os.path.join(outdir, f"srank{rank}.npz"), out=out.detach().numpy(),
+                 shard=shard.numpy(), gm=m.grad.numpy(), gv=v.grad.numpy(), gc=c.grad.numpy(),
+                 touch=x.touch.numpy(), owner=x.owner.numpy(), moved=x.rows_moved())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spatial_shards_support_exchange(tmp_path, oracle, world):
+    """SpatialShardedGaussianSampler: strips of the points along y; the gradient
+    sum travels only for Gaussians whose exact-zero cut (or a torus image of it) reaches another
+    rank's strip.  Every row a rank can touch equals the single-process gradient over all points;
+    the others are exactly zero there; fewer rows move than a dense all-reduce would."""
+    mp.spawn(_spatial_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    means, values, covs, conics, samples, w = _spatial_problem()
+    ranks = [np.load(tmp_path / f"srank{r}.npz") for r in range(world)]
+    from diff_gaussian_sampling.distributed import global_tile_grid
+    grid, off = global_tile_grid(samples)
+    ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy(), grid, off)
+    ref = ob.forward("derivative", values.numpy(), conics.numpy())
+    got = np.zeros_like(ref)
+    for r in ranks:
+        got[r["shard"]] = r["out"].reshape(len(r["shard"]), 2, 2)
+    assert np.array_equal(got, ref)
+    dm, dv, dc = ob.backward("derivative", values.numpy(), conics.numpy(), w.numpy())
+    P = means.shape[0]
+    for ri, r in enumerate(ranks):
+        t = r["touch"][:, ri]
+        assert 0 < t.sum() < P  # strips: not every Gaussian reaches every rank
+        for k, exp in (("gm", dm), ("gv", dv), ("gc", dc)):
+            np.testing.assert_allclose(r[k][t], exp[t], rtol=1e-5, atol=1e-5 * np.abs(exp).max())
+            assert np.all(r[k][~t] == 0)
+        assert r["moved"] < 0.5 * t.sum()
+    # every Gaussian has one owner, the same on every rank
+    for r in ranks[1:]:
+        assert np.array_equal(r["owner"], ranks[0]["owner"]) and np.array_equal(r["touch"], ranks[0]["touch"])
+
+
+def test_support_halfwidth_bounds_the_live_pairs(oracle):
+    """The y-extent sqrt(210 (A^-1)_yy) of the cut bounds every pair with a non-zero exponent:
+    count live pairs (power >= -104) whose |dy| (after the torus wrap) exceeds it -- none."""
+    from diff_gaussian_sampling import synthetic as syn
+    from diff_gaussian_sampling.distributed import support_halfwidth
+    means, values, covs, conics = syn.gaussians(300, 2, 1, seed=311)
+    samples = syn.samples(4000, 2, seed=312)
+    e = support_halfwidth(means, conics).numpy()
+    X = means.numpy()[:, None, :].astype(np.float64) - samples.numpy()[None, :, :]
+    X = np.where(np.abs(X) > 1, np.fmod(X, 2.0) - 2.0 * np.sign(X), X)
+    c = conics.numpy().astype(np.float64)
+    q = c[:, None, 0] * X[..., 0] ** 2 + 2 * c[:, None, 1] * X[..., 0] * X[..., 1] + c[:, None, 2] * X[..., 1] ** 2
+    live = -0.5 * q >= -104.0
+    assert live.any()
+    assert not np.any(live & (np.abs(X[..., 1]) > e[:, None]))
