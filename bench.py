@@ -138,9 +138,17 @@ def main():
     if world != args.gpus:
         print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
         return 2
+    # DGS_BENCH_SHARE_GPU=1: rehearsal of the N-rank path with the ranks sharing the visible
+    # GPU(s) (a 1-GPU box; RCCL refuses two ranks on one device, so gloo); never a measurement
+    share = os.environ.get("DGS_BENCH_SHARE_GPU") == "1"
+    if share:
+        local = local % max(torch.cuda.device_count(), 1)
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if share:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     dev = torch.device("cuda", local)
     if args.op == "aggregate":
         return bench_aggregate(args, world, rank, dev, torch, dist)
@@ -195,12 +203,13 @@ def bench_sample(args, world, rank, dev, torch, dist):
     pre_ms = sorted(pre_times[1:])[len(pre_times[1:]) // 2] if args.pre_reps > 0 else pre_first_ms
     R, gb, sb, rg, srg, radii = binned
     xchg, xsetup_ms = None, 0.0
-    if spatial:  # the exchange sets: per binning (the PIGS loop re-bins, so it is part of that step)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        xchg = SupportExchange(means, conics, shard_extents(samples), rank)
-        torch.cuda.synchronize()
-        xsetup_ms = (time.perf_counter() - t0) * 1e3
+    if spatial:  # the exchange sets: per binning (the PIGS loop re-bins, so part of its step); warm
+        for _ in range(2):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            xchg = SupportExchange(means, conics, shard_extents(samples), rank)
+            torch.cuda.synchronize()
+            xsetup_ms = (time.perf_counter() - t0) * 1e3
     fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative,
            "laplacian": dgs.sample_gaussians_laplacian,
            "third": dgs.sample_gaussians_third_derivative}[fn]

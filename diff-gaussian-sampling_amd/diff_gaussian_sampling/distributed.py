@@ -167,20 +167,34 @@ class SupportExchange:
         owner = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
         self.rank, self.world, self.group = rank, W, group
         self.touch, self.owner = touch, owner
-        mine = touch[:, rank]
-        # rows this rank sends to each owner, and the rows it receives from each rank (both
-        # ascending Gaussian id)
-        self.send_idx = [torch.nonzero(mine & (owner == o) & (o != rank)).flatten() for o in range(W)]
-        self.recv_idx = [torch.nonzero(touch[:, r] & (owner == rank)).flatten() if r != rank
-                         else torch.zeros(0, dtype=torch.long, device=dev) for r in range(W)]
-        self.send_splits = [int(i.numel()) for i in self.send_idx]
-        self.recv_splits = [int(i.numel()) for i in self.recv_idx]
-        self.send_cat = torch.cat(self.send_idx)
-        self.recv_cat = torch.cat(self.recv_idx)
+        # rows this rank sends, grouped by owner (ascending id within a group), and the rows it
+        # receives, grouped by source rank: two nonzero passes, one host read of the counts
+        snd = torch.nonzero(touch[:, rank] & (owner != rank)).flatten()
+        so = owner[snd]
+        order = torch.argsort(so, stable=True)
+        self.send_cat = snd[order]
+        mine = torch.nonzero(owner == rank).flatten()
+        tm = touch[mine].clone()
+        tm[:, rank] = False
+        rg = torch.nonzero(tm.t())  # (source rank, position in `mine`), rank-major
+        self.recv_cat = mine[rg[:, 1]]
+        counts = torch.stack([torch.bincount(so, minlength=W), torch.bincount(rg[:, 0], minlength=W)]).cpu()
+        self.send_splits = [int(x) for x in counts[0]]
+        self.recv_splits = [int(x) for x in counts[1]]
+        self.send_idx = list(torch.split(self.send_cat, self.send_splits))
+        self.recv_idx = list(torch.split(self.recv_cat, self.recv_splits))
 
     def rows_moved(self):
         """Gaussian rows this rank sends per step (each way)."""
         return sum(self.send_splits)
+
+    def _a2a(self, out, inp, out_splits, in_splits):
+        if inp.is_cuda and dist.get_backend(self.group) == "gloo":  # gloo: host staging
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
     def exchange(self, G):
         """G [P, F] float32, this rank's partial sums (modified in place): afterwards every row
@@ -191,7 +205,7 @@ class SupportExchange:
         # 1. partials to the owners, added in rank order (deterministic: no duplicates per add)
         send = G.index_select(0, self.send_cat).contiguous()
         recv = torch.empty((sum(self.recv_splits), F), dtype=G.dtype, device=G.device)
-        dist.all_to_all_single(recv, send, self.recv_splits, self.send_splits, group=self.group)
+        self._a2a(recv, send, self.recv_splits, self.send_splits)
         o = 0
         for r in range(self.world):
             n = self.recv_splits[r]
@@ -201,7 +215,7 @@ class SupportExchange:
         # 2. the owners' sums back to every contributing rank
         back = G.index_select(0, self.recv_cat).contiguous()
         got = torch.empty((sum(self.send_splits), F), dtype=G.dtype, device=G.device)
-        dist.all_to_all_single(got, back, self.send_splits, self.recv_splits, group=self.group)
+        self._a2a(got, back, self.send_splits, self.recv_splits)
         G.index_copy_(0, self.send_cat, got)
         return G
 
