@@ -65,6 +65,11 @@ def algorithmic_bytes(function, P, N, C, D=2):
     return fwd, bwd
 
 
+def _count(n):
+    """1000000 -> '1M', 256000 -> '256k' (metric labels)."""
+    return f"{n // 1_000_000}M" if n % 1_000_000 == 0 else (f"{n // 1000}k" if n % 1000 == 0 else str(n))
+
+
 def log(rank, *a):
     if rank == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -313,8 +318,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
                 + ((", spatial strips + sparse gradient exchange" if spatial else ", RCCL all-reduce of grads")
                    if world > 1 else ""))
     result = {
-        "metric": "sampled points/sec (fwd+bwd), 1M Gaussians x "
-                  + (f"{N * world // 1_000_000}M queries over {world} GPUs" if world > 1 else f"{N // 1_000_000}M queries")
+        "metric": f"sampled points/sec (fwd+bwd), {_count(P)} Gaussians x "
+                  + (f"{_count(N * world)} queries over {world} GPUs" if world > 1 else f"{_count(N)} queries")
                   + (f", fused functions {fname}" if multi else "")
                   + (f", function {fn}" if fn != "gaussian" and not multi else ""),
         "value": value,

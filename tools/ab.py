@@ -37,5 +37,5 @@ for r in range(a.rounds):
         res[v].append(j)
         print(r, v, json.dumps(j), flush=True)
 for v, js in res.items():
-    med = {k: statistics.median(j[k] for j in js) for k in ("fwd_ms", "bwd_ms", "call_pair_ms")}
+    med = {k: statistics.median(j[k] for j in js) for k in ("fwd_ms", "bwd_ms", "call_pair_ms", "prep_ms") if k in js[0]}
     print("MEDIAN", v, json.dumps(med), flush=True)

@@ -34,8 +34,13 @@ means, values, covs, conics = (t.to(dev) for t in syn.gaussians(a.P, D, a.C, see
 samples = syn.samples(a.N, D, seed=4).to(dev)
 dL = syn.grad_out(a.N, D ** fi, a.C, seed=5).to(dev).reshape((a.N,) + (D,) * fi + (a.C,))
 R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
+prep_ms = []
 for _ in range(a.prep):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
     R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
+    torch.cuda.synchronize()
+    prep_ms.append((time.perf_counter() - t0) * 1e3)
 name = "sample_gaussians" + ["", "_derivative", "_laplacian", "_third_derivative"][fi]
 fwd, bwd = getattr(dgs._C, name), getattr(dgs._C, name + "_backward")
 
@@ -60,4 +65,5 @@ dgs._C.timing_enable(False)
 nf, fms = dgs._C.timing_read(0)
 nb, bms = dgs._C.timing_read(1)
 print(json.dumps({"lib": os.path.dirname(dgs.__file__), "fwd_ms": fms / max(nf, 1),
-                  "bwd_ms": bms / max(nb, 1), "call_pair_ms": el * 1e3 / a.steps}), flush=True)
+                  "bwd_ms": bms / max(nb, 1), "call_pair_ms": el * 1e3 / a.steps,
+                  "prep_ms": sorted(prep_ms)[len(prep_ms) // 2] if prep_ms else 0.0}), flush=True)
