@@ -711,25 +711,27 @@ struct ZeroList {
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Entry sort: (key, entry) pairs with keys of type KT (stored in u32 arrays; u16 view when the
-// keys fit 16 bits).
+// Every sort of the binning is a stable LSD radix sort of (key, u32 value) pairs on the onesweep
+// algorithm: rocprim's default switches to block sort + merge passes below 2^20 items (24
+// launches, ~170 us for the 1M home keys against ~25 us here), and one algorithm for all of them
+// keeps the code object small (its load is most of the first call's time).  Entry keys are u16
+// when every (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per entry and pass).
+using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                               rocprim::default_config, 0>;
+
 template <typename KT>
 static hipError_t sort_entries(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
                                const uint32_t *vin, uint32_t *vout, int64_t n, int bits, hipStream_t s) {
-    return rocprim::radix_sort_pairs(tmp, bytes, reinterpret_cast<const KT *>(kin), reinterpret_cast<KT *>(kout),
-                                     vin, vout, (size_t)n, 0u, (unsigned)bits, s);
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, reinterpret_cast<const KT *>(kin),
+                                                  reinterpret_cast<KT *>(kout), vin, vout, (size_t)n, 0u,
+                                                  (unsigned)bits, s);
 }
 
-// Stable LSD radix sort of (u32 key, u32 value) pairs, always the onesweep algorithm: rocprim's
-// default switches to block sort + merge passes below 2^20 items (24 launches, ~170 us for the
-// 1M home keys against ~25 us here).
 static hipError_t sort_pairs_onesweep(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
                                       const uint32_t *vin, uint32_t *vout, int n, int b0, int b1,
                                       hipStream_t s) {
-    using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                           rocprim::default_config, 0>;
-    return rocprim::radix_sort_pairs<Cfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n,
-                                          (unsigned)b0, (unsigned)b1, s);
+    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n,
+                                                  (unsigned)b0, (unsigned)b1, s);
 }
 
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
@@ -789,6 +791,55 @@ struct Scratch {
     }
 };
 
+
+// ------------------------------------------------------------ spatial shards
+// Per Gaussian, the ranks whose point range along the sharding axis (y at D = 2, x at D = 1)
+// meets its exact-zero cut X^T A X <= kQCut or a torus image of it (period 2,
+// forward.cu:149-157): bit r of mask[g]; and the owner, the rank whose range is nearest the mean
+// (first on ties).  The cut's half-width along the axis is sqrt(kQCut (A^-1)_axis), widened by
+// 1e-5; conics that are not positive definite reach every rank.
+constexpr int kMaxXchgRanks = 32;
+struct XchgRanks {
+    int W;
+    double lo[kMaxXchgRanks], hi[kMaxXchgRanks];
+};
+
+__global__ void k_xchg_sets(int P, int D, const float *__restrict__ means, const float *__restrict__ conics,
+                            XchgRanks R, uint32_t *__restrict__ mask, int32_t *__restrict__ owner) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P) return;
+    const int S = D * (D + 1) / 2;
+    const double y = means[g * D + (D - 1)];
+    double e;
+    bool pd;
+    if (D == 2) {
+        const double c0 = conics[g * S], c1 = conics[g * S + 1], c2 = conics[g * S + 2];
+        const double det = c0 * c2 - c1 * c1;
+        pd = c0 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY;
+        e = pd ? sqrt(kQCut * c0 / det) : INFINITY;
+    } else {
+        const double c0 = conics[g * S];
+        pd = c0 > 0.0 && c0 < INFINITY;
+        e = pd ? sqrt(kQCut / c0) : INFINITY;
+    }
+    e = e * (1.0 + 1e-5) + 1e-6;
+    uint32_t m = 0u;
+    int best = 0;
+    double bd = INFINITY;
+    for (int r = 0; r < R.W; ++r) {
+        const double lo = R.lo[r], hi = R.hi[r];
+        if (!pd) {
+            m |= 1u << r;
+        } else {  // some k with [y + 2k - e, y + 2k + e] meeting [lo, hi]
+            const double kmin = ceil((lo - y - e) * 0.5), kmax = floor((hi - y + e) * 0.5);
+            if (kmin <= kmax) m |= 1u << r;
+        }
+        const double d = fmax(fmax(lo - y, y - hi), 0.0);
+        if (d < bd) { bd = d; best = r; }
+    }
+    mask[g] = m;
+    owner[g] = best;
+}
 }  // namespace dgs
 
 using namespace dgs;
@@ -903,8 +954,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
     const int sbits = bit_length((uint64_t)ncells);
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, t_ssort, skeys, skeys_sorted, sids,
-                                                   (uint32_t *)sorted_sid, N, 0, sbits, s));
+    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_ssort, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0,
+                                    sbits, s));
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
                                                    perm, P, 0, hbits, s));
     DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, fcount, foffs, P, s));
@@ -941,8 +992,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
     DGS_LAUNCH_CHECK(s, debug);
     size_t tb = t_a;
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp_a, tb, skeys, skeys_sorted, sids,
-                                                   (uint32_t *)sorted_sid, N, 0, sbits, s));
+    DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0, sbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
@@ -1258,3 +1308,18 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     return rc;
 }
 
+
+extern "C" int dgs_exchange_sets(int P, int D, const float *means, const float *conics, int W,
+                                 const double *extents, uint32_t *mask_out, int32_t *owner_out,
+                                 dgs_stream_t stream) {
+    if (P < 0 || (D != 1 && D != 2) || W < 1 || W > kMaxXchgRanks || !extents)
+        return fail(DGS_ERR_ARG, "dgs_exchange_sets: bad arguments (1 <= W <= 32)");
+    if (P == 0) return DGS_OK;
+    XchgRanks R;
+    R.W = W;
+    for (int r = 0; r < W; ++r) { R.lo[r] = extents[2 * r]; R.hi[r] = extents[2 * r + 1]; }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    k_xchg_sets<<<grid_for(P), kBlock, 0, s>>>(P, D, means, conics, R, mask_out, owner_out);
+    DGS_TRY_HIP(hipGetLastError());
+    return DGS_OK;
+}

@@ -342,6 +342,21 @@ bool InputsMatch(const Tensor &means_in, const Tensor &conics_in, const Tensor &
 }
 
 // The C-ABI tile grid (device min/max, torch-CUDA arithmetic) -- for tests of dgs_tile_grid.
+// SupportExchange's sets (distributed.py): (mask int32 [P] bit per rank, owner int32 [P]).
+std::tuple<Tensor, Tensor> ExchangeSets(const Tensor &means_in, const Tensor &conics_in,
+                                        const std::vector<double> &extents) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const int P = (int)means.size(0), D = (int)means.size(-1);
+    const int W = (int)(extents.size() / 2);
+    Tensor mask = torch::empty({P}, means.options().dtype(torch::kInt32));
+    Tensor owner = torch::empty({P}, means.options().dtype(torch::kInt32));
+    check(dgs_exchange_sets(P, D, means.data_ptr<float>(), conics.data_ptr<float>(), W, extents.data(),
+                            reinterpret_cast<uint32_t *>(mask.data_ptr<int>()), owner.data_ptr<int>(),
+                            as_dgs(cur_stream())),
+          "exchange_sets");
+    return std::make_tuple(mask, owner);
+}
+
 std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_in) {
     const Tensor samples = f32(samples_in, "samples");
     const int N = (int)samples.size(0), D = (int)samples.size(-1);
@@ -526,6 +541,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("sample_gaussians_multi", &SampleGaussiansMulti);
     m.def("sample_gaussians_multi_backward", &SampleGaussiansMultiBackward);
     m.def("tile_grid", &TileGrid);
+    m.def("exchange_sets", &ExchangeSets);
     m.def("inputs_match", &InputsMatch);
     m.def("library_version", []() { return dgs_version(); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });

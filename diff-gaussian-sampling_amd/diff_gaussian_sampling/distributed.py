@@ -153,28 +153,42 @@ class SupportExchange:
     def __init__(self, means, conics, extents, rank, group=None):
         D = means.shape[1]
         dev = means.device
-        y = means.detach()[:, D - 1].double()
-        e = support_halfwidth(means, conics)
-        lo, hi = extents[:, 0].double().to(dev), extents[:, 1].double().to(dev)
-        W = lo.numel()
-        span = float((hi.max() - lo.min()).item()) if W else 0.0
-        kmax = int(math.ceil(span / 2.0)) + 1
-        touch = torch.zeros(y.numel(), W, dtype=torch.bool, device=dev)
-        for k in range(-kmax, kmax + 1):
-            a, b = y + 2.0 * k - e, y + 2.0 * k + e
-            touch |= (a[:, None] <= hi[None, :]) & (b[:, None] >= lo[None, :])
-        dist_r = torch.clamp(torch.maximum(lo[None, :] - y[:, None], y[:, None] - hi[None, :]), min=0.0)
-        owner = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
+        ext = extents.detach().double().cpu()
+        W = ext.shape[0]
         self.rank, self.world, self.group = rank, W, group
-        self.touch, self.owner = touch, owner
+        if means.is_cuda and W <= 32:
+            # native (dgs_exchange_sets): bit r of mask[g] = rank r can touch g; owner[g]
+            mask, owner = _C.exchange_sets(means.detach(), conics.detach(), [float(v) for v in ext.reshape(-1)])
+            mask, owner = mask.long(), owner.long()
+            touch_me = ((mask >> rank) & 1).bool()
+            self._mask = mask
+            self.touch = None
+        else:  # host tensors (the CPU tests): a P x W matrix in torch ops
+            y = means.detach()[:, D - 1].double()
+            e = support_halfwidth(means, conics)
+            lo, hi = ext[:, 0].to(dev), ext[:, 1].to(dev)
+            span = float(ext[:, 1].max() - ext[:, 0].min()) if W else 0.0
+            kmax = int(math.ceil(span / 2.0)) + 1
+            touch = torch.zeros(y.numel(), W, dtype=torch.bool, device=dev)
+            for k in range(-kmax, kmax + 1):
+                a, b = y + 2.0 * k - e, y + 2.0 * k + e
+                touch |= (a[:, None] <= hi[None, :]) & (b[:, None] >= lo[None, :])
+            dist_r = torch.clamp(torch.maximum(lo[None, :] - y[:, None], y[:, None] - hi[None, :]), min=0.0)
+            owner = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
+            touch_me = touch[:, rank]
+            self._mask = None
+            self.touch = touch
+        self.owner = owner
         # rows this rank sends, grouped by owner (ascending id within a group), and the rows it
         # receives, grouped by source rank: two nonzero passes, one host read of the counts
-        snd = torch.nonzero(touch[:, rank] & (owner != rank)).flatten()
+        snd = torch.nonzero(touch_me & (owner != rank)).flatten()
         so = owner[snd]
-        order = torch.argsort(so, stable=True)
-        self.send_cat = snd[order]
+        self.send_cat = snd[torch.argsort(so, stable=True)]
         mine = torch.nonzero(owner == rank).flatten()
-        tm = touch[mine].clone()
+        if self._mask is not None:
+            tm = ((self._mask[mine][:, None] >> torch.arange(W, device=dev)) & 1).bool()
+        else:
+            tm = self.touch[mine].clone()
         tm[:, rank] = False
         rg = torch.nonzero(tm.t())  # (source rank, position in `mine`), rank-major
         self.recv_cat = mine[rg[:, 1]]
@@ -183,6 +197,12 @@ class SupportExchange:
         self.recv_splits = [int(x) for x in counts[1]]
         self.send_idx = list(torch.split(self.send_cat, self.send_splits))
         self.recv_idx = list(torch.split(self.recv_cat, self.recv_splits))
+
+    def touches(self, r):
+        """Bool [P]: the Gaussians whose partial gradient can be non-zero on rank r."""
+        if self.touch is not None:
+            return self.touch[:, r]
+        return ((self._mask >> r) & 1).bool()
 
     def rows_moved(self):
         """Gaussian rows this rank sends per step (each way)."""

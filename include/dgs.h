@@ -91,6 +91,16 @@ int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *co
                         void *alloc_ctx, int64_t *num_rendered, int *grid_out, float *offset_out,
                         dgs_stream_t stream, int debug);
 
+/* Spatial sharding (diff_gaussian_sampling.distributed.SupportExchange): for
+ * each Gaussian, bit r of mask_out[g] is set when rank r's point range extents[r] = [lo, hi]
+ * along the sharding axis (y at D = 2, x at D = 1) meets the Gaussian's exact-zero cut
+ * X^T A X <= 210 or one of its torus images (period 2, forward.cu:149-157), i.e. when rank r's
+ * partial gradient for it can be non-zero; owner_out[g] is the rank nearest its mean.
+ * extents: host array [W][2]; 1 <= W <= 32. */
+int dgs_exchange_sets(int P, int D, const float *means, const float *conics, int W,
+                      const double *extents, uint32_t *mask_out, int32_t *owner_out,
+                      dgs_stream_t stream);
+
 /* Workspace bytes needed by dgs_sample_forward (backward == 0) or dgs_sample_backward. */
 size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward);
 

@@ -122,7 +122,8 @@ def _spatial_worker(rank, world, port, outdir):
         x = sampler.xchg
         np.savez(os.path.join(outdir, f"srank{rank}.npz"), out=out.detach().numpy(),
                  shard=shard.numpy(), gm=m.grad.numpy(), gv=v.grad.numpy(), gc=c.grad.numpy(),
-                 touch=x.touch.numpy(), owner=x.owner.numpy(), moved=x.rows_moved())
+                 touch=np.stack([x.touches(r).numpy() for r in range(world)], 1),
+                 owner=x.owner.numpy(), moved=x.rows_moved())
     finally:
         dist.destroy_process_group()
 
