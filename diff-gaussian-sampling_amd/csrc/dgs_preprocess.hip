@@ -13,7 +13,6 @@
 //   * samples sorted by fine cell, per-cell sample ranges, forward work units (cell, 64 samples)
 //   * Gaussians renumbered by spatial home cell (perm), per-cell Gaussian lists in ascending
 //     internal id, backward work units (cell, 64 list entries)
-#include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
@@ -711,27 +710,137 @@ struct ZeroList {
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Every sort of the binning is a stable LSD radix sort of (key, u32 value) pairs on the onesweep
-// algorithm: rocprim's default switches to block sort + merge passes below 2^20 items (24
-// launches, ~170 us for the 1M home keys against ~25 us here), and one algorithm for all of them
-// keeps the code object small (its load is most of the first call's time).  Entry keys are u16
-// when every (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per entry and pass).
-using OnesweepCfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                               rocprim::default_config, 0>;
+// Every sort of the binning is a stable LSD radix sort of (key, u32 value) pairs on rocprim's
+// onesweep algorithm, called directly (rocprim::detail::radix_sort_onesweep_impl, the branch
+// rocprim::radix_sort_pairs takes for large inputs).  The public entry also instantiates a block
+// sort and a merge sort for small inputs: ~250 more kernels in this code object, whose load is
+// most of the first call's time.  Below 2^20 items rocprim would otherwise pick those (24
+// launches, ~170 us for the 1M home keys against ~25 us here).  Entry keys are u16 when every
+// (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per entry and pass).
+template <typename KT>
+static hipError_t onesweep_pairs(void *tmp, size_t &bytes, const KT *kin, KT *kout, const uint32_t *vin,
+                                 uint32_t *vout, size_t n, unsigned b0, unsigned b1, hipStream_t s) {
+    if (n == 0) {  // (rocprim's block-sort branch returns here)
+        if (tmp == nullptr) bytes = 4;
+        return hipSuccess;
+    }
+    bool in_output = true;
+    return rocprim::detail::radix_sort_onesweep_impl<rocprim::default_config, false>(
+        tmp, bytes, kin, static_cast<KT *>(nullptr), kout, vin, static_cast<uint32_t *>(nullptr), vout, n,
+        in_output, rocprim::identity_decomposer{}, b0, b1, s, false, false);
+}
 
 template <typename KT>
 static hipError_t sort_entries(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
                                const uint32_t *vin, uint32_t *vout, int64_t n, int bits, hipStream_t s) {
-    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, reinterpret_cast<const KT *>(kin),
-                                                  reinterpret_cast<KT *>(kout), vin, vout, (size_t)n, 0u,
-                                                  (unsigned)bits, s);
+    return onesweep_pairs<KT>(tmp, bytes, reinterpret_cast<const KT *>(kin), reinterpret_cast<KT *>(kout), vin,
+                              vout, (size_t)n, 0u, (unsigned)bits, s);
 }
 
 static hipError_t sort_pairs_onesweep(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
                                       const uint32_t *vin, uint32_t *vout, int n, int b0, int b1,
                                       hipStream_t s) {
-    return rocprim::radix_sort_pairs<OnesweepCfg>(tmp, bytes, kin, kout, vin, vout, (size_t)n,
-                                                  (unsigned)b0, (unsigned)b1, s);
+    return onesweep_pairs<uint32_t>(tmp, bytes, kin, kout, vin, vout, (size_t)n, (unsigned)b0, (unsigned)b1, s);
+}
+
+// Exclusive prefix sums of one or two count arrays of length n: tile sums, one block scanning
+// them, then a downsweep (3 launches for both arrays).  Replaces hipcub::DeviceScan, whose ~210
+// kernel instantiations were a third of this code object.
+constexpr int kScanItems = 8, kScanTile = kBlock * kScanItems;
+
+static inline int64_t scan_tiles(int64_t n) { return (n + kScanTile - 1) / kScanTile; }
+template <typename T>
+static inline size_t scan_scratch_bytes(int64_t n) { return sizeof(T) * 2 * (size_t)std::max<int64_t>(scan_tiles(n), 1); }
+
+// exclusive scan of x over the block; total = the block's sum
+template <typename T>
+__device__ __forceinline__ T block_excl_scan(T x, T &total) {
+    __shared__ T wsum[kWavesPerBlock];
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    T inc = x;
+#pragma unroll
+    for (int d = 1; d < kWave; d <<= 1) {
+        const T y = __shfl_up(inc, d, kWave);
+        if (lane >= d) inc += y;
+    }
+    if (lane == kWave - 1) wsum[w] = inc;
+    __syncthreads();
+    T pre = 0;
+    total = 0;
+#pragma unroll
+    for (int i = 0; i < kWavesPerBlock; ++i) {
+        if (i < w) pre += wsum[i];
+        total += wsum[i];
+    }
+    __syncthreads();
+    return pre + inc - x;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scan_reduce(int64_t n, const T *__restrict__ a, const T *__restrict__ b,
+                                                        T *__restrict__ part) {
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    T sa = 0, sb = 0;
+#pragma unroll
+    for (int k = 0; k < kScanItems; ++k) {
+        const int64_t i = base + k * kBlock + threadIdx.x;
+        if (i < n) {
+            sa += a[i];
+            if (b) sb += b[i];
+        }
+    }
+    T ta, tb = 0;
+    (void)block_excl_scan(sa, ta);
+    if (b) (void)block_excl_scan(sb, tb);
+    if (threadIdx.x == 0) {
+        part[blockIdx.x] = ta;
+        if (b) part[gridDim.x + blockIdx.x] = tb;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scan_parts(int64_t nt, int arrays, T *__restrict__ part) {
+    for (int r = 0; r < arrays; ++r) {
+        T carry = 0;
+        for (int64_t c0 = 0; c0 < nt; c0 += kBlock) {
+            const int64_t i = c0 + threadIdx.x;
+            const T x = i < nt ? part[r * nt + i] : (T)0;
+            T tot;
+            const T e = block_excl_scan(x, tot);
+            if (i < nt) part[r * nt + i] = carry + e;
+            carry += tot;
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void k_scan_down(int64_t n, const T *__restrict__ a, T *__restrict__ ao,
+                                                      const T *__restrict__ b, T *__restrict__ bo,
+                                                      const T *__restrict__ part) {
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    for (int r = 0; r < (b ? 2 : 1); ++r) {
+        const T *in = r ? b : a;
+        T *out = r ? bo : ao;
+        T carry = part[r * (int64_t)gridDim.x + blockIdx.x];
+        for (int k = 0; k < kScanItems; ++k) {
+            const int64_t i = base + k * kBlock + threadIdx.x;
+            const T x = i < n ? in[i] : (T)0;
+            T tot;
+            const T e = block_excl_scan(x, tot);
+            if (i < n) out[i] = carry + e;
+            carry += tot;
+        }
+    }
+}
+
+// ao = exclusive scan of a, bo = of b (b may be null); part: scan_scratch_bytes<T>(n)
+template <typename T>
+static void scan_excl(int64_t n, const T *a, T *ao, const T *b, T *bo, T *part, hipStream_t s) {
+    if (n <= 0) return;
+    const int64_t nt = scan_tiles(n);
+    k_scan_reduce<T><<<(unsigned)nt, kBlock, 0, s>>>(n, a, b, part);
+    k_scan_parts<T><<<1, kBlock, 0, s>>>(nt, b ? 2 : 1, part);
+    k_scan_down<T><<<(unsigned)nt, kBlock, 0, s>>>(n, a, ao, b, bo, part);
 }
 
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
@@ -950,7 +1059,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint64_t *toffs = ca.take<uint64_t>(P);
     int64_t *totals = ca.take<int64_t>(4);
 
-    // hipcub temp storage: one piece sized for the largest phase-A primitive (size queries only)
+    // sort / scan temp storage: one piece sized for the largest phase-A primitive
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
     const int sbits = bit_length((uint64_t)ncells);
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
@@ -958,7 +1067,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                     sbits, s));
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
                                                    perm, P, 0, hbits, s));
-    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, fcount, foffs, P, s));
+    t_scan = scan_scratch_bytes<uint64_t>(P);
     const size_t t_a = std::max(std::max(t_ssort, t_hsort), t_scan);
     void *tmp_a = ca.take<char>(t_a);
     {
@@ -1013,10 +1122,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
                                                 cell_send, cell_box, fcount);
     DGS_LAUNCH_CHECK(s, debug);
-    tb = t_a;
-    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, fcount, foffs, P, s));
-    tb = t_a;
-    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_a, tb, touched, toffs, P, s));
+    scan_excl<uint64_t>(P, fcount, foffs, touched, toffs, static_cast<uint64_t *>(tmp_a), s);
+    DGS_LAUNCH_CHECK(s, debug);
     k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, dgrid, doff, totals);
     DGS_LAUNCH_CHECK(s, debug);
     // ---- Gaussian-side buffer and phase-B scratch for capacities (Ecap, Rcap).  Set up BEFORE
@@ -1061,7 +1168,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                    B.ebits, s)
                           : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, entries, Ecap,
                                                    B.ebits, s));
-        DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(nullptr, t_cscan, B.fcnt, B.foff, ncells, s));
+        t_cscan = scan_scratch_bytes<uint32_t>(ncells);
         B.t_b = std::max(std::max(t_esort, t_cscan), t_rsort);
         B.tmp_b = cb.take<char>(B.t_b);
         char *base = S.get<char>(cb.off);
@@ -1166,10 +1273,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
                                                       cell_gend, fcnt, bcnt);
     DGS_LAUNCH_CHECK(s, debug);
-    tb = t_b;
-    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, fcnt, foff, ncells, s));
-    tb = t_b;
-    DGS_TRY_HIP(hipcub::DeviceScan::ExclusiveSum(tmp_b, tb, bcnt, boff, ncells, s));
+    scan_excl<uint32_t>(ncells, fcnt, foff, bcnt, boff, static_cast<uint32_t *>(tmp_b), s);
+    DGS_LAUNCH_CHECK(s, debug);
     k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
                                                     boff, fwd_units, bwd_units, counters);
     DGS_LAUNCH_CHECK(s, debug);

@@ -483,6 +483,155 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
     }
 }
 
+// (c) Matrix-core form (wide accumulators, CB >= 8).  For a unit's samples the forward is
+// out[s][u][ch] = sum_g A_u[s][g] v[g][ch] with A_u = G t_u (the exponent and the terms of
+// forward.cu:225-332): a [samples x Gaussians] by [Gaussians x channels] product.  A_u comes
+// from the VALU (one pair per lane per step), the product from v_mfma_f32_16x16x4_f32, whose
+// f32 accumulation is an exact fmaf chain.  Unit = (cell, 64 samples) as in k_forward.  A
+// 4-Gaussian step gives 16-lane group kq = lane >> 4 the list entry e + kq; lane col = lane & 15
+// evaluates samples 16 b + col (b = 0..3) against it and holds channel col of its values (the
+// B operand); accumulator tile b ends with samples 16 b + 4 kq + r (r = 0..3), channel col.
+// The Gaussian rows arrive by vector loads (a 16-lane group shares one row), so neither the
+// scalar cache's random-row rate (the lane-per-sample form's bound) nor a per-pass
+// re-walk of the list (the transposed form's) is paid.
+#ifndef DGS_FWD_MX
+#define DGS_FWD_MX 1
+#endif
+template <int FN, int D, int CB>
+__host__ __device__ constexpr bool fwd_mfma() {
+    return DGS_FWD_MX && !is_multi(FN) && CB >= 8;
+}
+
+template <int FN, int D, int CB, bool FLAGGED>
+__device__ __forceinline__ void fwd_mx_groups(const Bins &bins, const float *__restrict__ grows, int eb, int ee,
+                                              int kq, int col, const float (&sx)[4], const float (&sy)[4],
+                                              const float *ctr, f32x4_t (&acc)[Traits<FN, D>::U][4]) {
+    constexpr int U = Traits<FN, D>::U, RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    constexpr int HB = (B + 3) / 4 * 4;  // row head (mean, exponent coefficients, conic) in float4s
+    if (eb >= ee) return;
+    const int last = ee - 1;
+    const float one = 1.0f;
+    // software-pipelined: the next step group's rows and the one after's entries are in flight
+    // while a group is evaluated (each group otherwise starts with two dependent round trips)
+    auto load_ent = [&](int e, uint32_t (&en)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) en[t] = bins.entries[min(e + 4 * t + kq, last)];
+    };
+    auto load_rows = [&](const uint32_t (&en)[4], float (&h)[4][HB], float (&v)[4]) {
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            const float *row = grows + (int64_t)(en[t] & kIdMask) * RS;
+#pragma unroll
+            for (int k = 0; k < HB; k += 4) {
+                const float4 q = *reinterpret_cast<const float4 *>(row + k);
+                h[t][k] = q.x; h[t][k + 1] = q.y; h[t][k + 2] = q.z; h[t][k + 3] = q.w;
+            }
+            v[t] = (CB >= 16 || col < CB) ? row[B + (CB >= 16 ? col : min(col, CB - 1))] : 0.0f;
+        }
+    };
+    uint32_t ent[4], ent_n[4];
+    float hd[4][HB], vv[4];
+    load_ent(eb, ent);
+    load_rows(ent, hd, vv);
+    load_ent(eb + 16, ent_n);
+    for (int e0 = eb; e0 < ee; e0 += 16) {
+        float hd_n[4][HB], vv_n[4];
+        uint32_t ent_nn[4];
+        load_rows(ent_n, hd_n, vv_n);
+        load_ent(e0 + 32, ent_nn);
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+            bool act = e0 + 4 * t + kq < ee;
+            float sh[2] = {0.0f, 0.0f};
+            if constexpr (FLAGGED) {
+                act = act && !(ent[t] & kUnsafe);  // unsafe conics: the tail pass
+                if (act && (ent[t] & kGeneral)) {
+#pragma unroll
+                    for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(hd[t][d] - ctr[d]);
+                }
+            }
+            float c[3];
+            row_conic<FN, D, HB>(hd[t], c);
+            const float bv = act ? vv[t] : 0.0f;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                float X[2] = {hd[t][0] - sx[b], D == 2 ? hd[t][1] - sy[b] : 0.0f};
+                if constexpr (FLAGGED) {  // fl(m - s) - shift: exact (see fwd_t_pairs)
+                    X[0] = X[0] - sh[0];
+                    if constexpr (D == 2) X[1] = X[1] - sh[1];
+                }
+                const float G = fast_prob<D, float>(X, &hd[t][D]);
+                float tu[U][1];
+#pragma unroll
+                for (int u = 0; u < U; ++u) tu[u][0] = 0.0f;
+                fwd_terms<FN, D, 1, float>(X, c, G, &one, tu);
+#pragma unroll
+                for (int u = 0; u < U; ++u)
+                    acc[u][b] = __builtin_amdgcn_mfma_f32_16x16x4f32(act ? tu[u][0] : 0.0f, bv, acc[u][b], 0, 0, 0);
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+#pragma unroll
+            for (int k = 0; k < HB; ++k) hd[t][k] = hd_n[t][k];
+            vv[t] = vv_n[t];
+            ent[t] = ent_n[t];
+            ent_n[t] = ent_nn[t];
+        }
+    }
+}
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_forward_mx(const char *__restrict__ gbuf,
+                                                       const char *__restrict__ sbuf,
+                                                       const float *__restrict__ grows,
+                                                       const Outs outs, int C, int cbase,
+                                                       const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
+    constexpr int U = Traits<FN, D>::U;
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumFwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1), col = lane & 15, kq = lane >> 4;
+    const int nch = min(CB, C - cbase);
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+        const FwdUnit fu = fwd_unit_at(bins, unit);
+        float sx[4], sy[4];  // samples 16 b + col
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {  // samples outside the cell: a valid one (not stored)
+            int j = fu.sb + 16 * b + col;
+            j = (j >= fu.lo && j < fu.hi) ? j : fu.lo;
+            const float *pr = bins.fsrows + (int64_t)(j >> 1) * (2 * D) + (j & 1);
+            sx[b] = pr[0];
+            sy[b] = D == 2 ? pr[2] : 0.0f;
+        }
+        const int gb = sload(&bins.cell_gbeg[fu.cell]), ge = sload(&bins.cell_gend[fu.cell]);
+        const int gm = sload(&bins.cell_gmid[fu.cell]);
+        float ctr[2];
+        cell_center<D>(bins, fu.cell, ctr);
+        f32x4_t acc[U][4];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) acc[u][b] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+        fwd_mx_groups<FN, D, CB, false>(bins, grows, gb, gm, kq, col, sx, sy, ctr, acc);
+        if (gm < ge) fwd_mx_groups<FN, D, CB, true>(bins, grows, gm, ge, kq, col, sx, sy, ctr, acc);
+        if (col < nch) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int j = fu.sb + 16 * b + 4 * kq + r;
+                    if (j >= fu.lo && j < fu.hi) {
+                        const int64_t sid = bins.sorted_sid[j];
+#pragma unroll
+                        for (int u = 0; u < U; ++u) store_unique<FN, D, false>(outs, sid, u, C, cbase + col, acc[u][b][r]);
+                    }
+                }
+        }
+    }
+}
+
 // ------------------------------------------------------------------ backward kernel
 // MODE 0: fast path; 1: plus the lane's constant torus-wrap shift sh (kGeneral entries);
 // 2: the fully general per-pair path (some lane has a kUnsafe entry).
@@ -855,7 +1004,7 @@ static int run_forward(const Call &a) {
     float *grows = reinterpret_cast<float *>(a.ws);
     uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
-    constexpr bool T = fwd_transposed<FN, D, CB>();
+    constexpr bool T = fwd_transposed<FN, D, CB>(), MX = !T && fwd_mfma<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
     hint.nunsafe = -1;
     const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
@@ -871,12 +1020,14 @@ static int run_forward(const Call &a) {
             KernelTimer t(0, a.s);
             if constexpr (T)
                 k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
+            else if constexpr (MX)
+                k_forward_mx<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else
                 k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                           a.samples, a.outs, a.C, cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        if constexpr (T) {
+        if constexpr (T || MX) {
             if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
                 // (grid-strided over a capped grid: it exits at once when the device-side
                 // unsafe count is 0, which the host does not know without a sync)
