@@ -27,7 +27,6 @@
 // gradient is A^T dL over the rows' a (a second, small kernel); the neighbours' feature and
 // key gradients are scattered with float atomics as in the reference; the distance-transform
 // and frequency gradients are per-lane LDS partials, flushed once per wave.
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cmath>
@@ -36,6 +35,7 @@
 
 #include "dgs_internal.h"
 #include "dgs_render.h"
+#include "dgs_scan.h"
 
 namespace dgs {
 
@@ -1284,15 +1284,15 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     size_t tsort = 0, tscan = 0;
     int bits = 1;
     while (bits < 32 && (1u << bits) <= (uint32_t)ncells) ++bits;
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(nullptr, tsort, keys, keys_s, ids, ids_s, P, 0, bits, s));
-    DGS_TRY_HIP(hipcub::DeviceScan::InclusiveSum(nullptr, tscan, counts, ranges, P, s));
+    DGS_TRY_HIP(onesweep_pairs<uint32_t>(nullptr, tsort, keys, keys_s, ids, ids_s, (size_t)P, 0u, (unsigned)bits, s));
+    tscan = scan_scratch_bytes<int64_t>(P);
     size_t tb = std::max(tsort, tscan);
     void *tmp = scratch(tb);
     if (!tmp) return fail(DGS_ERR_ALLOC, "aggregate: scratch allocation failed");
 
     k_agg_keys<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, g, means, radii, keys, ids);
     DGS_LAUNCH_CHECK(s, debug);
-    DGS_TRY_HIP(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_s, ids, ids_s, P, 0, bits, s));
+    DGS_TRY_HIP(onesweep_pairs<uint32_t>(tmp, tb, keys, keys_s, ids, ids_s, (size_t)P, 0u, (unsigned)bits, s));
     k_agg_pack<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, D, ids_s, means, radii, cand);
     DGS_LAUNCH_CHECK(s, debug);
     k_agg_cell_start<<<agg_elem_blocks((int64_t)ncells + 1), kBlock, 0, s>>>(ncells, P, keys_s, cstart);
@@ -1300,8 +1300,8 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     const unsigned wblocks = agg_row_blocks(P);
     k_agg_count<<<wblocks, kBlock, 0, s>>>(P, g, means, radii, cand, cstart, ids_s, counts);
     DGS_LAUNCH_CHECK(s, debug);
-    tb = std::max(tsort, tscan);
-    DGS_TRY_HIP(hipcub::DeviceScan::InclusiveSum(tmp, tb, counts, ranges, P, s));
+    scan_excl<int64_t>(P, counts, ranges, nullptr, nullptr, static_cast<int64_t *>(tmp), s, true);
+    DGS_LAUNCH_CHECK(s, debug);
     int64_t len = 0;
     DGS_TRY_HIP(hipMemcpyAsync(&len, ranges + (P - 1), sizeof(len), hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));

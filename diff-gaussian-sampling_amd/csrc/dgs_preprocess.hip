@@ -13,7 +13,6 @@
 //   * samples sorted by fine cell, per-cell sample ranges, forward work units (cell, 64 samples)
 //   * Gaussians renumbered by spatial home cell (perm), per-cell Gaussian lists in ascending
 //     internal id, backward work units (cell, 64 list entries)
-#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 #include <cstdlib>
@@ -26,6 +25,7 @@
 #include <vector>
 
 #include "dgs_internal.h"
+#include "dgs_scan.h"
 
 namespace dgs {
 
@@ -718,19 +718,6 @@ static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) 
 // launches, ~170 us for the 1M home keys against ~25 us here).  Entry keys are u16 when every
 // (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per entry and pass).
 template <typename KT>
-static hipError_t onesweep_pairs(void *tmp, size_t &bytes, const KT *kin, KT *kout, const uint32_t *vin,
-                                 uint32_t *vout, size_t n, unsigned b0, unsigned b1, hipStream_t s) {
-    if (n == 0) {  // (rocprim's block-sort branch returns here)
-        if (tmp == nullptr) bytes = 4;
-        return hipSuccess;
-    }
-    bool in_output = true;
-    return rocprim::detail::radix_sort_onesweep_impl<rocprim::default_config, false>(
-        tmp, bytes, kin, static_cast<KT *>(nullptr), kout, vin, static_cast<uint32_t *>(nullptr), vout, n,
-        in_output, rocprim::identity_decomposer{}, b0, b1, s, false, false);
-}
-
-template <typename KT>
 static hipError_t sort_entries(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
                                const uint32_t *vin, uint32_t *vout, int64_t n, int bits, hipStream_t s) {
     return onesweep_pairs<KT>(tmp, bytes, reinterpret_cast<const KT *>(kin), reinterpret_cast<KT *>(kout), vin,
@@ -741,106 +728,6 @@ static hipError_t sort_pairs_onesweep(void *tmp, size_t &bytes, const uint32_t *
                                       const uint32_t *vin, uint32_t *vout, int n, int b0, int b1,
                                       hipStream_t s) {
     return onesweep_pairs<uint32_t>(tmp, bytes, kin, kout, vin, vout, (size_t)n, (unsigned)b0, (unsigned)b1, s);
-}
-
-// Exclusive prefix sums of one or two count arrays of length n: tile sums, one block scanning
-// them, then a downsweep (3 launches for both arrays).  Replaces hipcub::DeviceScan, whose ~210
-// kernel instantiations were a third of this code object.
-constexpr int kScanItems = 8, kScanTile = kBlock * kScanItems;
-
-static inline int64_t scan_tiles(int64_t n) { return (n + kScanTile - 1) / kScanTile; }
-template <typename T>
-static inline size_t scan_scratch_bytes(int64_t n) { return sizeof(T) * 2 * (size_t)std::max<int64_t>(scan_tiles(n), 1); }
-
-// exclusive scan of x over the block; total = the block's sum
-template <typename T>
-__device__ __forceinline__ T block_excl_scan(T x, T &total) {
-    __shared__ T wsum[kWavesPerBlock];
-    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-    T inc = x;
-#pragma unroll
-    for (int d = 1; d < kWave; d <<= 1) {
-        const T y = __shfl_up(inc, d, kWave);
-        if (lane >= d) inc += y;
-    }
-    if (lane == kWave - 1) wsum[w] = inc;
-    __syncthreads();
-    T pre = 0;
-    total = 0;
-#pragma unroll
-    for (int i = 0; i < kWavesPerBlock; ++i) {
-        if (i < w) pre += wsum[i];
-        total += wsum[i];
-    }
-    __syncthreads();
-    return pre + inc - x;
-}
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_scan_reduce(int64_t n, const T *__restrict__ a, const T *__restrict__ b,
-                                                        T *__restrict__ part) {
-    const int64_t base = (int64_t)blockIdx.x * kScanTile;
-    T sa = 0, sb = 0;
-#pragma unroll
-    for (int k = 0; k < kScanItems; ++k) {
-        const int64_t i = base + k * kBlock + threadIdx.x;
-        if (i < n) {
-            sa += a[i];
-            if (b) sb += b[i];
-        }
-    }
-    T ta, tb = 0;
-    (void)block_excl_scan(sa, ta);
-    if (b) (void)block_excl_scan(sb, tb);
-    if (threadIdx.x == 0) {
-        part[blockIdx.x] = ta;
-        if (b) part[gridDim.x + blockIdx.x] = tb;
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_scan_parts(int64_t nt, int arrays, T *__restrict__ part) {
-    for (int r = 0; r < arrays; ++r) {
-        T carry = 0;
-        for (int64_t c0 = 0; c0 < nt; c0 += kBlock) {
-            const int64_t i = c0 + threadIdx.x;
-            const T x = i < nt ? part[r * nt + i] : (T)0;
-            T tot;
-            const T e = block_excl_scan(x, tot);
-            if (i < nt) part[r * nt + i] = carry + e;
-            carry += tot;
-        }
-    }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kBlock) void k_scan_down(int64_t n, const T *__restrict__ a, T *__restrict__ ao,
-                                                      const T *__restrict__ b, T *__restrict__ bo,
-                                                      const T *__restrict__ part) {
-    const int64_t base = (int64_t)blockIdx.x * kScanTile;
-    for (int r = 0; r < (b ? 2 : 1); ++r) {
-        const T *in = r ? b : a;
-        T *out = r ? bo : ao;
-        T carry = part[r * (int64_t)gridDim.x + blockIdx.x];
-        for (int k = 0; k < kScanItems; ++k) {
-            const int64_t i = base + k * kBlock + threadIdx.x;
-            const T x = i < n ? in[i] : (T)0;
-            T tot;
-            const T e = block_excl_scan(x, tot);
-            if (i < n) out[i] = carry + e;
-            carry += tot;
-        }
-    }
-}
-
-// ao = exclusive scan of a, bo = of b (b may be null); part: scan_scratch_bytes<T>(n)
-template <typename T>
-static void scan_excl(int64_t n, const T *a, T *ao, const T *b, T *bo, T *part, hipStream_t s) {
-    if (n <= 0) return;
-    const int64_t nt = scan_tiles(n);
-    k_scan_reduce<T><<<(unsigned)nt, kBlock, 0, s>>>(n, a, b, part);
-    k_scan_parts<T><<<1, kBlock, 0, s>>>(nt, b ? 2 : 1, part);
-    k_scan_down<T><<<(unsigned)nt, kBlock, 0, s>>>(n, a, ao, b, bo, part);
 }
 
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
