@@ -494,6 +494,9 @@ __global__ __launch_bounds__(kBlock) void k_forward(const char *__restrict__ gbu
 // The Gaussian rows arrive by vector loads (a 16-lane group shares one row), so neither the
 // scalar cache's random-row rate (the lane-per-sample form's bound) nor a per-pass
 // re-walk of the list (the transposed form's) is paid.
+#ifndef DGS_QFORM
+#define DGS_QFORM 1
+#endif
 #ifndef DGS_FWD_MX
 #define DGS_FWD_MX 1
 #endif
@@ -649,6 +652,20 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
     if constexpr (MODE == 1) {
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
+    }
+    if constexpr (FN == 0 && D == 2 && CB == 1 && MODE != 2 && DGS_QFORM && DGS_VFACTOR) {
+        // gaussian, C = 1: the exponent from the quadratic monomials q = (X0^2, X0 X1, X1^2)
+        // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16
+        const V q0 = X[0] * X[0], q1 = X[0] * X[1], q2 = X[1] * X[1];
+        const V t = vexp2(vfma(bc<V>(kk[2]), q2, vfma(bc<V>(kk[1]), q1, kk[0] * q0))) * dl[0][0];
+        V *gm = acc, *gv = acc + 2, *gc = acc + 3;
+        gv[0] += t;
+        gm[0] = vfma(t, X[0], gm[0]);
+        gm[1] = vfma(t, X[1], gm[1]);
+        gc[0] = vfma(t, q0, gc[0]);
+        gc[1] = vfma(t, q1, gc[1]);
+        gc[2] = vfma(t, q2, gc[2]);
+        return;
     }
     V G;
     if constexpr (MODE == 2) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
