@@ -248,38 +248,157 @@ __device__ inline bool box_hits_ellipse(double xa, double xb, double ya, double 
     return best <= qcut * (1.0 + 1e-6) + 1e-12;
 }
 
+#ifndef DGS_CUT_EXACT
+#define DGS_CUT_EXACT 1
+#endif
+#if DGS_CUT_EXACT
+#define DGS_CUT_CONTRACT _Pragma("clang fp contract(off)")
+#else
+#define DGS_CUT_CONTRACT
+#endif
+// ---- the cut geometry of one Gaussian, shared by the per-Gaussian enumeration (enumerate_fine,
+// the sort path) and the per-cell gather (k_gather): both must take the same decisions bit for
+// bit, so these helpers run with contraction off.
+struct Cut {
+    double e[2], md[2], epsx[2], c0, c1, c2;
+    bool pd, cull;
+};
+
+__device__ inline Cut gauss_cut(const Geom &G, const float *m, const float *con) {
+    DGS_CUT_CONTRACT
+    const int D = G.D;
+    Cut k;
+    k.c0 = con[0];
+    k.c1 = D == 2 ? con[1] : 0.0;
+    k.c2 = D == 2 ? con[2] : 0.0;
+    k.e[0] = k.e[1] = INFINITY;
+    if (D == 1) {
+        k.pd = k.c0 > 0.0 && k.c0 < INFINITY;
+        if (k.pd) k.e[0] = sqrt(kQCut / k.c0) * (1.0 + 1e-6);
+    } else {
+        const double det = k.c0 * k.c2 - k.c1 * k.c1;
+        k.pd = k.c0 > 0.0 && det > 0.0 && det < INFINITY && k.c0 < INFINITY && k.c2 < INFINITY;
+        if (k.pd) {
+            k.e[0] = sqrt(kQCut * k.c2 / det) * (1.0 + 1e-6);
+            k.e[1] = sqrt(kQCut * k.c0 / det) * (1.0 + 1e-6);
+        }
+    }
+    k.cull = k.pd && k.e[0] < 0.5 && (D == 1 || k.e[1] < 0.5);
+    for (int d = 0; d < 2; ++d) {
+        k.md[d] = d < D ? (double)m[d] - (double)G.off[d] : 0.0;
+        k.epsx[d] = 1e-6 * (1.0 + fabs((double)m[d]) + fabs((double)G.off[d]));
+    }
+    return k;
+}
+
+// One axis of a tile visit: the torus shift ks and the fine-index range [flo, fhi] the cut can
+// reach in tile coordinate tcd; false if none.
+__device__ inline bool axis_setup(const Geom &G, const Cut &k, int d, int tcd, int &ks, int &flo, int &fhi) {
+    DGS_CUT_CONTRACT
+    ks = 0;
+    if (!k.cull) {
+        flo = 0;
+        fhi = G.n - 1;
+        return true;
+    }
+    const double BS = (double)kTile, slack = kCellSlack * G.fs;
+    const double o = tcd * BS;
+    const double xa = k.md[d] - (o + BS + slack) - k.epsx[d];
+    const double xb = k.md[d] - (o - slack) + k.epsx[d];
+    const double klo = ceil((xa - k.e[d]) * 0.5), khi = floor((xb + k.e[d]) * 0.5);
+    if (klo > khi) return false;
+    ks = (int)klo;  // e < 0.5 and a tile narrower than 1: at most one k
+    const double dl = k.md[d] - 2.0 * klo - k.e[d] - k.epsx[d];
+    const double dh = k.md[d] - 2.0 * klo + k.e[d] + k.epsx[d];
+    const int lo = (int)floor(fmax((dl - o) / G.fs - kCellSlack, -1.0));
+    const int hi = (int)floor(fmin((dh - o) / G.fs + kCellSlack, (double)G.n));
+    flo = lo < 0 ? 0 : lo;
+    fhi = hi > G.n - 1 ? G.n - 1 : hi;
+    return flo <= fhi;
+}
+
+// The row's cells that meet the ellipse X^T A X <= q (D = 2, culled): project the ellipse's
+// slice over the row's X1 band onto X0 (a slice of a convex set is convex, so "box meets
+// ellipse" <=> the cell's X0 range meets that interval).  Same margins as box_hits_ellipse,
+// widened slightly: an extra candidate only evaluates exact zeros.  row_slice gives the
+// interval [xl, xu] for fine row fy of tile row tc1 (false: the band misses the cut), row_cols
+// narrows [fxl, fxh] of tile column tc0 to it.
+__device__ inline bool row_slice(const Geom &G, const Cut &k, int tc1, int fy, int ks1, double &xl, double &xu,
+                                 double &tol) {
+    DGS_CUT_CONTRACT
+    const double BS = (double)kTile, slack = kCellSlack * G.fs;
+    const double o1 = tc1 * BS;
+    const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
+    double ya = k.md[1] - (o1 + (fy + 1) * G.fs + slack) - k.epsx[1] - 2.0 * ks1;
+    double yb = k.md[1] - (o1 + fy * G.fs - slack) + k.epsx[1] - 2.0 * ks1;
+    ya = fmax(ya, -k.e[1]);
+    yb = fmin(yb, k.e[1]);
+    if (ya > yb) return false;
+    const double c0 = k.c0, c1 = k.c1, c2 = k.c2;
+    const double det = c0 * c2 - c1 * c1;
+    const double e0 = sqrt(qc * c2 / det);
+    const double yu = fmin(fmax(-c1 * e0 / c2, ya), yb);  // argmax of the upper root
+    const double yl = fmin(fmax(c1 * e0 / c2, ya), yb);   // argmin of the lower root
+    xu = (-c1 * yu + sqrt(fmax(qc * c0 - det * yu * yu, 0.0))) / c0;
+    xl = (-c1 * yl - sqrt(fmax(qc * c0 - det * yl * yl, 0.0))) / c0;
+    tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
+    return true;
+}
+
+__device__ inline void row_cols(const Geom &G, const Cut &k, int tc0, int ks0, double xl, double xu, double tol,
+                                int &fxl, int &fxh) {
+    DGS_CUT_CONTRACT
+    const double slack = kCellSlack * G.fs;
+    const double o0 = tc0 * (double)kTile;
+    const double A = k.md[0] - o0 - slack - k.epsx[0] - 2.0 * ks0;
+    const double B = k.md[0] - o0 + slack + k.epsx[0] - 2.0 * ks0;
+    const double fa = ceil((A - (xu + tol)) / G.fs - 1.0 - 1e-9);
+    const double fb2 = floor((B - (xl - tol)) / G.fs + 1e-9);
+    if (fa > (double)fxl) fxl = fa > (double)G.n ? G.n : (int)fa;
+    if (fb2 < (double)fxh) fxh = fb2 < -1.0 ? -1 : (int)fb2;
+}
+
+// A tile visit is `local` when the cut reaches it unshifted (ks = 0) and stays well inside one
+// period, so every cell it meets holds |X| < 1 (no wrap, no sample-box test).
+__device__ inline bool visit_local(const Geom &G, const Cut &k, const int *ks) {
+    return k.cull && ks[0] == 0 && ks[1] == 0 && k.e[0] + 3.0 * G.fs < 0.9 &&
+           (G.D == 1 || k.e[1] + 3.0 * G.fs < 0.9);
+}
+
+// Gather-path Gaussians ("regular"): D = 2, culled, well-conditioned, its mean inside the fine
+// grid and its cut within kGatherReach fine cells of the mean's (home) cell.  Their local
+// entries are produced per cell by k_gather (no sort); everything else goes through the
+// per-Gaussian enumeration and the entry sort.  Returns the reach in cells, 0 if not regular.
+constexpr int kGatherReach = 6, kGatherRows = 2 * kGatherReach + 1;
+__device__ inline int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k) {
+    if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2])) return 0;
+    if (!(k.e[0] + 3.0 * G.fs < 0.9 && k.e[1] + 3.0 * G.fs < 0.9)) return 0;
+    // every tile visited at most once (a rect wider than the grid visits a tile repeatedly,
+    // which the enumeration reproduces entry by entry)
+    const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
+    if (kr.x1 - kr.x0 > G.grid[0] || kr.y1 - kr.y0 > G.grid[1]) return 0;
+    const int lim[2] = {G.grid[0] * G.n, G.grid[1] * G.n};
+    int reach = 0;
+    for (int d = 0; d < 2; ++d) {
+        const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
+        if (!(u >= 0.0 && u < (double)lim[d])) return 0;  // (the home cell is clamped)
+        reach = max(reach, (int)ceil(k.e[d] / G.fs + 2.0));
+    }
+    return reach <= kGatherReach ? reach : 0;
+}
+
 // Enumerate the fine entries (cell, id|flag) of one Gaussian, in the reference's tile-key
 // order (sampler_impl.cu:94-124), restricted to non-empty cells that pass the exact cull.
+// skip_local: leave out the cells of the direct local tile visits (a regular Gaussian's:
+// k_gather makes them).
 template <class Emit>
-__device__ inline void enumerate_fine(const Geom &G, const float *m, float r, const float *con,
-                                      const int32_t *__restrict__ sbeg,
+__device__ inline void enumerate_fine(const Geom &G, const float *m, float r, const float *con, const Cut &k,
+                                      bool skip_local, const int32_t *__restrict__ sbeg,
                                       const int32_t *__restrict__ send,
                                       const float4 *__restrict__ box, uint32_t id, Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
-    const double c0 = con[0], c1 = D == 2 ? con[1] : 0.0, c2 = D == 2 ? con[2] : 0.0;
-    double e[2] = {INFINITY, INFINITY};
-    bool pd;
-    if (D == 1) {
-        pd = c0 > 0.0 && c0 < INFINITY;
-        if (pd) e[0] = sqrt(kQCut / c0) * (1.0 + 1e-6);
-    } else {
-        const double det = c0 * c2 - c1 * c1;
-        pd = c0 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY;
-        if (pd) {
-            e[0] = sqrt(kQCut * c2 / det) * (1.0 + 1e-6);
-            e[1] = sqrt(kQCut * c0 / det) * (1.0 + 1e-6);
-        }
-    }
-    const bool cull = pd && e[0] < 0.5 && (D == 1 || e[1] < 0.5);
     const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
-    const double slack = kCellSlack * G.fs;
-    double md[2], epsx[2];
-    for (int d = 0; d < 2; ++d) {
-        md[d] = d < D ? (double)m[d] - (double)G.off[d] : 0.0;
-        epsx[d] = 1e-6 * (1.0 + fabs((double)m[d]) + fabs((double)G.off[d]));
-    }
-    const double BS = (double)kTile;
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             const uint32_t key = key_of(D, x, y, G.grid);
@@ -289,69 +408,31 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
             const uint32_t base = key * (uint32_t)G.CT;
             int flo[2] = {0, 0}, fhi[2] = {0, 0}, ks[2] = {0, 0};
             bool any = true;
-            for (int d = 0; d < D; ++d) {
-                const double o = tc[d] * BS;
-                if (!cull) {
-                    flo[d] = 0;
-                    fhi[d] = G.n - 1;
-                    continue;
-                }
-                const double xa = md[d] - (o + BS + slack) - epsx[d];
-                const double xb = md[d] - (o - slack) + epsx[d];
-                const double klo = ceil((xa - e[d]) * 0.5), khi = floor((xb + e[d]) * 0.5);
-                if (klo > khi) { any = false; break; }
-                ks[d] = (int)klo;  // e < 0.5 and a tile narrower than 1: at most one k
-                const double dl = md[d] - 2.0 * klo - e[d] - epsx[d];
-                const double dh = md[d] - 2.0 * klo + e[d] + epsx[d];
-                int lo = (int)floor(fmax((dl - o) / G.fs - kCellSlack, -1.0));
-                int hi = (int)floor(fmin((dh - o) / G.fs + kCellSlack, (double)G.n));
-                flo[d] = lo < 0 ? 0 : lo;
-                fhi[d] = hi > G.n - 1 ? G.n - 1 : hi;
-                if (flo[d] > fhi[d]) { any = false; break; }
-            }
-            const bool local = cull && ks[0] == 0 && ks[1] == 0 && e[0] + 3.0 * G.fs < 0.9 &&
-                               (D == 1 || e[1] + 3.0 * G.fs < 0.9);
-            if (any) {
+            for (int d = 0; d < D; ++d)
+                if (!axis_setup(G, k, d, tc[d], ks[d], flo[d], fhi[d])) { any = false; break; }
+            const bool local = visit_local(G, k, ks);
+            // (k_gather makes the direct -- unwrapped -- local visits of a regular Gaussian)
+            const bool direct = x >= 0 && x < G.grid[0] && (D == 1 || (y >= 0 && y < G.grid[1]));
+            if (any && !(skip_local && local && direct)) {
                 const int ylo = D == 2 ? flo[1] : 0, yhi = D == 2 ? fhi[1] : 0;
                 for (int fy = ylo; fy <= yhi; ++fy) {
                     int fxl = flo[0], fxh = fhi[0];
-                    if (cull && D == 2) {
-                        // The row's cells that meet the ellipse X^T A X <= q: project the
-                        // ellipse's slice over the row's X1 band onto X0 (a slice of a convex
-                        // set is convex, so "box meets ellipse" <=> the cell's X0 range meets
-                        // that interval).  Same margins as box_hits_ellipse, widened slightly:
-                        // an extra candidate only evaluates exact zeros.
-                        const double o1 = tc[1] * BS, o0 = tc[0] * BS;
-                        const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
-                        double ya = md[1] - (o1 + (fy + 1) * G.fs + slack) - epsx[1] - 2.0 * ks[1];
-                        double yb = md[1] - (o1 + fy * G.fs - slack) + epsx[1] - 2.0 * ks[1];
-                        ya = fmax(ya, -e[1]);
-                        yb = fmin(yb, e[1]);
-                        if (ya > yb) continue;
-                        const double det = c0 * c2 - c1 * c1;
-                        const double e0 = sqrt(qc * c2 / det);
-                        const double yu = fmin(fmax(-c1 * e0 / c2, ya), yb);  // argmax of the upper root
-                        const double yl = fmin(fmax(c1 * e0 / c2, ya), yb);   // argmin of the lower root
-                        const double xu = (-c1 * yu + sqrt(fmax(qc * c0 - det * yu * yu, 0.0))) / c0;
-                        const double xl = (-c1 * yl - sqrt(fmax(qc * c0 - det * yl * yl, 0.0))) / c0;
-                        const double tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
-                        const double A = md[0] - o0 - slack - epsx[0] - 2.0 * ks[0];
-                        const double B = md[0] - o0 + slack + epsx[0] - 2.0 * ks[0];
-                        const double fa = ceil((A - (xu + tol)) / G.fs - 1.0 - 1e-9);
-                        const double fb2 = floor((B - (xl - tol)) / G.fs + 1e-9);
-                        if (fa > (double)fxl) fxl = fa > (double)G.n ? G.n : (int)fa;
-                        if (fb2 < (double)fxh) fxh = fb2 < -1.0 ? -1 : (int)fb2;
+                    if (k.cull && D == 2) {
+                        double xl, xu, tol;
+                        if (!row_slice(G, k, tc[1], fy, ks[1], xl, xu, tol)) continue;
+                        row_cols(G, k, tc[0], ks[0], xl, xu, tol, fxl, fxh);
                     }
                     for (int fx = fxl; fx <= fxh; ++fx) {
                         const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
                         // (empty cells get no units, so an entry there is never read: only
                         // the box-classified cells need the two loads of this test)
                         if (!local && send[cell] <= sbeg[cell]) continue;
-                        if (cull && D == 1) {
-                            const double o = tc[0] * BS;
+                        if (k.cull && D == 1) {
+                            const double slack = kCellSlack * G.fs;
+                            const double o = tc[0] * (double)kTile;
                             const double dlo = o + fx * G.fs - slack, dhi = o + (fx + 1) * G.fs + slack;
-                            const double xa = md[0] - dhi - epsx[0], xb = md[0] - dlo + epsx[0];
-                            if (!(xa - 2.0 * ks[0] <= e[0] && xb - 2.0 * ks[0] >= -e[0])) continue;
+                            const double xa = k.md[0] - dhi - k.epsx[0], xb = k.md[0] - dlo + k.epsx[0];
+                            if (!(xa - 2.0 * ks[0] <= k.e[0] && xb - 2.0 * ks[0] >= -k.e[0])) continue;
                         }
                         // Wrap class from the cell's actual samples (box = their bounding box;
                         // the nominal cell may reach past the last sample): kGeneral when some
@@ -380,6 +461,54 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
             const uint32_t fb = base + (uint32_t)(G.CT - 1);
             if (send[fb] > sbeg[fb]) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
         }
+}
+
+// Global fine cell (gx, gy) -> cell id (tile-major: tile * CT + fy * n + fx).
+__device__ inline uint32_t cell_of(const Geom &G, int gx, int gy) {
+    const int tx = gx / G.n, ty = gy / G.n;
+    return (uint32_t)(ty * G.grid[0] + tx) * (uint32_t)G.CT + (uint32_t)((gy - ty * G.n) * G.n + (gx - tx * G.n));
+}
+
+// The cells a regular Gaussian's direct local tile visits emit (exactly those enumerate_fine
+// skips for it), written as one global column range per global fine row: lrows[KR + dy][i] for
+// row home_y + dy (|dy| <= reach), packed lo | hi << 16 (lo > hi: none).  Rows are walked in
+// order, each row's tiles in turn, so a row's range is merged in registers and stored once.
+// False if some row's cells are not one range (never for a convex cut; the Gaussian then stays
+// on the sort path).
+__device__ inline bool local_rows(const Geom &G, const float *m, float r, const Cut &k, int home_y, int reach,
+                                  int64_t P, int64_t i, uint32_t *__restrict__ lrows) {
+    const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
+    const int tx0 = max(kr.x0, 0), tx1 = min(kr.x1, G.grid[0]);
+    uint32_t written = 0u;  // bit KR + dy: row home_y + dy stored
+    for (int ty = max(kr.y0, 0); ty < min(kr.y1, G.grid[1]); ++ty) {  // direct visits only
+        int ks1, flo1, fhi1;
+        if (!axis_setup(G, k, 1, ty, ks1, flo1, fhi1) || ks1 != 0) continue;
+        for (int fy = flo1; fy <= fhi1; ++fy) {
+            double xl, xu, tol;
+            if (!row_slice(G, k, ty, fy, 0, xl, xu, tol)) continue;
+            int lo = 0xffff, hi = 0;
+            for (int tx = tx0; tx < tx1; ++tx) {
+                int ks[2] = {0, 0}, flo0, fhi0;
+                if (!axis_setup(G, k, 0, tx, ks[0], flo0, fhi0) || !visit_local(G, k, ks)) continue;
+                int fxl = flo0, fxh = fhi0;
+                row_cols(G, k, tx, 0, xl, xu, tol, fxl, fxh);
+                if (fxl > fxh) continue;
+                const int a = tx * G.n + fxl, b = tx * G.n + fxh;
+                if (lo > hi) { lo = a; hi = b; }
+                else if (a == hi + 1) hi = b;
+                else if (b + 1 == lo) lo = a;
+                else return false;
+            }
+            if (lo > hi) continue;
+            const int dy = ty * G.n + fy - home_y;
+            if (dy < -reach || dy > reach) return false;
+            lrows[(int64_t)(kGatherReach + dy) * P + i] = (uint32_t)lo | ((uint32_t)hi << 16);
+            written |= 1u << (kGatherReach + dy);
+        }
+    }
+    for (int q = kGatherReach - reach; q <= kGatherReach + reach; ++q)
+        if (!((written >> q) & 1u)) lrows[(int64_t)q * P + i] = 0x0000ffffu;
+    return true;
 }
 
 __device__ inline void load_gauss(int D, const float *__restrict__ means,
@@ -422,23 +551,38 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const in
     if (lane == 0) box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
 }
 
-// Number of fine entries of each Gaussian (k_fine_fill writes them).
-__global__ void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
-                             const float *__restrict__ means, const float *__restrict__ conics,
-                             const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
-                             const int32_t *__restrict__ send, const float4 *__restrict__ box,
-                             uint64_t *__restrict__ counts) {
+// Number of sort-path fine entries of each Gaussian (k_fine_fill writes them).  For the regular
+// (gather-path) Gaussians also their reach and local row ranges (k_gather reads them as
+// lrows[KR + dy][i]: coalesced over the contiguous id range of a home row), and the largest reach.
+__global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
+                                                       const float *__restrict__ means, const float *__restrict__ conics,
+                                                       const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+                                                       const int32_t *__restrict__ send, const float4 *__restrict__ box,
+                                                       uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
+                                                       uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const int64_t g = perm[i];
-    const float r = radii[g];
-    uint64_t n = 0;
-    if (r > 0.0f) {
-        float m[2], c[3];
-        load_gauss(G.D, means, conics, g, m, c);
-        enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t, uint32_t) { ++n; });
+    int reach = 0;
+    if (i < P) {
+        const int64_t g = perm[i];
+        const float r = radii[g];
+        uint64_t n = 0;
+        if (r > 0.0f) {
+            float m[2], c[3];
+            load_gauss(G.D, means, conics, g, m, c);
+            const Cut k = gauss_cut(G, m, c);
+            reach = gather_reach(G, m, r, c, k);
+            if (reach > 0) {
+                const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) / G.fs);
+                if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
+            }
+            enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, (uint32_t)i,
+                           [&](uint32_t, uint32_t) { ++n; });
+        }
+        counts[i] = n;
+        greach[i] = (int8_t)reach;
     }
-    counts[i] = n;
+    for (int off = kWave / 2; off > 0; off >>= 1) reach = max(reach, __shfl_xor(reach, off));
+    if ((threadIdx.x & (kWave - 1)) == 0 && reach > 0) atomicMax(rmax, reach);
 }
 
 // The block's Gaussians own one contiguous output range (offs is an exclusive scan in i
@@ -453,8 +597,8 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     int P, Geom G, const uint32_t *__restrict__ perm, const float *__restrict__ means,
     const float *__restrict__ conics, const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
-    const uint64_t *__restrict__ cnts, KT *__restrict__ ekeys, uint32_t *__restrict__ evals,
-    int32_t *__restrict__ counters) {
+    const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, KT *__restrict__ ekeys,
+    uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
     const int64_t i = i0 + threadIdx.x;
@@ -462,26 +606,26 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     const uint64_t base = offs[i0], end = offs[ilast] + cnts[ilast];
     const bool stage = end - base <= (uint64_t)kFillCap;
     uint32_t nunsafe = 0;
-    if (i < P) {
+    if (i < P && cnts[i] > 0) {
         const int64_t g = perm[i];
         const float r = radii[g];
-        if (r > 0.0f) {
-            float m[2], c[3];
-            load_gauss(G.D, means, conics, g, m, c);
-            uint64_t o = offs[i];
-            enumerate_fine(G, m, r, c, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
-                const uint32_t key = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
-                if (stage) {
-                    skey[o - base] = key;
-                    sval[o - base] = val;
-                } else {
-                    ekeys[o] = (KT)key;
-                    evals[o] = val;
-                }
-                nunsafe += (val & kUnsafe) ? 1u : 0u;
-                ++o;
-            });
-        }
+        float m[2], c[3];
+        load_gauss(G.D, means, conics, g, m, c);
+        const Cut k = gauss_cut(G, m, c);
+        const bool skip = greach[i] > 0;  // (k_fine_count's decision)
+        uint64_t o = offs[i];
+        enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
+            const uint32_t key = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
+            if (stage) {
+                skey[o - base] = key;
+                sval[o - base] = val;
+            } else {
+                ekeys[o] = (KT)key;
+                evals[o] = val;
+            }
+            nunsafe += (val & kUnsafe) ? 1u : 0u;
+            ++o;
+        });
     }
     if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
     if (stage) {
@@ -494,27 +638,149 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     }
 }
 
-// Half-cell ranges (key = cell << 1 | flagged) -> per-cell [gbeg, gmid, gend).
-__global__ void k_cell_ranges(int ncells, const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
-                              int32_t *__restrict__ gbeg, int32_t *__restrict__ gmid,
-                              int32_t *__restrict__ gend) {
+// hstart[h] = first internal id whose home cell is >= h (lower bound in the sorted home keys),
+// h in [0, HK]; home cell h's Gaussians are ids [hstart[h], hstart[h + 1]).
+__global__ void k_home_start(int P, int HK, const uint32_t *__restrict__ home_sorted, uint32_t *__restrict__ hstart) {
+    const int h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h > HK) return;
+    int lo = 0, hi = P;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (home_sorted[mid] < (uint32_t)h) lo = mid + 1;
+        else hi = mid;
+    }
+    hstart[h] = (uint32_t)lo;
+}
+
+// Per-cell gather of the regular Gaussians' local entries (D = 2): one wave per (strip of
+// kStripW cells of a global fine row gy, home row offset dy).  Its candidates are the Gaussians
+// homed in row gy - dy within the largest reach R of the strip -- one contiguous id range, read
+// in ascending id with their precomputed column ranges for row gy (lrows).  !FILL: count per
+// (cell, dy) and in total (eg); FILL: write them, home rows in ascending order (dy descending)
+// after each other, so every cell's gathered entries are in ascending id (the backward's atomics
+// need that order) with no sort.
+constexpr int kStripW = 32;
+template <bool FILL>
+__global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *__restrict__ greach,
+                                                   const uint32_t *__restrict__ lrows,
+                                                   const uint32_t *__restrict__ hstart,
+                                                   const int32_t *__restrict__ rmax, uint32_t *__restrict__ cnt2,
+                                                   unsigned long long *__restrict__ eg,
+                                                   const int32_t *__restrict__ gbeg, uint32_t *__restrict__ entries) {
+    const int home_w = G.grid[0] * G.n, home_h = G.grid[1] * G.n;
+    const int spr = (home_w + kStripW - 1) / kStripW;
+    const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
+    const int strip = wid / kGatherRows, q = wid - strip * kGatherRows, dy = q - kGatherReach;
+    if (strip >= home_h * spr) return;
+    const int R = sload(rmax);
+    const int gy = strip / spr, gx0 = (strip - gy * spr) * kStripW, nw = min(kStripW, home_w - gx0);
+    const int hy = gy - dy;
+    if (dy < -R || dy > R || hy < 0 || hy >= home_h) return;  // (cnt2 stays 0 there)
+    const int lane = threadIdx.x & (kWave - 1);
+    // lane j < nw keeps cell gx0 + j's cursor (FILL: its next slot; else its count)
+    uint32_t cur = 0;
+    if (FILL && lane < nw) {
+        const uint32_t c = cell_of(G, gx0 + lane, gy);
+        cur = (uint32_t)gbeg[c];
+        for (int q2 = q + 1; q2 < kGatherRows; ++q2) cur += cnt2[(int64_t)c * kGatherRows + q2];  // lower home rows
+    }
+    const int clo = max(gx0 - R, 0), chi = min(gx0 + nw - 1 + R, home_w - 1);
+    const uint32_t ib = sload(&hstart[hy * home_w + clo]), ie = sload(&hstart[hy * home_w + chi + 1]);
+    const int ady = dy < 0 ? -dy : dy;
+    const uint32_t *__restrict__ lq = lrows + (int64_t)q * P;
+    // the next chunk's reach and row range are loaded while a chunk is processed (both at once:
+    // a row range past the Gaussian's reach is never used, only read)
+    int rch_n = 0;
+    uint32_t rr_n = 0u;
+    if (ib + lane < ie) { rch_n = greach[ib + lane]; rr_n = lq[ib + lane]; }
+    for (uint32_t i0 = ib; i0 < ie; i0 += kWave) {
+        const uint32_t i = i0 + lane;
+        const int rch = rch_n;
+        const uint32_t rr = rr_n;
+        if (i + kWave < ie) { rch_n = greach[i + kWave]; rr_n = lq[i + kWave]; }
+        uint32_t mask = 0u;
+        if (i < ie && rch >= ady && rch > 0) {
+            const int a = max((int)(rr & 0xffffu), gx0) - gx0, b = min((int)(rr >> 16), gx0 + nw - 1) - gx0;
+            if (a <= b) mask = (b >= 31 ? 0xffffffffu : ((2u << b) - 1u)) & ~((1u << a) - 1u);
+        }
+        uint32_t any = mask;
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) any |= __shfl_xor(any, off);
+        any = __builtin_amdgcn_readfirstlane(any);
+        while (any) {
+            const int j = __builtin_ctz(any);
+            any &= any - 1u;
+            const bool hit = (mask >> j) & 1u;
+            const uint64_t bal = __ballot(hit);
+            if (FILL) {
+                const uint32_t base = __builtin_amdgcn_readlane(cur, j);
+                const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
+                                                                __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+                if (hit) entries[base + rank] = i;
+            }
+            if (lane == j) cur += (uint32_t)__popcll(bal);
+        }
+    }
+    if (!FILL) {
+        if (lane < nw) cnt2[(int64_t)cell_of(G, gx0 + lane, gy) * kGatherRows + q] = cur;
+        unsigned long long t = lane < nw ? cur : 0u;
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if (lane == 0 && t) atomicAdd(eg, t);
+    }
+}
+
+// Final per-cell list sizes: the gathered entries, then the sorted path's unflagged and flagged
+// half-cells (hb/he over the sorted keys cell << 1 | flag).
+__global__ void k_cell_tot(int ncells, const uint32_t *__restrict__ cnt2, const int32_t *__restrict__ hb,
+                           const int32_t *__restrict__ he, uint32_t *__restrict__ gcnt, uint32_t *__restrict__ tot) {
     const int c = blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= ncells) return;
-    const int fb = hb[2 * c], fe = he[2 * c], sb = hb[2 * c + 1], se = he[2 * c + 1];
-    const bool fast = fe > fb, slow = se > sb;
-    const int b = fast ? fb : (slow ? sb : 0);
+    uint32_t g = 0;
+    for (int q = 0; q < kGatherRows; ++q) g += cnt2[(int64_t)c * kGatherRows + q];
+    gcnt[c] = g;
+    tot[c] = g + (uint32_t)(he[2 * c] - hb[2 * c]) + (uint32_t)(he[2 * c + 1] - hb[2 * c + 1]);
+}
+
+// [gbeg, gmid, gend) of each cell from the scanned sizes: gathered + unflagged, then flagged.
+__global__ void k_cell_layout(int ncells, const uint32_t *__restrict__ gcnt, const int32_t *__restrict__ hb,
+                              const int32_t *__restrict__ he, const uint32_t *__restrict__ coff,
+                              int32_t *__restrict__ gbeg, int32_t *__restrict__ gmid, int32_t *__restrict__ gend) {
+    const int c = blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncells) return;
+    const int32_t b = (int32_t)coff[c];
+    const int32_t mid = b + (int32_t)gcnt[c] + (he[2 * c] - hb[2 * c]);
     gbeg[c] = b;
-    gmid[c] = fast ? fe : b;
-    gend[c] = slow ? se : (fast ? fe : 0);
+    gmid[c] = mid;
+    gend[c] = mid + (he[2 * c + 1] - hb[2 * c + 1]);
+}
+
+// The sorted path's half-cells copied behind each cell's gathered entries (one wave per cell).
+__global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32_t *__restrict__ gcnt,
+                                                        const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
+                                                        const int32_t *__restrict__ gbeg,
+                                                        const int32_t *__restrict__ gmid,
+                                                        const uint32_t *__restrict__ svals,
+                                                        uint32_t *__restrict__ entries) {
+    const int c = blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
+    if (c >= ncells) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int32_t u0 = hb[2 * c], u1 = he[2 * c], f0 = hb[2 * c + 1], f1 = he[2 * c + 1];
+    const int32_t du = gbeg[c] + (int32_t)gcnt[c], df = gmid[c];
+    for (int32_t k = lane; k < u1 - u0; k += kWave) entries[du + k] = svals[u0 + k];
+    for (int32_t k = lane; k < f1 - f0; k += kWave) entries[df + k] = svals[f0 + k];
 }
 
 __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
                          const uint64_t *__restrict__ toffs, const uint64_t *__restrict__ touched,
                          const int *__restrict__ dgrid, const float *__restrict__ doff,
-                         int64_t *__restrict__ out) {
+                         const unsigned long long *__restrict__ eg, int64_t *__restrict__ out) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     out[0] = P > 0 ? (int64_t)(toffs[P - 1] + touched[P - 1]) : 0;  // num_rendered (sampler_impl.cu:253-257)
-    out[1] = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;
+    const int64_t es = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;  // sort-path entries
+    out[1] = es + (int64_t)*eg;                                             // all entries
+    out[4] = es;
+    out[5] = (int64_t)*eg;
     // the device-computed tile grid (dgs_preprocess_auto): read back with the totals
     int32_t *g = reinterpret_cast<int32_t *>(out + 2);
     g[0] = dgrid ? dgrid[0] : 0;
@@ -688,11 +954,12 @@ __global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, cons
     for (int f = 0; f < D; ++f) row[2 * f] = s[f];
 }
 
-// Zero-fills up to 8 word-aligned regions in one launch (each hipMemsetAsync is a launch of its
-// own, ~5 us of GPU time even for a few bytes; the binning needed ten).
+// Zero-fills up to kZeroMax word-aligned regions in one launch (each hipMemsetAsync is a launch
+// of its own, ~5 us of GPU time even for a few bytes; the binning needs eleven).
+constexpr int kZeroMax = 12;
 struct ZeroSpec {
-    uint32_t *p[8];
-    int64_t n[8];  // words
+    uint32_t *p[kZeroMax];
+    int64_t n[kZeroMax];  // words
     int count;
 };
 
@@ -704,8 +971,17 @@ __global__ void k_zero_multi(ZeroSpec z) {
 
 struct ZeroList {
     ZeroSpec z{};
-    void add(void *p, size_t bytes) { z.p[z.count] = static_cast<uint32_t *>(p); z.n[z.count++] = (int64_t)(bytes / 4); }
-    void launch(hipStream_t s) { k_zero_multi<<<256, 256, 0, s>>>(z); }
+    bool overflow = false;
+    void add(void *p, size_t bytes) {
+        if (z.count >= kZeroMax) { overflow = true; return; }
+        z.p[z.count] = static_cast<uint32_t *>(p);
+        z.n[z.count++] = (int64_t)(bytes / 4);
+    }
+    hipError_t launch(hipStream_t s) {
+        if (overflow) return hipErrorInvalidValue;  // (a programming error: raise kZeroMax)
+        k_zero_multi<<<256, 256, 0, s>>>(z);
+        return hipGetLastError();
+    }
 };
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
@@ -944,7 +1220,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *perm = ca.take<uint32_t>(P);
     uint64_t *touched = ca.take<uint64_t>(P), *fcount = ca.take<uint64_t>(P), *foffs = ca.take<uint64_t>(P);
     uint64_t *toffs = ca.take<uint64_t>(P);
-    int64_t *totals = ca.take<int64_t>(4);
+    int64_t *totals = ca.take<int64_t>(6);
+    const int HK = home_w * home_h;  // (home cell keys; HK = absent)
+    int8_t *greach = ca.take<int8_t>(P);
+    uint32_t *lrows = ca.take<uint32_t>((size_t)kGatherRows * P);
+    uint32_t *hstart = ca.take<uint32_t>((size_t)HK + 1), *gcnt = ca.take<uint32_t>(ncells);
+    uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
+    unsigned long long *eg = ca.take<unsigned long long>(1);
+    int32_t *rmax = ca.take<int32_t>(1);
 
     // sort / scan temp storage: one piece sized for the largest phase-A primitive
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
@@ -964,6 +1247,13 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             Carve::rebase(*q, base);
         for (uint64_t **q : {&touched, &fcount, &foffs, &toffs}) Carve::rebase(*q, base);
         Carve::rebase(totals, base);
+        Carve::rebase(greach, base);
+        Carve::rebase(lrows, base);
+        Carve::rebase(cnt2, base);
+        Carve::rebase(hstart, base);
+        Carve::rebase(gcnt, base);
+        Carve::rebase(eg, base);
+        Carve::rebase(rmax, base);
         char *t = static_cast<char *>(tmp_a);
         Carve::rebase(t, base);
         tmp_a = t;
@@ -980,7 +1270,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(reinterpret_cast<char *>(fsrows) + fs_written, fsrows_bytes(N, D) - fs_written);
         zl.add(rbuf, (size_t)G.T * 8 + 8);
         zl.add(srbuf, (size_t)G.T * 8 + 8);
-        zl.launch(s);
+        zl.add(cnt2, sizeof(uint32_t) * kGatherRows * (size_t)ncells);
+        zl.add(eg, 8);
+        zl.add(rmax, 4);
+        DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
     }
 
@@ -1007,11 +1300,19 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                cell_send, cell_box, fcount);
+                                                cell_send, cell_box, fcount, greach, lrows, rmax);
     DGS_LAUNCH_CHECK(s, debug);
+    const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
+                                               kWavesPerBlock - 1) / kWavesPerBlock);
+    if (D == 2) {  // the regular Gaussians' local entries, per cell (k_gather)
+        k_home_start<<<grid_for((int64_t)HK + 1), kBlock, 0, s>>>(P, HK, home_sorted, hstart);
+        DGS_LAUNCH_CHECK(s, debug);
+        k_gather<false><<<gather_blocks, kBlock, 0, s>>>(G, P, greach, lrows, hstart, rmax, cnt2, eg, nullptr, nullptr);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     scan_excl<uint64_t>(P, fcount, foffs, touched, toffs, static_cast<uint64_t *>(tmp_a), s);
     DGS_LAUNCH_CHECK(s, debug);
-    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, dgrid, doff, totals);
+    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, dgrid, doff, eg, totals);
     DGS_LAUNCH_CHECK(s, debug);
     // ---- Gaussian-side buffer and phase-B scratch for capacities (Ecap, Rcap).  Set up BEFORE
     // the host sync with the previous call's sizes (+1/8) when known, so the allocations and the
@@ -1021,7 +1322,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int64_t Ecap = -1, Rcap = -1, bwd_cap = 0;
         Layout L;
         char *gbuf = nullptr;
-        uint32_t *ekeys, *evals, *ekeys_sorted, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
+        uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
@@ -1037,31 +1338,30 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         if (!B.gbuf) return fail(DGS_ERR_ALLOC, "binning buffer allocation failed");
         Carve cb;
         B.ekeys = cb.take<uint32_t>(Ecap + 1); B.evals = cb.take<uint32_t>(Ecap + 1);
-        B.ekeys_sorted = cb.take<uint32_t>(Ecap + 1);
+        B.ekeys_sorted = cb.take<uint32_t>(Ecap + 1); B.svals = cb.take<uint32_t>(Ecap + 1);
         B.fcnt = cb.take<uint32_t>(ncells); B.bcnt = cb.take<uint32_t>(ncells);
         B.hbeg = cb.take<int32_t>(2 * (size_t)ncells); B.hend = cb.take<int32_t>(2 * (size_t)ncells);
         B.foff = cb.take<uint32_t>(ncells); B.boff = cb.take<uint32_t>(ncells);
         B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
         B.rvals = cb.take<uint32_t>(Rcap + 1);
         uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
-        uint32_t *entries = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_entries);
         size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
         B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
         DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_rsort, B.rkeys, B.rkeys_sorted, B.rvals, rlist, (int)Rcap, 0,
                                         B.rbits, s));
         B.ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
         B.k16 = B.ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
-        DGS_TRY_HIP(B.k16 ? sort_entries<uint16_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, entries, Ecap,
+        DGS_TRY_HIP(B.k16 ? sort_entries<uint16_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s)
-                          : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, entries, Ecap,
+                          : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s));
         t_cscan = scan_scratch_bytes<uint32_t>(ncells);
         B.t_b = std::max(std::max(t_esort, t_cscan), t_rsort);
         B.tmp_b = cb.take<char>(B.t_b);
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
-        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.fcnt, &B.bcnt, &B.foff, &B.boff, &B.rkeys,
-                             &B.rkeys_sorted, &B.rvals})
+        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.fcnt, &B.bcnt, &B.foff, &B.boff,
+                             &B.rkeys, &B.rkeys_sorted, &B.rvals})
             Carve::rebase(*q, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
@@ -1072,7 +1372,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.gbuf + B.L.o_counts, 16);
         zl.add(B.hbeg, sizeof(int32_t) * 2 * (size_t)ncells);
         zl.add(B.hend, sizeof(int32_t) * 2 * (size_t)ncells);
-        zl.launch(s);
+        DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
         k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
                                                   reinterpret_cast<float2 *>(B.gbuf + B.L.o_gmean),
@@ -1081,7 +1381,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
-    int64_t htot[4] = {0, 0, 0, 0};
+    int64_t htot[6] = {0, 0, 0, 0, 0, 0};
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
     // the one host sync (num_rendered is a Python int): on an event right after the copy, so the
     // speculative phase B enqueued behind it keeps the GPU busy while the host reads the totals
@@ -1099,7 +1399,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         if (rc) return rc;
     }
     DGS_TRY_HIP(hipEventSynchronize(copied));
-    const int64_t R = htot[0], E = htot[1];
+    const int64_t R = htot[0], E = htot[1], Es = htot[4];
     *num_rendered = R;
     if (dev_grid) {
         const int32_t *g = reinterpret_cast<const int32_t *>(htot + 2);
@@ -1124,7 +1424,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     int32_t *cell_gend = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gend);
     uint32_t *entries = reinterpret_cast<uint32_t *>(gbuf + L.o_entries);
     uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
-    uint32_t *ekeys = B.ekeys, *evals = B.evals, *ekeys_sorted = B.ekeys_sorted;
+    uint32_t *ekeys = B.ekeys, *evals = B.evals, *ekeys_sorted = B.ekeys_sorted, *svals = B.svals;
     uint32_t *fcnt = B.fcnt, *bcnt = B.bcnt, *foff = B.foff, *boff = B.boff;
     uint32_t *rkeys = B.rkeys, *rkeys_sorted = B.rkeys_sorted, *rvals = B.rvals;
     int32_t *hbeg = B.hbeg, *hend = B.hend;
@@ -1134,29 +1434,45 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     const bool k16 = B.k16;
     const int ebits = B.ebits, rbits = B.rbits;
 
-    if (E > 0) {
+    // ---- cell lists: the sort path's entries (sorted by (cell, flag)), then per cell the
+    // gathered local entries (ascending id), the sorted unflagged and the flagged ones
+    if (Es > 0) {
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
         if (k16)
             k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
-                                                            cell_box, foffs, fcount,
+                                                            cell_box, foffs, fcount, greach,
                                                             reinterpret_cast<uint16_t *>(ekeys), evals, counters);
         else
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
-                                                            cell_box, foffs, fcount, ekeys, evals, counters);
+                                                            cell_box, foffs, fcount, greach, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = t_b;
-        DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s)
-                        : sort_entries<uint32_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, entries, E, ebits, s));
+        DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, svals, Es, ebits, s)
+                        : sort_entries<uint32_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, svals, Es, ebits, s));
         DGS_LAUNCH_CHECK(s, debug);
         if (k16)
-            k_identify<uint16_t><<<grid_for(E), kBlock, 0, s>>>(E, reinterpret_cast<const uint16_t *>(ekeys_sorted),
-                                                                2u * (uint32_t)ncells, hbeg, hend, 0);
+            k_identify<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(Es, reinterpret_cast<const uint16_t *>(ekeys_sorted),
+                                                                 2u * (uint32_t)ncells, hbeg, hend, 0);
         else
-            k_identify<uint32_t><<<grid_for(E), kBlock, 0, s>>>(E, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
+            k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    k_cell_ranges<<<grid_for(ncells), kBlock, 0, s>>>(ncells, hbeg, hend, cell_gbeg, cell_gmid, cell_gend);
+    k_cell_tot<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cnt2, hbeg, hend, gcnt, fcnt);
     DGS_LAUNCH_CHECK(s, debug);
+    scan_excl<uint32_t>(ncells, fcnt, foff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_cell_layout<<<grid_for(ncells), kBlock, 0, s>>>(ncells, gcnt, hbeg, hend, foff, cell_gbeg, cell_gmid, cell_gend);
+    DGS_LAUNCH_CHECK(s, debug);
+    if (D == 2 && E > Es) {
+        k_gather<true><<<gather_blocks, kBlock, 0, s>>>(G, P, greach, lrows, hstart, rmax, cnt2, nullptr, cell_gbeg,
+                                                        entries);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
+    if (Es > 0) {
+        k_copy_sorted<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
+            ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, entries);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
                                                       cell_gend, fcnt, bcnt);
     DGS_LAUNCH_CHECK(s, debug);
