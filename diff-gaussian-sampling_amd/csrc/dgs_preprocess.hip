@@ -477,26 +477,58 @@ __device__ inline uint32_t cell_of(const Geom &G, int gx, int gy) {
 // on the sort path).
 __device__ inline bool local_rows(const Geom &G, const float *m, float r, const Cut &k, int home_y, int reach,
                                   int64_t P, int64_t i, uint32_t *__restrict__ lrows) {
+    // Per Gaussian: the x tiles its cut can reach as a direct local visit (at most two: the cut is
+    // narrower than a tile) with their cell ranges, and the slice constants.  These need not
+    // match enumerate_fine bit for bit (it skips exactly these visits and emits all others); the
+    // margins of the cut cover the rounding either way.
     const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
-    const int tx0 = max(kr.x0, 0), tx1 = min(kr.x1, G.grid[0]);
+    const double BS = (double)kTile, slack = kCellSlack * G.fs, ifs = 1.0 / G.fs;
+    // (widened by a cell: every tile axis_setup can give a cell is among them)
+    const double wx = k.e[0] + slack + k.epsx[0] + G.fs;
+    const int ta = max(max(kr.x0, 0), (int)floor((k.md[0] - wx) / BS));
+    const int tb = min(min(kr.x1, G.grid[0]) - 1, (int)floor((k.md[0] + wx) / BS));
+    int xlo[2] = {1, 1}, xhi[2] = {0, 0};  // cell ranges of tiles ta, ta + 1 (empty: lo > hi)
+    for (int t = 0; t < 2; ++t) {
+        const int tx = ta + t;
+        if (tx > tb) break;
+        int ks[2] = {0, 0};
+        if (axis_setup(G, k, 0, tx, ks[0], xlo[t], xhi[t]) && visit_local(G, k, ks)) continue;
+        xlo[t] = 1; xhi[t] = 0;
+    }
+    if (tb > ta + 1) return false;  // (wider than two tiles: not for this path)
+    const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
+    const double c0 = k.c0, c1 = k.c1, c2 = k.c2, det = c0 * c2 - c1 * c1;
+    const double e0 = sqrt(qc * c2 / det), ic0 = 1.0 / c0;
+    const double yu0 = -c1 * e0 / c2, yl0 = c1 * e0 / c2, qcc0 = qc * c0;
     uint32_t written = 0u;  // bit KR + dy: row home_y + dy stored
     for (int ty = max(kr.y0, 0); ty < min(kr.y1, G.grid[1]); ++ty) {  // direct visits only
         int ks1, flo1, fhi1;
         if (!axis_setup(G, k, 1, ty, ks1, flo1, fhi1) || ks1 != 0) continue;
+        const double o1 = ty * BS;
         for (int fy = flo1; fy <= fhi1; ++fy) {
-            double xl, xu, tol;
-            if (!row_slice(G, k, ty, fy, 0, xl, xu, tol)) continue;
+            double ya = k.md[1] - (o1 + (fy + 1) * G.fs + slack) - k.epsx[1];
+            double yb = k.md[1] - (o1 + fy * G.fs - slack) + k.epsx[1];
+            ya = fmax(ya, -k.e[1]);
+            yb = fmin(yb, k.e[1]);
+            if (ya > yb) continue;
+            const double yu = fmin(fmax(yu0, ya), yb), yl = fmin(fmax(yl0, ya), yb);
+            const double xu = (-c1 * yu + sqrt(fmax(qcc0 - det * yu * yu, 0.0))) * ic0;
+            const double xl = (-c1 * yl - sqrt(fmax(qcc0 - det * yl * yl, 0.0))) * ic0;
+            const double tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
             int lo = 0xffff, hi = 0;
-            for (int tx = tx0; tx < tx1; ++tx) {
-                int ks[2] = {0, 0}, flo0, fhi0;
-                if (!axis_setup(G, k, 0, tx, ks[0], flo0, fhi0) || !visit_local(G, k, ks)) continue;
-                int fxl = flo0, fxh = fhi0;
-                row_cols(G, k, tx, 0, xl, xu, tol, fxl, fxh);
+            for (int t = 0; t < 2; ++t) {
+                if (xlo[t] > xhi[t]) continue;
+                const int tx = ta + t;
+                const double o0 = tx * BS;
+                const double A = k.md[0] - o0 - slack - k.epsx[0], B = k.md[0] - o0 + slack + k.epsx[0];
+                const double fa = ceil((A - (xu + tol)) * ifs - 1.0 - 1e-9);
+                const double fb = floor((B - (xl - tol)) * ifs + 1e-9);
+                const int fxl = fa > (double)xlo[t] ? (fa > (double)G.n ? G.n : (int)fa) : xlo[t];
+                const int fxh = fb < (double)xhi[t] ? (fb < -1.0 ? -1 : (int)fb) : xhi[t];
                 if (fxl > fxh) continue;
                 const int a = tx * G.n + fxl, b = tx * G.n + fxh;
                 if (lo > hi) { lo = a; hi = b; }
                 else if (a == hi + 1) hi = b;
-                else if (b + 1 == lo) lo = a;
                 else return false;
             }
             if (lo > hi) continue;
