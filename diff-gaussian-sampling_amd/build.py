@@ -42,7 +42,7 @@ def _run(cmd):
 
 
 def build_lib(force=False, debug=False):
-    headers = glob.glob(os.path.join(CSRC, "*.h")) + [os.path.join(INCLUDE, "dgs.h")]
+    headers = glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(INCLUDE, "*.h"))
     sources = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     os.makedirs(OBJ, exist_ok=True)
     flags = ["-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-I", INCLUDE, "-I", CSRC,
@@ -70,7 +70,7 @@ def build_ext(force=False):
     import torch.utils.cpp_extension as ce
 
     src = os.path.join(CSRC, "torch_ext.cpp")
-    if not (force or _newer(EXT, [src, LIB, os.path.join(INCLUDE, "dgs.h")])):
+    if not (force or _newer(EXT, [src, LIB] + glob.glob(os.path.join(INCLUDE, "*.h")))):
         return EXT
     tlib = os.path.join(os.path.dirname(torch.__file__), "lib")
     abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)

@@ -1,0 +1,849 @@
+// dgs_volume.hip -- D = 3 Gaussian fields (include/dgs_volume.h).
+//
+// The reference has no D = 3 path (its device functions stop at D = 2, forward.cu:164-275), so
+// this one carries its per-pair arithmetic to three dimensions and sums over every Gaussian
+// whose contribution is not exactly 0 in fp32.  Design:
+//   * one uniform grid of cells over the bounding box of the samples and the small Gaussians'
+//     means, each cell at least the largest exact-zero cut half-width E_d = sqrt(210 Sigma_dd)
+//     (at most 128 cells per axis); Gaussians and samples radix-sorted by cell;
+//   * "small" Gaussians (well-conditioned positive-definite conic, every E_d <= 0.45) meet a
+//     sample only through the torus images of the cut: per axis the displacement x = m - s
+//     lies in [-E, E] (image k = 0), [2k - E, 2k] (k > 0) or [2k, 2k + E] (k < 0), the sets
+//     the reference's wrap (forward.cu:149-157) maps into [-E, E].  Each pair is visited
+//     through exactly one image (the image index of its own x, checked per candidate), so no
+//     pair is counted twice even when the windows' cell ranges overlap;
+//   * "big" Gaussians (everything else) sit in one extra cell and meet every sample;
+//   * forward: lane = sample (in cell order), outputs summed in registers, no atomics;
+//     backward: lane = Gaussian (in cell order) walking the samples of its images, gradients
+//     in registers, no atomics; big Gaussians: one block each over every sample.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "dgs.h"
+#include "dgs_internal.h"
+#include "dgs_scan.h"
+#include "dgs_volume.h"
+
+namespace dgs {
+namespace vol {
+
+constexpr uint32_t kVolMagic = 0x33564744u;  // "DGV3"
+constexpr int kAxisCells = 128;
+constexpr float kMaxReach = 0.45f;
+constexpr double kVolCut = 210.0;      // X^T A X above this: power < -105, expf(power) == +0
+constexpr double kVolCond = 1.0e4;     // bound on ||A||_F^3 / det A for the cut to hold in fp32
+
+struct Hdr {
+    uint32_t magic;
+    int P, N, nsmall, nbig, ncells;
+    int n[3];
+    float lo[3], cs[3], E[3];
+    int64_t o_gext, o_gids, o_sids, o_gstart, o_sstart;
+};
+constexpr size_t kHdrBytes = 256;
+static_assert(sizeof(Hdr) <= kHdrBytes, "volume header too large");
+
+static inline size_t a256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// packed conic index of the symmetric entry (i, j): [c00 c01 c02 c11 c12 c22]
+__host__ __device__ constexpr int pidx(int i, int j) {
+    return i <= j ? i * 3 - i * (i - 1) / 2 + (j - i) : j * 3 - j * (j - 1) / 2 + (i - j);
+}
+// unique (sorted) index of a symmetric 3-index component i <= j <= k, in lexicographic order
+__host__ __device__ constexpr int uidx3s(int i, int j, int k) {
+    int n = 0;
+    for (int a = 0; a < 3; ++a)
+        for (int b = a; b < 3; ++b)
+            for (int c = b; c < 3; ++c) {
+                if (a == i && b == j && c == k) return n;
+                ++n;
+            }
+    return -1;
+}
+__host__ __device__ constexpr int sort3_idx(int i, int j, int k) {
+    const int a = i < j ? i : j, b = i < j ? j : i;  // a <= b
+    const int lo = k < a ? k : a;
+    const int hi = k > b ? k : b;
+    const int mid = i + j + k - lo - hi;
+    return uidx3s(lo, mid, hi);
+}
+
+template <int FN>
+struct VTr;
+template <> struct VTr<0> { static constexpr int KU = 1, K = 1; };
+template <> struct VTr<1> { static constexpr int KU = 3, K = 3; };
+template <> struct VTr<2> { static constexpr int KU = 6, K = 9; };
+template <> struct VTr<3> { static constexpr int KU = 10, K = 27; };
+
+// unique component of the full output index f (row-major over the 3^FN indices)
+template <int FN>
+__host__ __device__ constexpr int umap(int f) {
+    if (FN == 0) return 0;
+    if (FN == 1) return f;
+    if (FN == 2) return pidx(f / 3, f % 3);
+    return sort3_idx(f / 9, (f / 3) % 3, f % 3);
+}
+// the index triple of unique component u (FN = 2: pair (i, j) = first two)
+__host__ __device__ constexpr int u2i(int u, int w) {
+    return w == 0 ? (u < 3 ? 0 : u < 5 ? 1 : 2) : (u < 3 ? u : u < 5 ? u - 2 : 2);
+}
+__host__ __device__ constexpr int u3i(int u, int w) {
+    int n = 0;
+    for (int a = 0; a < 3; ++a)
+        for (int b = a; b < 3; ++b)
+            for (int c = b; c < 3; ++c) {
+                if (n == u) return w == 0 ? a : w == 1 ? b : c;
+                ++n;
+            }
+    return 0;
+}
+
+__device__ __forceinline__ float wrap1(float x) {  // forward.cu:149-157, one axis
+    if (fabsf(x) > 1.0f) x = x >= 0.0f ? fmodf(x, 2.0f) - 2.0f : fmodf(x, 2.0f) + 2.0f;
+    return x;
+}
+// image index of a displacement (0 inside [-1, 1]; k for [2k - 2, 2k] beyond it)
+__device__ __forceinline__ int image_of(float x) {
+    if (fabsf(x) <= 1.0f) return 0;
+    return x > 0.0f ? (int)ceilf(0.5f * x) : -(int)ceilf(-0.5f * x);
+}
+
+// One pair: wrapped X, power (exact operation order of include/dgs_volume.h, no contraction,
+// so that the numpy oracle reproduces it bit for bit), G and a = A X.  False: power > 0.
+__device__ __forceinline__ bool pair_eval(const float *m, const float *s, const float *c, float *X,
+                                          float &G, float *a) {
+    DGS_NO_CONTRACT
+    for (int d = 0; d < 3; ++d) X[d] = wrap1(m[d] - s[d]);
+    const float qd = c[0] * X[0] * X[0] + c[3] * X[1] * X[1] + c[5] * X[2] * X[2];
+    const float qo = c[1] * X[0] * X[1] + c[2] * X[0] * X[2] + c[4] * X[1] * X[2];
+    const float power = -0.5f * qd - qo;
+    if (power > 0.0f) return false;
+    G = expf(power);
+    a[0] = c[0] * X[0] + c[1] * X[1] + c[2] * X[2];
+    a[1] = c[1] * X[0] + c[3] * X[1] + c[4] * X[2];
+    a[2] = c[2] * X[0] + c[4] * X[1] + c[5] * X[2];
+    return true;
+}
+
+template <int FN>
+__device__ __forceinline__ void terms(const float *a, const float *c, float *t) {
+    DGS_NO_CONTRACT
+    if constexpr (FN == 0) {
+        t[0] = 1.0f;
+    } else if constexpr (FN == 1) {
+        for (int i = 0; i < 3; ++i) t[i] = a[i];
+    } else if constexpr (FN == 2) {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            const int i = u2i(u, 0), j = u2i(u, 1);
+            t[u] = a[i] * a[j] - c[pidx(i, j)];
+        }
+    } else {
+#pragma unroll
+        for (int u = 0; u < 10; ++u) {
+            const int i = u3i(u, 0), j = u3i(u, 1), k = u3i(u, 2);
+            t[u] = c[pidx(i, j)] * a[k] + c[pidx(i, k)] * a[j] + c[pidx(j, k)] * a[i] - a[i] * a[j] * a[k];
+        }
+    }
+}
+
+// g = d phi / d a and e = d phi / d c (explicit, packed conic) for phi = sum_u h_u t_u.
+template <int FN>
+__device__ __forceinline__ void phi_grads(const float *h, const float *a, const float *c, float *g, float *e) {
+    for (int i = 0; i < 3; ++i) g[i] = 0.0f;
+    for (int q = 0; q < 6; ++q) e[q] = 0.0f;
+    if constexpr (FN == 1) {
+        for (int i = 0; i < 3; ++i) g[i] = h[i];
+    } else if constexpr (FN == 2) {
+#pragma unroll
+        for (int u = 0; u < 6; ++u) {
+            const int i = u2i(u, 0), j = u2i(u, 1);
+            g[i] += h[u] * a[j];
+            g[j] += h[u] * a[i];
+            e[pidx(i, j)] -= h[u];
+        }
+    } else if constexpr (FN == 3) {
+#pragma unroll
+        for (int u = 0; u < 10; ++u) {
+            const int i = u3i(u, 0), j = u3i(u, 1), k = u3i(u, 2);
+            g[k] += h[u] * c[pidx(i, j)];
+            g[j] += h[u] * c[pidx(i, k)];
+            g[i] += h[u] * c[pidx(j, k)];
+            g[i] -= h[u] * a[j] * a[k];
+            g[j] -= h[u] * a[i] * a[k];
+            g[k] -= h[u] * a[i] * a[j];
+            e[pidx(i, j)] += h[u] * a[k];
+            e[pidx(i, k)] += h[u] * a[j];
+            e[pidx(j, k)] += h[u] * a[i];
+        }
+    }
+}
+
+// Adds one pair's gradients: dX (= d/d mean) and d/d conic (packed), for loss G * phi.
+__device__ __forceinline__ void pair_grads(float G, float phi, const float *X, const float *a, const float *c,
+                                           const float *g, const float *e, float *dm, float *dc) {
+    for (int m = 0; m < 3; ++m) {
+        float Ag = 0.0f;
+        for (int i = 0; i < 3; ++i) Ag += c[pidx(i, m)] * g[i];
+        dm[m] += G * (Ag - a[m] * phi);
+    }
+    for (int p = 0; p < 3; ++p)
+        for (int q = p; q < 3; ++q) {
+            const float dpow = p == q ? -0.5f * X[p] * X[p] : -X[p] * X[q];
+            const float da = p == q ? g[p] * X[p] : g[p] * X[q] + g[q] * X[p];
+            dc[pidx(p, q)] += G * (phi * dpow + da + e[pidx(p, q)]);
+        }
+}
+
+__device__ __forceinline__ int cell_axis(const Hdr &h, int d, float x) {
+    const int c = (int)floorf((x - h.lo[d]) / h.cs[d]);
+    return min(max(c, 0), h.n[d] - 1);
+}
+
+// Image windows of one axis for a point p and reach r: image k covers p + [xa(k), xb(k)] with
+// xa/xb the displacement window (target - p).  sign = +1: targets are means (x = target - p is
+// -(m - s): used with the sample as p); the windows are written for the x = m - s convention
+// through `flip`.
+struct Win {
+    int k0, k1;  // image range
+};
+// range of images k whose window can reach [lo, hi] (target coordinates)
+__device__ __forceinline__ Win image_range(float p, float r, float lo, float hi, bool target_is_mean) {
+    // target = p + x (means, x = m - s with p = s) or p - x (samples, p = m)
+    // image k >= 1 window in x: [2k - r, 2k]; k <= -1: [2k, 2k + r]
+    const float tlo = target_is_mean ? lo - p : p - hi;  // x range the targets allow
+    const float thi = target_is_mean ? hi - p : p - lo;
+    Win w;
+    w.k1 = thi >= 2.0f - r ? (int)floorf((thi + r) * 0.5f) : 0;
+    w.k0 = tlo <= -2.0f + r ? -(int)floorf((r - tlo) * 0.5f) : 0;
+    return w;
+}
+// x window of image k (x = m - s), widened by a rounding margin
+__device__ __forceinline__ void image_window(int k, float r, float &xa, float &xb) {
+    const float tol = 1e-5f;
+    if (k == 0) { xa = -r - tol; xb = r + tol; }
+    else if (k > 0) { xa = 2.0f * k - r - tol; xb = 2.0f * k + tol; }
+    else { xa = 2.0f * k - tol; xb = 2.0f * k + r + tol; }
+}
+
+__device__ __forceinline__ const Hdr &hdr_of(const char *buf) { return *reinterpret_cast<const Hdr *>(buf); }
+
+// ------------------------------------------------------------------------------ preprocess
+struct Red {
+    float mlo[3], mhi[3], slo[3], shi[3], E[3];
+    int nbig, pad[3];
+};
+
+__global__ void k_vol_init(Red *r) {
+    if (threadIdx.x == 0) {
+        for (int d = 0; d < 3; ++d) {
+            r->mlo[d] = r->slo[d] = INFINITY;
+            r->mhi[d] = r->shi[d] = -INFINITY;
+            r->E[d] = 0.0f;
+        }
+        r->nbig = 0;
+    }
+}
+
+__device__ __forceinline__ void atomic_min_f(float *p, float v) {
+    if (!(v == v)) return;
+    int *ip = reinterpret_cast<int *>(p);
+    int old = *ip;
+    while (v < __int_as_float(old)) {
+        const int prev = atomicCAS(ip, old, __float_as_int(v));
+        if (prev == old) break;
+        old = prev;
+    }
+}
+__device__ __forceinline__ void atomic_max_f(float *p, float v) {
+    if (!(v == v)) return;
+    int *ip = reinterpret_cast<int *>(p);
+    int old = *ip;
+    while (v > __int_as_float(old)) {
+        const int prev = atomicCAS(ip, old, __float_as_int(v));
+        if (prev == old) break;
+        old = prev;
+    }
+}
+__device__ __forceinline__ float wave_min(float v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o));
+    return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+    for (int o = kWave / 2; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+    return v;
+}
+
+// Per Gaussian: the exact-zero cut half-widths E_d = sqrt(210 Sigma_dd) (fp64 from the conic)
+// and whether the Gaussian is small (gext.w = 1); bounds of the small means, the largest E,
+// the big count.
+__global__ __launch_bounds__(kBlock) void k_vol_classify(int P, const float *__restrict__ means,
+                                                         const float *__restrict__ conics,
+                                                         float4 *__restrict__ gext, Red *__restrict__ red) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    float E[3] = {0.0f, 0.0f, 0.0f};
+    int big = 0;
+    if (i < P) {
+        double c[6], m[3];
+        for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)i * 6 + q];
+        for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)i * 3 + d];
+        const double a00 = c[0], a01 = c[1], a02 = c[2], a11 = c[3], a12 = c[4], a22 = c[5];
+        const double m01 = a00 * a11 - a01 * a01;
+        const double det = a00 * (a11 * a22 - a12 * a12) - a01 * (a01 * a22 - a12 * a02) + a02 * (a01 * a12 - a11 * a02);
+        double fro = 0.0;
+        for (int q = 0; q < 6; ++q) fro += (q == 0 || q == 3 || q == 5 ? 1.0 : 2.0) * c[q] * c[q];
+        fro = sqrt(fro);
+        bool small = a00 > 0.0 && m01 > 0.0 && det > 0.0 && isfinite(det) && fro * fro * fro < kVolCond * det;
+        float e[3] = {0.0f, 0.0f, 0.0f};
+        if (small) {
+            const double s00 = (a11 * a22 - a12 * a12) / det, s11 = (a00 * a22 - a02 * a02) / det,
+                         s22 = m01 / det;
+            const double sd[3] = {s00, s11, s22};
+            for (int d = 0; d < 3; ++d) {
+                const double ed = sqrt(kVolCut * (1.0 + 1e-6) * sd[d]) * (1.0 + 1e-6) + 1e-7;
+                e[d] = (float)ed;
+                small = small && sd[d] > 0.0 && ed <= (double)kMaxReach && isfinite(m[d]);
+            }
+        }
+        gext[i] = make_float4(e[0], e[1], e[2], small ? 1.0f : 0.0f);
+        if (small) {
+            for (int d = 0; d < 3; ++d) {
+                lo[d] = hi[d] = (float)m[d];
+                E[d] = e[d];
+            }
+        } else {
+            big = 1;
+        }
+    }
+    for (int d = 0; d < 3; ++d) {
+        lo[d] = wave_min(lo[d]);
+        hi[d] = wave_max(hi[d]);
+        E[d] = wave_max(E[d]);
+    }
+    for (int o = kWave / 2; o > 0; o >>= 1) big += __shfl_xor(big, o);
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        for (int d = 0; d < 3; ++d) {
+            atomic_min_f(&red->mlo[d], lo[d]);
+            atomic_max_f(&red->mhi[d], hi[d]);
+            atomic_max_f(&red->E[d], E[d]);
+        }
+        if (big) atomicAdd(&red->nbig, big);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_vol_sbounds(int N, const float *__restrict__ samples, Red *__restrict__ red) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t j = (int64_t)blockIdx.x * kBlock + threadIdx.x; j < N; j += (int64_t)gridDim.x * kBlock)
+        for (int d = 0; d < 3; ++d) {
+            const float v = samples[j * 3 + d];
+            lo[d] = fminf(lo[d], v);
+            hi[d] = fmaxf(hi[d], v);
+        }
+    for (int d = 0; d < 3; ++d) {
+        lo[d] = wave_min(lo[d]);
+        hi[d] = wave_max(hi[d]);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0)
+        for (int d = 0; d < 3; ++d) {
+            atomic_min_f(&red->slo[d], lo[d]);
+            atomic_max_f(&red->shi[d], hi[d]);
+        }
+}
+
+// cell keys (big Gaussians: the extra cell ncells) and the identity values
+__global__ __launch_bounds__(kBlock) void k_vol_keys(int n, Hdr h, const float *__restrict__ pts,
+                                                     const float4 *__restrict__ gext, uint32_t *__restrict__ keys,
+                                                     uint32_t *__restrict__ vals) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    uint32_t key = (uint32_t)h.ncells;
+    if (!gext || gext[i].w != 0.0f) {
+        int c[3];
+        for (int d = 0; d < 3; ++d) {
+            const float x = pts[(int64_t)i * 3 + d];
+            c[d] = x == x ? cell_axis(h, d, x) : 0;
+        }
+        key = (uint32_t)((c[2] * h.n[1] + c[1]) * h.n[0] + c[0]);
+    }
+    keys[i] = key;
+    vals[i] = (uint32_t)i;
+}
+
+// start[c] = first sorted position with key >= c, for c in [0, ncells + 1]; start[ncells + 1] = n
+__global__ __launch_bounds__(kBlock) void k_vol_starts(int n, int ncells, const uint32_t *__restrict__ keys,
+                                                       int32_t *__restrict__ start) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (n == 0) {
+        for (int c = i; c <= ncells + 1; c += gridDim.x * kBlock) start[c] = 0;
+        return;
+    }
+    if (i >= n) return;
+    const int kprev = i == 0 ? -1 : (int)keys[i - 1];
+    const int k = (int)keys[i];
+    for (int c = kprev + 1; c <= k; ++c) start[c] = i;
+    if (i == n - 1)
+        for (int c = k + 1; c <= ncells + 1; ++c) start[c] = n;
+}
+
+__global__ void k_vol_header(Hdr h, char *buf) {
+    if (threadIdx.x == 0) *reinterpret_cast<Hdr *>(buf) = h;
+}
+
+// ------------------------------------------------------------------------------ forward
+// Lane = sample (sorted by cell).  Images of the sample's cut windows (reach E, the largest
+// small-Gaussian cut) over the Gaussian grid; the candidates of a row of cells are one range of
+// the cell-sorted ids; each candidate is evaluated only through the image of its own
+// displacement.  Then every big Gaussian.
+template <int FN, int CB>
+__global__ __launch_bounds__(kBlock) void k_vol_forward(const char *__restrict__ buf, int P, int N, int C, int cbase,
+                                                        const float *__restrict__ means,
+                                                        const float *__restrict__ values,
+                                                        const float *__restrict__ conics,
+                                                        const float *__restrict__ samples, float *__restrict__ out) {
+    constexpr int KU = VTr<FN>::KU, K = VTr<FN>::K;
+    const Hdr h = hdr_of(buf);
+    const int j = blockIdx.x * kBlock + threadIdx.x;
+    if (j >= N) return;
+    const int nch = min(CB, C - cbase);
+    if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
+        for (int f = 0; f < K; ++f)
+            for (int ch = 0; ch < nch; ++ch) out[((int64_t)j * K + f) * C + cbase + ch] = NAN;
+        return;
+    }
+    const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
+    const int32_t *__restrict__ sids = reinterpret_cast<const int32_t *>(buf + h.o_sids);
+    const int32_t *__restrict__ gstart = reinterpret_cast<const int32_t *>(buf + h.o_gstart);
+    const int sid = sids[j];
+    float s[3];
+    for (int d = 0; d < 3; ++d) s[d] = samples[(int64_t)sid * 3 + d];
+    float acc[KU][CB];
+    for (int u = 0; u < KU; ++u)
+        for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
+
+    auto visit = [&](int g) {
+        float m[3], c[6], X[3], a[3], G, t[KU];
+        for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
+        for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
+        if (!pair_eval(m, s, c, X, G, a)) return;
+        terms<FN>(a, c, t);
+        for (int ch = 0; ch < nch; ++ch) {
+            const float v = values[(int64_t)g * C + cbase + ch];
+            for (int u = 0; u < KU; ++u) acc[u][ch] += v * G * t[u];
+        }
+    };
+
+    if (h.nsmall > 0) {
+        Win w[3];
+        bool ok = true;
+        for (int d = 0; d < 3; ++d) {
+            w[d] = image_range(s[d], h.E[d], h.lo[d], h.lo[d] + h.cs[d] * h.n[d], true);
+            ok = ok && s[d] == s[d];
+        }
+        if (ok)
+            for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
+                for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
+                    for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
+                        const int kk[3] = {kx, ky, kz};
+                        int c0[3], c1[3];
+                        bool any = true;
+                        for (int d = 0; d < 3; ++d) {
+                            float xa, xb;
+                            image_window(kk[d], h.E[d], xa, xb);
+                            const float ta = s[d] + xa, tb = s[d] + xb;  // mean window
+                            const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
+                            if (tb < glo || ta > ghi) { any = false; break; }
+                            c0[d] = cell_axis(h, d, ta);
+                            c1[d] = cell_axis(h, d, tb);
+                        }
+                        if (!any) continue;
+                        for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                            for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                                const int row = (cz * h.n[1] + cy) * h.n[0];
+                                const int b = gstart[row + c0[0]], e = gstart[row + c1[0] + 1];
+                                for (int q = b; q < e; ++q) {
+                                    const int g = gids[q];
+                                    bool mine = true;
+                                    for (int d = 0; d < 3; ++d)
+                                        mine = mine && image_of(means[(int64_t)g * 3 + d] - s[d]) == kk[d];
+                                    if (mine) visit(g);
+                                }
+                            }
+                    }
+    }
+    for (int q = gstart[h.ncells]; q < gstart[h.ncells + 1]; ++q) visit(gids[q]);  // big ones
+
+    for (int f = 0; f < K; ++f) {
+        const int u = umap<FN>(f);
+        for (int ch = 0; ch < nch; ++ch) out[((int64_t)sid * K + f) * C + cbase + ch] = acc[u][ch];
+    }
+}
+
+// ------------------------------------------------------------------------------ backward
+// hs[sid][u][ch]: dL summed over the full components that share unique component u
+template <int FN>
+__global__ __launch_bounds__(kBlock) void k_vol_hsum(int N, int C, const float *__restrict__ dL, float *__restrict__ hs) {
+    constexpr int KU = VTr<FN>::KU, K = VTr<FN>::K;
+    const int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (t >= (int64_t)N * C) return;
+    const int64_t sid = t / C;
+    const int ch = (int)(t - sid * C);
+    float h[KU];
+    for (int u = 0; u < KU; ++u) h[u] = 0.0f;
+#pragma unroll
+    for (int f = 0; f < K; ++f) h[umap<FN>(f)] += dL[(sid * K + f) * C + ch];
+    for (int u = 0; u < KU; ++u) hs[(sid * KU + u) * C + ch] = h[u];
+}
+
+// One pair's contribution to a Gaussian's gradient sums.
+template <int FN, int CB>
+__device__ __forceinline__ void bwd_pair(const float *m, const float *c, const float *__restrict__ values, int g,
+                                         int C, int cbase, int nch, const float *__restrict__ samples,
+                                         const float *__restrict__ hs, int sid, float *dm, float *dc, float *dv) {
+    constexpr int KU = VTr<FN>::KU;
+    float s[3], X[3], a[3], G, t[KU];
+    for (int d = 0; d < 3; ++d) s[d] = samples[(int64_t)sid * 3 + d];
+    if (!pair_eval(m, s, c, X, G, a)) return;
+    terms<FN>(a, c, t);
+    const float *hrow = hs + (int64_t)sid * KU * C;
+    float hv[KU];
+    for (int u = 0; u < KU; ++u) hv[u] = 0.0f;
+    for (int ch = 0; ch < C; ++ch) {
+        const float v = values[(int64_t)g * C + ch];
+        for (int u = 0; u < KU; ++u) hv[u] += v * hrow[u * C + ch];
+    }
+    for (int ch = 0; ch < nch; ++ch) {
+        float p = 0.0f;
+        for (int u = 0; u < KU; ++u) p += hrow[u * C + cbase + ch] * t[u];
+        dv[ch] += G * p;
+    }
+    float phi = 0.0f;
+    for (int u = 0; u < KU; ++u) phi += hv[u] * t[u];
+    float gg[3], e[6];
+    phi_grads<FN>(hv, a, c, gg, e);
+    pair_grads(G, phi, X, a, c, gg, e, dm, dc);
+}
+
+template <int CB>
+__device__ __forceinline__ void bwd_store(int g, int C, int cbase, int nch, const float *dm, const float *dc,
+                                          const float *dv, float *__restrict__ dmeans, float *__restrict__ dvalues,
+                                          float *__restrict__ dconics) {
+    if (cbase == 0) {
+        for (int d = 0; d < 3; ++d) dmeans[(int64_t)g * 3 + d] = dm[d];
+        for (int q = 0; q < 6; ++q) dconics[(int64_t)g * 6 + q] = dc[q];
+    }
+    for (int ch = 0; ch < nch; ++ch) dvalues[(int64_t)g * C + cbase + ch] = dv[ch];
+}
+
+// Lane = small Gaussian (sorted by cell): the samples of its cut's images.
+template <int FN, int CB>
+__global__ __launch_bounds__(kBlock) void k_vol_backward(const char *__restrict__ buf, int P, int N, int C, int cbase,
+                                                         const float *__restrict__ means,
+                                                         const float *__restrict__ values,
+                                                         const float *__restrict__ conics,
+                                                         const float *__restrict__ samples,
+                                                         const float *__restrict__ hs, float *__restrict__ dmeans,
+                                                         float *__restrict__ dvalues, float *__restrict__ dconics) {
+    const Hdr h = hdr_of(buf);
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
+        if (i < P) {
+            const float nan[9] = {NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
+            bwd_store<CB>(i, C, cbase, min(CB, C - cbase), nan, nan, nan, dmeans, dvalues, dconics);
+        }
+        return;
+    }
+    if (i >= h.nsmall) return;
+    const int nch = min(CB, C - cbase);
+    const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
+    const int32_t *__restrict__ sids = reinterpret_cast<const int32_t *>(buf + h.o_sids);
+    const int32_t *__restrict__ sstart = reinterpret_cast<const int32_t *>(buf + h.o_sstart);
+    const float4 *__restrict__ gext = reinterpret_cast<const float4 *>(buf + h.o_gext);
+    const int g = gids[i];
+    const float4 ex = gext[g];
+    const float r[3] = {ex.x, ex.y, ex.z};
+    float m[3], c[6];
+    for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
+    for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
+    float dm[3] = {0.0f, 0.0f, 0.0f}, dc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dv[CB];
+    for (int ch = 0; ch < CB; ++ch) dv[ch] = 0.0f;
+    Win w[3];
+    for (int d = 0; d < 3; ++d) w[d] = image_range(m[d], r[d], h.lo[d], h.lo[d] + h.cs[d] * h.n[d], false);
+    for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
+        for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
+            for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
+                const int kk[3] = {kx, ky, kz};
+                int c0[3], c1[3];
+                bool any = true;
+                for (int d = 0; d < 3; ++d) {
+                    float xa, xb;
+                    image_window(kk[d], r[d], xa, xb);
+                    const float ta = m[d] - xb, tb = m[d] - xa;  // sample window
+                    const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
+                    if (tb < glo || ta > ghi) { any = false; break; }
+                    c0[d] = cell_axis(h, d, ta);
+                    c1[d] = cell_axis(h, d, tb);
+                }
+                if (!any) continue;
+                for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                    for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                        const int row = (cz * h.n[1] + cy) * h.n[0];
+                        const int b = sstart[row + c0[0]], e = sstart[row + c1[0] + 1];
+                        for (int q = b; q < e; ++q) {
+                            const int sid = sids[q];
+                            bool mine = true;
+                            for (int d = 0; d < 3; ++d)
+                                mine = mine && image_of(m[d] - samples[(int64_t)sid * 3 + d]) == kk[d];
+                            if (mine) bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, samples, hs, sid, dm, dc, dv);
+                        }
+                    }
+            }
+    bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics);
+}
+
+// Big Gaussians: one block each, threads striding over every sample, block sums.
+template <int FN, int CB>
+__global__ __launch_bounds__(kBlock) void k_vol_backward_big(const char *__restrict__ buf, int P, int N, int C,
+                                                             int cbase, const float *__restrict__ means,
+                                                             const float *__restrict__ values,
+                                                             const float *__restrict__ conics,
+                                                             const float *__restrict__ samples,
+                                                             const float *__restrict__ hs,
+                                                             float *__restrict__ dmeans,
+                                                             float *__restrict__ dvalues,
+                                                             float *__restrict__ dconics) {
+    constexpr int NV = 9 + CB;
+    __shared__ float part[kWavesPerBlock][NV];
+    const Hdr h = hdr_of(buf);
+    if (h.magic != kVolMagic || h.P != P || h.N != N) return;  // (k_vol_backward flags it)
+    const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
+    const int nch = min(CB, C - cbase);
+    const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+    for (int b = blockIdx.x; b < h.nbig; b += gridDim.x) {
+        const int g = gids[h.nsmall + b];
+        float m[3], c[6];
+        for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
+        for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
+        float v[NV];
+        for (int k = 0; k < NV; ++k) v[k] = 0.0f;
+        for (int sid = threadIdx.x; sid < N; sid += kBlock)
+            bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, samples, hs, sid, v, v + 3, v + 9);
+        for (int k = 0; k < NV; ++k)
+            for (int o = kWave / 2; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
+        if (lane == 0)
+            for (int k = 0; k < NV; ++k) part[w][k] = v[k];
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            float t[NV];
+            for (int k = 0; k < NV; ++k) {
+                t[k] = 0.0f;
+                for (int q = 0; q < kWavesPerBlock; ++q) t[k] += part[q][k];
+            }
+            bwd_store<CB>(g, C, cbase, nch, t, t + 3, t + 9, dmeans, dvalues, dconics);
+        }
+        __syncthreads();
+    }
+}
+
+static int vol_cb(int C) { return C <= 1 ? 1 : C <= 4 ? 4 : 8; }
+
+template <int FN, int CB>
+static void launch_fwd(const char *buf, int P, int N, int C, const float *means, const float *values,
+                       const float *conics, const float *samples, float *out, hipStream_t s) {
+    for (int cb = 0; cb < C; cb += CB)
+        k_vol_forward<FN, CB><<<(unsigned)((N + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+            buf, P, N, C, cb, means, values, conics, samples, out);
+}
+template <int FN, int CB>
+static void launch_bwd(const char *buf, int P, int N, int C, const float *means, const float *values,
+                       const float *conics, const float *samples, const float *dL, float *hs, float *dm,
+                       float *dv, float *dc, hipStream_t s) {
+    const int64_t nh = (int64_t)N * C;
+    if (nh > 0) k_vol_hsum<FN><<<(unsigned)((nh + kBlock - 1) / kBlock), kBlock, 0, s>>>(N, C, dL, hs);
+    for (int cb = 0; cb < C; cb += CB) {
+        if (P > 0)
+            k_vol_backward<FN, CB><<<(unsigned)((P + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+                buf, P, N, C, cb, means, values, conics, samples, hs, dm, dv, dc);
+        k_vol_backward_big<FN, CB><<<256, kBlock, 0, s>>>(buf, P, N, C, cb, means, values, conics, samples, hs,
+                                                           dm, dv, dc);
+    }
+}
+
+template <int FN>
+static void dispatch_fwd(int C, const char *buf, int P, int N, const float *m, const float *v, const float *c,
+                         const float *sm, float *out, hipStream_t s) {
+    switch (vol_cb(C)) {
+        case 1: launch_fwd<FN, 1>(buf, P, N, C, m, v, c, sm, out, s); break;
+        case 4: launch_fwd<FN, 4>(buf, P, N, C, m, v, c, sm, out, s); break;
+        default: launch_fwd<FN, 8>(buf, P, N, C, m, v, c, sm, out, s); break;
+    }
+}
+template <int FN>
+static void dispatch_bwd(int C, const char *buf, int P, int N, const float *m, const float *v, const float *c,
+                         const float *sm, const float *dL, float *hs, float *dm, float *dv, float *dc,
+                         hipStream_t s) {
+    switch (vol_cb(C)) {
+        case 1: launch_bwd<FN, 1>(buf, P, N, C, m, v, c, sm, dL, hs, dm, dv, dc, s); break;
+        case 4: launch_bwd<FN, 4>(buf, P, N, C, m, v, c, sm, dL, hs, dm, dv, dc, s); break;
+        default: launch_bwd<FN, 8>(buf, P, N, C, m, v, c, sm, dL, hs, dm, dv, dc, s); break;
+    }
+}
+
+static const int kKU[4] = {1, 3, 6, 10};
+
+}  // namespace vol
+}  // namespace dgs
+
+using namespace dgs;
+using namespace dgs::vol;
+
+extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const float *conics, const float *samples,
+                                     dgs_alloc_fn alloc, void *alloc_ctx, dgs_stream_t stream, int debug) {
+    if (P < 0 || N < 0 || !alloc || (P > 0 && (!means || !conics)) || (N > 0 && !samples))
+        return fail(DGS_ERR_ARG, "dgs_volume_preprocess: bad arguments");
+    if ((int64_t)P >= (1LL << 31) - 1 || (int64_t)N >= (1LL << 31) - 1)
+        return fail(DGS_ERR_ARG, "dgs_volume_preprocess: too many Gaussians or samples");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // cell cap: at most 128^3 cells, and no more than ~2 per point
+    const int64_t cap = std::min<int64_t>((int64_t)kAxisCells * kAxisCells * kAxisCells,
+                                          std::max<int64_t>(64, 2 * ((int64_t)P + N)));
+    const int64_t nmax = std::max<int64_t>(std::max(P, N), 1);
+    Hdr h{};
+    h.magic = kVolMagic;
+    h.P = P;
+    h.N = N;
+    h.o_gext = kHdrBytes;
+    h.o_gids = h.o_gext + a256((size_t)P * 16);
+    h.o_sids = h.o_gids + a256((size_t)P * 4);
+    h.o_gstart = h.o_sids + a256((size_t)N * 4);
+    h.o_sstart = h.o_gstart + a256((size_t)(cap + 2) * 4);
+    const size_t total = h.o_sstart + a256((size_t)(cap + 2) * 4);
+    char *buf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_BINNING, total));
+    if (!buf) return fail(DGS_ERR_ALLOC, "dgs_volume_preprocess: binning buffer");
+    size_t sort_tmp = 0;
+    DGS_TRY_HIP(onesweep_pairs<uint32_t>(nullptr, sort_tmp, nullptr, nullptr, nullptr, nullptr, (size_t)nmax, 0, 24, s));
+    const size_t o_keys = 256, o_keys2 = o_keys + a256(nmax * 4), o_vals = o_keys2 + a256(nmax * 4),
+                 o_tmp = o_vals + a256(nmax * 4);
+    char *scr = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, o_tmp + a256(sort_tmp)));
+    if (!scr) return fail(DGS_ERR_ALLOC, "dgs_volume_preprocess: scratch");
+    Red *red = reinterpret_cast<Red *>(scr);
+    uint32_t *keys = reinterpret_cast<uint32_t *>(scr + o_keys), *keys2 = reinterpret_cast<uint32_t *>(scr + o_keys2);
+    uint32_t *vals = reinterpret_cast<uint32_t *>(scr + o_vals);
+    float4 *gext = reinterpret_cast<float4 *>(buf + h.o_gext);
+    k_vol_init<<<1, 64, 0, s>>>(red);
+    if (P > 0) k_vol_classify<<<(unsigned)((P + kBlock - 1) / kBlock), kBlock, 0, s>>>(P, means, conics, gext, red);
+    if (N > 0) k_vol_sbounds<<<(unsigned)std::min<int64_t>((N + kBlock - 1) / kBlock, 1024), kBlock, 0, s>>>(N, samples, red);
+    DGS_LAUNCH_CHECK(s, debug);
+    Red hr;
+    DGS_TRY_HIP(hipMemcpyAsync(&hr, red, sizeof(Red), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));  // the one host sync: grid sizing
+    h.nbig = hr.nbig;
+    h.nsmall = P - hr.nbig;
+    int64_t ncells = 1;
+    for (int d = 0; d < 3; ++d) {
+        float lo = std::min(hr.mlo[d], hr.slo[d]), hi = std::max(hr.mhi[d], hr.shi[d]);
+        if (!(lo <= hi)) lo = hi = 0.0f;  // (no small Gaussian and no sample)
+        if (!std::isfinite(lo) || !std::isfinite(hi)) return fail(DGS_ERR_ARG, "dgs_volume_preprocess: non-finite samples");
+        h.lo[d] = lo;
+        h.E[d] = hr.E[d];
+        const float ext = hi - lo;
+        h.cs[d] = std::max({hr.E[d], ext / (float)kAxisCells, 1e-6f, ext * 1e-6f});
+    }
+    for (int it = 0; it < 64; ++it) {
+        ncells = 1;
+        for (int d = 0; d < 3; ++d) {
+            const float ext = std::max(hr.mhi[d], hr.shi[d]) - h.lo[d];
+            const int n = (std::isfinite(ext) && ext > 0.0f) ? (int)std::floor(ext / h.cs[d]) + 1 : 1;
+            h.n[d] = std::min(std::max(n, 1), kAxisCells);
+            ncells *= h.n[d];
+        }
+        if (ncells <= cap) break;
+        for (int d = 0; d < 3; ++d) h.cs[d] *= 1.26f;
+    }
+    // grid end lo + cs * n must cover hi: floor(ext / cs) + 1 cells do, unless capped at 128 (then
+    // cs >= ext / 128 already makes 128 cells cover it)
+    h.ncells = (int)ncells;
+    unsigned bits = 1;
+    while ((1ull << bits) <= (uint64_t)ncells) ++bits;
+    int32_t *gstart = reinterpret_cast<int32_t *>(buf + h.o_gstart);
+    int32_t *sstart = reinterpret_cast<int32_t *>(buf + h.o_sstart);
+    for (int side = 0; side < 2; ++side) {
+        const int n = side == 0 ? P : N;
+        const float *pts = side == 0 ? means : samples;
+        int32_t *ids = reinterpret_cast<int32_t *>(buf + (side == 0 ? h.o_gids : h.o_sids));
+        int32_t *start = side == 0 ? gstart : sstart;
+        if (n > 0) {
+            k_vol_keys<<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, s>>>(n, h, pts, side == 0 ? gext : nullptr,
+                                                                              keys, vals);
+            size_t tb = sort_tmp;
+            DGS_TRY_HIP(onesweep_pairs<uint32_t>(scr + o_tmp, tb, keys, keys2, vals, reinterpret_cast<uint32_t *>(ids),
+                                                 (size_t)n, 0, bits, s));
+        }
+        const int64_t nthr = std::max<int64_t>(n, 1);
+        k_vol_starts<<<(unsigned)((nthr + kBlock - 1) / kBlock), kBlock, 0, s>>>(n, h.ncells, keys2, start);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
+    k_vol_header<<<1, 64, 0, s>>>(h, buf);
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+extern "C" size_t dgs_volume_workspace_size(int function, int P, int N, int C, int backward) {
+    if (!backward || function < 0 || function > 3 || N <= 0 || C <= 0) return 0;
+    return (size_t)N * kKU[function] * C * 4;
+}
+
+static int vol_check(int function, int P, int N, int C, const void *binning, size_t bytes) {
+    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "dgs_volume: function must be 0..3");
+    if (P < 0 || N < 0 || C < 1) return fail(DGS_ERR_ARG, "dgs_volume: bad sizes");
+    if (!binning || bytes < kHdrBytes) return fail(DGS_ERR_BUFFER, "dgs_volume: binning buffer missing or too small");
+    return DGS_OK;
+}
+
+extern "C" int dgs_volume_forward(int function, int P, int N, int C, const float *means, const float *values,
+                                  const float *conics, const float *samples, const void *binning,
+                                  size_t binning_bytes, float *out, dgs_stream_t stream, int debug) {
+    if (int rc = vol_check(function, P, N, C, binning, binning_bytes)) return rc;
+    if (N == 0) return DGS_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const char *buf = static_cast<const char *>(binning);
+    switch (function) {
+        case 0: dispatch_fwd<0>(C, buf, P, N, means, values, conics, samples, out, s); break;
+        case 1: dispatch_fwd<1>(C, buf, P, N, means, values, conics, samples, out, s); break;
+        case 2: dispatch_fwd<2>(C, buf, P, N, means, values, conics, samples, out, s); break;
+        default: dispatch_fwd<3>(C, buf, P, N, means, values, conics, samples, out, s); break;
+    }
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+extern "C" int dgs_volume_backward(int function, int P, int N, int C, const float *means, const float *values,
+                                   const float *conics, const float *samples, const float *dL_dout,
+                                   const void *binning, size_t binning_bytes, float *dL_dmeans, float *dL_dvalues,
+                                   float *dL_dconics, void *workspace, size_t workspace_bytes, dgs_stream_t stream,
+                                   int debug) {
+    if (int rc = vol_check(function, P, N, C, binning, binning_bytes)) return rc;
+    if (workspace_bytes < dgs_volume_workspace_size(function, P, N, C, 1))
+        return fail(DGS_ERR_ARG, "dgs_volume_backward: workspace too small");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0) return DGS_OK;
+    if (N == 0) {
+        DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, (size_t)P * 12, s));
+        DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, (size_t)P * C * 4, s));
+        DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, (size_t)P * 24, s));
+        return DGS_OK;
+    }
+    const char *buf = static_cast<const char *>(binning);
+    float *hs = static_cast<float *>(workspace);
+    switch (function) {
+        case 0: dispatch_bwd<0>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
+        case 1: dispatch_bwd<1>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
+        case 2: dispatch_bwd<2>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
+        default: dispatch_bwd<3>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
+    }
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}

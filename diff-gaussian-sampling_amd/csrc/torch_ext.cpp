@@ -19,6 +19,7 @@
 #include <vector>
 
 #include "dgs.h"
+#include "dgs_volume.h"
 
 namespace {
 
@@ -518,6 +519,74 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
     return std::make_tuple(dfeat, dtrans, dq, dkeys, dfreq, ddt);
 }
 
+// ---- D = 3 fields (include/dgs_volume.h; beyond the reference) --------
+void vol_shapes(const Tensor &means, const Tensor &conics, const Tensor &samples) {
+    TORCH_CHECK(means.dim() == 2 && means.size(1) == 3, "volume: means must be [P, 3]");
+    TORCH_CHECK(conics.dim() == 2 && conics.size(1) == 6 && conics.size(0) == means.size(0),
+                "volume: conics must be [P, 6] (packed c00 c01 c02 c11 c12 c22)");
+    TORCH_CHECK(samples.dim() == 2 && samples.size(1) == 3, "volume: samples must be [N, 3]");
+}
+
+Tensor VolumePreprocess(const Tensor &means_in, const Tensor &conics_in, const Tensor &samples_in,
+                        const bool debug) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples");
+    vol_shapes(means, conics, samples);
+    AllocCtx ctx{means.device(), {}, {}};
+    check(dgs_volume_preprocess((int)means.size(0), (int)samples.size(0), means.data_ptr<float>(),
+                                conics.data_ptr<float>(), samples.data_ptr<float>(), alloc_cb, &ctx,
+                                as_dgs(cur_stream()), debug ? 1 : 0),
+          "volume_preprocess");
+    return ctx.bufs[DGS_BUF_BINNING];
+}
+
+Tensor VolumeForward(int function, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
+                     const Tensor &samples_in, const Tensor &binning_in, const bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const Tensor binning = u8(binning_in, "binning_buffer");
+    vol_shapes(means, conics, samples);
+    TORCH_CHECK(function >= 0 && function <= 3, "volume: function must be 0..3");
+    TORCH_CHECK(values.dim() == 2 && values.size(0) == means.size(0), "volume: values must be [P, C]");
+    const int64_t P = means.size(0), N = samples.size(0), C = values.size(1);
+    std::vector<int64_t> shape{N};
+    for (int k = 0; k < function; ++k) shape.push_back(3);
+    shape.push_back(C);
+    Tensor out = torch::zeros(shape, means.options());
+    if (N == 0 || C == 0) return out;
+    check(dgs_volume_forward(function, (int)P, (int)N, (int)C, means.data_ptr<float>(), values.data_ptr<float>(),
+                             conics.data_ptr<float>(), samples.data_ptr<float>(), binning.data_ptr(),
+                             (size_t)binning.numel(), out.data_ptr<float>(), as_dgs(cur_stream()), debug ? 1 : 0),
+          "volume_forward");
+    return out;
+}
+
+std::tuple<Tensor, Tensor, Tensor> VolumeBackward(int function, const Tensor &means_in, const Tensor &values_in,
+                                                  const Tensor &conics_in, const Tensor &samples_in,
+                                                  const Tensor &binning_in, const Tensor &dL_in, const bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const Tensor binning = u8(binning_in, "binning_buffer"), dL = f32(dL_in, "dL_dout");
+    vol_shapes(means, conics, samples);
+    TORCH_CHECK(function >= 0 && function <= 3, "volume: function must be 0..3");
+    const int64_t P = means.size(0), N = samples.size(0), C = values.size(1);
+    int64_t K = 1;
+    for (int k = 0; k < function; ++k) K *= 3;
+    TORCH_CHECK(dL.numel() == N * K * C, "volume: dL_dout must be [N, 3^function, C]");
+    Tensor dm = torch::zeros({P, 3}, means.options()), dv = torch::zeros({P, C}, means.options());
+    Tensor dc = torch::zeros({P, 6}, means.options());
+    if (P == 0 || C == 0) return std::make_tuple(dm, dv, dc);
+    const size_t ws = dgs_volume_workspace_size(function, (int)P, (int)N, (int)C, 1);
+    Tensor work = torch::empty({(int64_t)std::max<size_t>(ws, 4)}, means.options().dtype(torch::kUInt8));
+    check(dgs_volume_backward(function, (int)P, (int)N, (int)C, means.data_ptr<float>(), values.data_ptr<float>(),
+                              conics.data_ptr<float>(), samples.data_ptr<float>(), dL.data_ptr<float>(),
+                              binning.data_ptr(), (size_t)binning.numel(), dm.data_ptr<float>(),
+                              dv.data_ptr<float>(), dc.data_ptr<float>(), work.data_ptr(), ws,
+                              as_dgs(cur_stream()), debug ? 1 : 0),
+          "volume_backward");
+    return std::make_tuple(dm, dv, dc);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -543,6 +612,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("tile_grid", &TileGrid);
     m.def("exchange_sets", &ExchangeSets);
     m.def("inputs_match", &InputsMatch);
+    m.def("volume_preprocess", &VolumePreprocess);
+    m.def("volume_forward", &VolumeForward);
+    m.def("volume_backward", &VolumeBackward);
     m.def("library_version", []() { return dgs_version(); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });
     m.def("timing_read", [](int which) {

@@ -10,12 +10,14 @@ import pytest
 from conftest import PKG_ROOT, REPO
 
 HEADER = os.path.join(REPO, "include", "dgs.h")
+HEADERS = sorted(os.path.join(REPO, "include", f) for f in os.listdir(os.path.join(REPO, "include"))
+                 if f.endswith(".h"))
 LIB = os.path.join(PKG_ROOT, "diff_gaussian_sampling", "libdgs.so")
 DGS_ERR_ARG, DGS_ERR_BUFFER = 1, 4
 
 
 def declared_functions():
-    text = open(HEADER).read()
+    text = "\n".join(open(h).read() for h in HEADERS)
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(dgs_[a-z_0-9]+)\s*\(", text, flags=re.M)
     return sorted(set(names))
@@ -32,7 +34,8 @@ def test_header_declares_the_entry_points():
     names = declared_functions()
     for n in ["dgs_last_error", "dgs_version", "dgs_tile_grid", "dgs_preprocess",
               "dgs_sample_workspace_size", "dgs_sample_forward", "dgs_sample_backward",
-              "dgs_count_pairs", "dgs_timing_enable", "dgs_timing_read"]:
+              "dgs_count_pairs", "dgs_timing_enable", "dgs_timing_read", "dgs_volume_preprocess",
+              "dgs_volume_forward", "dgs_volume_backward", "dgs_volume_workspace_size"]:
         assert n in names, n
 
 
@@ -44,7 +47,8 @@ def test_library_exports_every_declared_symbol(lib):
 def test_header_compiles_as_c(tmp_path):
     """include/dgs.h is plain C (no C++ or torch types)."""
     src = tmp_path / "t.c"
-    src.write_text('#include "dgs.h"\nint main(void) { return dgs_version() > 0 ? 0 : 1; }\n')
+    src.write_text('#include "dgs.h"\n#include "dgs_volume.h"\n'
+                   'int main(void) { return dgs_version() > 0 ? 0 : 1; }\n')
     import subprocess
     r = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.dirname(HEADER),
                         "-c", str(src), "-o", str(tmp_path / "t.o")], capture_output=True, text=True)
@@ -94,3 +98,19 @@ def test_timing_read_without_records(lib):
     ms = ctypes.c_double(0)
     assert lib.dgs_timing_read(0, ctypes.byref(ms)) == 0 and ms.value == 0.0
     assert lib.dgs_timing_read(5, ctypes.byref(ms)) < 0
+
+
+def test_volume_host_validation(lib):
+    """dgs_volume_*: workspace sizing and argument errors before any device work."""
+    ws = lib.dgs_volume_workspace_size
+    ws.restype = ctypes.c_size_t
+    ws.argtypes = [ctypes.c_int] * 5
+    assert ws(0, 10, 100, 1, 0) == 0
+    assert ws(3, 10, 100, 2, 1) == 100 * 10 * 2 * 4  # hs[N][10 unique components][C]
+    f = lib.dgs_volume_forward
+    f.restype = ctypes.c_int
+    assert f(7, 1, 1, 1, None, None, None, None, None, ctypes.c_size_t(0), None, None, 0) == DGS_ERR_ARG
+    assert f(0, 1, 1, 1, None, None, None, None, None, ctypes.c_size_t(0), None, None, 0) == DGS_ERR_BUFFER
+    p = lib.dgs_volume_preprocess
+    p.restype = ctypes.c_int
+    assert p(-1, 1, None, None, None, None, None, None, 0) == DGS_ERR_ARG
