@@ -125,7 +125,9 @@ def main():
     ap.add_argument("--cpu-oracle-samples", type=int, default=2048,
                     help="query points of the 1-thread C-oracle CPU baseline sample")
     ap.add_argument("--pre-reps", type=int, default=5, help="warm preprocess repetitions (median)")
-    ap.add_argument("--op", default="sample", choices=["sample", "aggregate"],
+    ap.add_argument("--grid3", type=int, default=128,
+                    help="--op volume: query points on a g^3 lattice (BASELINE config 5 names 256)")
+    ap.add_argument("--op", default="sample", choices=["sample", "aggregate", "volume"],
                     help="sample: the headline (default); aggregate: aggregate_neighbors at SURVEY "
                          "config 5 (P = 1M, K = L = 16, F = 4), one GPU or N replicas")
     ap.add_argument("--cpu-rows", type=int, default=20000, help="aggregate CPU-baseline rows")
@@ -157,6 +159,8 @@ def main():
     dev = torch.device("cuda", local)
     if args.op == "aggregate":
         return bench_aggregate(args, world, rank, dev, torch, dist)
+    if args.op == "volume":
+        return bench_volume(args, world, rank, dev, torch, dist)
     return bench_sample(args, world, rank, dev, torch, dist)
 
 
@@ -412,6 +416,88 @@ def cpu_baselines(result, means, values, covs, conics, samples, dL, fn, w_live_t
                    "sample": f"first {len(sub)} of the {N} query points in tile order (W_live {wl}), "
                              f"1-thread C oracle fwd+bwd, binning excluded ({dt:.1f} s); scaled by "
                              f"W_live(total) / W_live(sample)"}
+
+
+def bench_volume(args, world, rank, dev, torch, dist):
+    """D = 3 fields (beyond the reference): P Gaussians (default 1M) against a
+    g^3 lattice of query points (--grid3, config 5's "256^3 grid"), one function, forward +
+    backward through VolumeSampler's autograd Function per step; the binning (preprocess) is
+    timed separately.  N > 1 runs N independent replicas."""
+    from diff_gaussian_sampling import synthetic as syn
+    from diff_gaussian_sampling.volume import VolumeSampler
+    P, C, fn = args.P, args.C, args.function
+    code = FUNCS[fn]
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians3(P, C, seed=0))
+    samples = syn.grid_samples3(args.grid3).to(dev)
+    N = samples.shape[0]
+    for t in (means, values, conics):
+        t.requires_grad_(True)
+    vs = VolumeSampler(False)
+    pre = []
+    for _ in range(1 + max(args.pre_reps, 1)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        vs.preprocess(means, values, covs, conics, samples)
+        torch.cuda.synchronize()
+        pre.append((time.perf_counter() - t0) * 1e3)
+    pre_ms = sorted(pre[1:])[len(pre[1:]) // 2]
+    run = [vs.sample_gaussians, vs.sample_gaussians_derivative, vs.sample_gaussians_laplacian,
+           vs.sample_gaussians_third_derivative][code]
+    dL = torch.randn((N,) + (3,) * code + (C,), generator=torch.Generator().manual_seed(5)).to(dev)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    fwd_ms, bwd_ms = [], []
+
+    def step(timed):
+        for t in (means, values, conics):
+            t.grad = None
+        if timed:
+            ev[0].record()
+        out = run()
+        if timed:
+            ev[1].record()
+        out.backward(dL)
+        if timed:
+            ev[2].record()
+            torch.cuda.synchronize()
+            fwd_ms.append(ev[0].elapsed_time(ev[1]))
+            bwd_ms.append(ev[1].elapsed_time(ev[2]))
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(False)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    step(True)
+    ms = elapsed * 1e3 / args.steps
+    result = {
+        "metric": f"sampled points/sec (fwd+bwd), D=3, {P // 1000}k Gaussians x {args.grid3}^3 lattice",
+        "value": N * world / (ms / 1e3), "unit": "points/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic (seeded uniform means, rotated anisotropic covariances, N(0,1) values)",
+        "config": {"workload": f"D=3 {fn}, P={P}, {args.grid3}^3 query lattice, C={C}, fwd+bwd",
+                   "query_points": N, "parallelism": f"replicas x{world}",
+                   "note": "beyond the reference (no D = 3 path there); SURVEY 8f row f4"},
+        "preprocess_ms": pre_ms, "preprocess_first_call_ms": pre[0],
+        "phases_ms": {"forward": fwd_ms[-1], "backward": bwd_ms[-1]},
+        "roofline": None, "cpu_baseline": None,
+    }
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    return 0
 
 
 def bench_aggregate(args, world, rank, dev, torch, dist):

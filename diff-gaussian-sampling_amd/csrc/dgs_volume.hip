@@ -41,7 +41,7 @@ struct Hdr {
     int P, N, nsmall, nbig, ncells;
     int n[3];
     float lo[3], cs[3], E[3];
-    int64_t o_gext, o_gids, o_sids, o_gstart, o_sstart;
+    int64_t o_gext, o_gids, o_sids, o_gstart, o_sstart, o_gpk, o_gek;
 };
 constexpr size_t kHdrBytes = 256;
 static_assert(sizeof(Hdr) <= kHdrBytes, "volume header too large");
@@ -389,6 +389,20 @@ __global__ __launch_bounds__(kBlock) void k_vol_starts(int n, int ncells, const 
         for (int c = k + 1; c <= ncells + 1; ++c) start[c] = n;
 }
 
+// Cell-sorted copies of the small Gaussians' means (id in .w) and cut half-widths: the
+// forward's candidate scan reads them contiguously and rejects a candidate outside its own cut
+// box before touching its conic.
+__global__ __launch_bounds__(kBlock) void k_vol_pack(int nsmall, const int32_t *__restrict__ gids,
+                                                     const float *__restrict__ means,
+                                                     const float4 *__restrict__ gext, float4 *__restrict__ gpk,
+                                                     float4 *__restrict__ gek) {
+    const int i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= nsmall) return;
+    const int g = gids[i];
+    gpk[i] = make_float4(means[(int64_t)g * 3], means[(int64_t)g * 3 + 1], means[(int64_t)g * 3 + 2], __int_as_float(g));
+    gek[i] = gext[g];
+}
+
 __global__ void k_vol_header(Hdr h, char *buf) {
     if (threadIdx.x == 0) *reinterpret_cast<Hdr *>(buf) = h;
 }
@@ -417,6 +431,8 @@ __global__ __launch_bounds__(kBlock) void k_vol_forward(const char *__restrict__
     const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
     const int32_t *__restrict__ sids = reinterpret_cast<const int32_t *>(buf + h.o_sids);
     const int32_t *__restrict__ gstart = reinterpret_cast<const int32_t *>(buf + h.o_gstart);
+    const float4 *__restrict__ gpk = reinterpret_cast<const float4 *>(buf + h.o_gpk);
+    const float4 *__restrict__ gek = reinterpret_cast<const float4 *>(buf + h.o_gek);
     const int sid = sids[j];
     float s[3];
     for (int d = 0; d < 3; ++d) s[d] = samples[(int64_t)sid * 3 + d];
@@ -465,11 +481,14 @@ __global__ __launch_bounds__(kBlock) void k_vol_forward(const char *__restrict__
                                 const int row = (cz * h.n[1] + cy) * h.n[0];
                                 const int b = gstart[row + c0[0]], e = gstart[row + c1[0] + 1];
                                 for (int q = b; q < e; ++q) {
-                                    const int g = gids[q];
+                                    const float4 mp = gpk[q], ge = gek[q];
+                                    const float x[3] = {mp.x - s[0], mp.y - s[1], mp.z - s[2]};
+                                    const float r[3] = {ge.x, ge.y, ge.z};
                                     bool mine = true;
-                                    for (int d = 0; d < 3; ++d)
-                                        mine = mine && image_of(means[(int64_t)g * 3 + d] - s[d]) == kk[d];
-                                    if (mine) visit(g);
+                                    for (int d = 0; d < 3; ++d)  // its own image, inside its own cut box
+                                        mine = mine && image_of(x[d]) == kk[d] &&
+                                               fabsf(x[d] - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                                    if (mine) visit(__float_as_int(mp.w));
                                 }
                             }
                     }
@@ -595,8 +614,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_backward(const char *__restrict_
                         for (int q = b; q < e; ++q) {
                             const int sid = sids[q];
                             bool mine = true;
-                            for (int d = 0; d < 3; ++d)
-                                mine = mine && image_of(m[d] - samples[(int64_t)sid * 3 + d]) == kk[d];
+                            for (int d = 0; d < 3; ++d) {  // its image, inside the cut box
+                                const float x = m[d] - samples[(int64_t)sid * 3 + d];
+                                mine = mine && image_of(x) == kk[d] && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                            }
                             if (mine) bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, samples, hs, sid, dm, dc, dv);
                         }
                     }
@@ -720,7 +741,9 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
     h.o_sids = h.o_gids + a256((size_t)P * 4);
     h.o_gstart = h.o_sids + a256((size_t)N * 4);
     h.o_sstart = h.o_gstart + a256((size_t)(cap + 2) * 4);
-    const size_t total = h.o_sstart + a256((size_t)(cap + 2) * 4);
+    h.o_gpk = h.o_sstart + a256((size_t)(cap + 2) * 4);
+    h.o_gek = h.o_gpk + a256((size_t)P * 16);
+    const size_t total = h.o_gek + a256((size_t)P * 16);
     char *buf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_BINNING, total));
     if (!buf) return fail(DGS_ERR_ALLOC, "dgs_volume_preprocess: binning buffer");
     size_t sort_tmp = 0;
@@ -750,7 +773,9 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
         h.lo[d] = lo;
         h.E[d] = hr.E[d];
         const float ext = hi - lo;
-        h.cs[d] = std::max({hr.E[d], ext / (float)kAxisCells, 1e-6f, ext * 1e-6f});
+        // a quarter of the largest cut: an image window then spans <= 10 cells per axis and its
+        // candidate volume (2E + E/4)^3 instead of (3E)^3 at cell = E
+        h.cs[d] = std::max({0.25f * hr.E[d], ext / (float)kAxisCells, 1e-6f, ext * 1e-6f});
     }
     for (int it = 0; it < 64; ++it) {
         ncells = 1;
@@ -786,6 +811,10 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
         k_vol_starts<<<(unsigned)((nthr + kBlock - 1) / kBlock), kBlock, 0, s>>>(n, h.ncells, keys2, start);
         DGS_LAUNCH_CHECK(s, debug);
     }
+    if (h.nsmall > 0)
+        k_vol_pack<<<(unsigned)((h.nsmall + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+            h.nsmall, reinterpret_cast<const int32_t *>(buf + h.o_gids), means, gext,
+            reinterpret_cast<float4 *>(buf + h.o_gpk), reinterpret_cast<float4 *>(buf + h.o_gek));
     k_vol_header<<<1, 64, 0, s>>>(h, buf);
     DGS_LAUNCH_CHECK(s, debug);
     return DGS_OK;

@@ -63,3 +63,28 @@ def out_components(function, D):
 
 def grad_out(N, K, C, seed=5):
     return torch.randn(N, K, C, generator=_gen(seed), dtype=torch.float64).float()
+
+
+def gaussians3(P, C=1, seed=0, scale=1.0):
+    """D = 3 field: means ~ U[-1, 1)^3, per-axis sigma ~ h U[0.5, 1.5] with
+    h = 2 / P^(1/3), a random rotation (QR of a normal matrix); conics packed
+    [c00 c01 c02 c11 c12 c22] (include/dgs_volume.h), covariances likewise.  float32 CPU."""
+    g = _gen(seed)
+    means = torch.rand(P, 3, generator=g, dtype=torch.float64) * 2.0 - 1.0
+    h = 2.0 / (max(P, 1) ** (1.0 / 3.0)) * scale
+    sig = h * (0.5 + torch.rand(P, 3, generator=_gen(seed + 1), dtype=torch.float64))
+    q, _ = torch.linalg.qr(torch.randn(P, 3, 3, generator=_gen(seed + 2), dtype=torch.float64))
+    cov = q @ torch.diag_embed(sig ** 2) @ q.transpose(1, 2)
+    inv = torch.linalg.inv(cov)
+    iu = [(0, 0), (0, 1), (0, 2), (1, 1), (1, 2), (2, 2)]
+    conics = torch.stack([inv[:, i, j] for i, j in iu], -1)
+    covs = torch.stack([cov[:, i, j] for i, j in iu], -1)
+    values = torch.randn(P, C, generator=_gen(seed + 3), dtype=torch.float64)
+    return means.float(), values.float(), covs.float(), conics.float()
+
+
+def grid_samples3(n):
+    """A regular n^3 lattice on [-1, 1)^3 (the "256^3 grid" of BASELINE config 5)."""
+    ax = torch.arange(n, dtype=torch.float64) * (2.0 / n) - 1.0
+    z, y, x = torch.meshgrid(ax, ax, ax, indexing="ij")
+    return torch.stack([x.reshape(-1), y.reshape(-1), z.reshape(-1)], -1).float()
