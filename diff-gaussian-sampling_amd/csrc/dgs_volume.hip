@@ -112,7 +112,8 @@ __device__ __forceinline__ int image_of(float x) {
 }
 
 // One pair: wrapped X, power (exact operation order of include/dgs_volume.h, no contraction,
-// so that the numpy oracle reproduces it bit for bit), G and a = A X.  False: power > 0.
+// so that the numpy oracle reproduces it bit for bit), G and a = A X.  False: power > 0 (the
+// reference's skip) or G == +0 (the pair adds exactly nothing; half of the cut box's pairs).
 __device__ __forceinline__ bool pair_eval(const float *m, const float *s, const float *c, float *X,
                                           float &G, float *a) {
     DGS_NO_CONTRACT
@@ -122,6 +123,7 @@ __device__ __forceinline__ bool pair_eval(const float *m, const float *s, const 
     const float power = -0.5f * qd - qo;
     if (power > 0.0f) return false;
     G = expf(power);
+    if (G == 0.0f) return false;  // exactly 0: adds nothing (finite values and terms)
     a[0] = c[0] * X[0] + c[1] * X[1] + c[2] * X[2];
     a[1] = c[1] * X[0] + c[3] * X[1] + c[4] * X[2];
     a[2] = c[2] * X[0] + c[4] * X[1] + c[5] * X[2];
@@ -408,96 +410,152 @@ __global__ void k_vol_header(Hdr h, char *buf) {
 }
 
 // ------------------------------------------------------------------------------ forward
-// Lane = sample (sorted by cell).  Images of the sample's cut windows (reach E, the largest
-// small-Gaussian cut) over the Gaussian grid; the candidates of a row of cells are one range of
-// the cell-sorted ids; each candidate is evaluated only through the image of its own
-// displacement.  Then every big Gaussian.
+// One wave per (sample cell, 64 of its samples), lane = sample.  The wave walks the image
+// windows of the whole cell (reach E, the largest small-Gaussian cut): the candidates of a row
+// of cells are one range of the cell-sorted Gaussians, staged 64 at a time in LDS (one
+// coalesced load per lane: mean, cut widths, conic) and read back as broadcasts.  Each lane
+// keeps a candidate only through the image of its own displacement and inside the candidate's
+// own cut box, then evaluates the pair.  Then every big Gaussian.  Outputs summed in registers.
+constexpr int kVolFwdBlocks = 8192;
+
+struct VCand {
+    float4 mp;  // mean, id bits in .w
+    float4 ge;  // cut half-widths
+    float c[6];
+};
+
 template <int FN, int CB>
-__global__ __launch_bounds__(kBlock) void k_vol_forward(const char *__restrict__ buf, int P, int N, int C, int cbase,
-                                                        const float *__restrict__ means,
-                                                        const float *__restrict__ values,
-                                                        const float *__restrict__ conics,
-                                                        const float *__restrict__ samples, float *__restrict__ out) {
+__global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ buf, int P, int N, int C, int cbase,
+                                                       const float *__restrict__ means,
+                                                       const float *__restrict__ values,
+                                                       const float *__restrict__ conics,
+                                                       const float *__restrict__ samples, float *__restrict__ out) {
     constexpr int KU = VTr<FN>::KU, K = VTr<FN>::K;
+    __shared__ VCand cand[kWave];
     const Hdr h = hdr_of(buf);
-    const int j = blockIdx.x * kBlock + threadIdx.x;
-    if (j >= N) return;
+    const int lane = threadIdx.x;
     const int nch = min(CB, C - cbase);
     if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
-        for (int f = 0; f < K; ++f)
-            for (int ch = 0; ch < nch; ++ch) out[((int64_t)j * K + f) * C + cbase + ch] = NAN;
+        for (int64_t j = (int64_t)blockIdx.x * kWave + lane; j < N; j += (int64_t)gridDim.x * kWave)
+            for (int f = 0; f < K; ++f)
+                for (int ch = 0; ch < nch; ++ch) out[(j * K + f) * C + cbase + ch] = NAN;
         return;
     }
     const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
     const int32_t *__restrict__ sids = reinterpret_cast<const int32_t *>(buf + h.o_sids);
     const int32_t *__restrict__ gstart = reinterpret_cast<const int32_t *>(buf + h.o_gstart);
+    const int32_t *__restrict__ sstart = reinterpret_cast<const int32_t *>(buf + h.o_sstart);
     const float4 *__restrict__ gpk = reinterpret_cast<const float4 *>(buf + h.o_gpk);
     const float4 *__restrict__ gek = reinterpret_cast<const float4 *>(buf + h.o_gek);
-    const int sid = sids[j];
-    float s[3];
-    for (int d = 0; d < 3; ++d) s[d] = samples[(int64_t)sid * 3 + d];
-    float acc[KU][CB];
-    for (int u = 0; u < KU; ++u)
-        for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
 
-    auto visit = [&](int g) {
-        float m[3], c[6], X[3], a[3], G, t[KU];
-        for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
-        for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
-        if (!pair_eval(m, s, c, X, G, a)) return;
-        terms<FN>(a, c, t);
-        for (int ch = 0; ch < nch; ++ch) {
-            const float v = values[(int64_t)g * C + cbase + ch];
-            for (int u = 0; u < KU; ++u) acc[u][ch] += v * G * t[u];
-        }
-    };
-
-    if (h.nsmall > 0) {
-        Win w[3];
-        bool ok = true;
-        for (int d = 0; d < 3; ++d) {
-            w[d] = image_range(s[d], h.E[d], h.lo[d], h.lo[d] + h.cs[d] * h.n[d], true);
-            ok = ok && s[d] == s[d];
-        }
-        if (ok)
-            for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
-                for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
-                    for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
-                        const int kk[3] = {kx, ky, kz};
-                        int c0[3], c1[3];
-                        bool any = true;
-                        for (int d = 0; d < 3; ++d) {
-                            float xa, xb;
-                            image_window(kk[d], h.E[d], xa, xb);
-                            const float ta = s[d] + xa, tb = s[d] + xb;  // mean window
-                            const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
-                            if (tb < glo || ta > ghi) { any = false; break; }
-                            c0[d] = cell_axis(h, d, ta);
-                            c1[d] = cell_axis(h, d, tb);
-                        }
-                        if (!any) continue;
-                        for (int cz = c0[2]; cz <= c1[2]; ++cz)
-                            for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                                const int row = (cz * h.n[1] + cy) * h.n[0];
-                                const int b = gstart[row + c0[0]], e = gstart[row + c1[0] + 1];
-                                for (int q = b; q < e; ++q) {
-                                    const float4 mp = gpk[q], ge = gek[q];
-                                    const float x[3] = {mp.x - s[0], mp.y - s[1], mp.z - s[2]};
-                                    const float r[3] = {ge.x, ge.y, ge.z};
-                                    bool mine = true;
-                                    for (int d = 0; d < 3; ++d)  // its own image, inside its own cut box
-                                        mine = mine && image_of(x[d]) == kk[d] &&
-                                               fabsf(x[d] - 2.0f * kk[d]) <= r[d] + 1e-5f;
-                                    if (mine) visit(__float_as_int(mp.w));
-                                }
-                            }
+    for (int cell = blockIdx.x; cell < h.ncells; cell += gridDim.x) {
+        const int sb = sstart[cell], se = sstart[cell + 1];
+        const int cc[3] = {cell % h.n[0], (cell / h.n[0]) % h.n[1], cell / (h.n[0] * h.n[1])};
+        for (int j0 = sb; j0 < se; j0 += kWave) {
+            const int j = j0 + lane;
+            const bool active = j < se;
+            const int sid = active ? sids[j] : 0;
+            float s[3];
+            for (int d = 0; d < 3; ++d) s[d] = active ? samples[(int64_t)sid * 3 + d] : 0.0f;
+            float acc[KU][CB];
+            for (int u = 0; u < KU; ++u)
+                for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
+            auto eval = [&](int g, const float *m, const float *c) {
+                float X[3], a[3], G, t[KU];
+                if (!pair_eval(m, s, c, X, G, a)) return;
+                terms<FN>(a, c, t);
+                for (int ch = 0; ch < nch; ++ch) {
+                    const float v = values[(int64_t)g * C + cbase + ch];
+                    for (int u = 0; u < KU; ++u) acc[u][ch] += v * G * t[u];
+                }
+            };
+            if (h.nsmall > 0) {
+                // the chunk's sample box (its cell's, widened by the rounding of the grid)
+                float bl[3], bh[3];
+                Win w[3];
+                for (int d = 0; d < 3; ++d) {
+                    bl[d] = h.lo[d] + h.cs[d] * cc[d] - 1e-5f;
+                    bh[d] = h.lo[d] + h.cs[d] * (cc[d] + 1) + 1e-5f;
+                    if (cc[d] == 0) bl[d] = -INFINITY;  // (clamped cells hold everything below / above)
+                    if (cc[d] == h.n[d] - 1) bh[d] = INFINITY;
+                    float mn = INFINITY, mx = -INFINITY;
+                    if (active) { mn = s[d]; mx = s[d]; }
+                    for (int o = kWave / 2; o > 0; o >>= 1) {
+                        mn = fminf(mn, __shfl_xor(mn, o));
+                        mx = fmaxf(mx, __shfl_xor(mx, o));
                     }
-    }
-    for (int q = gstart[h.ncells]; q < gstart[h.ncells + 1]; ++q) visit(gids[q]);  // big ones
-
-    for (int f = 0; f < K; ++f) {
-        const int u = umap<FN>(f);
-        for (int ch = 0; ch < nch; ++ch) out[((int64_t)sid * K + f) * C + cbase + ch] = acc[u][ch];
+                    bl[d] = fmaxf(bl[d], mn);
+                    bh[d] = fminf(bh[d], mx);
+                    const float ghi = h.lo[d] + h.cs[d] * h.n[d];
+                    const Win wa = image_range(bl[d], h.E[d], h.lo[d], ghi, true);
+                    const Win wb = image_range(bh[d], h.E[d], h.lo[d], ghi, true);
+                    w[d].k0 = min(wa.k0, wb.k0);
+                    w[d].k1 = max(wa.k1, wb.k1);
+                }
+                for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
+                    for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
+                        for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
+                            const int kk[3] = {kx, ky, kz};
+                            int c0[3], c1[3];
+                            bool any = true;
+                            for (int d = 0; d < 3; ++d) {
+                                float xa, xb;
+                                image_window(kk[d], h.E[d], xa, xb);
+                                const float ta = bl[d] + xa, tb = bh[d] + xb;  // mean window
+                                const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
+                                if (tb < glo || ta > ghi) { any = false; break; }
+                                c0[d] = cell_axis(h, d, ta);
+                                c1[d] = cell_axis(h, d, tb);
+                            }
+                            if (!any) continue;
+                            for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                                for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                                    const int row = (cz * h.n[1] + cy) * h.n[0];
+                                    const int b = gstart[row + c0[0]], e = gstart[row + c1[0] + 1];
+                                    for (int q0 = b; q0 < e; q0 += kWave) {
+                                        const int q = q0 + lane;
+                                        __syncthreads();
+                                        if (q < e) {
+                                            VCand v;
+                                            v.mp = gpk[q];
+                                            v.ge = gek[q];
+                                            const int g = __float_as_int(v.mp.w);
+                                            for (int k = 0; k < 6; ++k) v.c[k] = conics[(int64_t)g * 6 + k];
+                                            cand[lane] = v;
+                                        }
+                                        __syncthreads();
+                                        const int cnt = min(kWave, e - q0);
+                                        if (active)
+                                            for (int u = 0; u < cnt; ++u) {
+                                                const float4 mp = cand[u].mp, ge = cand[u].ge;
+                                                const float m[3] = {mp.x, mp.y, mp.z};
+                                                const float r[3] = {ge.x, ge.y, ge.z};
+                                                bool mine = true;
+                                                for (int d = 0; d < 3; ++d) {  // own image, own cut box
+                                                    const float x = m[d] - s[d];
+                                                    mine = mine && image_of(x) == kk[d] &&
+                                                           fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                                                }
+                                                if (mine) eval(__float_as_int(mp.w), m, cand[u].c);
+                                            }
+                                    }
+                                }
+                        }
+            }
+            if (active) {
+                for (int q = gstart[h.ncells]; q < gstart[h.ncells + 1]; ++q) {  // big ones
+                    const int g = gids[q];
+                    float m[3], c[6];
+                    for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
+                    for (int k = 0; k < 6; ++k) c[k] = conics[(int64_t)g * 6 + k];
+                    eval(g, m, c);
+                }
+                for (int f = 0; f < K; ++f) {
+                    const int u = umap<FN>(f);
+                    for (int ch = 0; ch < nch; ++ch) out[((int64_t)sid * K + f) * C + cbase + ch] = acc[u][ch];
+                }
+            }
+        }
     }
 }
 
@@ -520,11 +578,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_hsum(int N, int C, const float *
 // One pair's contribution to a Gaussian's gradient sums.
 template <int FN, int CB>
 __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const float *__restrict__ values, int g,
-                                         int C, int cbase, int nch, const float *__restrict__ samples,
+                                         int C, int cbase, int nch, const float *s,
                                          const float *__restrict__ hs, int sid, float *dm, float *dc, float *dv) {
     constexpr int KU = VTr<FN>::KU;
-    float s[3], X[3], a[3], G, t[KU];
-    for (int d = 0; d < 3; ++d) s[d] = samples[(int64_t)sid * 3 + d];
+    float X[3], a[3], G, t[KU];
     if (!pair_eval(m, s, c, X, G, a)) return;
     terms<FN>(a, c, t);
     const float *hrow = hs + (int64_t)sid * KU * C;
@@ -557,72 +614,120 @@ __device__ __forceinline__ void bwd_store(int g, int C, int cbase, int nch, cons
     for (int ch = 0; ch < nch; ++ch) dvalues[(int64_t)g * C + cbase + ch] = dv[ch];
 }
 
-// Lane = small Gaussian (sorted by cell): the samples of its cut's images.
+// One wave per (Gaussian cell, 64 of its small Gaussians), lane = Gaussian.  The wave walks
+// the image windows of its Gaussians' union (means box, largest cut among them): the samples of
+// a row of cells are one range of the cell-sorted samples, staged 64 at a time in LDS (one
+// coalesced load per lane) and read back as broadcasts.  Each lane keeps a sample only through
+// the image of its own displacement and inside its own cut box; gradients summed in registers
+// and written once (no atomics).
+constexpr int kVolBwdBlocks = 8192;
+
 template <int FN, int CB>
-__global__ __launch_bounds__(kBlock) void k_vol_backward(const char *__restrict__ buf, int P, int N, int C, int cbase,
-                                                         const float *__restrict__ means,
-                                                         const float *__restrict__ values,
-                                                         const float *__restrict__ conics,
-                                                         const float *__restrict__ samples,
-                                                         const float *__restrict__ hs, float *__restrict__ dmeans,
-                                                         float *__restrict__ dvalues, float *__restrict__ dconics) {
+__global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__ buf, int P, int N, int C, int cbase,
+                                                        const float *__restrict__ means,
+                                                        const float *__restrict__ values,
+                                                        const float *__restrict__ conics,
+                                                        const float *__restrict__ samples,
+                                                        const float *__restrict__ hs, float *__restrict__ dmeans,
+                                                        float *__restrict__ dvalues, float *__restrict__ dconics) {
+    __shared__ float4 scand[kWave];
     const Hdr h = hdr_of(buf);
-    const int i = blockIdx.x * kBlock + threadIdx.x;
+    const int lane = threadIdx.x;
+    const int nch = min(CB, C - cbase);
     if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
-        if (i < P) {
-            const float nan[9] = {NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
-            bwd_store<CB>(i, C, cbase, min(CB, C - cbase), nan, nan, nan, dmeans, dvalues, dconics);
-        }
+        const float nan[9] = {NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
+        for (int64_t i = (int64_t)blockIdx.x * kWave + lane; i < P; i += (int64_t)gridDim.x * kWave)
+            bwd_store<CB>((int)i, C, cbase, nch, nan, nan, nan, dmeans, dvalues, dconics);
         return;
     }
-    if (i >= h.nsmall) return;
-    const int nch = min(CB, C - cbase);
     const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
     const int32_t *__restrict__ sids = reinterpret_cast<const int32_t *>(buf + h.o_sids);
+    const int32_t *__restrict__ gstart = reinterpret_cast<const int32_t *>(buf + h.o_gstart);
     const int32_t *__restrict__ sstart = reinterpret_cast<const int32_t *>(buf + h.o_sstart);
-    const float4 *__restrict__ gext = reinterpret_cast<const float4 *>(buf + h.o_gext);
-    const int g = gids[i];
-    const float4 ex = gext[g];
-    const float r[3] = {ex.x, ex.y, ex.z};
-    float m[3], c[6];
-    for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
-    for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
-    float dm[3] = {0.0f, 0.0f, 0.0f}, dc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dv[CB];
-    for (int ch = 0; ch < CB; ++ch) dv[ch] = 0.0f;
-    Win w[3];
-    for (int d = 0; d < 3; ++d) w[d] = image_range(m[d], r[d], h.lo[d], h.lo[d] + h.cs[d] * h.n[d], false);
-    for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
-        for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
-            for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
-                const int kk[3] = {kx, ky, kz};
-                int c0[3], c1[3];
-                bool any = true;
-                for (int d = 0; d < 3; ++d) {
-                    float xa, xb;
-                    image_window(kk[d], r[d], xa, xb);
-                    const float ta = m[d] - xb, tb = m[d] - xa;  // sample window
-                    const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
-                    if (tb < glo || ta > ghi) { any = false; break; }
-                    c0[d] = cell_axis(h, d, ta);
-                    c1[d] = cell_axis(h, d, tb);
-                }
-                if (!any) continue;
-                for (int cz = c0[2]; cz <= c1[2]; ++cz)
-                    for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                        const int row = (cz * h.n[1] + cy) * h.n[0];
-                        const int b = sstart[row + c0[0]], e = sstart[row + c1[0] + 1];
-                        for (int q = b; q < e; ++q) {
-                            const int sid = sids[q];
-                            bool mine = true;
-                            for (int d = 0; d < 3; ++d) {  // its image, inside the cut box
-                                const float x = m[d] - samples[(int64_t)sid * 3 + d];
-                                mine = mine && image_of(x) == kk[d] && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
-                            }
-                            if (mine) bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, samples, hs, sid, dm, dc, dv);
-                        }
-                    }
+    const float4 *__restrict__ gpk = reinterpret_cast<const float4 *>(buf + h.o_gpk);
+    const float4 *__restrict__ gek = reinterpret_cast<const float4 *>(buf + h.o_gek);
+    for (int cell = blockIdx.x; cell < h.ncells; cell += gridDim.x) {
+        const int gb = gstart[cell], ge = gstart[cell + 1];
+        for (int i0 = gb; i0 < ge; i0 += kWave) {
+            const int i = i0 + lane;
+            const bool active = i < ge;
+            float m[3] = {0.0f, 0.0f, 0.0f}, r[3] = {0.0f, 0.0f, 0.0f}, c[6];
+            int g = 0;
+            if (active) {
+                const float4 mp = gpk[i], ex = gek[i];
+                g = __float_as_int(mp.w);
+                m[0] = mp.x; m[1] = mp.y; m[2] = mp.z;
+                r[0] = ex.x; r[1] = ex.y; r[2] = ex.z;
+                for (int k = 0; k < 6; ++k) c[k] = conics[(int64_t)g * 6 + k];
+            } else {
+                for (int k = 0; k < 6; ++k) c[k] = 0.0f;
             }
-    bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics);
+            float dm[3] = {0.0f, 0.0f, 0.0f}, dc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dv[CB];
+            for (int ch = 0; ch < CB; ++ch) dv[ch] = 0.0f;
+            float ml[3], mh[3], R[3];
+            Win w[3];
+            for (int d = 0; d < 3; ++d) {
+                float mn = active ? m[d] : INFINITY, mx = active ? m[d] : -INFINITY, rr = r[d];
+                for (int o = kWave / 2; o > 0; o >>= 1) {
+                    mn = fminf(mn, __shfl_xor(mn, o));
+                    mx = fmaxf(mx, __shfl_xor(mx, o));
+                    rr = fmaxf(rr, __shfl_xor(rr, o));
+                }
+                ml[d] = mn; mh[d] = mx; R[d] = rr;
+                const float ghi = h.lo[d] + h.cs[d] * h.n[d];
+                const Win wa = image_range(mn, rr, h.lo[d], ghi, false);
+                const Win wb = image_range(mx, rr, h.lo[d], ghi, false);
+                w[d].k0 = min(wa.k0, wb.k0);
+                w[d].k1 = max(wa.k1, wb.k1);
+            }
+            for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
+                for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
+                    for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
+                        const int kk[3] = {kx, ky, kz};
+                        int c0[3], c1[3];
+                        bool any = true;
+                        for (int d = 0; d < 3; ++d) {
+                            float xa, xb;
+                            image_window(kk[d], R[d], xa, xb);
+                            const float ta = ml[d] - xb, tb = mh[d] - xa;  // sample window
+                            const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
+                            if (tb < glo || ta > ghi) { any = false; break; }
+                            c0[d] = cell_axis(h, d, ta);
+                            c1[d] = cell_axis(h, d, tb);
+                        }
+                        if (!any) continue;
+                        for (int cz = c0[2]; cz <= c1[2]; ++cz)
+                            for (int cy = c0[1]; cy <= c1[1]; ++cy) {
+                                const int row = (cz * h.n[1] + cy) * h.n[0];
+                                const int b = sstart[row + c0[0]], e = sstart[row + c1[0] + 1];
+                                for (int q0 = b; q0 < e; q0 += kWave) {
+                                    const int q = q0 + lane;
+                                    __syncthreads();
+                                    if (q < e) {
+                                        const int sid = sids[q];
+                                        scand[lane] = make_float4(samples[(int64_t)sid * 3], samples[(int64_t)sid * 3 + 1],
+                                                                  samples[(int64_t)sid * 3 + 2], __int_as_float(sid));
+                                    }
+                                    __syncthreads();
+                                    const int cnt = min(kWave, e - q0);
+                                    if (active)
+                                        for (int u = 0; u < cnt; ++u) {
+                                            const float4 sp = scand[u];
+                                            const float sv[3] = {sp.x, sp.y, sp.z};
+                                            bool mine = true;
+                                            for (int d = 0; d < 3; ++d) {  // own image, own cut box
+                                                const float x = m[d] - sv[d];
+                                                mine = mine && image_of(x) == kk[d] && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                                            }
+                                            if (mine)
+                                                bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, sv, hs, __float_as_int(sp.w), dm, dc, dv);
+                                        }
+                                }
+                            }
+                    }
+            if (active) bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics);
+        }
+    }
 }
 
 // Big Gaussians: one block each, threads striding over every sample, block sums.
@@ -650,8 +755,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_backward_big(const char *__restr
         for (int q = 0; q < 6; ++q) c[q] = conics[(int64_t)g * 6 + q];
         float v[NV];
         for (int k = 0; k < NV; ++k) v[k] = 0.0f;
-        for (int sid = threadIdx.x; sid < N; sid += kBlock)
-            bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, samples, hs, sid, v, v + 3, v + 9);
+        for (int sid = threadIdx.x; sid < N; sid += kBlock) {
+            const float sp[3] = {samples[(int64_t)sid * 3], samples[(int64_t)sid * 3 + 1], samples[(int64_t)sid * 3 + 2]};
+            bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, sp, hs, sid, v, v + 3, v + 9);
+        }
         for (int k = 0; k < NV; ++k)
             for (int o = kWave / 2; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
         if (lane == 0)
@@ -675,7 +782,7 @@ template <int FN, int CB>
 static void launch_fwd(const char *buf, int P, int N, int C, const float *means, const float *values,
                        const float *conics, const float *samples, float *out, hipStream_t s) {
     for (int cb = 0; cb < C; cb += CB)
-        k_vol_forward<FN, CB><<<(unsigned)((N + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+        k_vol_forward<FN, CB><<<kVolFwdBlocks, kWave, 0, s>>>(
             buf, P, N, C, cb, means, values, conics, samples, out);
 }
 template <int FN, int CB>
@@ -686,8 +793,8 @@ static void launch_bwd(const char *buf, int P, int N, int C, const float *means,
     if (nh > 0) k_vol_hsum<FN><<<(unsigned)((nh + kBlock - 1) / kBlock), kBlock, 0, s>>>(N, C, dL, hs);
     for (int cb = 0; cb < C; cb += CB) {
         if (P > 0)
-            k_vol_backward<FN, CB><<<(unsigned)((P + kBlock - 1) / kBlock), kBlock, 0, s>>>(
-                buf, P, N, C, cb, means, values, conics, samples, hs, dm, dv, dc);
+            k_vol_backward<FN, CB><<<kVolBwdBlocks, kWave, 0, s>>>(buf, P, N, C, cb, means, values, conics, samples,
+                                                                   hs, dm, dv, dc);
         k_vol_backward_big<FN, CB><<<256, kBlock, 0, s>>>(buf, P, N, C, cb, means, values, conics, samples, hs,
                                                            dm, dv, dc);
     }
