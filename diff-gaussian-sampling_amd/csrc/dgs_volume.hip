@@ -418,10 +418,12 @@ __global__ void k_vol_header(Hdr h, char *buf) {
 // own cut box, then evaluates the pair.  Then every big Gaussian.  Outputs summed in registers.
 constexpr int kVolFwdBlocks = 8192;
 
+template <int CB>
 struct VCand {
     float4 mp;  // mean, id bits in .w
     float4 ge;  // cut half-widths
     float c[6];
+    float v[CB];  // values of the launch's channel block
 };
 
 template <int FN, int CB>
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                                                        const float *__restrict__ conics,
                                                        const float *__restrict__ samples, float *__restrict__ out) {
     constexpr int KU = VTr<FN>::KU, K = VTr<FN>::K;
-    __shared__ VCand cand[kWave];
+    __shared__ VCand<CB> cand[kWave];
     const Hdr h = hdr_of(buf);
     const int lane = threadIdx.x;
     const int nch = min(CB, C - cbase);
@@ -460,12 +462,12 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
             float acc[KU][CB];
             for (int u = 0; u < KU; ++u)
                 for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
-            auto eval = [&](int g, const float *m, const float *c) {
+            auto eval = [&](const float *m, const float *c, const float *vr) {
                 float X[3], a[3], G, t[KU];
                 if (!pair_eval(m, s, c, X, G, a)) return;
                 terms<FN>(a, c, t);
                 for (int ch = 0; ch < nch; ++ch) {
-                    const float v = values[(int64_t)g * C + cbase + ch];
+                    const float v = vr[ch];
                     for (int u = 0; u < KU; ++u) acc[u][ch] += v * G * t[u];
                 }
             };
@@ -516,11 +518,13 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                                         const int q = q0 + lane;
                                         __syncthreads();
                                         if (q < e) {
-                                            VCand v;
+                                            VCand<CB> v;
                                             v.mp = gpk[q];
                                             v.ge = gek[q];
                                             const int g = __float_as_int(v.mp.w);
                                             for (int k = 0; k < 6; ++k) v.c[k] = conics[(int64_t)g * 6 + k];
+                                            for (int ch = 0; ch < CB; ++ch)
+                                                v.v[ch] = ch < nch ? values[(int64_t)g * C + cbase + ch] : 0.0f;
                                             cand[lane] = v;
                                         }
                                         __syncthreads();
@@ -536,7 +540,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                                                     mine = mine && image_of(x) == kk[d] &&
                                                            fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
                                                 }
-                                                if (mine) eval(__float_as_int(mp.w), m, cand[u].c);
+                                                if (mine) eval(m, cand[u].c, cand[u].v);
                                             }
                                     }
                                 }
@@ -548,7 +552,9 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                     float m[3], c[6];
                     for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
                     for (int k = 0; k < 6; ++k) c[k] = conics[(int64_t)g * 6 + k];
-                    eval(g, m, c);
+                    float vr[CB];
+                    for (int ch = 0; ch < CB; ++ch) vr[ch] = ch < nch ? values[(int64_t)g * C + cbase + ch] : 0.0f;
+                    eval(m, c, vr);
                 }
                 for (int f = 0; f < K; ++f) {
                     const int u = umap<FN>(f);
@@ -575,26 +581,35 @@ __global__ __launch_bounds__(kBlock) void k_vol_hsum(int N, int C, const float *
     for (int u = 0; u < KU; ++u) hs[(sid * KU + u) * C + ch] = h[u];
 }
 
-// One pair's contribution to a Gaussian's gradient sums.
+// One pair's contribution to a Gaussian's gradient sums.  hrow: the sample's h row [KU][C]
+// (LDS or global); CB == 1 means C == 1, with the Gaussian's value v0 in a register.
 template <int FN, int CB>
 __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const float *__restrict__ values, int g,
-                                         int C, int cbase, int nch, const float *s,
-                                         const float *__restrict__ hs, int sid, float *dm, float *dc, float *dv) {
+                                         float v0, int C, int cbase, int nch, const float *s, const float *hrow,
+                                         float *dm, float *dc, float *dv) {
     constexpr int KU = VTr<FN>::KU;
     float X[3], a[3], G, t[KU];
     if (!pair_eval(m, s, c, X, G, a)) return;
     terms<FN>(a, c, t);
-    const float *hrow = hs + (int64_t)sid * KU * C;
     float hv[KU];
-    for (int u = 0; u < KU; ++u) hv[u] = 0.0f;
-    for (int ch = 0; ch < C; ++ch) {
-        const float v = values[(int64_t)g * C + ch];
-        for (int u = 0; u < KU; ++u) hv[u] += v * hrow[u * C + ch];
-    }
-    for (int ch = 0; ch < nch; ++ch) {
+    if constexpr (CB == 1) {
         float p = 0.0f;
-        for (int u = 0; u < KU; ++u) p += hrow[u * C + cbase + ch] * t[u];
-        dv[ch] += G * p;
+        for (int u = 0; u < KU; ++u) {
+            hv[u] = v0 * hrow[u];
+            p += hrow[u] * t[u];
+        }
+        dv[0] += G * p;
+    } else {
+        for (int u = 0; u < KU; ++u) hv[u] = 0.0f;
+        for (int ch = 0; ch < C; ++ch) {
+            const float v = values[(int64_t)g * C + ch];
+            for (int u = 0; u < KU; ++u) hv[u] += v * hrow[u * C + ch];
+        }
+        for (int ch = 0; ch < nch; ++ch) {
+            float p = 0.0f;
+            for (int u = 0; u < KU; ++u) p += hrow[u * C + cbase + ch] * t[u];
+            dv[ch] += G * p;
+        }
     }
     float phi = 0.0f;
     for (int u = 0; u < KU; ++u) phi += hv[u] * t[u];
@@ -630,7 +645,9 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                                         const float *__restrict__ samples,
                                                         const float *__restrict__ hs, float *__restrict__ dmeans,
                                                         float *__restrict__ dvalues, float *__restrict__ dconics) {
+    constexpr int KU = VTr<FN>::KU;
     __shared__ float4 scand[kWave];
+    __shared__ float shrow[kWave][CB == 1 ? KU : 1];  // C == 1: the candidates' h rows
     const Hdr h = hdr_of(buf);
     const int lane = threadIdx.x;
     const int nch = min(CB, C - cbase);
@@ -653,9 +670,11 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
             const bool active = i < ge;
             float m[3] = {0.0f, 0.0f, 0.0f}, r[3] = {0.0f, 0.0f, 0.0f}, c[6];
             int g = 0;
+            float v0 = 0.0f;
             if (active) {
                 const float4 mp = gpk[i], ex = gek[i];
                 g = __float_as_int(mp.w);
+                if constexpr (CB == 1) v0 = values[g];
                 m[0] = mp.x; m[1] = mp.y; m[2] = mp.z;
                 r[0] = ex.x; r[1] = ex.y; r[2] = ex.z;
                 for (int k = 0; k < 6; ++k) c[k] = conics[(int64_t)g * 6 + k];
@@ -707,6 +726,8 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                         const int sid = sids[q];
                                         scand[lane] = make_float4(samples[(int64_t)sid * 3], samples[(int64_t)sid * 3 + 1],
                                                                   samples[(int64_t)sid * 3 + 2], __int_as_float(sid));
+                                        if constexpr (CB == 1)
+                                            for (int u = 0; u < KU; ++u) shrow[lane][u] = hs[(int64_t)sid * KU + u];
                                     }
                                     __syncthreads();
                                     const int cnt = min(kWave, e - q0);
@@ -719,8 +740,11 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                                 const float x = m[d] - sv[d];
                                                 mine = mine && image_of(x) == kk[d] && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
                                             }
-                                            if (mine)
-                                                bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, sv, hs, __float_as_int(sp.w), dm, dc, dv);
+                                            if (mine) {
+                                                const float *hrow = CB == 1 ? &shrow[u][0]
+                                                                            : hs + (int64_t)__float_as_int(sp.w) * KU * C;
+                                                bwd_pair<FN, CB>(m, c, values, g, v0, C, cbase, nch, sv, hrow, dm, dc, dv);
+                                            }
                                         }
                                 }
                             }
@@ -757,7 +781,8 @@ __global__ __launch_bounds__(kBlock) void k_vol_backward_big(const char *__restr
         for (int k = 0; k < NV; ++k) v[k] = 0.0f;
         for (int sid = threadIdx.x; sid < N; sid += kBlock) {
             const float sp[3] = {samples[(int64_t)sid * 3], samples[(int64_t)sid * 3 + 1], samples[(int64_t)sid * 3 + 2]};
-            bwd_pair<FN, CB>(m, c, values, g, C, cbase, nch, sp, hs, sid, v, v + 3, v + 9);
+            bwd_pair<FN, CB>(m, c, values, g, CB == 1 ? values[g] : 0.0f, C, cbase, nch, sp,
+                             hs + (int64_t)sid * VTr<FN>::KU * C, v, v + 3, v + 9);
         }
         for (int k = 0; k < NV; ++k)
             for (int o = kWave / 2; o > 0; o >>= 1) v[k] += __shfl_xor(v[k], o);
