@@ -480,6 +480,16 @@ def bench_volume(args, world, rank, dev, torch, dist):
         elapsed = float(e.item())
     step(True)
     ms = elapsed * 1e3 / args.steps
+    from diff_gaussian_sampling import _C
+    w_eval, w_live = _C.volume_count_pairs(means.detach(), conics.detach(), samples, vs.binning)
+    # forward FLOPs per live pair of the D = 3 expressions (include/dgs_volume.h), C = 1: X 3,
+    # the two quadratic sums 8 + 8, power 2, expf 4 (FLOP-eq), a = A X 15 (functions >= 1), the
+    # unique terms (laplacian 6 x 2, third 10 x 8) and v G t accumulated, 3 per unique component
+    # and channel
+    KU = [1, 3, 6, 10][code]
+    f_fwd = 25 + [0, 15, 15, 15][code] + [0, 0, 12, 80][code] + 3 * KU * C
+    fwd_s = fwd_ms[-1] * 1e-3
+    ach = w_live * f_fwd / fwd_s / 1e12
     result = {
         "metric": f"sampled points/sec (fwd+bwd), D=3, {P // 1000}k Gaussians x {args.grid3}^3 lattice",
         "value": N * world / (ms / 1e3), "unit": "points/s", "n_gpus": world, "steps": args.steps,
@@ -491,7 +501,11 @@ def bench_volume(args, world, rank, dev, torch, dist):
                    "note": "beyond the reference (no D = 3 path there); SURVEY 8f row f4"},
         "preprocess_ms": pre_ms, "preprocess_first_call_ms": pre[0],
         "phases_ms": {"forward": fwd_ms[-1], "backward": bwd_ms[-1]},
-        "roofline": None, "cpu_baseline": None,
+        "pairs": {"W_eval": int(w_eval), "W_live": int(w_live)},
+        "roofline": {"bound": "valu", "kernel": "k_vol_forward", "achieved": ach, "peak": PEAK_FP32_VALU_TFLOPS,
+                     "unit": "TFLOP/s", "frac": ach / PEAK_FP32_VALU_TFLOPS, "traffic": None,
+                     "flops_per_live_pair": f_fwd, "flops_basis": "D = 3 expressions, DESIGN.md 4.8"},
+        "cpu_baseline": None,
     }
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -9,9 +9,12 @@
 //   * "small" Gaussians (well-conditioned positive-definite conic, every E_d <= 0.45) meet a
 //     sample only through the torus images of the cut: per axis the displacement x = m - s
 //     lies in [-E, E] (image k = 0), [2k - E, 2k] (k > 0) or [2k, 2k + E] (k < 0), the sets
-//     the reference's wrap (forward.cu:149-157) maps into [-E, E].  Each pair is visited
-//     through exactly one image (the image index of its own x, checked per candidate), so no
-//     pair is counted twice even when the windows' cell ranges overlap;
+//     the reference's wrap (forward.cu:149-157) maps into [-E, E].  A candidate is kept under
+//     image k only if |x - 2k| <= its own cut half-width r (< 0.45): these boxes are disjoint
+//     over k, so no pair is evaluated twice even when the windows' cell ranges overlap, and
+//     every pair with a non-zero contribution has |wrap(x)| = |x - 2k| <= r for its own image k.
+//     (A pair kept under an image that is not its own has |wrap(x)| > 1.5: G is exactly 0.
+//     pair_eval always applies the reference's wrap, so its value never depends on the window.)
 //   * "big" Gaussians (everything else) sit in one extra cell and meet every sample;
 //   * forward: lane = sample (in cell order), outputs summed in registers, no atomics;
 //     backward: lane = Gaussian (in cell order) walking the samples of its images, gradients
@@ -105,12 +108,6 @@ __device__ __forceinline__ float wrap1(float x) {  // forward.cu:149-157, one ax
     if (fabsf(x) > 1.0f) x = x >= 0.0f ? fmodf(x, 2.0f) - 2.0f : fmodf(x, 2.0f) + 2.0f;
     return x;
 }
-// image index of a displacement (0 inside [-1, 1]; k for [2k - 2, 2k] beyond it)
-__device__ __forceinline__ int image_of(float x) {
-    if (fabsf(x) <= 1.0f) return 0;
-    return x > 0.0f ? (int)ceilf(0.5f * x) : -(int)ceilf(-0.5f * x);
-}
-
 // One pair: wrapped X, power (exact operation order of include/dgs_volume.h, no contraction,
 // so that the numpy oracle reproduces it bit for bit), G and a = A X.  False: power > 0 (the
 // reference's skip) or G == +0 (the pair adds exactly nothing; half of the cut box's pairs).
@@ -426,12 +423,15 @@ struct VCand {
     float v[CB];  // values of the launch's channel block
 };
 
-template <int FN, int CB>
+// COUNT (diagnostic, dgs_volume_count_pairs): instead of the outputs, counts[0] += the pairs
+// evaluated (candidates inside their cut box) and counts[1] += the live ones (G > 0).
+template <int FN, int CB, bool COUNT = false>
 __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ buf, int P, int N, int C, int cbase,
                                                        const float *__restrict__ means,
                                                        const float *__restrict__ values,
                                                        const float *__restrict__ conics,
-                                                       const float *__restrict__ samples, float *__restrict__ out) {
+                                                       const float *__restrict__ samples, float *__restrict__ out,
+                                                       unsigned long long *__restrict__ counts = nullptr) {
     constexpr int KU = VTr<FN>::KU, K = VTr<FN>::K;
     __shared__ VCand<CB> cand[kWave];
     const Hdr h = hdr_of(buf);
@@ -462,8 +462,14 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
             float acc[KU][CB];
             for (int u = 0; u < KU; ++u)
                 for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
+            unsigned long long n_cand = 0, n_live = 0;
             auto eval = [&](const float *m, const float *c, const float *vr) {
                 float X[3], a[3], G, t[KU];
+                if constexpr (COUNT) {
+                    ++n_cand;
+                    if (pair_eval(m, s, c, X, G, a)) ++n_live;
+                    return;
+                }
                 if (!pair_eval(m, s, c, X, G, a)) return;
                 terms<FN>(a, c, t);
                 for (int ch = 0; ch < nch; ++ch) {
@@ -535,10 +541,9 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                                                 const float m[3] = {mp.x, mp.y, mp.z};
                                                 const float r[3] = {ge.x, ge.y, ge.z};
                                                 bool mine = true;
-                                                for (int d = 0; d < 3; ++d) {  // own image, own cut box
+                                                for (int d = 0; d < 3; ++d) {  // inside its cut box at image kk
                                                     const float x = m[d] - s[d];
-                                                    mine = mine && image_of(x) == kk[d] &&
-                                                           fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                                                    mine = mine && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
                                                 }
                                                 if (mine) eval(m, cand[u].c, cand[u].v);
                                             }
@@ -556,9 +561,14 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                     for (int ch = 0; ch < CB; ++ch) vr[ch] = ch < nch ? values[(int64_t)g * C + cbase + ch] : 0.0f;
                     eval(m, c, vr);
                 }
-                for (int f = 0; f < K; ++f) {
-                    const int u = umap<FN>(f);
-                    for (int ch = 0; ch < nch; ++ch) out[((int64_t)sid * K + f) * C + cbase + ch] = acc[u][ch];
+                if constexpr (COUNT) {
+                    atomicAdd(&counts[0], n_cand);
+                    atomicAdd(&counts[1], n_live);
+                } else {
+                    for (int f = 0; f < K; ++f) {
+                        const int u = umap<FN>(f);
+                        for (int ch = 0; ch < nch; ++ch) out[((int64_t)sid * K + f) * C + cbase + ch] = acc[u][ch];
+                    }
                 }
             }
         }
@@ -736,9 +746,9 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                             const float4 sp = scand[u];
                                             const float sv[3] = {sp.x, sp.y, sp.z};
                                             bool mine = true;
-                                            for (int d = 0; d < 3; ++d) {  // own image, own cut box
+                                            for (int d = 0; d < 3; ++d) {  // inside its cut box at image kk
                                                 const float x = m[d] - sv[d];
-                                                mine = mine && image_of(x) == kk[d] && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
+                                                mine = mine && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
                                             }
                                             if (mine) {
                                                 const float *hrow = CB == 1 ? &shrow[u][0]
@@ -1006,5 +1016,28 @@ extern "C" int dgs_volume_backward(int function, int P, int N, int C, const floa
         default: dispatch_bwd<3>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
     }
     DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+extern "C" int dgs_volume_count_pairs(int P, int N, const float *means, const float *conics, const float *samples,
+                                      const void *binning, size_t binning_bytes, int64_t *counts,
+                                      dgs_stream_t stream) {
+    if (int rc = vol_check(0, P, N, 1, binning, binning_bytes)) return rc;
+    if (!counts) return fail(DGS_ERR_ARG, "dgs_volume_count_pairs: counts required");
+    counts[0] = counts[1] = 0;
+    if (N == 0 || P == 0) return DGS_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    unsigned long long *d = nullptr;
+    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&d), 16, s));
+    DGS_TRY_HIP(hipMemsetAsync(d, 0, 16, s));
+    // values are not read in COUNT mode; conics stand in for the pointer
+    k_vol_forward<0, 1, true><<<kVolFwdBlocks, kWave, 0, s>>>(static_cast<const char *>(binning), P, N, 1, 0, means,
+                                                              conics, conics, samples, nullptr, d);
+    unsigned long long h[2] = {0, 0};
+    DGS_TRY_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipFreeAsync(d, s));
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    counts[0] = (int64_t)h[0];
+    counts[1] = (int64_t)h[1];
     return DGS_OK;
 }

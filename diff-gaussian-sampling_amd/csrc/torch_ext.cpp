@@ -587,6 +587,19 @@ std::tuple<Tensor, Tensor, Tensor> VolumeBackward(int function, const Tensor &me
     return std::make_tuple(dm, dv, dc);
 }
 
+std::tuple<int64_t, int64_t> VolumeCountPairs(const Tensor &means_in, const Tensor &conics_in,
+                                              const Tensor &samples_in, const Tensor &binning_in) {
+    const Tensor means = f32(means_in, "means"), conics = f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples"), binning = u8(binning_in, "binning_buffer");
+    vol_shapes(means, conics, samples);
+    int64_t c[2] = {0, 0};
+    check(dgs_volume_count_pairs((int)means.size(0), (int)samples.size(0), means.data_ptr<float>(),
+                                 conics.data_ptr<float>(), samples.data_ptr<float>(), binning.data_ptr(),
+                                 (size_t)binning.numel(), c, as_dgs(cur_stream())),
+          "volume_count_pairs");
+    return std::make_tuple(c[0], c[1]);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -615,6 +628,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("volume_preprocess", &VolumePreprocess);
     m.def("volume_forward", &VolumeForward);
     m.def("volume_backward", &VolumeBackward);
+    m.def("volume_count_pairs", &VolumeCountPairs);
     m.def("library_version", []() { return dgs_version(); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });
     m.def("timing_read", [](int which) {

@@ -55,6 +55,11 @@ int dgs_volume_backward(int function, int P, int N, int C, const float *means, c
                         float *dL_dvalues, float *dL_dconics, void *workspace,
                         size_t workspace_bytes, dgs_stream_t stream, int debug);
 
+/* Diagnostic (not on any reference API): counts[0] = pairs the forward evaluates (candidates
+ * inside their own cut box), counts[1] = live pairs (G = expf(power) > 0).  Host, syncs. */
+int dgs_volume_count_pairs(int P, int N, const float *means, const float *conics, const float *samples,
+                           const void *binning, size_t binning_bytes, int64_t *counts, dgs_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif
