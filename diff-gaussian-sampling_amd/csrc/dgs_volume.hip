@@ -44,6 +44,8 @@ struct Hdr {
     int P, N, nsmall, nbig, ncells;
     int n[3];
     float lo[3], cs[3], E[3];
+    float split;     // small Gaussians with every cut half-width <= split: class 0, else class 1
+    float Ec[2][3];  // per class, the largest cut half-width per axis (the window reach)
     int64_t o_gext, o_gids, o_sids, o_gstart, o_sstart, o_gpk, o_gek;
 };
 constexpr size_t kHdrBytes = 256;
@@ -353,13 +355,14 @@ __global__ __launch_bounds__(kBlock) void k_vol_sbounds(int N, const float *__re
         }
 }
 
-// cell keys (big Gaussians: the extra cell ncells) and the identity values
+// cell keys and the identity values.  Gaussians: class * ncells + cell (class 1: some cut
+// half-width above split), big ones 2 * ncells; samples: the cell.
 __global__ __launch_bounds__(kBlock) void k_vol_keys(int n, Hdr h, const float *__restrict__ pts,
                                                      const float4 *__restrict__ gext, uint32_t *__restrict__ keys,
                                                      uint32_t *__restrict__ vals) {
     const int i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
-    uint32_t key = (uint32_t)h.ncells;
+    uint32_t key = (uint32_t)(2 * h.ncells);  // (Gaussians: class-major cells, then the big ones)
     if (!gext || gext[i].w != 0.0f) {
         int c[3];
         for (int d = 0; d < 3; ++d) {
@@ -367,6 +370,10 @@ __global__ __launch_bounds__(kBlock) void k_vol_keys(int n, Hdr h, const float *
             c[d] = x == x ? cell_axis(h, d, x) : 0;
         }
         key = (uint32_t)((c[2] * h.n[1] + c[1]) * h.n[0] + c[0]);
+        if (gext) {
+            const float4 e = gext[i];
+            if (fmaxf(fmaxf(e.x, e.y), e.z) > h.split) key += (uint32_t)h.ncells;
+        }
     }
     keys[i] = key;
     vals[i] = (uint32_t)i;
@@ -500,6 +507,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                     w[d].k0 = min(wa.k0, wb.k0);
                     w[d].k1 = max(wa.k1, wb.k1);
                 }
+                for (int cls = 0; cls < 2; ++cls)  // per class: its own reach
                 for (int kz = w[2].k0; kz <= w[2].k1; ++kz)
                     for (int ky = w[1].k0; ky <= w[1].k1; ++ky)
                         for (int kx = w[0].k0; kx <= w[0].k1; ++kx) {
@@ -508,7 +516,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                             bool any = true;
                             for (int d = 0; d < 3; ++d) {
                                 float xa, xb;
-                                image_window(kk[d], h.E[d], xa, xb);
+                                image_window(kk[d], h.Ec[cls][d], xa, xb);
                                 const float ta = bl[d] + xa, tb = bh[d] + xb;  // mean window
                                 const float glo = h.lo[d], ghi = h.lo[d] + h.cs[d] * h.n[d];
                                 if (tb < glo || ta > ghi) { any = false; break; }
@@ -518,7 +526,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                             if (!any) continue;
                             for (int cz = c0[2]; cz <= c1[2]; ++cz)
                                 for (int cy = c0[1]; cy <= c1[1]; ++cy) {
-                                    const int row = (cz * h.n[1] + cy) * h.n[0];
+                                    const int row = cls * h.ncells + (cz * h.n[1] + cy) * h.n[0];
                                     const int b = gstart[row + c0[0]], e = gstart[row + c1[0] + 1];
                                     for (int q0 = b; q0 < e; q0 += kWave) {
                                         const int q = q0 + lane;
@@ -552,7 +560,7 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
                         }
             }
             if (active) {
-                for (int q = gstart[h.ncells]; q < gstart[h.ncells + 1]; ++q) {  // big ones
+                for (int q = gstart[2 * h.ncells]; q < gstart[2 * h.ncells + 1]; ++q) {  // big ones
                     const int g = gids[q];
                     float m[3], c[6];
                     for (int d = 0; d < 3; ++d) m[d] = means[(int64_t)g * 3 + d];
@@ -673,7 +681,7 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
     const int32_t *__restrict__ sstart = reinterpret_cast<const int32_t *>(buf + h.o_sstart);
     const float4 *__restrict__ gpk = reinterpret_cast<const float4 *>(buf + h.o_gpk);
     const float4 *__restrict__ gek = reinterpret_cast<const float4 *>(buf + h.o_gek);
-    for (int cell = blockIdx.x; cell < h.ncells; cell += gridDim.x) {
+    for (int cell = blockIdx.x; cell < 2 * h.ncells; cell += gridDim.x) {  // (class-major cells)
         const int gb = gstart[cell], ge = gstart[cell + 1];
         for (int i0 = gb; i0 < ge; i0 += kWave) {
             const int i = i0 + lane;
@@ -882,7 +890,7 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
     h.o_gids = h.o_gext + a256((size_t)P * 16);
     h.o_sids = h.o_gids + a256((size_t)P * 4);
     h.o_gstart = h.o_sids + a256((size_t)N * 4);
-    h.o_sstart = h.o_gstart + a256((size_t)(cap + 2) * 4);
+    h.o_sstart = h.o_gstart + a256((size_t)(2 * cap + 2) * 4);
     h.o_gpk = h.o_sstart + a256((size_t)(cap + 2) * 4);
     h.o_gek = h.o_gpk + a256((size_t)P * 16);
     const size_t total = h.o_gek + a256((size_t)P * 16);
@@ -933,8 +941,15 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
     // grid end lo + cs * n must cover hi: floor(ext / cs) + 1 cells do, unless capped at 128 (then
     // cs >= ext / 128 already makes 128 cells cover it)
     h.ncells = (int)ncells;
+    // two reach classes: the window of a class is its own largest cut (about half the small
+    // Gaussians fall in class 0 for a uniform spread of sizes)
+    h.split = 0.7f * std::max({hr.E[0], hr.E[1], hr.E[2]});
+    for (int d = 0; d < 3; ++d) {
+        h.Ec[0][d] = std::min(hr.E[d], h.split);
+        h.Ec[1][d] = hr.E[d];
+    }
     unsigned bits = 1;
-    while ((1ull << bits) <= (uint64_t)ncells) ++bits;
+    while ((1ull << bits) <= (uint64_t)(2 * ncells)) ++bits;
     int32_t *gstart = reinterpret_cast<int32_t *>(buf + h.o_gstart);
     int32_t *sstart = reinterpret_cast<int32_t *>(buf + h.o_sstart);
     for (int side = 0; side < 2; ++side) {
@@ -950,7 +965,8 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
                                                  (size_t)n, 0, bits, s));
         }
         const int64_t nthr = std::max<int64_t>(n, 1);
-        k_vol_starts<<<(unsigned)((nthr + kBlock - 1) / kBlock), kBlock, 0, s>>>(n, h.ncells, keys2, start);
+        k_vol_starts<<<(unsigned)((nthr + kBlock - 1) / kBlock), kBlock, 0, s>>>(
+            n, side == 0 ? 2 * h.ncells : h.ncells, keys2, start);
         DGS_LAUNCH_CHECK(s, debug);
     }
     if (h.nsmall > 0)
