@@ -600,7 +600,8 @@ __global__ __launch_bounds__(kBlock) void k_vol_hsum(int N, int C, const float *
 }
 
 // One pair's contribution to a Gaussian's gradient sums.  hrow: the sample's h row [KU][C]
-// (LDS or global); CB == 1 means C == 1, with the Gaussian's value v0 in a register.
+// (LDS or global).  CB == 1 means C == 1: phi, g and e are linear in h v0, so the pair uses h
+// alone and the caller scales the mean / conic sums by v0 once (bwd_store's scale).
 template <int FN, int CB>
 __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const float *__restrict__ values, int g,
                                          float v0, int C, int cbase, int nch, const float *s, const float *hrow,
@@ -612,11 +613,12 @@ __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const f
     float hv[KU];
     if constexpr (CB == 1) {
         float p = 0.0f;
-        for (int u = 0; u < KU; ++u) {
-            hv[u] = v0 * hrow[u];
-            p += hrow[u] * t[u];
-        }
+        for (int u = 0; u < KU; ++u) p += hrow[u] * t[u];
         dv[0] += G * p;
+        float gg[3], e[6];
+        phi_grads<FN>(hrow, a, c, gg, e);
+        pair_grads(G, p, X, a, c, gg, e, dm, dc);
+        return;
     } else {
         for (int u = 0; u < KU; ++u) hv[u] = 0.0f;
         for (int ch = 0; ch < C; ++ch) {
@@ -639,10 +641,10 @@ __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const f
 template <int CB>
 __device__ __forceinline__ void bwd_store(int g, int C, int cbase, int nch, const float *dm, const float *dc,
                                           const float *dv, float *__restrict__ dmeans, float *__restrict__ dvalues,
-                                          float *__restrict__ dconics) {
+                                          float *__restrict__ dconics, float scale = 1.0f) {
     if (cbase == 0) {
-        for (int d = 0; d < 3; ++d) dmeans[(int64_t)g * 3 + d] = dm[d];
-        for (int q = 0; q < 6; ++q) dconics[(int64_t)g * 6 + q] = dc[q];
+        for (int d = 0; d < 3; ++d) dmeans[(int64_t)g * 3 + d] = scale * dm[d];
+        for (int q = 0; q < 6; ++q) dconics[(int64_t)g * 6 + q] = scale * dc[q];
     }
     for (int ch = 0; ch < nch; ++ch) dvalues[(int64_t)g * C + cbase + ch] = dv[ch];
 }
@@ -767,7 +769,7 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                 }
                             }
                     }
-            if (active) bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics);
+            if (active) bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics, CB == 1 ? v0 : 1.0f);
         }
     }
 }
@@ -813,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_backward_big(const char *__restr
                 t[k] = 0.0f;
                 for (int q = 0; q < kWavesPerBlock; ++q) t[k] += part[q][k];
             }
-            bwd_store<CB>(g, C, cbase, nch, t, t + 3, t + 9, dmeans, dvalues, dconics);
+            bwd_store<CB>(g, C, cbase, nch, t, t + 3, t + 9, dmeans, dvalues, dconics, CB == 1 ? values[g] : 1.0f);
         }
         __syncthreads();
     }
