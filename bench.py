@@ -167,7 +167,7 @@ def main():
 def bench_sample(args, world, rank, dev, torch, dist):
     import diff_gaussian_sampling as dgs
     from diff_gaussian_sampling import synthetic as syn
-    from diff_gaussian_sampling.distributed import (SupportExchange, global_tile_grid, pack_grads,
+    from diff_gaussian_sampling.distributed import (SupportExchange, grid_and_box, pack_grads,
                                                     shard_extents)
 
     P, C, D = args.P, args.C, 2
@@ -182,9 +182,10 @@ def bench_sample(args, world, rank, dev, torch, dist):
         samples = allpts[rank * per:(rank + 1) * per].to(dev)
         N = samples.shape[0]
     else:
-        samples = syn.samples(N, D, seed=4 + 1000 * rank).to(dev)
         if world > 1 and args.shard == "spatial":  # strip r of [-1, 1) along y: the union is uniform
-            samples[:, 1] = -1.0 + (2.0 / world) * (rank + 0.5 * (samples[:, 1] + 1.0))
+            samples = syn.strip_samples(N, D, rank, world, seed=4 + 1000 * rank).to(dev)
+        else:
+            samples = syn.samples(N, D, seed=4 + 1000 * rank).to(dev)
     spatial = world > 1 and args.shard == "spatial"
     dL = syn.grad_out(N, K, C, seed=5 + 1000 * rank).to(dev)
     for t in (means, values, conics):
@@ -195,12 +196,26 @@ def bench_sample(args, world, rank, dev, torch, dist):
     # every step because the means move)
     # one GPU: the reference API (grid computed on the device, one host sync per call); N > 1:
     # every shard bins with the global grid (distributed.global_tile_grid)
-    grid, off = global_tile_grid(samples) if world > 1 else (None, None)
+    grid = off = None
+    xchg, xsetup_ms, area = None, 0.0, 0.0
+    if world > 1:
+        grid, off, lo, hi = grid_and_box(samples)
+    if spatial:  # the owner / held sets: built once per run from the replicated parameters
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        xchg = SupportExchange(means, conics, shard_extents(samples), rank)
+        torch.cuda.synchronize()
+        xsetup_ms = (time.perf_counter() - t0) * 1e3
+        area = (hi[0] - lo[0]) * (hi[1] - lo[1])  # fine cells sized for the strip's own density
     pre_times = []
     for _ in range(1 + args.pre_reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        if world > 1:
+        if spatial:  # only the rows this rank holds (owned or reaching its strip)
+            binned = dgs._C.preprocess_gaussians_sharded(means.detach(), values.detach(), covs,
+                                                         conics.detach(), samples, grid, off, xchg.held,
+                                                         area, False)
+        elif world > 1:
             binned = dgs._C.preprocess_gaussians_bounded(means.detach(), values.detach(), covs,
                                                          conics.detach(), samples, grid, off, False)
         else:
@@ -211,14 +226,6 @@ def bench_sample(args, world, rank, dev, torch, dist):
     pre_first_ms = pre_times[0]
     pre_ms = sorted(pre_times[1:])[len(pre_times[1:]) // 2] if args.pre_reps > 0 else pre_first_ms
     R, gb, sb, rg, srg, radii = binned
-    xchg, xsetup_ms = None, 0.0
-    if spatial:  # the exchange sets: per binning (the PIGS loop re-bins, so part of its step); warm
-        for _ in range(2):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            xchg = SupportExchange(means, conics, shard_extents(samples), rank)
-            torch.cuda.synchronize()
-            xsetup_ms = (time.perf_counter() - t0) * 1e3
     fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative,
            "laplacian": dgs.sample_gaussians_laplacian,
            "third": dgs.sample_gaussians_third_derivative}[fn]
@@ -243,8 +250,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
             if timed:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-            if spatial:
-                xchg.exchange(pack_grads((means.grad, values.grad, conics.grad)))
+            if spatial:  # partial rows to their owners (owner-side optimizer, SupportExchange)
+                xchg.reduce(pack_grads((means.grad, values.grad, conics.grad)))
             else:
                 torch.cat([means.grad.reshape(-1), values.grad.reshape(-1), conics.grad.reshape(-1)], out=flat)
                 dist.all_reduce(flat)
@@ -285,6 +292,16 @@ def bench_sample(args, world, rank, dev, torch, dist):
     ms_per_step = elapsed * 1e3 / args.steps
     value = N * world / (ms_per_step / 1e3)
 
+    push_ms = 0.0
+    if spatial:  # the owners' rows to every rank their cut reaches: once per optimizer step
+        pushed = []
+        for _ in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            xchg.push([means, values, conics], means, conics)
+            torch.cuda.synchronize()
+            pushed.append((time.perf_counter() - t0) * 1e3)
+        push_ms = sorted(pushed)[1]
     # ---- live-pair count (diagnostic kernel, outside the timed region)
     w_cand, w_live = dgs._C.count_pairs(means.detach(), conics.detach(), samples, gb, sb, -104.0)
     avg_f = fms / max(nf, 1)
@@ -344,7 +361,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
                                       else ", 1 RCCL all-reduce per step") if world > 1 else "")},
         "preprocess_ms": pre_ms,
         # the Physics-Informed-GS loop re-bins every step (means move): its step time
-        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms + xsetup_ms,
+        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms + push_ms,
         "preprocess_first_call_ms": pre_first_ms,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
@@ -357,10 +374,13 @@ def bench_sample(args, world, rank, dev, torch, dist):
         result["distributed"] = {"backend": dist.get_backend(), "world_size": world, "shard": args.shard,
                                  "per_rank_ms_per_step": per_rank_ms,
                                  "gradient_sum_ms_rank0": ar_ms,
-                                 "gradient_sum_bytes_rank0": (int(xchg.rows_moved() * F * 4 * 2) if spatial
+                                 "gradient_sum_bytes_rank0": (int(xchg.rows_moved() * F * 4) if spatial
                                                               else int(flat.numel() * 4)),
                                  "dense_allreduce_bytes": int(flat.numel() * 4),
-                                 "exchange_setup_ms": xsetup_ms}
+                                 "exchange_setup_ms_once": xsetup_ms,
+                                 "push_ms": push_ms,
+                                 "held_rows_rank0": int(xchg.held.sum()) if spatial else P,
+                                 "w_cand_per_point_rank0": w_cand / N}
 
     if rank == 0 and world == 1 and not args.no_cpu and not multi:
         cpu_baselines(result, means.detach().cpu(), values.detach().cpu(), covs.cpu(),

@@ -186,7 +186,7 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
                              const float *__restrict__ covs, float *__restrict__ radii,
                              uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
                              uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
-                             int home_w, int home_h) {
+                             int home_w, int home_h, const uint8_t *__restrict__ present) {
     __shared__ uint32_t hist[kHistBins];  // grid-strided, capped grid: see k_sample_cells
     const bool lds = G.T <= kHistBins;
     if (lds)
@@ -198,7 +198,11 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         float r = 0.0f;
         float m[2] = {means[i * D], D == 2 ? means[i * D + 1] : 0.0f};
         float cv[3] = {covs[i * S], D == 2 ? covs[i * S + 1] : 0.0f, D == 2 ? covs[i * S + 2] : 0.0f};
-        const uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
+        uint32_t t = ref_touched(D, m, cv, G.grid, G.off, &r);
+        if (present && !present[i]) {  // left out of this binning, as a det == 0 Gaussian is
+            r = 0.0f;
+            t = 0u;
+        }
         radii[i] = r;
         touched[i] = t;
         ids[i] = (uint32_t)i;
@@ -1053,8 +1057,11 @@ static double cell_target() {
     return t;
 }
 
-static int choose_n(int D, int64_t N, int64_t T) {
-    const double per_tile = (double)N / (double)(T > 0 ? T : 1);
+// area > 0: the samples occupy `area` (D = 2; a length at D = 1) of the domain, e.g. one
+// rank's strip of a spatially sharded run -- the density is N / area, not N / (T tiles).
+static int choose_n(int D, int64_t N, int64_t T, double area) {
+    const double tile_area = D == 2 ? (double)kTile * (double)kTile : (double)kTile;
+    const double per_tile = area > 0.0 ? (double)N * tile_area / area : (double)N / (double)(T > 0 ? T : 1);
     const double target = cell_target();
     if (D == 2) {
         int n = (int)std::lround(std::sqrt(per_tile / target));
@@ -1100,7 +1107,7 @@ struct Scratch {
 // Per Gaussian, the ranks whose point range along the sharding axis (y at D = 2, x at D = 1)
 // meets its exact-zero cut X^T A X <= kQCut or a torus image of it (period 2,
 // forward.cu:149-157): bit r of mask[g]; and the owner, the rank whose range is nearest the mean
-// (first on ties).  The cut's half-width along the axis is sqrt(kQCut (A^-1)_axis), widened by
+// (first on ties) among the ranks it touches, the nearest of all if it touches none.  The cut's half-width along the axis is sqrt(kQCut (A^-1)_axis), widened by
 // 1e-5; conics that are not positive definite reach every rank.
 constexpr int kMaxXchgRanks = 32;
 struct XchgRanks {
@@ -1128,8 +1135,8 @@ __global__ void k_xchg_sets(int P, int D, const float *__restrict__ means, const
     }
     e = e * (1.0 + 1e-5) + 1e-6;
     uint32_t m = 0u;
-    int best = 0;
-    double bd = INFINITY;
+    int best = 0, tbest = -1;
+    double bd = INFINITY, tbd = INFINITY;
     for (int r = 0; r < R.W; ++r) {
         const double lo = R.lo[r], hi = R.hi[r];
         if (!pd) {
@@ -1140,9 +1147,10 @@ __global__ void k_xchg_sets(int P, int D, const float *__restrict__ means, const
         }
         const double d = fmax(fmax(lo - y, y - hi), 0.0);
         if (d < bd) { bd = d; best = r; }
+        if (((m >> r) & 1u) && d < tbd) { tbd = d; tbest = r; }
     }
     mask[g] = m;
-    owner[g] = best;
+    owner[g] = tbest >= 0 ? tbest : best;  // a rank that touches it; the nearest if none does
 }
 }  // namespace dgs
 
@@ -1203,7 +1211,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                            const float *conics, const float *samples, const int *grid,
                            const float *grid_offset, float *radii, dgs_alloc_fn alloc,
                            void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream, int debug,
-                           const int *dgrid, const float *doff, int *dev_grid, float *dev_off) {
+                           const int *dgrid, const float *doff, int *dev_grid, float *dev_off,
+                           const uint8_t *present = nullptr, double sample_area = 0.0) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
     if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^30 - 1)");
@@ -1222,7 +1231,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     const int64_t T64 = (int64_t)G.grid[0] * G.grid[1];
     if (T64 > (1 << 24)) return fail(DGS_ERR_ARG, "tile grid too large");
     G.T = (int)T64;
-    G.n = choose_n(D, N, G.T);
+    G.n = choose_n(D, N, G.T, sample_area);
     G.CT = (D == 2 ? G.n * G.n : G.n) + 1;
     const int64_t ncells64 = (int64_t)G.T * G.CT;
     if (ncells64 >= (1LL << 30)) return fail(DGS_ERR_ARG, "too many fine cells");
@@ -1325,7 +1334,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
     k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
-                                                home, gids, home_w, home_h);
+                                                home, gids, home_w, home_h, present);
     DGS_LAUNCH_CHECK(s, debug);
     tb = t_a;
     DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
@@ -1587,11 +1596,53 @@ extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const flo
                            alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr);
 }
 
-// The grid of the previous call (per D): the speculation of dgs_preprocess_auto.
+extern "C" int dgs_preprocess_ex(int P, int D, int N, const float *means, const float *covariances,
+                                 const float *conics, const float *samples, const int *grid,
+                                 const float *grid_offset, const dgs_bin_options *opts, float *radii,
+                                 dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
+                                 dgs_stream_t stream, int debug) {
+    const uint8_t *present = opts ? opts->present : nullptr;
+    const double area = opts ? opts->sample_area : 0.0;
+    if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_ex: sample_area must be >= 0");
+    return preprocess_body(P, D, N, means, covariances, conics, samples, grid, grid_offset, radii, alloc,
+                           alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present,
+                           area);
+}
+
+// The speculation of dgs_preprocess_auto, per sample set: keyed by (samples pointer, N, D), the
+// grid of the last call and whether to speculate on it.  A key speculates only once a read-first
+// call found the same grid as the call before it (fixed samples: every call after the second
+// bins once, with no extra sync).  A miss turns it back to read-first, so a loop that resamples
+// its points every step (samples.min moves, so the offset does) pays one small extra sync per
+// call instead of a second binning, and samplers that alternate keep one entry each.
+struct GridGuess {
+    const void *key = nullptr;
+    int N = 0, D = 0;
+    int grid[2] = {0, 0};
+    float off[2] = {0.0f, 0.0f};
+    bool speculate = false;
+    uint64_t used = 0;
+};
 static std::mutex g_grid_mu;
-static bool g_grid_known[3] = {false, false, false};
-static int g_grid_last[3][2];
-static float g_off_last[3][2];
+static GridGuess g_guess[8];
+static uint64_t g_guess_tick = 0;
+
+static GridGuess *guess_slot(const void *key, int N, int D) {  // caller holds g_grid_mu
+    GridGuess *lru = &g_guess[0];
+    for (GridGuess &e : g_guess) {
+        if (e.key == key && e.N == N && e.D == D && e.used) return &e;
+        if (e.used < lru->used) lru = &e;
+    }
+    *lru = GridGuess{};
+    lru->key = key; lru->N = N; lru->D = D;
+    return lru;
+}
+
+static bool same_grid(int D, const int *ga, const float *oa, const int *gb, const float *ob) {
+    for (int d = 0; d < D; ++d)
+        if (ga[d] != gb[d] || std::memcmp(&oa[d], &ob[d], 4) != 0) return false;
+    return true;
+}
 
 extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *covariances,
                                    const float *conics, const float *samples, float *radii,
@@ -1613,15 +1664,18 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, part);
     k_bounds_final<<<1, kBlock, 0, s>>>(nparts, D, part, dgrid, doff);
     DGS_LAUNCH_CHECK(s, debug);
-    int guess[2] = {1, 1};
-    float goff[2] = {0.0f, 0.0f};
-    bool known;
+    int guess[2] = {1, 1}, prev[2] = {0, 0};
+    float goff[2] = {0.0f, 0.0f}, poff[2] = {0.0f, 0.0f};
+    bool speculate, had;
     {
         std::lock_guard<std::mutex> lk(g_grid_mu);
-        known = g_grid_known[D];
-        for (int d = 0; d < D; ++d) { guess[d] = g_grid_last[D][d]; goff[d] = g_off_last[D][d]; }
+        GridGuess *e = guess_slot(samples, N, D);
+        had = e->used != 0;
+        speculate = had && e->speculate;
+        for (int d = 0; d < D; ++d) { prev[d] = guess[d] = e->grid[d]; poff[d] = goff[d] = e->off[d]; }
+        e->used = ++g_guess_tick;
     }
-    if (!known) {  // first call: read the grid (the one extra sync of a cold start)
+    if (!speculate) {  // read-first: one small extra sync, then one binning
         DGS_TRY_HIP(hipMemcpyAsync(guess, dgrid, sizeof(int) * D, hipMemcpyDeviceToHost, s));
         DGS_TRY_HIP(hipMemcpyAsync(goff, doff, sizeof(float) * D, hipMemcpyDeviceToHost, s));
         DGS_TRY_HIP(hipStreamSynchronize(s));
@@ -1633,15 +1687,15 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     int rc = preprocess_body(P, D, N, means, covariances, conics, samples, guess, goff, radii, alloc, alloc_ctx,
                              num_rendered, stream, debug, dgrid, doff, dg, dof);
     if (rc) return rc;
-    bool same = true;
-    for (int d = 0; d < D; ++d)
-        same = same && dg[d] == guess[d] && std::memcmp(&dof[d], &goff[d], 4) == 0;
+    const bool hit = same_grid(D, dg, dof, guess, goff);
     {
         std::lock_guard<std::mutex> lk(g_grid_mu);
-        g_grid_known[D] = true;
-        for (int d = 0; d < D; ++d) { g_grid_last[D][d] = dg[d]; g_off_last[D][d] = dof[d]; }
+        GridGuess *e = guess_slot(samples, N, D);
+        e->speculate = speculate ? hit : (had && same_grid(D, dg, dof, prev, poff));
+        for (int d = 0; d < D; ++d) { e->grid[d] = dg[d]; e->off[d] = dof[d]; }
+        e->used = ++g_guess_tick;
     }
-    if (!same)
+    if (!hit)
         rc = preprocess_body(P, D, N, means, covariances, conics, samples, dg, dof, radii, alloc, alloc_ctx,
                              num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr);
     for (int d = 0; d < D; ++d) { grid_out[d] = dg[d]; offset_out[d] = dof[d]; }

@@ -47,6 +47,7 @@ struct Hdr {
     float split;     // small Gaussians with every cut half-width <= split: class 0, else class 1
     float Ec[2][3];  // per class, the largest cut half-width per axis (the window reach)
     int64_t o_gext, o_gids, o_sids, o_gstart, o_sstart, o_gpk, o_gek;
+    int64_t o_mcopy, o_ccopy, o_scopy, o_flag;  // the binned tensors; flag = they differ from the call's
 };
 constexpr size_t kHdrBytes = 256;
 static_assert(sizeof(Hdr) <= kHdrBytes, "volume header too large");
@@ -409,6 +410,34 @@ __global__ __launch_bounds__(kBlock) void k_vol_pack(int nsmall, const int32_t *
     gek[i] = gext[g];
 }
 
+// Every forward / backward compares its means, conics and samples bitwise with the binned ones:
+// the cells and the packed means come from preprocess, so other tensors (an in-place optimizer
+// step, moved samples) would mix old and new parameters.  On a difference the call writes NaN,
+// like a stale buffer (VolumeSampler re-bins before that can happen).
+__global__ void k_vol_flag_reset(int P, int N, char *buf) {
+    const Hdr h = *reinterpret_cast<const Hdr *>(buf);
+    if (threadIdx.x == 0 && h.magic == kVolMagic && h.P == P && h.N == N) *reinterpret_cast<int *>(buf + h.o_flag) = 0;
+}
+
+__global__ void k_vol_verify(int P, int N, const uint32_t *__restrict__ m, const uint32_t *__restrict__ c,
+                             const uint32_t *__restrict__ sm, char *buf) {
+    const Hdr h = *reinterpret_cast<const Hdr *>(buf);
+    if (h.magic != kVolMagic || h.P != P || h.N != N) return;  // (the kernels flag a stale buffer)
+    const int64_t nm = (int64_t)P * 3, nc = (int64_t)P * 6, ns = (int64_t)N * 3;
+    const uint32_t *mc = reinterpret_cast<const uint32_t *>(buf + h.o_mcopy);
+    const uint32_t *cc = reinterpret_cast<const uint32_t *>(buf + h.o_ccopy);
+    const uint32_t *sc = reinterpret_cast<const uint32_t *>(buf + h.o_scopy);
+    bool diff = false;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nm + nc + ns; i += stride)
+        diff |= i < nm ? m[i] != mc[i] : (i < nm + nc ? c[i - nm] != cc[i - nm] : sm[i - nm - nc] != sc[i - nm - nc]);
+    if (__any(diff) && (threadIdx.x & (kWave - 1)) == 0) *reinterpret_cast<volatile int *>(buf + h.o_flag) = 1;
+}
+
+__device__ inline bool vol_flagged(const char *buf, const Hdr &h) {
+    return *reinterpret_cast<const volatile int *>(buf + h.o_flag) != 0;
+}
+
 __global__ void k_vol_header(Hdr h, char *buf) {
     if (threadIdx.x == 0) *reinterpret_cast<Hdr *>(buf) = h;
 }
@@ -444,7 +473,8 @@ __global__ __launch_bounds__(kWave) void k_vol_forward(const char *__restrict__ 
     const Hdr h = hdr_of(buf);
     const int lane = threadIdx.x;
     const int nch = min(CB, C - cbase);
-    if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
+    if (h.magic != kVolMagic || h.P != P || h.N != N || vol_flagged(buf, h)) {  // stale buffer / inputs: loud
+        if (COUNT) return;
         for (int64_t j = (int64_t)blockIdx.x * kWave + lane; j < N; j += (int64_t)gridDim.x * kWave)
             for (int f = 0; f < K; ++f)
                 for (int ch = 0; ch < nch; ++ch) out[(j * K + f) * C + cbase + ch] = NAN;
@@ -671,7 +701,7 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
     const Hdr h = hdr_of(buf);
     const int lane = threadIdx.x;
     const int nch = min(CB, C - cbase);
-    if (h.magic != kVolMagic || h.P != P || h.N != N) {  // stale buffer: loud
+    if (h.magic != kVolMagic || h.P != P || h.N != N || vol_flagged(buf, h)) {  // stale buffer / inputs: loud
         const float nan[9] = {NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN, NAN};
         for (int64_t i = (int64_t)blockIdx.x * kWave + lane; i < P; i += (int64_t)gridDim.x * kWave)
             bwd_store<CB>((int)i, C, cbase, nch, nan, nan, nan, dmeans, dvalues, dconics);
@@ -788,7 +818,7 @@ __global__ __launch_bounds__(kBlock) void k_vol_backward_big(const char *__restr
     constexpr int NV = 9 + CB;
     __shared__ float part[kWavesPerBlock][NV];
     const Hdr h = hdr_of(buf);
-    if (h.magic != kVolMagic || h.P != P || h.N != N) return;  // (k_vol_backward flags it)
+    if (h.magic != kVolMagic || h.P != P || h.N != N || vol_flagged(buf, h)) return;  // (k_vol_backward flags it)
     const int32_t *__restrict__ gids = reinterpret_cast<const int32_t *>(buf + h.o_gids);
     const int nch = min(CB, C - cbase);
     const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -895,7 +925,11 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
     h.o_sstart = h.o_gstart + a256((size_t)(2 * cap + 2) * 4);
     h.o_gpk = h.o_sstart + a256((size_t)(cap + 2) * 4);
     h.o_gek = h.o_gpk + a256((size_t)P * 16);
-    const size_t total = h.o_gek + a256((size_t)P * 16);
+    h.o_mcopy = h.o_gek + a256((size_t)P * 16);
+    h.o_ccopy = h.o_mcopy + a256((size_t)P * 12);
+    h.o_scopy = h.o_ccopy + a256((size_t)P * 24);
+    h.o_flag = h.o_scopy + a256((size_t)N * 12);
+    const size_t total = h.o_flag + 256;
     char *buf = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_BINNING, total));
     if (!buf) return fail(DGS_ERR_ALLOC, "dgs_volume_preprocess: binning buffer");
     size_t sort_tmp = 0;
@@ -975,8 +1009,27 @@ extern "C" int dgs_volume_preprocess(int P, int N, const float *means, const flo
         k_vol_pack<<<(unsigned)((h.nsmall + kBlock - 1) / kBlock), kBlock, 0, s>>>(
             h.nsmall, reinterpret_cast<const int32_t *>(buf + h.o_gids), means, gext,
             reinterpret_cast<float4 *>(buf + h.o_gpk), reinterpret_cast<float4 *>(buf + h.o_gek));
+    if (P > 0) DGS_TRY_HIP(hipMemcpyAsync(buf + h.o_mcopy, means, (size_t)P * 12, hipMemcpyDeviceToDevice, s));
+    if (P > 0) DGS_TRY_HIP(hipMemcpyAsync(buf + h.o_ccopy, conics, (size_t)P * 24, hipMemcpyDeviceToDevice, s));
+    if (N > 0) DGS_TRY_HIP(hipMemcpyAsync(buf + h.o_scopy, samples, (size_t)N * 12, hipMemcpyDeviceToDevice, s));
+    DGS_TRY_HIP(hipMemsetAsync(buf + h.o_flag, 0, 4, s));
     k_vol_header<<<1, 64, 0, s>>>(h, buf);
     DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+// The call-time check of k_vol_verify (the header's offsets are read on the device).
+static int vol_flag_reset_verify(int P, int N, const float *means, const float *conics, const float *samples,
+                                 const void *binning, size_t bytes, hipStream_t s) {
+    char *buf = static_cast<char *>(const_cast<void *>(binning));
+    const int64_t n = (int64_t)P * 9 + (int64_t)N * 3;
+    const unsigned blocks = (unsigned)std::min<int64_t>(std::max<int64_t>((n + kBlock - 1) / kBlock, 1), 2048);
+    k_vol_flag_reset<<<1, 64, 0, s>>>(P, N, buf);
+    k_vol_verify<<<blocks, kBlock, 0, s>>>(P, N, reinterpret_cast<const uint32_t *>(means),
+                                           reinterpret_cast<const uint32_t *>(conics),
+                                           reinterpret_cast<const uint32_t *>(samples), buf);
+    DGS_TRY_HIP(hipGetLastError());
+    (void)bytes;
     return DGS_OK;
 }
 
@@ -999,6 +1052,7 @@ extern "C" int dgs_volume_forward(int function, int P, int N, int C, const float
     if (N == 0) return DGS_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const char *buf = static_cast<const char *>(binning);
+    if (int rc = vol_flag_reset_verify(P, N, means, conics, samples, binning, binning_bytes, s)) return rc;
     switch (function) {
         case 0: dispatch_fwd<0>(C, buf, P, N, means, values, conics, samples, out, s); break;
         case 1: dispatch_fwd<1>(C, buf, P, N, means, values, conics, samples, out, s); break;
@@ -1026,6 +1080,7 @@ extern "C" int dgs_volume_backward(int function, int P, int N, int C, const floa
         return DGS_OK;
     }
     const char *buf = static_cast<const char *>(binning);
+    if (int rc = vol_flag_reset_verify(P, N, means, conics, samples, binning, binning_bytes, s)) return rc;
     float *hs = static_cast<float *>(workspace);
     switch (function) {
         case 0: dispatch_bwd<0>(C, buf, P, N, means, values, conics, samples, dL_dout, hs, dL_dmeans, dL_dvalues, dL_dconics, s); break;
@@ -1048,6 +1103,7 @@ extern "C" int dgs_volume_count_pairs(int P, int N, const float *means, const fl
     unsigned long long *d = nullptr;
     DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&d), 16, s));
     DGS_TRY_HIP(hipMemsetAsync(d, 0, 16, s));
+    if (int rc = vol_flag_reset_verify(P, N, means, conics, samples, binning, binning_bytes, s)) return rc;
     // values are not read in COUNT mode; conics stand in for the pointer
     k_vol_forward<0, 1, true><<<kVolFwdBlocks, kWave, 0, s>>>(static_cast<const char *>(binning), P, N, 1, 0, means,
                                                               conics, conics, samples, nullptr, d);

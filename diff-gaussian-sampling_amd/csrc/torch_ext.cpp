@@ -71,7 +71,7 @@ using PreOut = std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
 PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Tensor &cov_in,
                        const Tensor &conics_in, const Tensor &samples_in, const std::vector<int> *grid_in,
-                       const std::vector<float> *off_in, bool debug) {
+                       const std::vector<float> *off_in, bool debug, const dgs_bin_options *opts = nullptr) {
     const Tensor means = f32(means_in, "means"), covs = f32(cov_in, "covariances");
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     (void)values_in;
@@ -85,10 +85,10 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
         TORCH_CHECK(samples.size(-1) == D, "samples must have the same dimension as means");
         if (grid_in) {
             TORCH_CHECK((int)grid_in->size() == D && (int)off_in->size() == D, "grid/offset must have D entries");
-            check(dgs_preprocess(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
-                                 conics.data_ptr<float>(), samples.data_ptr<float>(), grid_in->data(),
-                                 off_in->data(), radii.data_ptr<float>(), alloc_cb, &ctx, &rendered,
-                                 as_dgs(cur_stream()), debug ? 1 : 0),
+            check(dgs_preprocess_ex(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
+                                    conics.data_ptr<float>(), samples.data_ptr<float>(), grid_in->data(),
+                                    off_in->data(), opts, radii.data_ptr<float>(), alloc_cb, &ctx, &rendered,
+                                    as_dgs(cur_stream()), debug ? 1 : 0),
                   "preprocess_gaussians");
         } else {  // the grid of sample_points.cu:70-74 on the device: one host sync per call
             int grid[2];
@@ -115,6 +115,27 @@ PreOut PreprocessBoundedCUDA(const Tensor &means, const Tensor &values, const Te
                              const Tensor &conics, const Tensor &samples, std::vector<int> grid,
                              std::vector<float> offset, const bool debug) {
     return preprocess_impl(means, values, covariances, conics, samples, &grid, &offset, debug);
+}
+
+// Spatially sharded ranks (distributed.SpatialShardedGaussianSampler): the global grid, only the
+// Gaussians with present[g] != 0 (uint8/bool [P], or None = all), fine cells sized for the
+// samples' own area (0 = the whole grid).
+PreOut PreprocessShardedCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances,
+                             const Tensor &conics, const Tensor &samples, std::vector<int> grid,
+                             std::vector<float> offset, const c10::optional<Tensor> &present_in,
+                             const double sample_area, const bool debug) {
+    dgs_bin_options o{};
+    Tensor present;
+    if (present_in.has_value() && present_in->defined()) {
+        TORCH_CHECK(present_in->scalar_type() == torch::kUInt8 || present_in->scalar_type() == torch::kBool,
+                    "present must be a uint8 or bool tensor");
+        TORCH_CHECK(present_in->is_cuda() && present_in->numel() == means.size(0), "present must be a GPU tensor of P");
+        present = present_in->contiguous().view(torch::kUInt8);
+        o.present = present.data_ptr<uint8_t>();
+    }
+    TORCH_CHECK(sample_area >= 0.0, "sample_area must be >= 0");
+    o.sample_area = sample_area;
+    return preprocess_impl(means, values, covariances, conics, samples, &grid, &offset, debug, &o);
 }
 
 Tensor sample_generic(int fn, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
@@ -619,6 +640,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("preprocess_aggregate", &AggregateNeighborsPreprocessCUDA);
     // extensions (not on the reference surface)
     m.def("preprocess_gaussians_bounded", &PreprocessBoundedCUDA);
+    m.def("preprocess_gaussians_sharded", &PreprocessShardedCUDA);
     m.def("count_pairs", &CountPairs);
     m.def("sample_gaussians_multi", &SampleGaussiansMulti);
     m.def("sample_gaussians_multi_backward", &SampleGaussiansMultiBackward);

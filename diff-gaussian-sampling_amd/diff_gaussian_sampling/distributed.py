@@ -11,13 +11,16 @@ the backward's per-Gaussian gradients are partial sums over each rank's points.
 
 * ShardedGaussianSampler: any split of the points; ONE all-reduce of the packed
   [dmeans | dvalues | dconics] buffer (P (D + C + S) floats: 24 MB at 1M Gaussians, C = 1).
-* SpatialShardedGaussianSampler: ranks own spatial strips of the points.  A
-  Gaussian's partial gradient can be non-zero only on the ranks whose points lie within its
-  exact-zero cut (X^T A X <= 210, the binning's culling bound; with the torus images 2k), so
-  the sum needs only those ranks: SupportExchange sends each such row to the Gaussian's owner
-  (an all-to-all whose splits every rank derives from the replicated means and conics, no
-  count exchange) and returns the sums to the contributing ranks.  With strips, only the
-  Gaussians near a strip boundary travel (~1 MB per rank at config 4 against 24 MB).
+* SpatialShardedGaussianSampler: a domain decomposition.  Rank r owns a
+  fixed strip of the points and a fixed set of Gaussians (their owner rank).  A Gaussian's
+  partial gradient can be non-zero only on the ranks whose strip meets its exact-zero cut
+  (X^T A X <= 210, the binning's culling bound; with the torus images 2k), so the backward sends
+  only those rows, to the owner (one all-to-all): afterwards a rank's gradient is the global
+  gradient on the rows it OWNS and 0 elsewhere, and an ordinary optimizer over the full tensors
+  updates exactly the owned rows.  `push` then sends the owners' updated rows to every rank
+  whose strip the updated cut reaches.  A rank bins only the rows it holds current copies of
+  (owned or pushed), so its results never read a stale row.  With strips, only the Gaussians
+  near a strip boundary travel (~1-2 MB per rank per step at config 4 against 24 MB).
 """
 import math
 
@@ -140,72 +143,106 @@ def support_halfwidth(means, conics):
     return torch.where(pd, e, torch.full_like(e, math.inf))
 
 
+def exchange_sets(means, conics, extents):
+    """(mask int64 [P], owner int64 [P]) for the rank ranges `extents` [W, 2] = [lo, hi] along the
+    sharding axis: bit r of mask[g] is set when rank r's range meets the cut of g or of one of its
+    torus images m + 2k (forward.cu:149-157 wraps X with period 2), i.e. when rank r's partial
+    gradient for g can be non-zero; owner[g] is the rank nearest the mean among those it touches
+    (the nearest of all when it touches none; first on ties).  GPU tensors: the native kernel
+    (dgs_exchange_sets, W <= 32); host tensors: the same predicate in torch ops."""
+    D = means.shape[1]
+    dev = means.device
+    ext = torch.as_tensor(extents).detach().double().cpu()
+    W = ext.shape[0]
+    if means.is_cuda and W <= 32:
+        mask, owner = _C.exchange_sets(means.detach(), conics.detach(), [float(v) for v in ext.reshape(-1)])
+        return mask.long() & 0xFFFFFFFF, owner.long()
+    y = means.detach()[:, D - 1].double()
+    e = support_halfwidth(means, conics)
+    lo, hi = ext[:, 0].to(dev), ext[:, 1].to(dev)
+    span = float(ext[:, 1].max() - ext[:, 0].min()) if W else 0.0
+    kmax = int(math.ceil(span / 2.0)) + 1
+    touch = torch.zeros(y.numel(), W, dtype=torch.bool, device=dev)
+    for k in range(-kmax, kmax + 1):
+        a, b = y + 2.0 * k - e, y + 2.0 * k + e
+        touch |= (a[:, None] <= hi[None, :]) & (b[:, None] >= lo[None, :])
+    dist_r = torch.clamp(torch.maximum(lo[None, :] - y[:, None], y[:, None] - hi[None, :]), min=0.0)
+    near_all = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
+    near_touch = torch.argmin(torch.where(touch, dist_r, torch.full_like(dist_r, math.inf)), dim=1)
+    owner = torch.where(touch.any(1), near_touch, near_all)
+    mask = (touch.long() << torch.arange(W, device=dev)).sum(1)
+    return mask, owner
+
+
+def _bits(mask, r):
+    return ((mask >> r) & 1).bool()
+
+
 class SupportExchange:
-    """Sparse sum of per-Gaussian partial gradients over the ranks that can touch them.
+    """The sparse communication of a spatially sharded run.
 
-    `extents` [W, 2]: every rank's point range [lo, hi] along the sharding axis (all-gathered).
-    Rank r's partial for Gaussian g can be non-zero only if some point of r lies within the
-    cut of g or of one of its torus images m + 2k (forward.cu:149-157 wraps X with period 2):
-    touch[g, r].  owner[g] = the rank whose range is nearest to the mean (first on ties).
-    The sets are computed identically on every rank from replicated inputs, so the all-to-all
-    splits need no exchange of counts."""
+    Every Gaussian g has a fixed owner rank, chosen once from the parameters given here (the
+    same on every rank).  Per step:
 
-    def __init__(self, means, conics, extents, rank, group=None):
-        D = means.shape[1]
+    * `reduce(G)` (in the backward): rank r sends its partial rows of the Gaussians it touches but
+      does not own to their owners (one all-to-all); the owner adds them, in rank order, to its own
+      partial.  Afterwards a rank's rows are the sums over all ranks on the rows it owns and 0
+      elsewhere -- so an ordinary optimizer over the full tensors updates the owned rows only.
+    * `push(tensors, means, conics)` (after the optimizer step): each owner recomputes the ranks
+      its updated Gaussians touch and sends those rows of `tensors` to them (ids + rows, one
+      count exchange).  A rank then HOLDS current copies of the rows it owns or was pushed --
+      every row whose cut reaches its strip -- and bins only those (`held`).  The push also fixes
+      the next reduce's row lists on both sides: the owner receives back exactly the rows it
+      pushed, so the reduce needs no count exchange.
+
+    `extents` [W, 2]: every rank's range [lo, hi] along the sharding axis (y at D = 2), fixed for
+    the run.  The constructor derives the first lists from the replicated parameters alone."""
+
+    def __init__(self, means, conics, extents, rank, group=None, debug=False):
         dev = means.device
-        ext = extents.detach().double().cpu()
-        W = ext.shape[0]
-        self.rank, self.world, self.group = rank, W, group
-        if means.is_cuda and W <= 32:
-            # native (dgs_exchange_sets): bit r of mask[g] = rank r can touch g; owner[g]
-            mask, owner = _C.exchange_sets(means.detach(), conics.detach(), [float(v) for v in ext.reshape(-1)])
-            mask, owner = mask.long(), owner.long()
-            touch_me = ((mask >> rank) & 1).bool()
-            self._mask = mask
-            self.touch = None
-        else:  # host tensors (the CPU tests): a P x W matrix in torch ops
-            y = means.detach()[:, D - 1].double()
-            e = support_halfwidth(means, conics)
-            lo, hi = ext[:, 0].to(dev), ext[:, 1].to(dev)
-            span = float(ext[:, 1].max() - ext[:, 0].min()) if W else 0.0
-            kmax = int(math.ceil(span / 2.0)) + 1
-            touch = torch.zeros(y.numel(), W, dtype=torch.bool, device=dev)
-            for k in range(-kmax, kmax + 1):
-                a, b = y + 2.0 * k - e, y + 2.0 * k + e
-                touch |= (a[:, None] <= hi[None, :]) & (b[:, None] >= lo[None, :])
-            dist_r = torch.clamp(torch.maximum(lo[None, :] - y[:, None], y[:, None] - hi[None, :]), min=0.0)
-            owner = torch.argmin(dist_r, dim=1)  # first minimum: deterministic
-            touch_me = touch[:, rank]
-            self._mask = None
-            self.touch = touch
+        self.extents = torch.as_tensor(extents).detach().double().cpu().clone()
+        W = self.extents.shape[0]
+        self.rank, self.world, self.group, self.debug = rank, W, group, debug
+        mask, owner = exchange_sets(means, conics, self.extents)
         self.owner = owner
-        # rows this rank sends, grouped by owner (ascending id within a group), and the rows it
-        # receives, grouped by source rank: two nonzero passes, one host read of the counts
-        snd = torch.nonzero(touch_me & (owner != rank)).flatten()
+        self.owned = owner == rank
+        touch_me = _bits(mask, rank)
+        self.held = touch_me | self.owned
+        # rows sent in the reduce, grouped by owner (ascending id within a group)
+        snd = torch.nonzero(touch_me & ~self.owned).flatten()
         so = owner[snd]
-        self.send_cat = snd[torch.argsort(so, stable=True)]
-        mine = torch.nonzero(owner == rank).flatten()
-        if self._mask is not None:
-            tm = ((self._mask[mine][:, None] >> torch.arange(W, device=dev)) & 1).bool()
-        else:
-            tm = self.touch[mine].clone()
-        tm[:, rank] = False
-        rg = torch.nonzero(tm.t())  # (source rank, position in `mine`), rank-major
-        self.recv_cat = mine[rg[:, 1]]
-        counts = torch.stack([torch.bincount(so, minlength=W), torch.bincount(rg[:, 0], minlength=W)]).cpu()
-        self.send_splits = [int(x) for x in counts[0]]
-        self.recv_splits = [int(x) for x in counts[1]]
-        self.send_idx = list(torch.split(self.send_cat, self.send_splits))
-        self.recv_idx = list(torch.split(self.recv_cat, self.recv_splits))
+        snd = snd[torch.argsort(so, stable=True)]
+        send_n = torch.bincount(so, minlength=W)
+        recv, recv_n = self._by_rank(mask, torch.nonzero(self.owned).flatten())
+        n = torch.stack([send_n, recv_n]).cpu()
+        self._set_lists(list(torch.split(snd, [int(v) for v in n[0]])), list(torch.split(recv, [int(v) for v in n[1]])))
 
-    def touches(self, r):
-        """Bool [P]: the Gaussians whose partial gradient can be non-zero on rank r."""
-        if self.touch is not None:
-            return self.touch[:, r]
-        return ((self._mask >> r) & 1).bool()
+    def _by_rank(self, mask, rows):
+        """`rows` grouped by every other rank whose bit is set in mask[rows] (a row appears once per
+        such rank; ascending within a group), and the group sizes (device)."""
+        W = self.world
+        bits = ((mask[rows][None, :] >> torch.arange(W, device=rows.device)[:, None]) & 1).bool()
+        bits[self.rank] = False
+        q, j = torch.nonzero(bits, as_tuple=True)  # rank-major, ascending row within a rank
+        return rows[j], torch.bincount(q, minlength=W)
+
+    def _set_lists(self, send, recv):
+        self.send_splits = [int(x.numel()) for x in send]
+        self.recv_splits = [int(x.numel()) for x in recv]
+        self.send_idx, self.recv_idx = send, recv
+        self.send_cat = torch.cat(send)
+        self.recv_cat = torch.cat(recv)
+
+    def _counts_a2a(self, counts):
+        """all-to-all of one int per rank pair (host lists in, host list out)."""
+        dev = torch.device("cpu") if dist.get_backend(self.group) == "gloo" else self.owner.device
+        mine = torch.tensor(counts, dtype=torch.long, device=dev)
+        got = torch.empty_like(mine)
+        dist.all_to_all_single(got, mine, [1] * self.world, [1] * self.world, group=self.group)
+        return [int(v) for v in got.cpu()]
 
     def rows_moved(self):
-        """Gaussian rows this rank sends per step (each way)."""
+        """Gaussian rows this rank sends in one reduce."""
         return sum(self.send_splits)
 
     def _a2a(self, out, inp, out_splits, in_splits):
@@ -216,28 +253,72 @@ class SupportExchange:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def exchange(self, G):
-        """G [P, F] float32, this rank's partial sums (modified in place): afterwards every row
-        this rank can touch holds the sum over all ranks."""
+    def _check_splits(self):
+        """debug: every rank's send count to q equals q's receive count from it (else raise on
+        every rank, before a mismatched all-to-all can hang or corrupt rows)."""
+        got = self._counts_a2a(self.send_splits)
+        dev = torch.device("cpu") if dist.get_backend(self.group) == "gloo" else self.owner.device
+        bad = torch.tensor([int(got != self.recv_splits)], device=dev)
+        dist.all_reduce(bad, group=self.group)
+        if int(bad.item()):
+            raise RuntimeError("SupportExchange: the ranks' row lists disagree -- the parameters were changed "
+                               "without push() (or differed between ranks at construction)")
+
+    def reduce(self, G):
+        """G [P, F] float32, this rank's partial sums (modified in place): afterwards the rows this
+        rank owns hold the sum over all ranks and every other row is 0."""
         if self.world == 1:
             return G
+        if self.debug:
+            self._check_splits()
         F = G.shape[1]
-        # 1. partials to the owners, added in rank order (deterministic: no duplicates per add)
         send = G.index_select(0, self.send_cat).contiguous()
         recv = torch.empty((sum(self.recv_splits), F), dtype=G.dtype, device=G.device)
         self._a2a(recv, send, self.recv_splits, self.send_splits)
+        G.masked_fill_(~self.owned[:, None], 0.0)
         o = 0
-        for r in range(self.world):
+        for r in range(self.world):  # added in rank order: deterministic
             n = self.recv_splits[r]
             if n:
                 G.index_add_(0, self.recv_idx[r], recv[o:o + n])
             o += n
-        # 2. the owners' sums back to every contributing rank
-        back = G.index_select(0, self.recv_cat).contiguous()
-        got = torch.empty((sum(self.send_splits), F), dtype=G.dtype, device=G.device)
-        self._a2a(got, back, self.send_splits, self.recv_splits)
-        G.index_copy_(0, self.send_cat, got)
         return G
+
+    @torch.no_grad()
+    def push(self, tensors, means, conics):
+        """After the optimizer step on the owned rows: send every owner's rows of `tensors` (each
+        [P, ...], float32; updated in place on the receivers) to the ranks its updated cut
+        reaches, computed from `means` / `conics` (the updated ones; only the owned rows are
+        read).  Updates `held` and the next reduce's row lists.  Returns the rows sent."""
+        W, me = self.world, self.rank
+        dev = self.owner.device
+        if W == 1:
+            return 0
+        mask, _ = exchange_sets(means, conics, self.extents)
+        ids, send_n = self._by_rank(mask, torch.nonzero(self.owned).flatten())
+        out_splits = [int(v) for v in send_n.cpu()]
+        in_splits = self._counts_a2a(out_splits)
+        out_ids = list(torch.split(ids, out_splits))
+        cols = [t.reshape(t.shape[0], -1) for t in tensors]
+        F = sum(c.shape[1] for c in cols)
+        rows = torch.cat([c.index_select(0, ids) for c in cols], 1) if F else torch.empty(0, 0, device=dev)
+        got_ids = torch.empty(sum(in_splits), dtype=torch.long, device=dev)
+        got_rows = torch.empty((sum(in_splits), F), dtype=torch.float32, device=dev)
+        self._a2a(got_ids, ids, in_splits, out_splits)
+        self._a2a(got_rows, rows.float().contiguous(), in_splits, out_splits)
+        o = 0
+        for t, c in zip(tensors, cols):
+            k = c.shape[1]
+            c.index_copy_(0, got_ids, got_rows[:, o:o + k].to(c.dtype))
+            if c.data_ptr() != t.data_ptr():  # a non-contiguous tensor: write back
+                t.copy_(c.reshape(t.shape))
+            o += k
+        held = self.owned.clone()
+        held[got_ids] = True
+        self.held = held
+        send = list(torch.split(got_ids, in_splits))  # ascending per owner (the owner sent them so)
+        self._set_lists(send, out_ids)
+        return int(ids.numel())
 
 
 def shard_extents(samples, group=None):
@@ -252,6 +333,21 @@ def shard_extents(samples, group=None):
     out = [torch.empty_like(mine) for _ in range(W)]
     dist.all_gather(out, mine.contiguous(), group=group)
     return torch.stack(out)
+
+
+def grid_and_box(samples, group=None):
+    """(grid, offset) of the union of every rank's samples (global_tile_grid) and this rank's
+    own bounding box (lo[D], hi[D]), read back in ONE host transfer."""
+    mn = samples.min(0).values
+    mx = samples.max(0).values
+    gmn, gmx = mn.clone(), mx.clone()
+    if _world(group) > 1:
+        dist.all_reduce(gmn, op=dist.ReduceOp.MIN, group=group)
+        dist.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
+    grid = torch.ceil((gmx - gmn + 1e-6) / 0.51).to(torch.float32)
+    h = torch.stack([grid, gmn, mn, mx]).cpu()
+    return ([int(g) for g in h[0]], [float(o) for o in h[1]], [float(v) for v in h[2]],
+            [float(v) for v in h[3]])
 
 
 def pack_grads(grads):
@@ -287,24 +383,66 @@ class _SpatialSample(torch.autograd.Function):
         grads = call_debug(bwd, ctx.debug, "spatial_bw", means, values, conics, samples,
                            ctx.num_rendered, grad_out.contiguous(), binning, sample_binning,
                            ranges, sample_ranges, ctx.debug)
-        G = ctx.xchg.exchange(pack_grads(grads))
+        G = ctx.xchg.reduce(pack_grads(grads))
         gm, gv, gc = unpack_grads(G, grads)
         return (None, None, gm, gv, gc) + (None,) * 7
 
 
 class SpatialShardedGaussianSampler(ShardedGaussianSampler):
-    """ShardedGaussianSampler for ranks that own spatial strips of the query points (SURVEY 8f
-    row f3): the same global grid and per-rank binning, and the gradients summed by
-    SupportExchange instead of a dense all-reduce.  After backward, every Gaussian that can touch
-    this rank's points carries the sum over all ranks; the other rows are this rank's partials,
-    exactly zero (no point of this rank is within their cut)."""
+    """ShardedGaussianSampler as a domain decomposition (see SupportExchange).
+
+    Rank r's `samples` must stay inside its strip along the sharding axis (y at D = 2): `extents`
+    [W, 2], or, by default, the all-gathered ranges of the first preprocess call.  The Gaussian
+    tensors keep all P rows on every rank, but only the rows this rank holds are current and
+    binned.  Training loop per step:
+
+        sampler.preprocess(means, values, covariances, conics, samples)
+        loss(sampler.sample_gaussians(), ...).backward()  # grads: global sums on the owned rows, 0 elsewhere
+        optimizer.step()                                    # moves the owned rows only
+        sampler.push([params...], means, conics)            # owners -> every rank their cut reaches
+
+    All ranks start from identical parameters.  Changing means, conics or samples in place between
+    preprocess and a sampling call raises (the exchange lists are those of the binned tensors)."""
+
+    def __init__(self, debug=False, group=None, extents=None):
+        super().__init__(debug, group)
+        self.xchg = None
+        self.extents = extents
 
     def preprocess(self, means, values, covariances, conics, samples):
-        super().preprocess(means, values, covariances, conics, samples)
-        rank = dist.get_rank(self.group) if _world(self.group) > 1 else 0
-        self.xchg = SupportExchange(means, conics, shard_extents(samples, self.group), rank, self.group)
+        W = _world(self.group)
+        rank = dist.get_rank(self.group) if W > 1 else 0
+        D = samples.shape[1]
+        grid, offset, lo, hi = grid_and_box(samples, self.group)
+        if self.xchg is None:
+            ext = self.extents if self.extents is not None else shard_extents(samples, self.group)
+            self.xchg = SupportExchange(means, conics, ext, rank, self.group, self.debug)
+        e = self.xchg.extents[rank]
+        if samples.shape[0] and (lo[D - 1] < float(e[0]) or hi[D - 1] > float(e[1])):
+            raise ValueError(f"rank {rank}: samples leave the rank's strip [{float(e[0])}, {float(e[1])}] "
+                             f"along the sharding axis ([{lo[D - 1]}, {hi[D - 1]}])")
+        area = 1.0
+        for d in range(D):
+            area *= max(hi[d] - lo[d], 0.0)
+        (self.num_rendered, self.binning_buffer, self.sample_binning_buffer, self.ranges,
+         self.sample_ranges, self.radii) = call_debug(
+            _C.preprocess_gaussians_sharded, self.debug, "spatial_preprocess", means, values,
+            covariances, conics, samples, grid, offset, self.xchg.held, area, self.debug)
+        self.grid, self.offset = grid, offset
+        self.means, self.values, self.conics, self.samples = means, values, conics, samples
+        self._versions = (means._version, conics._version, samples._version)
+
+    def push(self, tensors, means=None, conics=None):
+        """After optimizer.step(): the owners' rows of `tensors` to every rank their updated cut
+        reaches (SupportExchange.push).  `means` / `conics` default to the tensors the last
+        preprocess was given (right when they are the optimised leaves themselves)."""
+        return self.xchg.push(tensors, self.means if means is None else means,
+                              self.conics if conics is None else conics)
 
     def _sample(self, function):
+        if (self.means._version, self.conics._version, self.samples._version) != self._versions:
+            raise RuntimeError("SpatialShardedGaussianSampler: means, conics or samples were modified in place "
+                               "after preprocess; call push() (after an optimizer step) and preprocess() again")
         return _SpatialSample.apply(function, self.xchg, self.means, self.values, self.conics,
                                     self.samples, self.num_rendered, self.binning_buffer,
                                     self.sample_binning_buffer, self.ranges, self.sample_ranges,

@@ -48,6 +48,15 @@ def samples(N, D=2, seed=4):
     return (torch.rand(N, D, generator=_gen(seed), dtype=torch.float64) * 2.0 - 1.0).float()
 
 
+def strip_samples(N, D, rank, world, seed=4):
+    """Rank `rank`'s query points of a spatially sharded run (config 4): uniform over strip
+    `rank` of `world` equal strips of [-1, 1) along the last axis, so that the union over the
+    ranks is uniform on [-1, 1)^D."""
+    s = samples(N, D, seed)
+    s[:, D - 1] = -1.0 + (2.0 / world) * (rank + 0.5 * (s[:, D - 1] + 1.0))
+    return s
+
+
 def grid_samples(n, D=2):
     """A regular n^D lattice on [-1, 1)^D (the physics-informed collocation grid)."""
     ax = torch.arange(n, dtype=torch.float64) * (2.0 / n) - 1.0

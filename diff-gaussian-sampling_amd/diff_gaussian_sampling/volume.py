@@ -55,7 +55,10 @@ class VolumeSampler:
     """GaussianSampler's shape for D = 3: preprocess once per (means, conics, samples), then
     sample any of the four functions.  covariances are accepted for signature parity with
     GaussianSampler.preprocess (reference py:214-230) and unused, as the cut is derived from
-    the conics."""
+    the conics.  The tensors are kept by reference: when means, conics or samples were changed
+    in place since preprocess (an optimizer step), the next sampling call re-bins them first.
+    (The functional `sample_volume` with a stale binning writes NaN instead: every call compares
+    its tensors with the binned ones on the device, include/dgs_volume.h.)"""
 
     def __init__(self, debug=False):
         self.debug = debug
@@ -63,8 +66,15 @@ class VolumeSampler:
     def preprocess(self, means, values, covariances, conics, samples):
         self.binning = preprocess_volume(means, conics, samples, self.debug)
         self.means, self.values, self.conics, self.samples = means, values, conics, samples
+        self._versions = self._now()
+
+    def _now(self):
+        return (self.means._version, self.conics._version, self.samples._version)
 
     def _run(self, code):
+        if self._now() != self._versions:  # changed in place since the binning: re-bin
+            self.binning = preprocess_volume(self.means, self.conics, self.samples, self.debug)
+            self._versions = self._now()
         return sample_volume(code, self.means, self.values, self.conics, self.samples, self.binning,
                              self.debug)
 

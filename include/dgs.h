@@ -52,7 +52,12 @@ enum dgs_buffer {
 };
 
 /* Returns device memory of at least `bytes` bytes (16-byte aligned), or NULL on failure.
- * It may be called several times per buffer kind only for DGS_BUF_SCRATCH. */
+ * DGS_BUF_SCRATCH is requested several times per call.  Within one call the other kinds may be
+ * requested more than once too: dgs_preprocess sizes its lists before its host sync from the
+ * previous call's sizes and asks again if they do not fit, and dgs_preprocess_auto bins a
+ * second time when its grid guess was wrong.  The LAST pointer returned for a kind is the one
+ * the call's results live in; the earlier ones of that kind are unused once the call returns
+ * (a torch caller simply drops them; an arena caller should size for two of each). */
 typedef void *(*dgs_alloc_fn)(void *ctx, int which, size_t bytes);
 
 const char *dgs_last_error(void);
@@ -79,11 +84,36 @@ int dgs_preprocess(int P, int D, int N, const float *means, const float *covaria
                    const float *grid_offset, float *radii, dgs_alloc_fn alloc, void *alloc_ctx,
                    int64_t *num_rendered, dgs_stream_t stream, int debug);
 
+/* Options of dgs_preprocess_ex (zero-initialise, then set what is wanted). */
+typedef struct dgs_bin_options {
+    /* device uint8[P] or NULL.  Gaussians with present[g] == 0 are left out of the binning the
+     * way a det == 0 Gaussian is (radius 0, no tiles, no pairs; radii[g] = 0 and they do not
+     * count in num_rendered).  A rank of a spatially sharded run bins only the rows it holds
+     * current copies of (diff_gaussian_sampling.distributed.SpatialShardedGaussianSampler). */
+    const uint8_t *present;
+    /* > 0: the area (D = 2; a length at D = 1, domain units) the samples actually occupy.  The
+     * fine cells are then sized for the density N / sample_area instead of N / (T tiles): a
+     * shard's points fill only part of the global tile grid.  Results do not depend on it
+     * beyond float summation order; 0 = the whole grid. */
+    double sample_area;
+} dgs_bin_options;
+
+/* dgs_preprocess with options (NULL = dgs_preprocess). */
+int dgs_preprocess_ex(int P, int D, int N, const float *means, const float *covariances,
+                      const float *conics, const float *samples, const int *grid,
+                      const float *grid_offset, const dgs_bin_options *opts, float *radii,
+                      dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
+                      dgs_stream_t stream, int debug);
+
 /* dgs_preprocess with the tile grid of the reference host glue (sample_points.cu:70-74)
  * computed on the device (dgs_tile_grid's arithmetic) instead of passed in: the reference's
- * PreprocessCUDA as a whole, with ONE host sync per call.  The binning starts with the grid of
- * the previous call (per D) while the device computes this call's grid; both come back at the
- * binning's single sync, and only a changed grid (the first call, a new domain) re-bins.
+ * PreprocessCUDA as a whole.  Per sample set (the samples pointer, N and D; 8 sets remembered)
+ * the call either speculates -- bins with the set's previous grid while the device computes
+ * this call's, both read back at the binning's one host sync, re-binning only on a miss -- or
+ * reads the grid first (one small extra sync, then one binning).  A set speculates after two
+ * consecutive calls found the same grid, and a miss returns it to read-first: fixed samples
+ * pay one sync per call, resampled points (whose min, the offset, moves) one extra small one,
+ * and never a second binning after their first miss.
  * grid_out[D] / offset_out[D] (host): the grid used.  Replaces PreprocessCUDA
  * (sample_points.cu:38-98) + Sampler::preprocess (sampler_impl.cu:216-330). */
 int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *covariances,
@@ -95,7 +125,8 @@ int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *co
  * each Gaussian, bit r of mask_out[g] is set when rank r's point range extents[r] = [lo, hi]
  * along the sharding axis (y at D = 2, x at D = 1) meets the Gaussian's exact-zero cut
  * X^T A X <= 210 or one of its torus images (period 2, forward.cu:149-157), i.e. when rank r's
- * partial gradient for it can be non-zero; owner_out[g] is the rank nearest its mean.
+ * partial gradient for it can be non-zero; owner_out[g] is the rank nearest its mean among the
+ * ranks it touches (the nearest of all ranks when it touches none; first on ties).
  * extents: host array [W][2]; 1 <= W <= 32. */
 int dgs_exchange_sets(int P, int D, const float *means, const float *conics, int W,
                       const double *extents, uint32_t *mask_out, int32_t *owner_out,

@@ -33,7 +33,10 @@ extern "C" {
  * smaller than the largest exact-zero cut half-width.  means[P][3], conics[P][6], samples[N][3].
  * The opaque buffer (DGS_BUF_BINNING) is requested through `alloc`; scratch as DGS_BUF_SCRATCH.
  * Synchronises `stream` once (bounds, to size the grid).  forward/backward must be given the
- * same means, conics and samples (re-bin when they change). */
+ * same means, conics and samples (re-bin when they change): every forward / backward /
+ * count_pairs call compares its tensors bitwise with the binned ones on the device (no sync)
+ * and, on a difference, writes NaN to every output, as for a stale buffer.  The buffer holds
+ * a flag word that these calls write. */
 int dgs_volume_preprocess(int P, int N, const float *means, const float *conics,
                           const float *samples, dgs_alloc_fn alloc, void *alloc_ctx,
                           dgs_stream_t stream, int debug);

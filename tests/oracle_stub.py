@@ -31,6 +31,15 @@ class OracleC:
         as_bytes = lambda r: torch.from_numpy(np.concatenate([r.reshape(-1), pad]).view(np.uint8).copy())
         return ob.num_rendered, gb, sb, as_bytes(rg), as_bytes(srg), torch.from_numpy(ob.radii.copy())
 
+    def preprocess_gaussians_sharded(self, means, values, covariances, conics, samples, grid, offset,
+                                     present, sample_area, debug):
+        """`present` == 0 rows are left out as a det == 0 Gaussian is (zeroed covariance);
+        `sample_area` only sizes the GPU's fine cells, so the oracle ignores it."""
+        covs = covariances.detach().clone()
+        if present is not None:
+            covs[~present.bool().cpu()] = 0.0
+        return self.preprocess_gaussians_bounded(means, values, covs, conics, samples, grid, offset, debug)
+
     def preprocess_gaussians(self, means, values, covariances, conics, samples, debug):
         return self.preprocess_gaussians_bounded(means, values, covariances, conics, samples,
                                                  None, None, debug)

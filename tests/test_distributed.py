@@ -115,25 +115,27 @@ def _spatial_worker(rank, world, port, outdir):
         order = torch.argsort(samples[:, 1])  # spatial strips along y
         shard = torch.tensor_split(order, world)[rank].sort().values
         m, v, c = (t.clone().requires_grad_(True) for t in (means, values, conics))
-        sampler = dd.SpatialShardedGaussianSampler(False)
+        sampler = dd.SpatialShardedGaussianSampler(debug=True)
         sampler.preprocess(m, v, covs, c, samples[shard])
         out = sampler.sample_gaussians_derivative()
         (out * w[shard]).sum().backward()
         x = sampler.xchg
+        mask, _ = dd.exchange_sets(means, conics, x.extents)
         np.savez(os.path.join(outdir, f"srank{rank}.npz"), out=out.detach().numpy(),
                  shard=shard.numpy(), gm=m.grad.numpy(), gv=v.grad.numpy(), gc=c.grad.numpy(),
-                 touch=np.stack([x.touches(r).numpy() for r in range(world)], 1),
-                 owner=x.owner.numpy(), moved=x.rows_moved())
+                 touch=np.stack([((mask >> r) & 1).bool().numpy() for r in range(world)], 1),
+                 owner=x.owner.numpy(), held=x.held.numpy(), moved=x.rows_moved())
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_spatial_shards_support_exchange(tmp_path, oracle, world):
-    """SpatialShardedGaussianSampler: strips of the points along y; the gradient
-    sum travels only for Gaussians whose exact-zero cut (or a torus image of it) reaches another
-    rank's strip.  Every row a rank can touch equals the single-process gradient over all points;
-    the others are exactly zero there; fewer rows move than a dense all-reduce would."""
+    """SpatialShardedGaussianSampler: strips of the points along y, each rank binning
+    only the Gaussians it holds.  Outputs equal the single-process oracle bit for bit; after the
+    backward every rank holds the single-process gradient on the rows it owns and exactly 0
+    elsewhere; every row has one owner, a rank it touches when it touches any; fewer rows move
+    than are touched."""
     mp.spawn(_spatial_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     means, values, covs, conics, samples, w = _spatial_problem()
     ranks = [np.load(tmp_path / f"srank{r}.npz") for r in range(world)]
@@ -147,16 +149,90 @@ def test_spatial_shards_support_exchange(tmp_path, oracle, world):
     assert np.array_equal(got, ref)
     dm, dv, dc = ob.backward("derivative", values.numpy(), conics.numpy(), w.numpy())
     P = means.shape[0]
+    owner = ranks[0]["owner"]
+    touch = ranks[0]["touch"]
+    assert np.all(touch[np.arange(P), owner] | ~touch.any(1))  # the owner touches the row
     for ri, r in enumerate(ranks):
-        t = r["touch"][:, ri]
+        assert np.array_equal(r["owner"], owner) and np.array_equal(r["touch"], touch)
+        mine = owner == ri
+        t = touch[:, ri]
         assert 0 < t.sum() < P  # strips: not every Gaussian reaches every rank
+        assert np.array_equal(r["held"], t | mine)
         for k, exp in (("gm", dm), ("gv", dv), ("gc", dc)):
-            np.testing.assert_allclose(r[k][t], exp[t], rtol=1e-5, atol=1e-5 * np.abs(exp).max())
-            assert np.all(r[k][~t] == 0)
+            np.testing.assert_allclose(r[k][mine], exp[mine], rtol=1e-5, atol=1e-5 * np.abs(exp).max())
+            assert np.all(r[k][~mine] == 0)
         assert r["moved"] < 0.5 * t.sum()
-    # every Gaussian has one owner, the same on every rank
-    for r in ranks[1:]:
-        assert np.array_equal(r["owner"], ranks[0]["owner"]) and np.array_equal(r["touch"], ranks[0]["touch"])
+
+
+def _cov_of(conics):
+    """D = 2 covariances [xx, xy, yy] of packed conics [c0, c1, c2] (exact 2x2 inverse)."""
+    c = conics.detach().double()
+    det = c[:, 0] * c[:, 2] - c[:, 1] ** 2
+    return torch.stack([c[:, 2] / det, -c[:, 1] / det, c[:, 0] / det], 1).float()
+
+
+ADAM_STEPS, ADAM_LR = 3, 1e-3
+
+
+def _adam_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import diff_gaussian_sampling.distributed as dd
+        from oracle_stub import OracleC
+        dd._C = OracleC()
+        means, values, covs, conics, samples, w = _spatial_problem()
+        order = torch.argsort(samples[:, 1])
+        shard = torch.tensor_split(order, world)[rank].sort().values
+        m, v, c = (t.clone().requires_grad_(True) for t in (means, values, conics))
+        opt = torch.optim.Adam([m, v, c], lr=ADAM_LR)
+        sampler = dd.SpatialShardedGaussianSampler()
+        moved = []
+        for _ in range(ADAM_STEPS):
+            sampler.preprocess(m, v, _cov_of(c), c, samples[shard])
+            opt.zero_grad()
+            (sampler.sample_gaussians_derivative() * w[shard]).sum().backward()
+            opt.step()
+            moved.append(sampler.push([m, v, c]))
+        np.savez(os.path.join(outdir, f"adam{rank}.npz"), m=m.detach().numpy(), v=v.detach().numpy(),
+                 c=c.detach().numpy(), owned=sampler.xchg.owned.numpy(), held=sampler.xchg.held.numpy(),
+                 moved=np.asarray(moved))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_spatial_shards_adam_matches_single_process(tmp_path, oracle):
+    """Three Adam steps of a 2-rank spatially sharded run (owner-side reduce, optimizer over the
+    full tensors, push of the owners' rows) against the same loop in one process over all the
+    points: every rank's held rows -- the owned and the pushed ones, i.e. every row its strip
+    reads -- equal the single-process parameters."""
+    import diff_gaussian_sampling.distributed as dd
+    from oracle_stub import OracleC
+    world = 2
+    mp.spawn(_adam_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    means, values, covs, conics, samples, w = _spatial_problem()
+    saved = dd._C
+    dd._C = OracleC()
+    try:
+        m, v, c = (t.clone().requires_grad_(True) for t in (means, values, conics))
+        opt = torch.optim.Adam([m, v, c], lr=ADAM_LR)
+        sampler = dd.ShardedGaussianSampler()
+        for _ in range(ADAM_STEPS):
+            sampler.preprocess(m, v, _cov_of(c), c, samples)
+            opt.zero_grad()
+            (sampler.sample_gaussians_derivative() * w).sum().backward()
+            opt.step()
+    finally:
+        dd._C = saved
+    ref = {"m": m.detach().numpy(), "v": v.detach().numpy(), "c": c.detach().numpy()}
+    ranks = [np.load(tmp_path / f"adam{r}.npz") for r in range(world)]
+    assert np.array_equal(ranks[0]["owned"], ~ranks[1]["owned"])
+    for r in ranks:
+        h = r["held"]
+        assert 0 < h.sum() < len(h) and np.all(r["moved"] > 0)
+        for k in ("m", "v", "c"):
+            np.testing.assert_allclose(r[k][h], ref[k][h], rtol=2e-5, atol=1e-6 * np.abs(ref[k]).max())
+        assert not np.allclose(ref["m"], means.numpy())  # the steps moved the parameters
 
 
 def test_support_halfwidth_bounds_the_live_pairs(oracle):

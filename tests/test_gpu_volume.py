@@ -160,3 +160,42 @@ def test_volume_sampler_autograd(dgs):
     _close(m.grad.cpu().numpy(), rm, ATOL_BWD, "dmeans")
     _close(v.grad.cpu().numpy(), rv, ATOL_BWD, "dvalues")
     _close(c.grad.cpu().numpy(), rc, ATOL_BWD, "dconics")
+
+
+def test_volume_changed_inputs_are_loud(dgs):
+    """Same sizes, different tensors (an in-place step, moved samples): the device-side check of
+    every call writes NaN instead of mixing the binned means with the new ones."""
+    from diff_gaussian_sampling import _C
+    dev = torch.device("cuda:0")
+    means, values, _, conics = (torch.from_numpy(x).to(dev) for x in _field(400, 1, 2))
+    s = torch.from_numpy(vo.samples3(500, seed=2)).to(dev)
+    buf = _C.volume_preprocess(means, conics, s, False)
+    ok = _C.volume_forward(0, means, values, conics, s, buf, False)
+    assert torch.isfinite(ok).all()
+    for which in range(3):
+        m2, c2, s2 = means.clone(), conics.clone(), s.clone()
+        (m2, c2, s2)[which][7, 0] += 1e-3
+        out = _C.volume_forward(0, m2, values, c2, s2, buf, False)
+        assert torch.isnan(out).all(), which
+        dm, dv, dc = _C.volume_backward(0, m2, values, c2, s2, buf, torch.ones_like(out), False)
+        assert torch.isnan(dm).all() and torch.isnan(dc).all(), which
+    again = _C.volume_forward(0, means, values, conics, s, buf, False)  # the binned tensors: fine again
+    assert torch.equal(again, ok)
+
+
+def test_volume_sampler_rebins_after_inplace_step(dgs):
+    """VolumeSampler keeps its tensors by reference: after an in-place optimizer step the next
+    call re-bins, and the result equals the oracle at the new parameters."""
+    from diff_gaussian_sampling.volume import VolumeSampler
+    dev = torch.device("cuda:0")
+    means, values, covs, conics = _field(700, 1, 9)
+    samples = vo.samples3(900, seed=9)
+    m, v, cv, c, s = (torch.from_numpy(x).to(dev) for x in (means, values, covs, conics, samples))
+    vs = VolumeSampler(False)
+    vs.preprocess(m, v, cv, c, s)
+    vs.sample_gaussians()
+    with torch.no_grad():
+        m[:, 0] += 0.013  # moves every Gaussian by about a cell
+    out = vs.sample_gaussians_derivative()
+    ref = vo.forward(1, m.cpu().numpy(), values, conics, samples)
+    _close(out.cpu().numpy().reshape(900, 3, 1), ref, ATOL_FWD, "derivative after the in-place step")
