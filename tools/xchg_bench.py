@@ -1,4 +1,4 @@
-"""Time SupportExchange's set construction (distributed.py) at the config-4 shape in ONE process:
+"""Time SupportExchange's one-time set construction (distributed.py) at the config-4 shape in ONE process:
 1M headline Gaussians, 8 strips of [-1, 1) along y as the rank extents (no collective runs in
 the constructor).  Prints the warm median per rank and the rows each rank moves.
 
@@ -37,5 +37,5 @@ for r in (0, W // 2):
         torch.cuda.synchronize()
         ts.append((time.perf_counter() - t0) * 1e3)
     res[f"rank{r}"] = {"setup_ms_median": sorted(ts)[len(ts) // 2], "rows_sent": x.rows_moved(),
-                       "rows_received": sum(x.recv_splits), "touching": int(x.touches(r).sum())}
+                       "rows_received": sum(x.recv_splits), "held": int(x.held.sum())}
 print(json.dumps(res))
