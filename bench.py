@@ -226,6 +226,26 @@ def bench_sample(args, world, rank, dev, torch, dist):
     pre_first_ms = pre_times[0]
     pre_ms = sorted(pre_times[1:])[len(pre_times[1:]) // 2] if args.pre_reps > 0 else pre_first_ms
     R, gb, sb, rg, srg, radii = binned
+    pre_extra = {}
+    if world == 1 and args.pre_reps > 0:
+        # the PIGS loop's other binning patterns (one GPU, reference API): fresh collocation points
+        # every call (samples.min -- the grid offset -- moves each time), and two samplers whose
+        # domains alternate (interior / boundary points); inputs generated before the clock starts
+        med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
+        fresh = [torch.rand(N, D, device=dev) * 2.0 - 1.0 for _ in range(args.pre_reps + 1)]
+        other = torch.rand(N, D, device=dev) * 1.5 - 0.5
+        pats = {"preprocess_resampled_ms": [fresh[i] for i in range(args.pre_reps + 1)],
+                "preprocess_alternating_ms": [samples if i % 2 == 0 else other for i in range(2 * args.pre_reps + 2)]}
+        for key, seq in pats.items():
+            ts = []
+            for sm in seq:
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                dgs._C.preprocess_gaussians(means.detach(), values.detach(), covs, conics.detach(), sm, False)
+                torch.cuda.synchronize()
+                ts.append((time.perf_counter() - t0) * 1e3)
+            pre_extra[key] = med(ts[2:])
+        del fresh, other
     fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative,
            "laplacian": dgs.sample_gaussians_laplacian,
            "third": dgs.sample_gaussians_third_derivative}[fn]
@@ -363,6 +383,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
         # the Physics-Informed-GS loop re-bins every step (means move): its step time
         "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms + push_ms,
         "preprocess_first_call_ms": pre_first_ms,
+        **pre_extra,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
         "roofline": roofline,

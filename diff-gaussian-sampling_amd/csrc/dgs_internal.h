@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <algorithm>
 #include <string>
 
 #include "dgs.h"
@@ -19,7 +20,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 4;
+constexpr uint32_t kVersion = 5;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -38,6 +39,12 @@ constexpr int kWave = 64;
 // sample order (pairs (2p, 2p+1) are packed fp32 operands; a pair may straddle a cell edge,
 // its foreign sample is evaluated but not written).
 constexpr int kFwdUnit = kWave;
+// Sub-cells (D = 2): every fine cell is split 2 x 2 at its nominal mid-lines; samples are sorted
+// by (cell, sub-cell), and the forward walks per sub-cell the entries of its cell whose cut
+// meets the sub-cell's sample box (sub lists), in units of up to kSubPairs sample pairs.  The
+// backward keeps the cell lists (their per-cell flush is what the float atomics allow).
+constexpr int kSubPerCell = 4;
+constexpr int kSubPairs = 24;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
@@ -82,28 +89,45 @@ struct Header {
     uint64_t o_cell_box;  // sample buffer: per-cell bounding box of the cell's samples
     uint64_t o_gmean, o_gcon, o_fsrows;
     uint64_t o_mcopy, o_ccopy, o_rlist, o_rtab, o_scopy;
+    // sub-cells (D = 2; empty at D = 1): sample side [sub_sbeg/send int32[4 ncells]]
+    // [sub_box float4[4 ncells]] [fsub_units uint2[fsub_cap]]; Gaussian side
+    // [sub_lbeg/lmid/lend int32[4 ncells]] [sub_ent uint32[Esub_cap]]
+    uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
+    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
+    int64_t fsub_cap, esub_cap;
+    uint64_t o_sub_pos;  // uint16[Esub_cap]: cell-list position of each flag-free sub-list entry
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
 enum RefTab { kRtGStart = 0, kRtSStart = 1, kRtFwdUnits = 2, kRtBwdUnits = 3 };
 constexpr int kRefUnit = 64;  // call-time path: samples (forward) / list entries (backward) per unit
 
-enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1, kNumUnsafe = 2 };
+enum Counter { kNumFwdUnits = 0, kNumBwdUnits = 1, kNumUnsafe = 2, kNumFwdSubUnits = 3 };
 
 __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
     uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab;
+    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent, o_sub_pos;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
+    uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
 };
 
 // Forward sample pair rows: N rounded up to a pair, plus slack for a pass's wide scalar loads
 // (up to 32 pairs + one x16 load past the last pair).
 inline size_t fsrows_bytes(int64_t N, int D) { return ((size_t)N + 1) * D * 4 + 36 * 16; }
 
+// Sub-list capacity: an entry is in at most every sub-list of its cell (D = 2).
+inline int64_t esub_cap_of(int D, int64_t E) { return D == 2 ? kSubPerCell * E : 0; }
+inline int64_t fsub_cap_of(int D, int64_t N, int64_t ncells) {
+    // per non-empty sub-cell: ceil(pairs / kSubPairs) <= its samples / (2 kSubPairs) + 2
+    return D == 2 ? (N + 1) / 2 / kSubPairs + 2 * std::min<int64_t>(kSubPerCell * ncells, N) + 1 : 0;
+}
+
 inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int64_t ncells, int64_t E,
                           int64_t fwd_cap, int64_t bwd_cap) {
+    const int64_t nsub = D == 2 ? kSubPerCell * ncells : 0;
     const int S = D * (D + 1) / 2;
     Layout L;
     size_t o = kHeaderBytes;
@@ -120,6 +144,11 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_ccopy = o;     o = align_up(o + 4 * (size_t)P * S, 256);
     L.o_rlist = o;     o = align_up(o + 4 * (size_t)R + 64, 256);
     L.o_rtab = o;      o = align_up(o + 16 * ((size_t)T + 1), 256);
+    L.o_sub_lbeg = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_ent = o;   o = align_up(o + 4 * (size_t)esub_cap_of(D, E) + 64, 256);
+    L.o_sub_pos = o;   o = align_up(o + 2 * (size_t)esub_cap_of(D, E) + 64, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
     L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);
@@ -129,6 +158,10 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_cell_box = o;  o = align_up(o + 16 * (size_t)ncells, 256);
     L.o_fsrows = o;    o = align_up(o + fsrows_bytes(N, 2), 256);
     L.o_scopy = o;     o = align_up(o + 4 * (size_t)N * D, 256);
+    L.o_sub_sbeg = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_send = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_box = o;   o = align_up(o + 16 * (size_t)nsub, 256);
+    L.o_fsub_units = o; o = align_up(o + 8 * (size_t)fsub_cap_of(D, N, ncells), 256);
     L.s_bytes = o;
     return L;
 }
@@ -150,6 +183,12 @@ struct Bins {
     const float *fsrows;     // sample pair rows in sorted order
     const uint32_t *rlist;   // reference tile lists (ascending Gaussian id per tile)
     const uint32_t *rtab;    // [4][T+1] per-tile tables of the call-time path (RefTab)
+    const int32_t *sub_sbeg, *sub_send;  // sample range per sub-cell (cell * 4 + sub)
+    const float4 *sub_box;
+    const uint2 *fsub_units;             // (sub-cell, pair-aligned first sample)
+    const int32_t *sub_lbeg, *sub_lmid, *sub_lend;
+    const uint32_t *sub_ent;             // sub lists: entries of the cell list, flagged last
+    const uint16_t *sub_pos;             // their positions in the cell list (flag-free part)
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -199,6 +238,15 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.fsrows = reinterpret_cast<const float *>(sb + o_fsrows);
     B.rlist = reinterpret_cast<const uint32_t *>(gb + o_rlist);
     B.rtab = reinterpret_cast<const uint32_t *>(gb + o_rtab);
+    B.sub_sbeg = reinterpret_cast<const int32_t *>(sb + sload(&B.h->o_sub_sbeg));
+    B.sub_send = reinterpret_cast<const int32_t *>(sb + sload(&B.h->o_sub_send));
+    B.sub_box = reinterpret_cast<const float4 *>(sb + sload(&B.h->o_sub_box));
+    B.fsub_units = reinterpret_cast<const uint2 *>(sb + sload(&B.h->o_fsub_units));
+    B.sub_lbeg = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lbeg));
+    B.sub_lmid = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lmid));
+    B.sub_lend = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lend));
+    B.sub_ent = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_sub_ent));
+    B.sub_pos = reinterpret_cast<const uint16_t *>(gb + sload(&B.h->o_sub_pos));
     return B;
 }
 
@@ -424,6 +472,27 @@ __device__ inline uint32_t sample_cell(const Geom &G, const float *s) {
     return key * (uint32_t)G.CT + (uint32_t)(f[1] * G.n + f[0]);
 }
 
+// (cell, sub-cell) key = cell * 4 + sub: at D = 2 the sub-cell of a fine cell is the quadrant of
+// its nominal square (bit 0: x in the upper half, bit 1: y); the fallback cell and D = 1 use
+// sub 0.  Never-rendered samples: ncells * 4.
+__device__ inline uint32_t sample_cell_sub(const Geom &G, const float *s) {
+    DGS_NO_CONTRACT
+    const uint32_t cell = sample_cell(G, s);
+    if (cell >= (uint32_t)G.ncells) return (uint32_t)G.ncells * kSubPerCell;
+    const uint32_t local = cell % (uint32_t)G.CT;
+    if (G.D != 2 || local == (uint32_t)(G.CT - 1)) return cell * kSubPerCell;
+    const uint32_t tile = cell / (uint32_t)G.CT;
+    const int tc[2] = {(int)(tile % (uint32_t)G.grid[0]), (int)(tile / (uint32_t)G.grid[0])};
+    const int f[2] = {(int)(local % (uint32_t)G.n), (int)(local / (uint32_t)G.n)};
+    uint32_t sub = 0;
+    for (int i = 0; i < 2; ++i) {
+        const double d = (double)rsub(s[i], G.off[i]);
+        const double u = (d - (double)tc[i] * (double)kTile) / G.fs - (double)f[i];
+        if (u >= 0.5) sub |= 1u << i;
+    }
+    return cell * kSubPerCell + sub;
+}
+
 // ---------------------------------------------------------------------------------------
 // Host-side launch hints.  preprocess records the exact work-unit counts of the buffers it
 // created; forward/backward size their grids from them.  The kernels grid-stride over the
@@ -432,7 +501,7 @@ __device__ inline uint32_t sample_cell(const Geom &G, const float *s) {
 struct UnitHint {
     const void *gbuf, *sbuf;
     size_t gbytes, sbytes;
-    int64_t nfwd, nbwd;
+    int64_t nfwd, nbwd, nfsub, ncells;
     int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
     int64_t R;        // num_rendered (sizes the call-time path's backward grid)

@@ -152,7 +152,7 @@ __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
             if (lds) atomicAdd(&hist[key], 1u);
             else atomicAdd(&tile_count[key], 1u);
         }
-        keys[i] = sample_cell(G, s);
+        keys[i] = sample_cell_sub(G, s);  // (cell, sub-cell): cell ranges are keys >> 2
         ids[i] = (uint32_t)i;
     }
     __syncthreads();
@@ -595,16 +595,20 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                                                        const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
                                                        const int32_t *__restrict__ send, const float4 *__restrict__ box,
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
-                                                       uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax) {
+                                                       uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
+                                                       float2 *__restrict__ igm, float4 *__restrict__ igc) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int reach = 0;
     if (i < P) {
         const int64_t g = perm[i];
         const float r = radii[g];
         uint64_t n = 0;
+        float m[2], c[3];
+        load_gauss(G.D, means, conics, g, m, c);
+        // the one random gather of the Gaussians: internal-order copies for k_fine_fill / k_geo_pack
+        igm[i] = make_float2(m[0], m[1]);
+        igc[i] = make_float4(c[0], c[1], c[2], r);
         if (r > 0.0f) {
-            float m[2], c[3];
-            load_gauss(G.D, means, conics, g, m, c);
             const Cut k = gauss_cut(G, m, c);
             reach = gather_reach(G, m, r, c, k);
             if (reach > 0) {
@@ -630,8 +634,7 @@ constexpr int kFillBlock = 128, kFillCap = 3072;
 // then moves 6 instead of 8 bytes per entry and pass).
 template <typename KT>
 __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
-    int P, Geom G, const uint32_t *__restrict__ perm, const float *__restrict__ means,
-    const float *__restrict__ conics, const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+    int P, Geom G, const float2 *__restrict__ igm, const float4 *__restrict__ igc, const int32_t *__restrict__ sbeg,
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, KT *__restrict__ ekeys,
     uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
@@ -643,10 +646,10 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     const bool stage = end - base <= (uint64_t)kFillCap;
     uint32_t nunsafe = 0;
     if (i < P && cnts[i] > 0) {
-        const int64_t g = perm[i];
-        const float r = radii[g];
-        float m[2], c[3];
-        load_gauss(G.D, means, conics, g, m, c);
+        const float2 mm = igm[i];
+        const float4 cc = igc[i];
+        const float r = cc.w;
+        const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
         const Cut k = gauss_cut(G, m, c);
         const bool skip = greach[i] > 0;  // (k_fine_count's decision)
         uint64_t o = offs[i];
@@ -825,6 +828,156 @@ __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_
     g[3] = doff ? __float_as_int(doff[1]) : 0;
 }
 
+// D = 2: the bounding boxes of a cell's four sub-cells and of the cell (their union), one wave
+// per cell.  Empty sub-cells get an empty box (+inf lo, -inf hi).
+__global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, const int32_t *__restrict__ ssbeg,
+                                                    const int32_t *__restrict__ ssend,
+                                                    const float *__restrict__ rows, float4 *__restrict__ sbox,
+                                                    float4 *__restrict__ box) {
+    const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (c >= ncells) return;
+    float clo[2] = {INFINITY, INFINITY}, chi[2] = {-INFINITY, -INFINITY};
+    for (int k = 0; k < kSubPerCell; ++k) {
+        const int sc = c * kSubPerCell + k;
+        float lo[2] = {INFINITY, INFINITY}, hi[2] = {-INFINITY, -INFINITY};
+        const int e = ssend[sc];
+        for (int j = ssbeg[sc] + lane; j < e; j += kWave) {
+            const float *row = rows + (int64_t)(j >> 1) * 4 + (j & 1);
+            for (int d = 0; d < 2; ++d) {
+                const float v = row[2 * d];
+                lo[d] = fminf(lo[d], v);
+                hi[d] = fmaxf(hi[d], v);
+            }
+        }
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) {
+                lo[d] = fminf(lo[d], __shfl_xor(lo[d], off));
+                hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off));
+            }
+        if (lane == 0) sbox[sc] = make_float4(lo[0], lo[1], hi[0], hi[1]);
+        for (int d = 0; d < 2; ++d) { clo[d] = fminf(clo[d], lo[d]); chi[d] = fmaxf(chi[d], hi[d]); }
+    }
+    if (lane == 0) box[c] = make_float4(clo[0], clo[1], chi[0], chi[1]);
+}
+
+// Sub lists (D = 2).  For every entry of a cell list, the sub-cells whose sample box its cut
+// X^T A X <= kQCut meets (bit k = sub-cell k), tested with the displacement the forward uses:
+// X = m - s, minus the entry's constant wrap shift for kGeneral entries (wrap_shift_f of the mean
+// minus the cell-box centre, exactly as k_forward_t forms it).  kUnsafe entries get no bit (the
+// forward's tail pass adds them per cell).  Pass 1 (WRITE = false) stores the masks and counts
+// per sub-cell the flag-free and the flagged entries; pass 2 writes the lists in cell-list
+// order (flag-free first, ascending position), so each sub list is [lbeg, lmid) flag-free,
+// [lmid, lend) flagged.  One wave per cell.
+template <bool WRITE>
+__global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
+                                                      const int32_t *__restrict__ gmid,
+                                                      const int32_t *__restrict__ gend,
+                                                      const uint32_t *__restrict__ entries,
+                                                      const float2 *__restrict__ gmean,
+                                                      const float4 *__restrict__ gcon,
+                                                      const float4 *__restrict__ box,
+                                                      const float4 *__restrict__ sbox, int CT,
+                                                      uint8_t *__restrict__ masks,
+                                                      uint32_t *__restrict__ cnt_ff, uint32_t *__restrict__ cnt_fl,
+                                                      const int32_t *__restrict__ lbeg,
+                                                      const int32_t *__restrict__ lmid,
+                                                      uint32_t *__restrict__ sub_ent, uint16_t *__restrict__ sub_pos) {
+    const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & (kWave - 1);
+    if (c >= ncells) return;
+    const int b = gbeg[c], m_ = gmid[c], e = gend[c];
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
+    if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
+        const float4 bx = box[c];
+        const float ctr[2] = {0.5f * (bx.x + bx.z), 0.5f * (bx.y + bx.w)};  // = cell_center
+        float4 sb[kSubPerCell];
+        for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
+        for (int j0 = b; j0 < e; j0 += kWave) {
+            const int j = j0 + lane;
+            uint32_t mask = 0u;
+            if (!WRITE) {
+                if (j < e) {
+                    const uint32_t ent = entries[j];
+                    if (!(ent & kUnsafe)) {
+                        const uint32_t id = ent & kIdMask;
+                        const float2 mm = gmean[id];
+                        const float4 cc = gcon[id];
+                        float sh[2] = {0.0f, 0.0f};
+                        if (ent & kGeneral) {
+                            sh[0] = wrap_shift_f(mm.x - ctr[0]);
+                            sh[1] = wrap_shift_f(mm.y - ctr[1]);
+                        }
+                        const double m0 = (double)mm.x - (double)sh[0], m1 = (double)mm.y - (double)sh[1];
+                        for (int k = 0; k < kSubPerCell; ++k) {
+                            const float4 q = sb[k];
+                            if (!(q.x <= q.z)) continue;  // empty sub-cell
+                            const double e0 = 1e-6 * (1.0 + fabs((double)mm.x) + fmax(fabs((double)q.x), fabs((double)q.z)));
+                            const double e1 = 1e-6 * (1.0 + fabs((double)mm.y) + fmax(fabs((double)q.y), fabs((double)q.w)));
+                            if (box_hits_ellipse(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1,
+                                                 cc.x, cc.y, cc.z, kQCut))
+                                mask |= 1u << k;
+                        }
+                    }
+                    masks[j] = (uint8_t)mask;
+                }
+            } else {
+                mask = j < e ? (uint32_t)masks[j] : 0u;
+            }
+            const bool ff = j < m_;
+            for (int k = 0; k < kSubPerCell; ++k) {
+                const bool hit = (mask >> k) & 1u;
+                const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
+                if (WRITE && hit) {
+                    const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
+                    const int base = ff ? lbeg[c * kSubPerCell + k] + (int)nff[k] : lmid[c * kSubPerCell + k] + (int)nfl[k];
+                    sub_ent[base + below] = entries[j];
+                    if (ff) sub_pos[base + below] = (uint16_t)(j - b);  // (the backward's LDS slot; cells
+                                                                        //  over 65535 entries do not use it)
+                }
+                nff[k] += (uint32_t)__popcll(bf);
+                nfl[k] += (uint32_t)__popcll(bl);
+            }
+        }
+    }
+    if (!WRITE && lane == 0)
+        for (int k = 0; k < kSubPerCell; ++k) {
+            cnt_ff[c * kSubPerCell + k] = nff[k];
+            cnt_fl[c * kSubPerCell + k] = nfl[k];
+        }
+}
+
+// Sub-list layout from the exclusive scans of the sub-cells' counts: [lbeg, lmid) flag-free,
+// [lmid, lend) flagged; and the forward sub units per sub-cell (samples and entries both
+// present): ceil(pairs / kSubPairs), pair-aligned.
+__global__ void k_sub_layout(int nsub, const uint32_t *__restrict__ off_ff, const uint32_t *__restrict__ off_fl,
+                             const uint32_t *__restrict__ cnt_ff,
+                             const uint32_t *__restrict__ cnt_fl, const int32_t *__restrict__ ssbeg,
+                             const int32_t *__restrict__ ssend, int32_t *__restrict__ lbeg,
+                             int32_t *__restrict__ lmid, int32_t *__restrict__ lend, uint32_t *__restrict__ ucnt) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nsub) return;
+    const int a = (int)(off_ff[k] + off_fl[k]);  // exclusive scan of ff + fl
+    lbeg[k] = a;
+    lmid[k] = a + (int)cnt_ff[k];
+    lend[k] = a + (int)cnt_ff[k] + (int)cnt_fl[k];
+    const int ns = ssend[k] - ssbeg[k];
+    const int npairs = ((ssend[k] + 1) >> 1) - (ssbeg[k] >> 1);
+    ucnt[k] = ns > 0 && cnt_ff[k] + cnt_fl[k] > 0 ? (uint32_t)((npairs + kSubPairs - 1) / kSubPairs) : 0u;
+}
+
+__global__ void k_sub_units(int nsub, const int32_t *__restrict__ ssbeg, const uint32_t *__restrict__ ucnt,
+                            const uint32_t *__restrict__ uoff, uint2 *__restrict__ units,
+                            int32_t *__restrict__ counters) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nsub) return;
+    for (uint32_t b = 0; b < ucnt[k]; ++b)
+        units[uoff[k] + b] = make_uint2((uint32_t)k, (uint32_t)(ssbeg[k] & ~1) + b * 2u * kSubPairs);
+    if (k == nsub - 1) counters[kNumFwdSubUnits] = (int32_t)(uoff[k] + ucnt[k]);
+}
+
 // ----------------------------------------------------------------------- work units
 __global__ void k_unit_counts(int ncells, const int32_t *__restrict__ sbeg,
                               const int32_t *__restrict__ send, const int32_t *__restrict__ gbeg,
@@ -957,21 +1110,17 @@ __global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
 // Means and conics in internal order (the forward/backward read them coalesced from here).
 // Also stores perm (internal -> caller id) and its inverse back to back in gperm (one pass
 // over the permutation instead of two launches).
-__global__ void k_geo_pack(int P, int D, const uint32_t *__restrict__ perm, const float *__restrict__ means,
-                           const float *__restrict__ conics, float2 *__restrict__ gmean,
+__global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float2 *__restrict__ igm,
+                           const float4 *__restrict__ igc, float2 *__restrict__ gmean,
                            float4 *__restrict__ gcon, int32_t *__restrict__ gperm) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
     gperm[i] = (int32_t)g;
     gperm[P + g] = (int32_t)i;
-    if (D == 2) {
-        gmean[i] = make_float2(means[g * 2], means[g * 2 + 1]);
-        gcon[i] = make_float4(conics[g * 3], conics[g * 3 + 1], conics[g * 3 + 2], 0.0f);
-    } else {
-        gmean[i] = make_float2(means[g], 0.0f);
-        gcon[i] = make_float4(conics[g], 0.0f, 0.0f, 0.0f);
-    }
+    gmean[i] = igm[i];  // (k_fine_count's internal-order copies: coalesced, no second gather)
+    const float4 c = igc[i];
+    gcon[i] = make_float4(c.x, c.y, c.z, 0.0f);
 }
 
 // Forward sample pair rows in sorted order: pair p = samples 2p, 2p+1, field-interleaved
@@ -1252,6 +1401,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     int32_t *cell_sbeg = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_sbeg);
     int32_t *cell_send = reinterpret_cast<int32_t *>(sbuf + L0.o_cell_send);
     uint2 *fwd_units = reinterpret_cast<uint2 *>(sbuf + L0.o_fwd_units);
+    const int nsub = D == 2 ? kSubPerCell * ncells : 0;
+    int32_t *sub_sbeg = reinterpret_cast<int32_t *>(sbuf + L0.o_sub_sbeg);
+    int32_t *sub_send = reinterpret_cast<int32_t *>(sbuf + L0.o_sub_send);
+    float4 *sub_box = reinterpret_cast<float4 *>(sbuf + L0.o_sub_box);
+    uint2 *fsub_units = reinterpret_cast<uint2 *>(sbuf + L0.o_fsub_units);
 
     Scratch S{alloc, alloc_ctx};
     Carve ca;
@@ -1269,10 +1423,12 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
     unsigned long long *eg = ca.take<unsigned long long>(1);
     int32_t *rmax = ca.take<int32_t>(1);
+    float2 *igm = ca.take<float2>(P);
+    float4 *igc = ca.take<float4>(P);
 
     // sort / scan temp storage: one piece sized for the largest phase-A primitive
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
-    const int sbits = bit_length((uint64_t)ncells);
+    const int sbits = bit_length((uint64_t)ncells * kSubPerCell);  // (cell, sub-cell) keys
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_ssort, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0,
                                     sbits, s));
@@ -1295,6 +1451,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(gcnt, base);
         Carve::rebase(eg, base);
         Carve::rebase(rmax, base);
+        Carve::rebase(igm, base);
+        Carve::rebase(igc, base);
         char *t = static_cast<char *>(tmp_a);
         Carve::rebase(t, base);
         tmp_a = t;
@@ -1308,6 +1466,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(gtile, sizeof(uint32_t) * (G.T + 1));
         zl.add(cell_sbeg, sizeof(int32_t) * ncells);
         zl.add(cell_send, sizeof(int32_t) * ncells);
+        if (nsub) {
+            zl.add(sub_sbeg, sizeof(int32_t) * nsub);
+            zl.add(sub_send, sizeof(int32_t) * nsub);
+        }
         zl.add(reinterpret_cast<char *>(fsrows) + fs_written, fsrows_bytes(N, D) - fs_written);
         zl.add(rbuf, (size_t)G.T * 8 + 8);
         zl.add(srbuf, (size_t)G.T * 8 + 8);
@@ -1324,12 +1486,20 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     size_t tb = t_a;
     DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0, sbits, s));
     DGS_LAUNCH_CHECK(s, debug);
-    k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 0);
+    k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 2);
     DGS_LAUNCH_CHECK(s, debug);
+    if (nsub) {
+        k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)nsub, sub_sbeg, sub_send, 0);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
     DGS_LAUNCH_CHECK(s, debug);
-    k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
-        ncells, D, cell_sbeg, cell_send, fsrows, cell_box);
+    if (nsub)  // sub-cell boxes and the cell boxes (their union)
+        k_sub_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
+            ncells, sub_sbeg, sub_send, fsrows, sub_box, cell_box);
+    else
+        k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
+            ncells, D, cell_sbeg, cell_send, fsrows, cell_box);
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
@@ -1341,7 +1511,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
-                                                cell_send, cell_box, fcount, greach, lrows, rmax);
+                                                cell_send, cell_box, fcount, greach, lrows, rmax, igm, igc);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
                                                kWavesPerBlock - 1) / kWavesPerBlock);
@@ -1364,6 +1534,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Layout L;
         char *gbuf = nullptr;
         uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
+        uint32_t *sff, *sfl, *soff_ff, *soff_fl, *sucnt, *suoff;  // sub lists (D = 2)
+        uint8_t *smask;
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
@@ -1385,6 +1557,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.foff = cb.take<uint32_t>(ncells); B.boff = cb.take<uint32_t>(ncells);
         B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
         B.rvals = cb.take<uint32_t>(Rcap + 1);
+        B.sff = cb.take<uint32_t>(nsub + 1); B.sfl = cb.take<uint32_t>(nsub + 1);
+        B.soff_ff = cb.take<uint32_t>(nsub + 1); B.soff_fl = cb.take<uint32_t>(nsub + 1);
+        B.sucnt = cb.take<uint32_t>(nsub + 1); B.suoff = cb.take<uint32_t>(nsub + 1);
+        B.smask = cb.take<uint8_t>(nsub ? Ecap + 1 : 1);
         uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
         size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
         B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
@@ -1397,13 +1573,15 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                           : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s));
         t_cscan = scan_scratch_bytes<uint32_t>(ncells);
-        B.t_b = std::max(std::max(t_esort, t_cscan), t_rsort);
+        B.t_b = std::max(std::max(std::max(t_esort, t_cscan), t_rsort), scan_scratch_bytes<uint32_t>(std::max(nsub, 1)));
         B.tmp_b = cb.take<char>(B.t_b);
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
         for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.fcnt, &B.bcnt, &B.foff, &B.boff,
-                             &B.rkeys, &B.rkeys_sorted, &B.rvals})
+                             &B.rkeys, &B.rkeys_sorted, &B.rvals, &B.sff, &B.sfl, &B.soff_ff, &B.soff_fl, &B.sucnt,
+                             &B.suoff})
             Carve::rebase(*q, base);
+        Carve::rebase(B.smask, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
         char *t = static_cast<char *>(B.tmp_b);
@@ -1415,7 +1593,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.hend, sizeof(int32_t) * 2 * (size_t)ncells);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
-        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, D, perm, means, conics,
+        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc,
                                                   reinterpret_cast<float2 *>(B.gbuf + B.L.o_gmean),
                                                   reinterpret_cast<float4 *>(B.gbuf + B.L.o_gcon),
                                                   reinterpret_cast<int32_t *>(B.gbuf + B.L.o_perm));
@@ -1480,11 +1658,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     if (Es > 0) {
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
         if (k16)
-            k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
+            k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send,
                                                             cell_box, foffs, fcount, greach,
                                                             reinterpret_cast<uint16_t *>(ekeys), evals, counters);
         else
-            k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg, cell_send,
+            k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send,
                                                             cell_box, foffs, fcount, greach, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         tb = t_b;
@@ -1522,6 +1700,32 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
                                                     boff, fwd_units, bwd_units, counters);
     DGS_LAUNCH_CHECK(s, debug);
+    if (nsub) {  // the forward's sub lists and sub units (D = 2)
+        const unsigned wb = (unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave));
+        const float2 *gmean = reinterpret_cast<const float2 *>(gbuf + L.o_gmean);
+        const float4 *gcon = reinterpret_cast<const float4 *>(gbuf + L.o_gcon);
+        int32_t *sub_lbeg = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lbeg);
+        int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
+        int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
+        uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
+        k_sub_lists<false><<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
+                                                 cell_box, sub_box, G.CT, B.smask, B.sff, B.sfl, nullptr,
+                                                 nullptr, nullptr, nullptr);
+        DGS_LAUNCH_CHECK(s, debug);
+        scan_excl<uint32_t>(nsub, B.sff, B.soff_ff, B.sfl, B.soff_fl, static_cast<uint32_t *>(tmp_b), s);
+        DGS_LAUNCH_CHECK(s, debug);
+        k_sub_layout<<<grid_for(nsub), kBlock, 0, s>>>(nsub, B.soff_ff, B.soff_fl, B.sff, B.sfl, sub_sbeg, sub_send,
+                                                       sub_lbeg, sub_lmid, sub_lend, B.sucnt);
+        DGS_LAUNCH_CHECK(s, debug);
+        k_sub_lists<true><<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
+                                                cell_box, sub_box, G.CT, B.smask, nullptr, nullptr, sub_lbeg,
+                                                sub_lmid, sub_ent, reinterpret_cast<uint16_t *>(gbuf + L.o_sub_pos));
+        DGS_LAUNCH_CHECK(s, debug);
+        scan_excl<uint32_t>(nsub, B.sucnt, B.suoff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
+        DGS_LAUNCH_CHECK(s, debug);
+        k_sub_units<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, B.sucnt, B.suoff, fsub_units, counters);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
 
     // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled) and the
     // call-time path's tables: its tile lists (the reference's point_list) and unit counts
@@ -1571,6 +1775,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_gmean = L.o_gmean; h.o_gcon = L.o_gcon; h.o_fsrows = L0.o_fsrows;
     h.o_mcopy = L.o_mcopy; h.o_ccopy = L.o_ccopy; h.o_rlist = L.o_rlist; h.o_rtab = L.o_rtab;
     h.o_scopy = L0.o_scopy;
+    h.o_sub_sbeg = L0.o_sub_sbeg; h.o_sub_send = L0.o_sub_send; h.o_sub_box = L0.o_sub_box;
+    h.o_fsub_units = L0.o_fsub_units;
+    h.o_sub_lbeg = L.o_sub_lbeg; h.o_sub_lmid = L.o_sub_lmid; h.o_sub_lend = L.o_sub_lend; h.o_sub_ent = L.o_sub_ent;
+    h.fsub_cap = fsub_cap_of(D, N, ncells); h.esub_cap = esub_cap_of(D, E); h.o_sub_pos = L.o_sub_pos;
     h.stamp = ++stamp_counter;
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);
@@ -1581,6 +1789,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = -1;
+    uh.nfsub = fsub_cap_of(D, N, ncells);
+    uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R;
     hint_put(uh);
     return DGS_OK;

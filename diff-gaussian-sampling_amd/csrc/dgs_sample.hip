@@ -216,6 +216,15 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
+#ifndef DGS_BWD_SUB
+#define DGS_BWD_SUB 1  // D = 2, C = 1 backward over the sub-cell lists with a per-cell LDS flush
+#endif
+#ifndef DGS_FWD_SUB
+#define DGS_FWD_SUB 1  // D = 2 transposed forward over the sub-cell lists (k_forward_s)
+#endif
+#ifndef DGS_FWD_FULL
+#define DGS_FWD_FULL 1  // whole passes take the explicitly pipelined pair-row loads
+#endif
 #ifndef DGS_MULTI_T
 #define DGS_MULTI_T 1  // fused form: transposed forward (else lane-per-sample)
 #endif
@@ -228,28 +237,58 @@ __host__ __device__ constexpr bool fwd_transposed() {
 // WRAP: some lane's entry crosses the torus seam.  Its wrap (forward.cu:149-157) is a
 // constant even shift over the cell (preprocess sends the other seam entries to the general
 // path), subtracted exactly: sh = 0 for every other lane.
-template <int FN, int D, int CB, int NP, bool WRAP>
+template <int FN, int D, int CB, bool WRAP>
+__device__ __forceinline__ void fwd_t_pair(const float *pr, const float *m, const float *sh, const float *c,
+                                           const float *kk, const float *v, f2 (&acc)[Traits<FN, D>::U][CB]) {
+    f2 X[2] = {m[0] - f2{pr[0], pr[1]}, D == 2 ? m[1] - f2{pr[2], pr[3]} : bc<f2>(0.0f)};
+    if constexpr (WRAP) {
+        X[0] = X[0] - sh[0];
+        if constexpr (D == 2) X[1] = X[1] - sh[1];
+    }
+    const f2 G = fast_prob<D, f2>(X, kk);
+    fwd_terms<FN, D, CB, f2>(X, c, G, v, acc);
+}
+
+// s_waitcnt lgkmcnt(0) (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
+#define DGS_WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
+
+template <int FN, int D, int CB, int NP, bool WRAP, bool FULL>
 __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, int p0, int np,
                                             const float *m, const float *sh, const float *c,
                                             const float *kk, const float *v,
                                             f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
     constexpr int LW = 16;  // (x8 loads measured 6x slower: the unrolled pass stopped interleaving)
     constexpr int PRF = 2 * D, PPL = LW / PRF;  // floats per pair row, pairs per s_load_dwordx16
+    if constexpr (FULL) {
+        // A whole pass (np == NP): the next block of pair rows is in flight while this one is
+        // evaluated.  Scalar loads complete out of order, so a block can only be waited for
+        // with lgkmcnt(0); the wait is therefore placed explicitly BEFORE the next block's load
+        // is issued, and scheduling barriers keep the compiler from hoisting the loads (with a
+        // variable pass length it turned the exits into a cascade that issued them all first).
+        constexpr int NB = NP / PPL;
+        static_assert(NP % PPL == 0, "full passes are whole load blocks");
+        F32s<LW> cur = sload_f<LW>(fsrows + (int64_t)p0 * PRF);
 #pragma unroll
-    for (int q = 0; q < NP; q += PPL) {
-        if (q >= np) break;
-        const F32s<LW> sr = sload_f<LW>(fsrows + (int64_t)(p0 + q) * PRF);
+        for (int b = 0; b < NB; ++b) {
+            F32s<LW> nxt;
+            DGS_WAIT_LGKM0();
+            __builtin_amdgcn_sched_barrier(0);
+            if (b + 1 < NB) nxt = sload_f<LW>(fsrows + (int64_t)(p0 + (b + 1) * PPL) * PRF);
+            __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int j = 0; j < PPL; ++j) {
-            if (q + j < NP) {
-                const float *pr = &sr.v[j * PRF];
-                f2 X[2] = {m[0] - f2{pr[0], pr[1]}, D == 2 ? m[1] - f2{pr[2], pr[3]} : bc<f2>(0.0f)};
-                if constexpr (WRAP) {
-                    X[0] = X[0] - sh[0];
-                    if constexpr (D == 2) X[1] = X[1] - sh[1];
-                }
-                const f2 G = fast_prob<D, f2>(X, kk);
-                fwd_terms<FN, D, CB, f2>(X, c, G, v, acc[q + j]);
+            for (int j = 0; j < PPL; ++j)
+                fwd_t_pair<FN, D, CB, WRAP>(&cur.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
+            __builtin_amdgcn_sched_barrier(0);
+            if (b + 1 < NB) cur = nxt;
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < NP; q += PPL) {
+            if (q >= np) break;
+            const F32s<LW> sr = sload_f<LW>(fsrows + (int64_t)(p0 + q) * PRF);
+#pragma unroll
+            for (int j = 0; j < PPL; ++j) {
+                if (q + j < NP) fwd_t_pair<FN, D, CB, WRAP>(&sr.v[j * PRF], m, sh, c, kk, v, acc[q + j]);
             }
         }
     }
@@ -267,7 +306,7 @@ __device__ __forceinline__ void load_grow(const float *__restrict__ grows, uint3
 }
 
 // One group: the lane's row r (entry ent; `active` = a real entry) against the pass's pairs.
-template <int FN, int D, int CB, int NP, bool FLAGGED>
+template <int FN, int D, int CB, int NP, bool FLAGGED, bool FULL>
 __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, float (&r)[grow_stride<FN, D, CB>()],
                                             uint32_t ent, bool active, int p0, int np, const float *ctr,
                                             f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
@@ -296,13 +335,13 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
     }
-    fwd_t_pairs<FN, D, CB, NP, FLAGGED>(fsrows, p0, np, m, sh, c, &r[D], &r[B], acc);
+    fwd_t_pairs<FN, D, CB, NP, FLAGGED, FULL>(fsrows, p0, np, m, sh, c, &r[D], &r[B], acc);
 }
 
 // Software-pipelined over the groups: group g + 1's rows and group g + 2's entries are in
 // flight while group g is evaluated (each group otherwise starts with two dependent memory
 // round trips, entry then row).
-template <int FN, int D, int CB, int NP, bool FLAGGED>
+template <int FN, int D, int CB, int NP, bool FLAGGED, bool FULL>
 __device__ __forceinline__ void fwd_t_groups(const Bins &bins, const float *__restrict__ grows,
                                              const float *__restrict__ fsrows, int eb, int ee,
                                              int p0, int np, int lane, const float *ctr,
@@ -318,7 +357,7 @@ __device__ __forceinline__ void fwd_t_groups(const Bins &bins, const float *__re
         float r_nxt[RS];
         load_grow<RS>(grows, e_nxt, r_nxt);  // (a clamped, valid row past the list's end)
         const uint32_t e_nn = bins.entries[min(g0 + 2 * kWave + lane, last)];
-        fwd_t_group<FN, D, CB, NP, FLAGGED>(fsrows, r_cur, e_cur, g0 + lane < ee, p0, np, ctr, acc);
+        fwd_t_group<FN, D, CB, NP, FLAGGED, FULL>(fsrows, r_cur, e_cur, g0 + lane < ee, p0, np, ctr, acc);
 #pragma unroll
         for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
         e_cur = e_nxt;
@@ -361,9 +400,16 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
                     for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
             // flag-free prefix [gb, gm), then the flagged suffix [gm, ge) (seam wraps; the kUnsafe
             // entries there are left to the tail pass)
-            fwd_t_groups<FN, D, CB, NP, false>(bins, grows, fsrows, gb, gm, ps >> 1, np, lane, ctr, acc);
-            if (gm < ge)
-                fwd_t_groups<FN, D, CB, NP, true>(bins, grows, fsrows, gm, ge, ps >> 1, np, lane, ctr, acc);
+            constexpr bool kFullOk = DGS_FWD_FULL && NP % (8 / D) == 0;
+            if (kFullOk && np == NP) {  // whole pass: pipelined pair-row loads
+                fwd_t_groups<FN, D, CB, NP, false, kFullOk>(bins, grows, fsrows, gb, gm, ps >> 1, np, lane, ctr, acc);
+                if (gm < ge)
+                    fwd_t_groups<FN, D, CB, NP, true, kFullOk>(bins, grows, fsrows, gm, ge, ps >> 1, np, lane, ctr, acc);
+            } else {
+                fwd_t_groups<FN, D, CB, NP, false, false>(bins, grows, fsrows, gb, gm, ps >> 1, np, lane, ctr, acc);
+                if (gm < ge)
+                    fwd_t_groups<FN, D, CB, NP, true, false>(bins, grows, fsrows, gm, ge, ps >> 1, np, lane, ctr, acc);
+            }
             // value index = (2 * pair + half) * UC + (u * CB + ch)
             float x[64];
 #pragma unroll
@@ -381,6 +427,210 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
             const int slot = lane / UC, comp = lane - slot * UC;
             const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
             if (lane < NS * UC && j >= fu.lo && j < fu.hi && ch < nch) {
+                store_unique<FN, D, false>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
+            }
+        }
+    }
+}
+
+// (a') Sub-cell form (D = 2; SURVEY 8d: W_cand towards W_live).  The transposed kernel over the
+// sub units: a unit is (sub-cell, up to kSubPairs sample pairs) and walks the sub list -- the
+// entries of its cell whose cut meets the sub-cell's sample box -- instead of the whole cell
+// list.  The pass's first 16 pair rows are loaded once per pass, before the group loop, and stay
+// in SGPRs for every group (no scalar load, hence no out-of-order lgkmcnt(0) wait, for them
+// inside the loop).  Arithmetic, order per lane and the reduce-scatter are those of (a).
+// The first HB blocks of 4 pair rows are hoisted (64 SGPRs: more spill into VGPR lanes and cost a
+// v_readlane per dword inside the loop); the pass's later blocks, needed by the larger sub-cells
+// only, are loaded where they are used.
+template <int FN, int D, int CB, int NPH, int HB, bool WRAP>
+__device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const float *__restrict__ prow, int np,
+                                            const float *m, const float *sh, const float *c, const float *kk,
+                                            const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+    constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b * PPL >= np) break;  // wave-uniform: the rest of the pass is padding
+        F32s<16> t;
+        if (b < HB) t = hr[b < HB ? b : 0];
+        else t = sload_f<16>(prow + (int64_t)b * PPL * PRF);
+#pragma unroll
+        for (int j = 0; j < PPL; ++j)
+            if (b * PPL + j < NPH) fwd_t_pair<FN, D, CB, WRAP>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
+    }
+}
+
+#ifndef DGS_FWD_LDS
+#define DGS_FWD_LDS 1  // sub-cell forward: the pass's pair rows staged in LDS (else hoisted into SGPRs)
+#endif
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const v4f lds_cf4;
+
+// The LDS form: the pass's pair rows sit in the wave's LDS slot; each block of 4 pairs reads its
+// 4 rows (broadcast ds_read_b128, in order, so counted waits) right before its arithmetic.  The
+// slot address is re-laundered per group so the compiler cannot hoist the reads out of the list
+// walk (hoisted, they would need 4 VGPRs per pair for the whole walk).
+template <int FN, int D, int CB, int NPH, bool WRAP>
+__device__ __forceinline__ void fwd_l_pairs(uint32_t slot, int np, const float *m, const float *sh, const float *c,
+                                            const float *kk, const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+    constexpr int PPL = 4, NB = (NPH + PPL - 1) / PPL;
+    // One block of rows in flight: block b + 1 is read while block b is evaluated, into the other
+    // of two register buffers (compile-time parity: no copies).  Its address is laundered through
+    // the previous block's last sum, so the compiler can neither hoist the reads of the whole
+    // pass to the front (a cascade holding every row in VGPRs) nor out of the list walk.
+    float dep = 0.0f;
+    v4f buf[2][PPL];
+    {
+        uint32_t sl = slot;
+        asm volatile("" : "+v"(sl));
+        lds_cf4 *rows = (lds_cf4 *)(size_t)sl;
+#pragma unroll
+        for (int j = 0; j < PPL; ++j) buf[0][j] = rows[j];
+    }
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b * PPL < np) {  // wave-uniform
+            if (b + 1 < NB && (b + 1) * PPL < np) {
+                uint32_t sl = slot;
+                asm volatile("" : "+v"(sl) : "v"(dep));
+                lds_cf4 *rows = (lds_cf4 *)(size_t)sl;
+#pragma unroll
+                for (int j = 0; j < PPL; ++j) buf[(b + 1) & 1][j] = rows[(b + 1) * PPL + j];
+            }
+#pragma unroll
+            for (int j = 0; j < PPL; ++j) {
+                const v4f q = buf[b & 1][j];
+                const float pr[4] = {q[0], q[1], q[2], q[3]};
+                if (b * PPL + j < NPH) fwd_t_pair<FN, D, CB, WRAP>(pr, m, sh, c, kk, v, acc[b * PPL + j]);
+            }
+            dep = acc[min(b * PPL + PPL - 1, NPH - 1)][0][0].x;
+        }
+    }
+}
+
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
+__device__ __forceinline__ void fwd_s_group(const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
+                                            float (&r)[grow_stride<FN, D, CB>()],
+                                            uint32_t ent, bool active, int np, const float *ctr,
+                                            f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+    constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    if constexpr (FLAGGED) {
+        if (!active || (ent & kUnsafe)) {
+#pragma unroll
+            for (int k = 0; k < RS; ++k) r[k] = 0.0f;
+        }
+    } else {
+        if (!active) {
+#pragma unroll
+            for (int k = B; k < RS; ++k) r[k] = 0.0f;
+        }
+    }
+    float c[3];
+    row_conic<FN, D, RS>(r, c);
+    const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
+    float sh[2] = {0.0f, 0.0f};
+    if constexpr (FLAGGED) {
+        if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
+#pragma unroll
+            for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+        }
+    }
+    if constexpr (DGS_FWD_LDS)
+        fwd_l_pairs<FN, D, CB, NPH, FLAGGED>(slot, np, m, sh, c, &r[D], &r[B], acc);
+    else
+        fwd_s_pairs<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, np, m, sh, c, &r[D], &r[B], acc);
+}
+
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
+__device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, const float *__restrict__ grows,
+                                             const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
+                                             int eb, int ee, int np, int lane,
+                                             const float *ctr, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+    constexpr int RS = grow_stride<FN, D, CB>();
+    if (eb >= ee) return;
+    const int last = ee - 1;
+    uint32_t e_cur = ents[min(eb + lane, last)];
+    uint32_t e_nxt = ents[min(eb + kWave + lane, last)];
+    float r_cur[RS];
+    load_grow<RS>(grows, e_cur, r_cur);
+    for (int g0 = eb; g0 < ee; g0 += kWave) {
+        float r_nxt[RS];
+        load_grow<RS>(grows, e_nxt, r_nxt);
+        const uint32_t e_nn = ents[min(g0 + 2 * kWave + lane, last)];
+        fwd_s_group<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr, acc);
+#pragma unroll
+        for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
+        e_cur = e_nxt;
+        e_nxt = e_nn;
+    }
+}
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ gbuf,
+                                                      const char *__restrict__ sbuf,
+                                                      const float *__restrict__ grows,
+                                                      const Outs outs, int C, int cbase,
+                                                      const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
+    using Tr = Traits<FN, D>;
+    constexpr int U = Tr::U, UC = U * CB;
+    constexpr int NP0 = 32 / UC, NPH = NP0 < kSubPairs ? NP0 : kSubPairs, NS = 2 * NPH;
+    constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL, HB = NB < 4 ? NB : 4;
+    static_assert(D == 2 && NPH >= 1 && NS * UC <= 64, "sub-cell form: D = 2, reduce-scatter width");
+    const Bins bins = resolve(gbuf, sbuf);
+    const float *__restrict__ fsrows = bins.fsrows;
+    const int nunits = sload(&bins.counts[kNumFwdSubUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int nch = min(CB, C - cbase);
+    __shared__ v4f srows[kWavesPerBlock][kSubPairs];  // DGS_FWD_LDS: each wave's pass rows
+    const int wv = threadIdx.x >> 6;
+    const uint32_t slot = (uint32_t)(size_t)(lds_cf4 *)(&srows[wv][0]);  // (addrspacecast: the LDS offset)
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.fsub_units[unit]);
+        const int sc = (int)u.x, cell = sc / kSubPerCell, sb = (int)u.y;
+        const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
+        const int hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
+        const int gb = sload(&bins.sub_lbeg[sc]), gm = sload(&bins.sub_lmid[sc]), ge = sload(&bins.sub_lend[sc]);
+        float ctr[2];
+        cell_center<D>(bins, cell, ctr);
+        for (int ps = sb; ps < hi; ps += NS) {
+            // (provably wave-uniform: the block exits become scalar compares, not lane masks held in SGPRs)
+            const int np = __builtin_amdgcn_readfirstlane(min(NPH, (hi - ps + 1) >> 1));
+            const float *prow = fsrows + (int64_t)(ps >> 1) * PRF;
+            F32s<16> hr[DGS_FWD_LDS ? 1 : HB];  // the pass's first pair rows, in SGPRs for the whole list walk
+            if constexpr (DGS_FWD_LDS) {
+                if (lane < NPH) srows[wv][lane] = reinterpret_cast<const v4f *>(prow)[lane];
+            } else {
+#pragma unroll
+                for (int b = 0; b < HB; ++b) hr[b] = sload_f<16>(prow + (int64_t)b * PPL * PRF);
+            }
+            f2 acc[NPH][U][CB];
+#pragma unroll
+            for (int q = 0; q < NPH; ++q)
+#pragma unroll
+                for (int a = 0; a < U; ++a)
+#pragma unroll
+                    for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
+            constexpr int HBX = DGS_FWD_LDS ? 1 : HB;
+            fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
+            if (gm < ge)
+                fwd_s_groups<FN, D, CB, NPH, HBX, true>(bins.sub_ent, grows, hr, prow, slot, gm, ge, np, lane, ctr, acc);
+            float x[64];
+#pragma unroll
+            for (int i = 0; i < 64; ++i) x[i] = 0.0f;
+#pragma unroll
+            for (int q = 0; q < NPH; ++q)
+#pragma unroll
+                for (int a = 0; a < U; ++a)
+#pragma unroll
+                    for (int ch = 0; ch < CB; ++ch) {
+                        x[(2 * q) * UC + a * CB + ch] = acc[q][a][ch].x;
+                        x[(2 * q + 1) * UC + a * CB + ch] = acc[q][a][ch].y;
+                    }
+            const float sum = reduce_scatter64(x, lane);
+            const int slot = lane / UC, comp = lane - slot * UC;
+            const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
+            if (lane < NS * UC && j >= lo && j < hi && ch < nch) {
                 store_unique<FN, D, false>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
             }
         }
@@ -743,25 +993,20 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
     }
 }
 
-// One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
-// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane.
+// The gradient sums of one lane's Gaussian (entry ent, row r, conic cr) over the samples
+// [sb, se) of `cell` (sorted order), finished into sm[D], sc[S], sv[CB].  The mode (fast /
+// constant wrap shift / general) is chosen for the whole wave from its active lanes' flags.
 template <int FN, int D, int CB>
-__device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows,
-                                         float *__restrict__ acc, int P, int vrow0, uint2 u,
-                                         uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
-                                         float4 cr, int lane) {
+__device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restrict__ srows, int cell, int sb, int se,
+                                         uint32_t ent, bool active, const float (&r)[grow_stride<FN, D, CB>()],
+                                         float4 cr, float (&sm)[2], float (&sc)[3], float (&sv)[CB]) {
     using Tr = Traits<FN, D>;
     using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
-    constexpr int B = Tr::GBASE, S = Tr::S;
-    const int cell = (int)u.x, eb = (int)u.y;
-    const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
-    const bool active = eb + lane < ee;
-    const int64_t id = ent & kIdMask;
+    constexpr int B = Tr::GBASE;
     const bool wrap = (ent & kGeneral) != 0;
     const bool unsafe = (ent & kUnsafe) != 0;
     const float c[3] = {cr.x, cr.y, cr.z};
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
-    const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
     // register accumulators: [gm(2) gv(CB) gc(3)], or the kMomAcc sums of the moment form
     constexpr int NA = bwd_mom<FN, D, CB>() ? kMomAcc : 2 + CB + 3;
     V ra[NA];
@@ -781,28 +1026,44 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
     } else {
         bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     }
-    if (active) {
-        float sm[2], sc[3], sv[CB];
-        if constexpr (bwd_mom<FN, D, CB>()) {
-            float s[kMomAcc];
+    if constexpr (bwd_mom<FN, D, CB>()) {
+        float sum[kMomAcc];
 #pragma unroll
-            for (int k = 0; k < kMomAcc; ++k) s[k] = hsum(ra[k]);
-            bwd_mom_finish(c, r[B], s, sm, sc, sv[0]);
-        } else {
-            const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
-            sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
+        for (int k = 0; k < kMomAcc; ++k) sum[k] = hsum(ra[k]);
+        bwd_mom_finish(c, r[B], sum, sm, sc, sv[0]);
+    } else {
+        const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
+        sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
 #pragma unroll
-            for (int k = 0; k < 3; ++k) sc[k] = hsum(gc[k]);
+        for (int k = 0; k < 3; ++k) sc[k] = hsum(gc[k]);
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) sv[ch] = hsum(gv[ch]);
-            if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
+        for (int ch = 0; ch < CB; ++ch) sv[ch] = hsum(gv[ch]);
+        if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
 #pragma unroll
-                for (int d = 0; d < 2; ++d) sm[d] *= r[B];
+            for (int d = 0; d < 2; ++d) sm[d] *= r[B];
 #pragma unroll
-                for (int k = 0; k < 3; ++k) sc[k] *= r[B];
-            }
-            bwd_finish<FN, D>(c, sm, sc);
+            for (int k = 0; k < 3; ++k) sc[k] *= r[B];
         }
+        bwd_finish<FN, D>(c, sm, sc);
+    }
+}
+
+// One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
+// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane.
+template <int FN, int D, int CB>
+__device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows,
+                                         float *__restrict__ acc, int P, int vrow0, uint2 u,
+                                         uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
+                                         float4 cr, int lane) {
+    constexpr int S = Traits<FN, D>::S;
+    const int cell = (int)u.x, eb = (int)u.y;
+    const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
+    const bool active = eb + lane < ee;
+    const int64_t id = ent & kIdMask;
+    const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+    float sm[2], sc[3], sv[CB];
+    bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, cr, sm, sc, sv);
+    if (active) {
 #pragma unroll
         for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
 #pragma unroll
@@ -840,6 +1101,133 @@ __global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gb
         float r[RS];
         load_grow<RS>(grows, ent, r);
         bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane);
+    }
+}
+
+// (b') Sub-cell backward (D = 2, C = 1): one workgroup per cell.  The cell list's flag-free
+// entries are walked per sub-cell (the sub lists' positions: only the entries whose cut meets
+// the sub-cell's sample box, against only that sub-cell's samples), the flagged ones at cell
+// level as in k_backward; every lane adds its finished gradient to an LDS slot per list position
+// (ds_add), and the workgroup then flushes each position once to the global sums -- the same
+// number of global float atomics per (cell, Gaussian) as k_backward, which is what the
+// atomic rate allows, with the pairs of the finer sub-cells.  Positions exactly 0 (no live
+// pair, e.g. a cut that only grazes the cell's box) are not flushed at all.  Cells whose list
+// exceeds the 16-bit positions run every entry at cell level; long lists go in windows of
+// kBwdWin positions.
+constexpr int kBwdWin = 1024;
+
+__device__ __forceinline__ int lower_bound_u16(const uint16_t *__restrict__ a, int lo, int hi, int x) {
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int)a[mid] < x) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The block's cell, with the bijective XCD-aware remap of wave_unit_index (neighbouring cells,
+// which share Gaussians, on one XCD's L2).
+__device__ __forceinline__ int block_cell(int b, int nb) {
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock) void k_backward_s(const char *__restrict__ gbuf,
+                                                       const char *__restrict__ sbuf,
+                                                       const float *__restrict__ grows,
+                                                       const float *__restrict__ srows,
+                                                       float *__restrict__ acc, int P, int vrow0,
+                                                       const uint32_t *__restrict__ dirty) {
+    static_assert(D == 2 && CB == 1, "sub-cell backward: D = 2, one channel");
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
+    constexpr int RS = grow_stride<FN, D, CB>(), S = 3, NV = 6;
+    __shared__ float slots[NV][kBwdWin];
+    const Bins bins = resolve(gbuf, sbuf);
+    const uint16_t *__restrict__ sub_pos = bins.sub_pos;
+    const int ncells = sload(&bins.h->ncells);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int nb = min((int)gridDim.x, ncells);
+    if ((int)blockIdx.x >= nb) return;
+    for (int cb = block_cell(blockIdx.x, nb); cb < ncells; cb += nb) {
+        const int cell = cb;
+        const int gb = sload(&bins.cell_gbeg[cell]), gm = sload(&bins.cell_gmid[cell]), ge = sload(&bins.cell_gend[cell]);
+        const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+        if (gb >= ge || sb >= se) continue;
+        const int n = ge - gb, nff = gm - gb;
+        const bool big = n > 65535;
+        for (int p0 = 0; p0 < n; p0 += kBwdWin) {
+            const int wn = min(kBwdWin, n - p0);
+            for (int q = threadIdx.x; q < wn; q += kBlock)
+#pragma unroll
+                for (int k = 0; k < NV; ++k) slots[k][q] = 0.0f;
+            __syncthreads();
+            auto sink = [&](bool active, int pos, const float (&sm)[2], const float (&sc)[3], const float (&sv)[CB]) {
+                if (!active) return;
+                const int q = pos - p0;
+                atomicAdd(&slots[0][q], sm[0]);
+                atomicAdd(&slots[1][q], sm[1]);
+#pragma unroll
+                for (int k = 0; k < S; ++k) atomicAdd(&slots[2 + k][q], sc[k]);
+                atomicAdd(&slots[5][q], sv[0]);
+            };
+            if (!big) {  // flag-free entries of the window, per sub-cell
+#pragma unroll 1
+                for (int k = 0; k < kSubPerCell; ++k) {
+                    const int sc4 = cell * kSubPerCell + k;
+                    const int ss = sload(&bins.sub_sbeg[sc4]), sse = sload(&bins.sub_send[sc4]);
+                    if (ss >= sse) continue;
+                    const int la = sload(&bins.sub_lbeg[sc4]), lm = sload(&bins.sub_lmid[sc4]);
+                    const int ka = p0 == 0 ? la : lower_bound_u16(sub_pos, la, lm, p0);
+                    const int kb = p0 + wn >= nff ? lm : lower_bound_u16(sub_pos, ka, lm, p0 + wn);
+                    for (int e0 = ka + w * kWave; e0 < kb; e0 += kBlock) {
+                        const int e = e0 + lane;
+                        const bool active = e < kb;
+                        const int pos = (int)sub_pos[min(e, kb - 1)];
+                        const uint32_t ent = bins.entries[gb + pos];
+                        float r[RS];
+                        load_grow<RS>(grows, ent, r);
+                        float sm[2], scn[3], sv[CB];
+                        bwd_sums<FN, D, CB>(bins, srows, cell, ss, sse, ent, active, r, bins.gcon[ent & kIdMask],
+                                            sm, scn, sv);
+                        sink(active, pos, sm, scn, sv);
+                    }
+                }
+            }
+            {  // the flagged entries of the window (every entry of a big cell), at cell level
+                const int fa = big ? p0 : max(p0, nff), fb = p0 + wn;
+                for (int e0 = fa + w * kWave; e0 < fb; e0 += kBlock) {
+                    const int e = e0 + lane;
+                    const bool active = e < fb;
+                    const uint32_t ent = bins.entries[gb + min(e, fb - 1)];
+                    float r[RS];
+                    load_grow<RS>(grows, ent, r);
+                    float sm[2], scn[3], sv[CB];
+                    bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, bins.gcon[ent & kIdMask], sm, scn,
+                                        sv);
+                    sink(active, e, sm, scn, sv);
+                }
+            }
+            __syncthreads();
+            for (int q = threadIdx.x; q < wn; q += kBlock) {  // one flush per (cell, Gaussian)
+                float x[NV];
+                bool any = false;
+#pragma unroll
+                for (int k = 0; k < NV; ++k) {
+                    x[k] = slots[k][q];
+                    any = any || x[k] != 0.0f;
+                }
+                if (!any) continue;
+                const int64_t id = bins.entries[gb + p0 + q] & kIdMask;
+                atomicAdd(acc + id, x[0]);
+                atomicAdd(acc + (int64_t)P + id, x[1]);
+#pragma unroll
+                for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, x[2 + k]);
+                atomicAdd(acc + (int64_t)vrow0 * P + id, x[5]);
+            }
+            __syncthreads();
+        }
     }
 }
 
@@ -920,6 +1308,46 @@ __global__ __launch_bounds__(kBlock) void k_count(const char *__restrict__ gbuf,
     }
 }
 
+// W_cand / W_live over the sub lists (D = 2, k_forward_s): per sub unit, every sample of the unit
+// against every entry of its sub list (the kUnsafe entries of the cell are the tail pass's, a
+// handful, not counted).
+__global__ __launch_bounds__(kBlock) void k_count_s(const char *__restrict__ gbuf, const char *__restrict__ sbuf,
+                                                    const float *__restrict__ grows,
+                                                    const float *__restrict__ samples, float thr,
+                                                    unsigned long long *__restrict__ counts) {
+    constexpr int RS = grow_stride<0, 2, 1>();
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumFwdSubUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.fsub_units[unit]);
+        const int sc = (int)u.x, sb = (int)u.y;
+        const int lo = max(sb, sload(&bins.sub_sbeg[sc])), hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
+        const int gb = sload(&bins.sub_lbeg[sc]), ge = sload(&bins.sub_lend[sc]);
+        const int j = sb + (threadIdx.x & (kWave - 1));
+        const bool active = j >= lo && j < hi;
+        const int64_t sid = bins.sorted_sid[active ? j : lo];
+        const float s0 = samples[sid * 2], s1 = samples[sid * 2 + 1];
+        unsigned long long live = 0, cand = 0;
+        for (int e = gb; e < ge; ++e) {
+            const uint32_t ent = sload(&bins.sub_ent[e]);
+            if (ent & kUnsafe) continue;
+            const int64_t id = ent & kIdMask;
+            const float *row = grows + id * RS;
+            const float4 cr = sload(&bins.gcon[id]);
+            const float c[3] = {cr.x, cr.y, cr.z};
+            float X[2] = {ref_wrap(sload(row) - s0), ref_wrap(sload(row + 1) - s1)};
+            const float p = ref_power<0, 2>(X, c);
+            live += (p >= thr && p <= 0.0f) ? 1ull : 0ull;
+            ++cand;
+        }
+        if (active) {
+            atomicAdd(&counts[0], cand);
+            atomicAdd(&counts[1], live);
+        }
+    }
+}
+
 // ------------------------------------------------------------------ kernel timing
 // Optional HIP-event brackets around the render kernels (bench.py: the dominant kernel's
 // average duration on the stream it runs on).  Off by default.
@@ -975,11 +1403,11 @@ static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
 // Grid size in blocks: exact (from the preprocess hint) or a persistent-size fallback; the
 // kernels grid-stride over the device-side unit count either way.
 static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_t sbytes, bool bwd,
-                            int units_per_block = kWavesPerBlock) {
+                            int units_per_block = kWavesPerBlock, bool sub = false) {
     UnitHint h;
     int64_t units;
     if (hint_get(gb, gbytes, sb, sbytes, &h)) {
-        units = bwd ? h.nbwd : h.nfwd;
+        units = sub ? h.nfsub : bwd ? h.nbwd : h.nfwd;
     } else {
         units = 256 * 8 * kWavesPerBlock;  // 8 blocks per CU, striding
     }
@@ -1021,6 +1449,7 @@ static int run_forward(const Call &a) {
     float *grows = reinterpret_cast<float *>(a.ws);
     uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
+    const unsigned sub_blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false, kWavesPerBlock, true);
     constexpr bool T = fwd_transposed<FN, D, CB>(), MX = !T && fwd_mfma<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
     hint.nunsafe = -1;
@@ -1035,7 +1464,9 @@ static int run_forward(const Call &a) {
         }
         {
             KernelTimer t(0, a.s);
-            if constexpr (T)
+            if constexpr (T && D == 2 && DGS_FWD_SUB)  // sub-cell lists (units from the sub-unit hint)
+                k_forward_s<FN, D, CB><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
+            else if constexpr (T)
                 k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else if constexpr (MX)
                 k_forward_mx<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
@@ -1085,8 +1516,15 @@ static int run_backward(const Call &a) {
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s);
-            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc,
-                                                                a.P, D + S + cbase, flag);
+            if constexpr (D == 2 && CB == 1 && DGS_BWD_SUB) {  // sub-cell pairs, per-cell LDS flush
+                UnitHint h;
+                const int64_t ncells = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &h) ? h.ncells : 65536;
+                k_backward_s<FN, D, CB><<<(unsigned)std::max<int64_t>(1, std::min<int64_t>(ncells, 1 << 20)), kBlock, 0,
+                                          a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
+            } else {
+                k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc,
+                                                                    a.P, D + S + cbase, flag);
+            }
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
@@ -1345,7 +1783,11 @@ extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const fl
     const unsigned blocks = unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false);
     if (D == 2) {
         k_pack_gauss<0, 2, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows, nullptr);
-        k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
+        if (DGS_FWD_SUB)
+            k_count_s<<<unit_blocks(gb, binning_bytes, sb, sample_binning_bytes, false, kWavesPerBlock, true), kBlock, 0,
+                        s>>>(gb, sb, grows, samples, thr, dcnt);
+        else
+            k_count<2><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);
     } else {
         k_pack_gauss<0, 1, 1><<<grid_for(P), kBlock, 0, s>>>(P, gb, conics, 0, 0, grows, nullptr);
         k_count<1><<<blocks, kBlock, 0, s>>>(gb, sb, grows, samples, thr, dcnt);

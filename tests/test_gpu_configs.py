@@ -117,7 +117,7 @@ def test_aggregate_config5_subset(dgs, oracle):
     fd = [t.to(dev) for t in fe]
     w, e, f, out = dgs._C.aggregate_neighbors(*fd, idx, rg, X, dn, inv, False)
     args = [t.numpy() for t in fe]
-    w_r, e_r, f_r, _ = oracle.agg_forward_rows(*args, rows, r_idx, r_rg, r_X, r_dn, r_inv)
+    w_r, e_r, f_r, out_lit = oracle.agg_forward_rows(*args, rows, r_idx, r_rg, r_X, r_dn, r_inv)
     # neighbor_features / gradients: exact accumulation of the reference's per-slot float terms
     # (its own float order is ~1e-5 away from it at ~1100 slots per row; tests/test_gpu_aggregate.py)
     out_r = oracle.agg_forward_rows(*args, rows, r_idx, r_rg, r_X, r_dn, r_inv, exact=True)[3]
@@ -126,6 +126,9 @@ def test_aggregate_config5_subset(dgs, oracle):
     close(f[sel].cpu().numpy(), f_r, 1e-5, 1e-6, "factors")
     rws = torch.from_numpy(rows).long().to(dev)
     close(out[rws].cpu().numpy(), out_r, 1e-5, 1e-6, "neighbor_features")
+    # and against the reference's own (literal) float order at the stated looser bound
+    # (test_gpu_aggregate.py LIT_RTOL / LIT_ATOL)
+    close(out[rws].cpu().numpy(), out_lit, 3e-5, 3e-6, "neighbor_features vs the literal order")
     dL_rows = np.random.default_rng(223).normal(size=(len(rows), L)).astype(np.float32)
     dL = torch.zeros(P, L, device=dev)
     dL[rws] = torch.from_numpy(dL_rows).to(dev)
@@ -134,6 +137,9 @@ def test_aggregate_config5_subset(dgs, oracle):
                                    exact=True)
     for name, a, b in zip(AGG_FEATURES, got, ref):
         close(a.cpu().numpy().reshape(b.shape), b, 1e-5, 1e-5, f"d/d{name}")
+    lit = oracle.agg_backward_rows(*args, rows, r_idx, r_rg, r_X, r_dn, w_r, e_r, f_r, r_inv, dL_rows)
+    for name, a, b in zip(AGG_FEATURES, got, lit):
+        close(a.cpu().numpy().reshape(b.shape), b, 3e-5, 3e-5, f"d/d{name} vs the literal order")
 
 
 @pytest.mark.parametrize("function,C", [("gaussian", 1), ("derivative", 1), ("laplacian", 3)])

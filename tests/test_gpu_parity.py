@@ -234,6 +234,35 @@ def test_parity_wide_domain_32bit_entry_keys(dgs, oracle, function):
     _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
 
 
+def test_preprocess_speculation_per_sample_set(dgs, oracle):
+    """dgs_preprocess_auto keeps its grid guess per sample set (pointer, N, D): two samplers
+    whose domains alternate, and points resampled in place every call (the grid offset moves
+    each time), bin exactly as with the grid given explicitly (preprocess_gaussians_bounded with
+    the reference grid of sample_points.cu:70-74), call after call."""
+    dev = torch.device("cuda:0")
+    means, values, covs, conics = syn.gaussians(800, 2, 1, seed=71)
+    m, v, cv, c = (t.to(dev) for t in (means, values, covs, conics))
+    a = syn.samples(4000, 2, seed=72).to(dev)
+    b = (syn.samples(4000, 2, seed=73) * 0.6 + 0.3).to(dev)
+    inplace = syn.samples(4000, 2, seed=74).to(dev)
+
+    def both(s):
+        R, gb, sb, rg, srg, _ = dgs._C.preprocess_gaussians(m, v, cv, c, s, False)
+        out = dgs._C.sample_gaussians(m, v, c, s, R, gb, sb, rg, srg, False)
+        grid, off = oracle.tile_grid(s.cpu().numpy())
+        R2, gb2, sb2, rg2, srg2, _ = dgs._C.preprocess_gaussians_bounded(
+            m, v, cv, c, s, [int(x) for x in grid], [float(x) for x in off], False)
+        ref = dgs._C.sample_gaussians(m, v, c, s, R2, gb2, sb2, rg2, srg2, False)
+        assert R == R2 and torch.equal(rg, rg2) and torch.equal(srg, srg2)
+        assert torch.equal(out, ref)
+
+    for i in range(6):  # alternating domains, each pointer its own guess
+        both(a if i % 2 == 0 else b)
+    for i in range(5):  # resampled in place: same pointer, a new offset every call
+        inplace.copy_(syn.samples(4000, 2, seed=80 + i).to(dev) * (1.0 + 0.01 * i))
+        both(inplace)
+
+
 def test_preprocess_grid_changes_between_calls(dgs, oracle):
     """preprocess_gaussians computes the tile grid on the device and bins with the previous
     call's grid until the one host sync confirms it (dgs_preprocess_auto): a call whose domain
