@@ -645,6 +645,14 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
                      "achieved": atomic_b / (b_ms * 1e-3) / 1e9, "peak": PEAK_ATOMIC_GBS,
                      "unit": "GB/s (float-atomic added bytes)",
                      "frac": atomic_b / (b_ms * 1e-3) / 1e9 / PEAK_ATOMIC_GBS, "traffic": None},
+        # the forward: per slot it streams indices / dists / densities (20 B) and writes weights /
+        # embeddings / factors (12 B), reads the neighbour's feature and key rows (4 (L + K) B,
+        # mostly from cache: neighbours of adjacent rows coincide) and writes out once per row
+        "roofline_forward": {"bound": "hbm", "kernel": "k_agg_forward_s",
+                             "achieved": (32.0 * Lnb + 4.0 * P * (L + 2 * K + 2 * L)) / (f_ms * 1e-3) / 1e9,
+                             "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                             "frac": (32.0 * Lnb + 4.0 * P * (L + 2 * K + 2 * L)) / (f_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                             "gathered_row_bytes": 4.0 * (L + K) * Lnb, "traffic": None},
         "hbm": {"kernel": "k_agg_backward_s", "algorithmic_bytes": stream_b + atomic_b,
                 "achieved_GBs": (stream_b + atomic_b) / (b_ms * 1e-3) / 1e9, "peak_GBs": PEAK_HBM_GBS,
                 "frac": (stream_b + atomic_b) / (b_ms * 1e-3) / 1e9 / PEAK_HBM_GBS},
@@ -652,20 +660,30 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
     }
     if rank == 0 and world == 1 and not args.no_cpu:
         from oracle import oracle as orc
+        from oracle import torch_eager as te
         orc.build()
         host = lambda t: t.detach().cpu().numpy()  # noqa: E731
         args_np = [host(t) for t in feats_d]
         idx, rg, X, dn, inv = (host(t) for t in (sampler.indices, sampler.ranges, sampler.dists,
                                                 sampler.densities, sampler.inv_total_densities))
         rows = min(args.cpu_rows, P)
+        nslots = int(rg[rows - 1])
+        # PyTorch eager on the host cores (BASELINE.json north_star): the same math vectorised
+        # over the rows' slots, autograd backward (oracle/torch_eager.py aggregate_fwd_bwd)
+        t0 = time.perf_counter()
+        te.aggregate_fwd_bwd(*args_np, idx, rg, X, dn, inv, host(dL), rows=rows)
+        dt = time.perf_counter() - t0
+        result["cpu_baseline"] = {"value": nslots / dt, "unit": "slots/s", "cores": torch.get_num_threads(),
+                                  "kind": "port",
+                                  "sample": f"first {rows} rows ({nslots} slots) of the same lists, torch eager "
+                                            f"fwd + autograd bwd, neighbour search excluded ({dt:.1f} s)"}
         t0 = time.perf_counter()
         w, e_, f_, _ = orc.agg_forward(*args_np, idx, rg, X, dn, inv, rows=rows)
         orc.agg_backward(*args_np, idx, rg, X, dn, w, e_, f_, inv, host(dL), rows=rows)
         dt = time.perf_counter() - t0
-        nslots = int(rg[rows - 1])
-        result["cpu_baseline"] = {"value": nslots / dt, "unit": "slots/s", "cores": 1, "kind": "port",
-                                  "sample": f"first {rows} rows ({nslots} slots) of the same lists, "
-                                            f"fwd+bwd, neighbour search excluded ({dt:.1f} s)"}
+        result["cpu_baseline_oracle"] = {"value": nslots / dt, "unit": "slots/s", "cores": 1, "kind": "port",
+                                         "sample": f"first {rows} rows ({nslots} slots) of the same lists, "
+                                                   f"1-thread C oracle fwd+bwd, neighbour search excluded ({dt:.1f} s)"}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -44,6 +44,11 @@ constexpr int kFwdUnit = kWave;
 // meets the sub-cell's sample box (sub lists), in units of up to kSubPairs sample pairs.  The
 // backward keeps the cell lists (their per-cell flush is what the float atomics allow).
 constexpr int kSubPerCell = 4;
+// The backward over the sub lists (k_backward_s: per-cell workgroups, LDS flush) is correct but
+// measured 2x slower than k_backward at the headline (1.59 against 0.80 ms, tools/ab.py): off.
+#ifndef DGS_BWD_SUB
+#define DGS_BWD_SUB 0
+#endif
 constexpr int kSubPairs = 24;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
@@ -148,7 +153,7 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_ent = o;   o = align_up(o + 4 * (size_t)esub_cap_of(D, E) + 64, 256);
-    L.o_sub_pos = o;   o = align_up(o + 2 * (size_t)esub_cap_of(D, E) + 64, 256);
+    L.o_sub_pos = o;   o = align_up(o + (DGS_BWD_SUB ? 2 * (size_t)esub_cap_of(D, E) : 0) + 64, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
     L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);

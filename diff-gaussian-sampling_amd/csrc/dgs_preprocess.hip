@@ -934,7 +934,7 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                     const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
                     const int base = ff ? lbeg[c * kSubPerCell + k] + (int)nff[k] : lmid[c * kSubPerCell + k] + (int)nfl[k];
                     sub_ent[base + below] = entries[j];
-                    if (ff) sub_pos[base + below] = (uint16_t)(j - b);  // (the backward's LDS slot; cells
+                    if (ff && sub_pos) sub_pos[base + below] = (uint16_t)(j - b);  // (the backward's LDS slot; cells
                                                                         //  over 65535 entries do not use it)
                 }
                 nff[k] += (uint32_t)__popcll(bf);
@@ -1719,7 +1719,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         k_sub_lists<true><<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
                                                 cell_box, sub_box, G.CT, B.smask, nullptr, nullptr, sub_lbeg,
-                                                sub_lmid, sub_ent, reinterpret_cast<uint16_t *>(gbuf + L.o_sub_pos));
+                                                sub_lmid, sub_ent,
+                                                DGS_BWD_SUB ? reinterpret_cast<uint16_t *>(gbuf + L.o_sub_pos) : nullptr);
         DGS_LAUNCH_CHECK(s, debug);
         scan_excl<uint32_t>(nsub, B.sucnt, B.suoff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
         DGS_LAUNCH_CHECK(s, debug);

@@ -216,9 +216,6 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
-#ifndef DGS_BWD_SUB
-#define DGS_BWD_SUB 1  // D = 2, C = 1 backward over the sub-cell lists with a per-cell LDS flush
-#endif
 #ifndef DGS_FWD_SUB
 #define DGS_FWD_SUB 1  // D = 2 transposed forward over the sub-cell lists (k_forward_s)
 #endif
@@ -460,7 +457,7 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
 }
 
 #ifndef DGS_FWD_LDS
-#define DGS_FWD_LDS 1  // sub-cell forward: the pass's pair rows staged in LDS (else hoisted into SGPRs)
+#define DGS_FWD_LDS 0  // sub-cell forward: the pass's pair rows staged in LDS (else hoisted into SGPRs)
 #endif
 typedef float v4f __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) const v4f lds_cf4;

@@ -668,6 +668,104 @@ __device__ __forceinline__ void bwd_pair(const float *m, const float *c, const f
     pair_grads(G, phi, X, a, c, gg, e, dm, dc);
 }
 
+// ---- C = 1: the moment (tensor) form of the backward (the D = 2 form of 4.3b in
+// three dimensions).  With the sample's h scaled to the full symmetric tensor H (h_u divided by
+// the multiplicity of its index set, at staging), phi = sum_u h_u t_u and its partials are
+//   laplacian: phi = a.(H a) - H:c,          g = 2 H a,          e = -H (packed, off-diagonals x2)
+//   third    : E_pq = H_pqk a_k, M = E a,     w_k = c_ij H_ijk,
+//              phi = 3 w.a - M.a,            g = 3 (w - M),      e = 3 E (off-diagonals x2)
+// and the pair only adds moments: G phi, G g, G phi X, G phi X X^T, G (g X^T + X g^T), G e.  The
+// Gaussian's gradients follow once per lane (vol_mom_finish): dm = A (sum G g - sum G phi X),
+// dc = -1/2 sum G phi XX (off-diagonal -1) + sum G gX + sum G e, dv = sum G phi.  About 130
+// flops per pair for the third against ~300 for the per-pair terms (bwd_pair).
+struct VMom {
+    float sphi, sg[3], spx[3], spxx[6], sgx[6], se[6];
+};
+
+template <int FN>
+__host__ __device__ constexpr float vol_inv_mult(int u) {
+    if (FN == 2) return (u == 0 || u == 3 || u == 5) ? 1.0f : 0.5f;
+    if (FN == 3) return (u == 0 || u == 6 || u == 9) ? 1.0f : (u == 4 ? 1.0f / 6.0f : 1.0f / 3.0f);
+    return 1.0f;
+}
+
+template <int FN>
+__device__ __forceinline__ void bwd_pair_t(const float *m, const float *c, const float *c2, const float *s,
+                                           const float *H, VMom &M) {
+    float X[3], a[3], G;
+    if (!pair_eval(m, s, c, X, G, a)) return;
+    float phi, g[3] = {0.0f, 0.0f, 0.0f}, e[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f};
+    if constexpr (FN == 0) {
+        phi = H[0];
+    } else if constexpr (FN == 1) {
+        phi = H[0] * a[0] + H[1] * a[1] + H[2] * a[2];
+        g[0] = H[0]; g[1] = H[1]; g[2] = H[2];
+    } else if constexpr (FN == 2) {
+        const float ha0 = H[0] * a[0] + H[1] * a[1] + H[2] * a[2];
+        const float ha1 = H[1] * a[0] + H[3] * a[1] + H[4] * a[2];
+        const float ha2 = H[2] * a[0] + H[4] * a[1] + H[5] * a[2];
+        float hc = 0.0f;
+#pragma unroll
+        for (int q = 0; q < 6; ++q) hc += H[q] * c2[q];
+        phi = a[0] * ha0 + a[1] * ha1 + a[2] * ha2 - hc;
+        g[0] = 2.0f * ha0; g[1] = 2.0f * ha1; g[2] = 2.0f * ha2;
+        e[0] = -H[0]; e[1] = -2.0f * H[1]; e[2] = -2.0f * H[2]; e[3] = -H[3]; e[4] = -2.0f * H[4]; e[5] = -H[5];
+    } else {
+        // H000 H001 H002 H011 H012 H022 H111 H112 H122 H222 = H[0..9]
+        const float E00 = H[0] * a[0] + H[1] * a[1] + H[2] * a[2];
+        const float E01 = H[1] * a[0] + H[3] * a[1] + H[4] * a[2];
+        const float E02 = H[2] * a[0] + H[4] * a[1] + H[5] * a[2];
+        const float E11 = H[3] * a[0] + H[6] * a[1] + H[7] * a[2];
+        const float E12 = H[4] * a[0] + H[7] * a[1] + H[8] * a[2];
+        const float E22 = H[5] * a[0] + H[8] * a[1] + H[9] * a[2];
+        const float M0 = E00 * a[0] + E01 * a[1] + E02 * a[2];
+        const float M1 = E01 * a[0] + E11 * a[1] + E12 * a[2];
+        const float M2 = E02 * a[0] + E12 * a[1] + E22 * a[2];
+        // c2 = [c00 2c01 2c02 c11 2c12 c22]
+        const float w0 = c2[0] * H[0] + c2[3] * H[3] + c2[5] * H[5] + c2[1] * H[1] + c2[2] * H[2] + c2[4] * H[4];
+        const float w1 = c2[0] * H[1] + c2[3] * H[6] + c2[5] * H[8] + c2[1] * H[3] + c2[2] * H[4] + c2[4] * H[7];
+        const float w2 = c2[0] * H[2] + c2[3] * H[7] + c2[5] * H[9] + c2[1] * H[4] + c2[2] * H[5] + c2[4] * H[8];
+        phi = 3.0f * (w0 * a[0] + w1 * a[1] + w2 * a[2]) - (M0 * a[0] + M1 * a[1] + M2 * a[2]);
+        g[0] = 3.0f * (w0 - M0); g[1] = 3.0f * (w1 - M1); g[2] = 3.0f * (w2 - M2);
+        e[0] = 3.0f * E00; e[1] = 6.0f * E01; e[2] = 6.0f * E02; e[3] = 3.0f * E11; e[4] = 6.0f * E12; e[5] = 3.0f * E22;
+    }
+    const float Gp = G * phi;
+    M.sphi += Gp;
+    const float XX[6] = {X[0] * X[0], X[0] * X[1], X[0] * X[2], X[1] * X[1], X[1] * X[2], X[2] * X[2]};
+#pragma unroll
+    for (int d = 0; d < 3; ++d) M.spx[d] += Gp * X[d];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) M.spxx[q] += Gp * XX[q];
+    if constexpr (FN >= 1) {
+        const float Gg[3] = {G * g[0], G * g[1], G * g[2]};
+#pragma unroll
+        for (int d = 0; d < 3; ++d) M.sg[d] += Gg[d];
+        M.sgx[0] += Gg[0] * X[0];
+        M.sgx[1] += Gg[0] * X[1] + Gg[1] * X[0];
+        M.sgx[2] += Gg[0] * X[2] + Gg[2] * X[0];
+        M.sgx[3] += Gg[1] * X[1];
+        M.sgx[4] += Gg[1] * X[2] + Gg[2] * X[1];
+        M.sgx[5] += Gg[2] * X[2];
+    }
+    if constexpr (FN >= 2) {
+#pragma unroll
+        for (int q = 0; q < 6; ++q) M.se[q] += G * e[q];
+    }
+}
+
+__device__ __forceinline__ void vol_mom_finish(const float *c, const VMom &M, float *dm, float *dc, float *dv) {
+    const float d[3] = {M.sg[0] - M.spx[0], M.sg[1] - M.spx[1], M.sg[2] - M.spx[2]};
+    dm[0] = c[0] * d[0] + c[1] * d[1] + c[2] * d[2];
+    dm[1] = c[1] * d[0] + c[3] * d[1] + c[4] * d[2];
+    dm[2] = c[2] * d[0] + c[4] * d[1] + c[5] * d[2];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        const bool diag = q == 0 || q == 3 || q == 5;
+        dc[q] = (diag ? -0.5f : -1.0f) * M.spxx[q] + M.sgx[q] + M.se[q];
+    }
+    dv[0] = M.sphi;
+}
+
 template <int CB>
 __device__ __forceinline__ void bwd_store(int g, int C, int cbase, int nch, const float *dm, const float *dc,
                                           const float *dv, float *__restrict__ dmeans, float *__restrict__ dvalues,
@@ -733,6 +831,8 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
             }
             float dm[3] = {0.0f, 0.0f, 0.0f}, dc[6] = {0.0f, 0.0f, 0.0f, 0.0f, 0.0f, 0.0f}, dv[CB];
             for (int ch = 0; ch < CB; ++ch) dv[ch] = 0.0f;
+            VMom mom{};  // CB == 1: the moment form
+            const float c2[6] = {c[0], 2.0f * c[1], 2.0f * c[2], c[3], 2.0f * c[4], c[5]};
             float ml[3], mh[3], R[3];
             Win w[3];
             for (int d = 0; d < 3; ++d) {
@@ -776,8 +876,9 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                         const int sid = sids[q];
                                         scand[lane] = make_float4(samples[(int64_t)sid * 3], samples[(int64_t)sid * 3 + 1],
                                                                   samples[(int64_t)sid * 3 + 2], __int_as_float(sid));
-                                        if constexpr (CB == 1)
-                                            for (int u = 0; u < KU; ++u) shrow[lane][u] = hs[(int64_t)sid * KU + u];
+                                        if constexpr (CB == 1)  // the tensor H (bwd_pair_t)
+                                            for (int u = 0; u < KU; ++u)
+                                                shrow[lane][u] = hs[(int64_t)sid * KU + u] * vol_inv_mult<FN>(u);
                                     }
                                     __syncthreads();
                                     const int cnt = min(kWave, e - q0);
@@ -791,14 +892,18 @@ __global__ __launch_bounds__(kWave) void k_vol_backward(const char *__restrict__
                                                 mine = mine && fabsf(x - 2.0f * kk[d]) <= r[d] + 1e-5f;
                                             }
                                             if (mine) {
-                                                const float *hrow = CB == 1 ? &shrow[u][0]
-                                                                            : hs + (int64_t)__float_as_int(sp.w) * KU * C;
-                                                bwd_pair<FN, CB>(m, c, values, g, v0, C, cbase, nch, sv, hrow, dm, dc, dv);
+                                                if constexpr (CB == 1)
+                                                    bwd_pair_t<FN>(m, c, c2, sv, &shrow[u][0], mom);
+                                                else
+                                                    bwd_pair<FN, CB>(m, c, values, g, v0, C, cbase, nch, sv,
+                                                                     hs + (int64_t)__float_as_int(sp.w) * KU * C, dm,
+                                                                     dc, dv);
                                             }
                                         }
                                 }
                             }
                     }
+            if constexpr (CB == 1) vol_mom_finish(c, mom, dm, dc, dv);
             if (active) bwd_store<CB>(g, C, cbase, nch, dm, dc, dv, dmeans, dvalues, dconics, CB == 1 ? v0 : 1.0f);
         }
     }

@@ -53,3 +53,42 @@ def gaussian_fwd_bwd(ob, means, values, conics, samples, dL, subset, chunk=256):
             (o * g_out[sid]).sum().backward()
             out[torch.from_numpy(r.astype(np.int64))] = o.detach()
     return out, (m.grad, v.grad, c.grad)
+
+
+def aggregate_fwd_bwd(features, transform, queries, keys, frequencies, distance_transform, indices,
+                      ranges, dists, densities, inv_total, dL, rows):
+    """PyTorch-eager CPU evaluation of aggregate_neighbors (aggregate_neighbors.cu:129-208) for
+    the first `rows` rows of the given neighbour lists, forward + autograd backward (the
+    reference's aggregateNeighborsBackward gradients equal autograd of this forward,
+    tests/test_oracle_agg.py).  Vectorised over the rows' slots:
+      weight = q_i . k_j,  emb / fac = sum_{d,e} dt[.] sin / cos(f_e pi X_d) + bias,
+      dw = inv_total_i density_s weight,  out_i = T^T sum_s (dw emb 1 + dw fac feat_j).
+    Returns (out[rows, L], the six gradients)."""
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a))  # noqa: E731
+    feat, T, q, k = (t(a).float().requires_grad_(True) for a in (features, transform, queries, keys))
+    fr, dt = (t(a).float().requires_grad_(True) for a in (frequencies, distance_transform))
+    rg = np.asarray(ranges)
+    nslot = int(rg[rows - 1])
+    idx = t(np.asarray(indices)[:nslot]).long()
+    X = t(np.asarray(dists)[:nslot]).float().reshape(nslot, -1)
+    dens = t(np.asarray(densities)[:nslot]).float()
+    row_of = torch.repeat_interleave(torch.arange(rows), t(np.diff(np.concatenate([[0], rg[:rows]]))).long())
+    valid = idx >= 0
+    j = torch.where(valid, idx, torch.zeros_like(idx))
+    D, L = X.shape[1], feat.shape[1]
+    E = dt.shape[0] // 2
+    F = (E - 1) // D // 2
+    stride = (E - 1) // D
+    weight = (q[row_of] * k[j]).sum(1)
+    arg = fr[:F][None, None, :] * np.pi * X[:, :, None]           # [s, d, e]
+    sn, cs = torch.sin(arg), torch.cos(arg)
+    a_idx = torch.arange(D)[:, None] * stride + 2 * torch.arange(F)[None, :]
+    emb = (dt[a_idx] * sn + dt[a_idx + 1] * cs).sum((1, 2)) + dt[E - 1]
+    fac = (dt[E + a_idx] * sn + dt[E + a_idx + 1] * cs).sum((1, 2)) + dt[2 * E - 1]
+    dw = t(np.asarray(inv_total)).float()[row_of] * dens * weight
+    dw = torch.where(valid, dw, torch.zeros_like(dw))
+    embedded = (dw * emb)[:, None] + (dw * fac)[:, None] * feat[j]   # [s, L]
+    summed = torch.zeros(rows, L).index_add(0, row_of, embedded)
+    out = summed @ T
+    out.backward(t(np.asarray(dL)[:rows]).float())
+    return out.detach(), tuple(x.grad for x in (feat, T, q, k, fr, dt))

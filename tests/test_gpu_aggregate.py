@@ -19,8 +19,11 @@ up to ~1.3e-5 (relative) away from that value on these row lengths (tools/agg_er
 And, so that a summation regression shows against the reference's OWN numbers, every one of
 them is also bounded against the literal-order oracle (the reference's float summation order,
 aggregate_neighbors.cu:129-208 / 210-321) at the looser LIT_RTOL / LIT_ATOL = 3e-5: the
-reference's order is itself up to 1.9e-5 (scaled) away from the exact sum on these rows
-(profiles/r02_agg_margins.json, oracle_vs_exact), so 3e-5 leaves ~1.5x headroom and no more.
+reference's order is itself up to 2.1e-5 (scaled) away from the exact sum on these rows
+(profiles/r02_agg_margins.json, oracle_vs_exact), so 3e-5 leaves ~1.4x headroom and no more.  The
+frequency and distance-transform gradients are each ONE float sum over every slot of the
+problem, and there the reference's order is up to 7.4e-5 from the exact sum (long rows,
+2M slots): LIT_SHARED = 1e-4.
 """
 import numpy as np
 import pytest
@@ -32,6 +35,7 @@ from helpers import close
 
 pytestmark = pytest.mark.gpu
 LIT_RTOL = LIT_ATOL = 3e-5  # bound against the reference's literal float order (docstring)
+LIT_SHARED = 1e-4  # d/dfrequencies, d/ddistance_transform: float sums over EVERY slot (docstring)
 
 
 def _cuda(a):
@@ -71,8 +75,9 @@ def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared
         close(a.cpu().numpy().reshape(b.shape), b, 1e-5, atol, f"d/d{name}")
     lit = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
     for name, a, b in zip(AGG_FEATURES, got, lit):
-        atol = max(LIT_ATOL, 3 * shared_atol) if name in ("frequencies", "distance_transform") else LIT_ATOL
-        close(a.cpu().numpy().reshape(b.shape), b, LIT_RTOL, atol, f"d/d{name} vs the literal order")
+        shared = name in ("frequencies", "distance_transform")
+        tol = max(LIT_SHARED, 10 * shared_atol) if shared else LIT_RTOL
+        close(a.cpu().numpy().reshape(b.shape), b, tol, tol if shared else LIT_ATOL, f"d/d{name} vs the literal order")
 
 
 @pytest.mark.parametrize("D", [1, 2])

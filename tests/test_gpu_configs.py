@@ -138,8 +138,9 @@ def test_aggregate_config5_subset(dgs, oracle):
     for name, a, b in zip(AGG_FEATURES, got, ref):
         close(a.cpu().numpy().reshape(b.shape), b, 1e-5, 1e-5, f"d/d{name}")
     lit = oracle.agg_backward_rows(*args, rows, r_idx, r_rg, r_X, r_dn, w_r, e_r, f_r, r_inv, dL_rows)
-    for name, a, b in zip(AGG_FEATURES, got, lit):
-        close(a.cpu().numpy().reshape(b.shape), b, 3e-5, 3e-5, f"d/d{name} vs the literal order")
+    for name, a, b in zip(AGG_FEATURES, got, lit):  # (all-slot sums: 1e-4, test_gpu_aggregate.py LIT_SHARED)
+        tol = 1e-4 if name in ("frequencies", "distance_transform") else 3e-5
+        close(a.cpu().numpy().reshape(b.shape), b, tol, tol, f"d/d{name} vs the literal order")
 
 
 @pytest.mark.parametrize("function,C", [("gaussian", 1), ("derivative", 1), ("laplacian", 3)])

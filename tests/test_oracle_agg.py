@@ -153,3 +153,21 @@ def test_row_restricted_oracle_equals_full(oracle, D):
     got = oracle.agg_backward_rows(*args, rows, *sub[:4], ws, es, fs, sub[4], g[rows])
     for a, b in zip(got, ref):
         close(a, b, 1e-6, 1e-7, "row-restricted gradient")
+
+
+def test_torch_eager_aggregate_matches_oracle(oracle):
+    """bench.py's PyTorch-eager CPU baseline for aggregate_neighbors (oracle/torch_eager.py) is the
+    same math: forward and autograd gradients equal the oracle's exact accumulation."""
+    import numpy as np
+    from cases import AGG_FEATURES, agg_problem
+    from oracle import torch_eager as te
+    means, conics, radii, fe = agg_problem(P=500, D=2, L=16, K=16, F=4, seed=9)
+    idx, rg, X, dn, inv = oracle.agg_preprocess(means, conics, radii)
+    args = [fe[k] for k in AGG_FEATURES]
+    w, e, f, out = oracle.agg_forward(*args, idx, rg, X, dn, inv, exact=True)
+    g = np.random.default_rng(2).normal(size=out.shape).astype(np.float32)
+    ref = oracle.agg_backward(*args, idx, rg, X, dn, w, e, f, inv, g, exact=True)
+    o2, grads = te.aggregate_fwd_bwd(*args, idx, rg, X, dn, inv, g, rows=500)
+    np.testing.assert_allclose(o2.numpy(), out, rtol=1e-4, atol=1e-5 * np.abs(out).max())
+    for name, a, b in zip(AGG_FEATURES, grads, ref):
+        np.testing.assert_allclose(a.numpy().reshape(b.shape), b, rtol=1e-4, atol=1e-5 * np.abs(b).max(), err_msg=name)
