@@ -863,15 +863,36 @@ __global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, const int32_t *_
     if (lane == 0) box[c] = make_float4(clo[0], clo[1], chi[0], chi[1]);
 }
 
-// Sub lists (D = 2).  For every entry of a cell list, the sub-cells whose sample box its cut
-// X^T A X <= kQCut meets (bit k = sub-cell k), tested with the displacement the forward uses:
-// X = m - s, minus the entry's constant wrap shift for kGeneral entries (wrap_shift_f of the mean
-// minus the cell-box centre, exactly as k_forward_t forms it).  kUnsafe entries get no bit (the
-// forward's tail pass adds them per cell).  Pass 1 (WRITE = false) stores the masks and counts
-// per sub-cell the flag-free and the flagged entries; pass 2 writes the lists in cell-list
-// order (flag-free first, ascending position), so each sub list is [lbeg, lmid) flag-free,
-// [lmid, lend) flagged.  One wave per cell.
-template <bool WRITE>
+// Does the box [xa, xb] x [ya, yb] of displacements contain an X with X^T A X <= qcut?  fp32
+// with the reciprocals of c0 / c2 given (the sub-cell test runs once per entry and sub-cell).
+// Rounding moves the computed minimum by ~1e-6 relative; the callers' qcut has a 1e-4 margin and
+// the live pairs end at 207.9 (expf underflow), so a live pair is never culled.
+__device__ inline bool box_hits_ellipse_f(float xa, float xb, float ya, float yb, float c0, float c1, float c2,
+                                          float ic0, float ic2, float qcut) {
+    if (xa <= 0.0f && xb >= 0.0f && ya <= 0.0f && yb >= 0.0f) return true;
+    float best = INFINITY;
+    const float xs[2] = {xa, xb}, ys[2] = {ya, yb};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const float x = xs[k];
+        const float y = fminf(fmaxf(-c1 * x * ic2, ya), yb);
+        best = fminf(best, c0 * x * x + 2.0f * c1 * x * y + c2 * y * y);
+        const float yy = ys[k];
+        const float xx = fminf(fmaxf(-c1 * yy * ic0, xa), xb);
+        best = fminf(best, c0 * xx * xx + 2.0f * c1 * xx * yy + c2 * yy * yy);
+    }
+    return best <= qcut;
+}
+
+// Sub lists (D = 2), one pass, one wave per cell.  For every entry of the cell list, the
+// sub-cells whose sample box its cut X^T A X <= kQCut meets, tested with the displacement the
+// forward uses: X = m - s, minus the entry's constant wrap shift for kGeneral entries
+// (wrap_shift_f of the mean minus the cell-box centre, exactly as k_forward_t forms it).  kUnsafe
+// entries get no sub-cell (the forward's tail pass adds them per cell).  Sub list k of the cell
+// has the region [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at
+// most every sub list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the
+// flag-free entries and [lmid, lend) the flagged ones.  sub_pos (optional): each flag-free
+// entry's position in the cell list (the sub-cell backward's LDS slot).
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
                                                       const int32_t *__restrict__ gmid,
                                                       const int32_t *__restrict__ gend,
@@ -880,92 +901,86 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float4 *__restrict__ gcon,
                                                       const float4 *__restrict__ box,
                                                       const float4 *__restrict__ sbox, int CT,
-                                                      uint8_t *__restrict__ masks,
-                                                      uint32_t *__restrict__ cnt_ff, uint32_t *__restrict__ cnt_fl,
-                                                      const int32_t *__restrict__ lbeg,
-                                                      const int32_t *__restrict__ lmid,
-                                                      uint32_t *__restrict__ sub_ent, uint16_t *__restrict__ sub_pos) {
+                                                      int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
+                                                      int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent,
+                                                      uint16_t *__restrict__ sub_pos) {
     const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
-    const int b = gbeg[c], m_ = gmid[c], e = gend[c];
+    const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
     uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
+    const int64_t base = (int64_t)kSubPerCell * b;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
         const float ctr[2] = {0.5f * (bx.x + bx.z), 0.5f * (bx.y + bx.w)};  // = cell_center
         float4 sb[kSubPerCell];
         for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
+        const float qc = (float)(kQCut * (1.0 + 1e-4));
         for (int j0 = b; j0 < e; j0 += kWave) {
             const int j = j0 + lane;
-            uint32_t mask = 0u;
-            if (!WRITE) {
-                if (j < e) {
-                    const uint32_t ent = entries[j];
-                    if (!(ent & kUnsafe)) {
-                        const uint32_t id = ent & kIdMask;
-                        const float2 mm = gmean[id];
-                        const float4 cc = gcon[id];
-                        float sh[2] = {0.0f, 0.0f};
-                        if (ent & kGeneral) {
-                            sh[0] = wrap_shift_f(mm.x - ctr[0]);
-                            sh[1] = wrap_shift_f(mm.y - ctr[1]);
-                        }
-                        const double m0 = (double)mm.x - (double)sh[0], m1 = (double)mm.y - (double)sh[1];
-                        for (int k = 0; k < kSubPerCell; ++k) {
-                            const float4 q = sb[k];
-                            if (!(q.x <= q.z)) continue;  // empty sub-cell
-                            const double e0 = 1e-6 * (1.0 + fabs((double)mm.x) + fmax(fabs((double)q.x), fabs((double)q.z)));
-                            const double e1 = 1e-6 * (1.0 + fabs((double)mm.y) + fmax(fabs((double)q.y), fabs((double)q.w)));
-                            if (box_hits_ellipse(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1,
-                                                 cc.x, cc.y, cc.z, kQCut))
-                                mask |= 1u << k;
-                        }
+            uint32_t mask = 0u, ent = 0u;
+            if (j < e) {
+                ent = entries[j];
+                if (!(ent & kUnsafe)) {
+                    const uint32_t id = ent & kIdMask;
+                    const float2 mm = gmean[id];
+                    const float4 cc = gcon[id];
+                    float sh[2] = {0.0f, 0.0f};
+                    if (ent & kGeneral) {
+                        sh[0] = wrap_shift_f(mm.x - ctr[0]);
+                        sh[1] = wrap_shift_f(mm.y - ctr[1]);
                     }
-                    masks[j] = (uint8_t)mask;
+                    const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
+                    const float ic0 = 1.0f / cc.x, ic2 = 1.0f / cc.z;
+                    for (int k = 0; k < kSubPerCell; ++k) {
+                        const float4 q = sb[k];
+                        if (!(q.x <= q.z)) continue;  // empty sub-cell
+                        const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(q.x), fabsf(q.z)));
+                        const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(q.y), fabsf(q.w)));
+                        if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y,
+                                               cc.z, ic0, ic2, qc))
+                            mask |= 1u << k;
+                    }
                 }
-            } else {
-                mask = j < e ? (uint32_t)masks[j] : 0u;
             }
             const bool ff = j < m_;
             for (int k = 0; k < kSubPerCell; ++k) {
                 const bool hit = (mask >> k) & 1u;
                 const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
-                if (WRITE && hit) {
+                if (hit) {
                     const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
-                    const int base = ff ? lbeg[c * kSubPerCell + k] + (int)nff[k] : lmid[c * kSubPerCell + k] + (int)nfl[k];
-                    sub_ent[base + below] = entries[j];
-                    if (ff && sub_pos) sub_pos[base + below] = (uint16_t)(j - b);  // (the backward's LDS slot; cells
-                                                                        //  over 65535 entries do not use it)
+                    // flag-free entries precede the flagged ones in the cell list, so once a group
+                    // holds a flagged entry the flag-free count is final -- this group's own
+                    // flag-free hits included: the region fills [flag-free | flagged] in order
+                    const uint32_t nffk = nff[k] + (uint32_t)__popcll(bf);
+                    const int64_t o = base + (int64_t)k * n + (ff ? nff[k] : nffk + nfl[k]) + below;
+                    sub_ent[o] = ent;
+                    if (ff && sub_pos) sub_pos[o] = (uint16_t)(j - b);  // (cells over 65535 entries: unused)
                 }
                 nff[k] += (uint32_t)__popcll(bf);
                 nfl[k] += (uint32_t)__popcll(bl);
             }
         }
     }
-    if (!WRITE && lane == 0)
+    if (lane == 0)
         for (int k = 0; k < kSubPerCell; ++k) {
-            cnt_ff[c * kSubPerCell + k] = nff[k];
-            cnt_fl[c * kSubPerCell + k] = nfl[k];
+            const int a = (int)(base + (int64_t)k * n);
+            lbeg[c * kSubPerCell + k] = a;
+            lmid[c * kSubPerCell + k] = a + (int)nff[k];
+            lend[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);
         }
 }
 
-// Sub-list layout from the exclusive scans of the sub-cells' counts: [lbeg, lmid) flag-free,
-// [lmid, lend) flagged; and the forward sub units per sub-cell (samples and entries both
-// present): ceil(pairs / kSubPairs), pair-aligned.
-__global__ void k_sub_layout(int nsub, const uint32_t *__restrict__ off_ff, const uint32_t *__restrict__ off_fl,
-                             const uint32_t *__restrict__ cnt_ff,
-                             const uint32_t *__restrict__ cnt_fl, const int32_t *__restrict__ ssbeg,
-                             const int32_t *__restrict__ ssend, int32_t *__restrict__ lbeg,
-                             int32_t *__restrict__ lmid, int32_t *__restrict__ lend, uint32_t *__restrict__ ucnt) {
+// Forward sub units per sub-cell (samples and entries both present): ceil(pairs / kSubPairs),
+// pair-aligned.
+__global__ void k_sub_ucnt(int nsub, const int32_t *__restrict__ ssbeg, const int32_t *__restrict__ ssend,
+                           const int32_t *__restrict__ lbeg, const int32_t *__restrict__ lend,
+                           uint32_t *__restrict__ ucnt) {
     const int k = blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= nsub) return;
-    const int a = (int)(off_ff[k] + off_fl[k]);  // exclusive scan of ff + fl
-    lbeg[k] = a;
-    lmid[k] = a + (int)cnt_ff[k];
-    lend[k] = a + (int)cnt_ff[k] + (int)cnt_fl[k];
     const int ns = ssend[k] - ssbeg[k];
     const int npairs = ((ssend[k] + 1) >> 1) - (ssbeg[k] >> 1);
-    ucnt[k] = ns > 0 && cnt_ff[k] + cnt_fl[k] > 0 ? (uint32_t)((npairs + kSubPairs - 1) / kSubPairs) : 0u;
+    ucnt[k] = ns > 0 && lend[k] > lbeg[k] ? (uint32_t)((npairs + kSubPairs - 1) / kSubPairs) : 0u;
 }
 
 __global__ void k_sub_units(int nsub, const int32_t *__restrict__ ssbeg, const uint32_t *__restrict__ ucnt,
@@ -1534,8 +1549,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Layout L;
         char *gbuf = nullptr;
         uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
-        uint32_t *sff, *sfl, *soff_ff, *soff_fl, *sucnt, *suoff;  // sub lists (D = 2)
-        uint8_t *smask;
+        uint32_t *sucnt, *suoff;  // sub units (D = 2)
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
@@ -1557,10 +1571,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.foff = cb.take<uint32_t>(ncells); B.boff = cb.take<uint32_t>(ncells);
         B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
         B.rvals = cb.take<uint32_t>(Rcap + 1);
-        B.sff = cb.take<uint32_t>(nsub + 1); B.sfl = cb.take<uint32_t>(nsub + 1);
-        B.soff_ff = cb.take<uint32_t>(nsub + 1); B.soff_fl = cb.take<uint32_t>(nsub + 1);
         B.sucnt = cb.take<uint32_t>(nsub + 1); B.suoff = cb.take<uint32_t>(nsub + 1);
-        B.smask = cb.take<uint8_t>(nsub ? Ecap + 1 : 1);
         uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
         size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
         B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
@@ -1578,10 +1589,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
         for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.fcnt, &B.bcnt, &B.foff, &B.boff,
-                             &B.rkeys, &B.rkeys_sorted, &B.rvals, &B.sff, &B.sfl, &B.soff_ff, &B.soff_fl, &B.sucnt,
-                             &B.suoff})
+                             &B.rkeys, &B.rkeys_sorted, &B.rvals, &B.sucnt, &B.suoff})
             Carve::rebase(*q, base);
-        Carve::rebase(B.smask, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
         char *t = static_cast<char *>(B.tmp_b);
@@ -1708,19 +1717,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
-        k_sub_lists<false><<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
-                                                 cell_box, sub_box, G.CT, B.smask, B.sff, B.sfl, nullptr,
-                                                 nullptr, nullptr, nullptr);
+        k_sub_lists<<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box,
+                                          sub_box, G.CT, sub_lbeg, sub_lmid, sub_lend, sub_ent,
+                                          DGS_BWD_SUB ? reinterpret_cast<uint16_t *>(gbuf + L.o_sub_pos) : nullptr);
         DGS_LAUNCH_CHECK(s, debug);
-        scan_excl<uint32_t>(nsub, B.sff, B.soff_ff, B.sfl, B.soff_fl, static_cast<uint32_t *>(tmp_b), s);
-        DGS_LAUNCH_CHECK(s, debug);
-        k_sub_layout<<<grid_for(nsub), kBlock, 0, s>>>(nsub, B.soff_ff, B.soff_fl, B.sff, B.sfl, sub_sbeg, sub_send,
-                                                       sub_lbeg, sub_lmid, sub_lend, B.sucnt);
-        DGS_LAUNCH_CHECK(s, debug);
-        k_sub_lists<true><<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
-                                                cell_box, sub_box, G.CT, B.smask, nullptr, nullptr, sub_lbeg,
-                                                sub_lmid, sub_ent,
-                                                DGS_BWD_SUB ? reinterpret_cast<uint16_t *>(gbuf + L.o_sub_pos) : nullptr);
+        k_sub_ucnt<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, sub_send, sub_lbeg, sub_lend, B.sucnt);
         DGS_LAUNCH_CHECK(s, debug);
         scan_excl<uint32_t>(nsub, B.sucnt, B.suoff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
         DGS_LAUNCH_CHECK(s, debug);

@@ -216,6 +216,9 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
+#ifndef DGS_BWD_PIPE
+#define DGS_BWD_PIPE 1  // backward pair loop: the next batch of pair rows in flight during this one
+#endif
 #ifndef DGS_FWD_SUB
 #define DGS_FWD_SUB 1  // D = 2 transposed forward over the sub-cell lists (k_forward_s)
 #endif
@@ -969,12 +972,37 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
             bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
             ++p;
         }
-        for (; p + NB <= pf; p += NB) {
-            const F32s<NB * PR> sr = sload_f<NB * PR>(srows + (int64_t)p * PR);
+        if constexpr (DGS_BWD_PIPE) {
+            // The next batch of pair rows is in flight while this one is evaluated.  Scalar loads
+            // complete out of order, so each batch is waited for with lgkmcnt(0) BEFORE the next
+            // one is issued; scheduling barriers keep the compiler from moving the load across.
+            // (The look-ahead address is clamped to the last full batch: always in bounds.)
+            if (p + NB <= pf) {
+                const int plast = pf - NB;
+                F32s<NB * PR> cur = sload_f<NB * PR>(srows + (int64_t)p * PR);
+                for (; p + NB <= pf; p += NB) {
+                    DGS_WAIT_LGKM0();
+                    __builtin_amdgcn_sched_barrier(0);
+                    const F32s<NB * PR> nxt = sload_f<NB * PR>(srows + (int64_t)min(p + NB, plast) * PR);
+                    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-            for (int q = 0; q < NB; ++q) {
-                pair_fields<RSS, D>(&sr.v[q * PR], f, 0);
-                bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
+                    for (int q = 0; q < NB; ++q) {
+                        pair_fields<RSS, D>(&cur.v[q * PR], f, 0);
+                        bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    cur = nxt;
+                }
+                DGS_WAIT_LGKM0();  // (the last look-ahead, unused)
+            }
+        } else {
+            for (; p + NB <= pf; p += NB) {
+                const F32s<NB * PR> sr = sload_f<NB * PR>(srows + (int64_t)p * PR);
+#pragma unroll
+                for (int q = 0; q < NB; ++q) {
+                    pair_fields<RSS, D>(&sr.v[q * PR], f, 0);
+                    bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
+                }
             }
         }
         for (; p < pf; ++p) {
@@ -1080,7 +1108,7 @@ __device__ __forceinline__ uint32_t bwd_entry(const Bins &bins, uint2 u, int lan
 // persistent, software-pipelined form (rows of unit k + 1 in flight during unit k) measured
 // 5-15 % slower: the hardware's dynamic wave dispatch balances the uneven units better.
 template <int FN, int D, int CB>
-__global__ __launch_bounds__(kBlock) void k_backward(const char *__restrict__ gbuf,
+__global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__ gbuf,  // (5 waves per SIMD: <= 96 VGPRs)
                                                      const char *__restrict__ sbuf,
                                                      const float *__restrict__ grows,
                                                      const float *__restrict__ srows,
