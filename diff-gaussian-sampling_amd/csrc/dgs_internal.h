@@ -42,9 +42,8 @@ constexpr int kFwdUnit = kWave;
 // Sub-cells (D = 2): every fine cell is split 2 x 2 at its nominal mid-lines; samples are sorted
 // by (cell, sub-cell), and the forward walks per sub-cell the entries of its cell whose cut
 // meets the sub-cell's sample box (sub lists), in units of up to kSubPairs sample pairs.  The
-// backward keeps one flush per (cell, Gaussian) -- what the float atomics allow -- but walks a
-// copy of each cell list grouped by sub-cell mask (bwd lists): a unit of 64 entries then visits
-// only the samples of the sub-cells its entries' cuts meet.
+// backward keeps the cell lists: their one flush per (cell, Gaussian), in ascending-id runs, is
+// what the float atomics allow.
 constexpr int kSubPerCell = 4;
 constexpr int kSubPairs = 24;
 constexpr int kBlock = 256;
@@ -97,11 +96,6 @@ struct Header {
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     int64_t fsub_cap, esub_cap;
-    // bwd lists (D = 2): per cell [cell_gbeg, cell_bend) of bwd_ent, the cell list's entries
-    // grouped by (flag class, sub-cell mask) with the entries that meet no sub-cell left out;
-    // bwd_aux = each one's position in the cell list (0xffff past 16 bits) | its sub-cell mask
-    // (15 for kUnsafe entries) << 16
-    uint64_t o_bwd_ent, o_bwd_aux, o_cell_bend;
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
@@ -115,7 +109,7 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
     uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab;
-    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent, o_bwd_ent, o_bwd_aux, o_cell_bend;
+    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
 };
@@ -154,10 +148,6 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_ent = o;   o = align_up(o + 4 * (size_t)esub_cap_of(D, E) + 64, 256);
-    const size_t eb = D == 2 ? (size_t)E : 0;
-    L.o_bwd_ent = o;   o = align_up(o + 4 * eb + 64, 256);
-    L.o_bwd_aux = o;   o = align_up(o + 4 * eb + 64, 256);
-    L.o_cell_bend = o; o = align_up(o + (D == 2 ? 4 * (size_t)ncells : 0) + 64, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
     L.o_sorted = o;    o = align_up(o + 4 * (size_t)N, 256);
@@ -197,9 +187,6 @@ struct Bins {
     const uint2 *fsub_units;             // (sub-cell, pair-aligned first sample)
     const int32_t *sub_lbeg, *sub_lmid, *sub_lend;
     const uint32_t *sub_ent;             // sub lists: entries of the cell list, flagged last
-    const uint32_t *bwd_ent;             // bwd lists (D = 2): [cell_gbeg, cell_bend) per cell
-    const uint32_t *bwd_aux;             // their cell-list positions | sub-cell masks << 16
-    const int32_t *cell_bend;
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -257,9 +244,6 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.sub_lmid = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lmid));
     B.sub_lend = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lend));
     B.sub_ent = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_sub_ent));
-    B.bwd_ent = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_bwd_ent));
-    B.bwd_aux = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_bwd_aux));
-    B.cell_bend = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_cell_bend));
     return B;
 }
 

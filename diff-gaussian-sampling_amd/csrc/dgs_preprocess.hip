@@ -884,54 +884,14 @@ __device__ inline bool box_hits_ellipse_f(float xa, float xb, float ya, float yb
     return best <= qcut;
 }
 
-// Sub lists and bwd lists (D = 2), one workgroup per cell, two passes over the cell list.
-// Pass 1: every entry's sub-cell mask -- the sub-cells whose sample box its cut
-// X^T A X <= kQCut meets, tested with the displacement the forward uses: X = m - s, minus the
-// entry's constant wrap shift for kGeneral entries (wrap_shift_f of the mean minus the cell-box
-// centre, exactly as k_forward_t forms it) -- kept in emask, and the list sizes.  kUnsafe entries
-// get no sub-cell (the forward's tail pass adds them per cell).  Pass 2: the stable writes.
-//   sub list k of the cell: the region [4 gbeg + k n, + n) of sub_ent (n = the cell list's
-//   length: an entry is in at most every sub list of its cell), in cell-list order, so
-//   [lbeg, lmid) holds the flag-free entries and [lmid, lend) the flagged ones;
-//   bwd list: [gbeg, bend) of bwd_ent, grouped by class = (flag class, mask) in the order of
-//   kBwdRank (flag-free, then kGeneral, then kUnsafe with mask 15), cell-list order within a
-//   class, with bwd_aux = position in the cell list | mask << 16; entries that meet no sub-cell
-//   (all their pairs are exact zeros) are left out.  A
-//   backward unit of 64 consecutive entries then visits only the samples of the union of its
-//   entries' masks.  Class order: nested masks next to each other (a unit straddling two
-//   classes visits their union), the whole cell first.
-constexpr int kBwdCls = 32, kSubKeys = 2 * kSubPerCell;
-// rank of mask m (1..15) = nibble m: 15 7 3 1 5 13 12 4 14 10 2 11 9 8 6 -> 0 .. 14
-constexpr uint64_t kBwdRank = (0ull << 60) | (1ull << 28) | (2ull << 12) | (3ull << 4) | (4ull << 20) |
-                              (5ull << 52) | (6ull << 48) | (7ull << 16) | (8ull << 56) | (9ull << 40) |
-                              (10ull << 8) | (11ull << 44) | (12ull << 36) | (13ull << 32) | (14ull << 24);
-__device__ inline int bwd_class(uint32_t ent, uint32_t mask, bool ff) {
-    if (ent & kUnsafe) return 30;
-    if (!mask) return -1;
-    return (ff ? 0 : 15) + (int)((kBwdRank >> (4 * mask)) & 15u);
-}
-
-// The wave's lanes of the caller's class (cls < 0: none) and, per sub key q = (sub k,
-// flagged), the lanes whose entry goes to that list.
-__device__ inline uint64_t class_peers(int cls) {
-    uint64_t peers = __ballot(cls >= 0);
-#pragma unroll
-    for (int bit = 0; bit < 5; ++bit) {
-        const uint64_t bb = __ballot(cls >= 0 && ((cls >> bit) & 1));
-        peers &= ((cls >> bit) & 1) ? bb : ~bb;
-    }
-    return peers;
-}
-__device__ inline uint32_t sub_key_ballots(bool valid, uint32_t mask, bool ff, int lane, uint64_t (&kb)[kSubKeys]) {
-    uint32_t mine = 0u;  // lane q < kSubKeys: the count of key q
-#pragma unroll
-    for (int q = 0; q < kSubKeys; ++q) {
-        kb[q] = __ballot(valid && ((mask >> (q >> 1)) & 1u) && (ff == ((q & 1) == 0)));
-        if (lane == q) mine = (uint32_t)__popcll(kb[q]);
-    }
-    return mine;
-}
-
+// Sub lists (D = 2), one pass, one wave per cell.  For every entry of the cell list, the
+// sub-cells whose sample box its cut X^T A X <= kQCut meets, tested with the displacement the
+// forward uses: X = m - s, minus the entry's constant wrap shift for kGeneral entries
+// (wrap_shift_f of the mean minus the cell-box centre, exactly as k_forward_t forms it).  kUnsafe
+// entries get no sub-cell (the forward's tail pass adds them per cell).  Sub list k of the cell
+// has the region [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at
+// most every sub list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the
+// flag-free entries and [lmid, lend) the flagged ones.
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
                                                       const int32_t *__restrict__ gmid,
                                                       const int32_t *__restrict__ gend,
@@ -939,123 +899,73 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float2 *__restrict__ gmean,
                                                       const float4 *__restrict__ gcon,
                                                       const float4 *__restrict__ box,
-                                                      const float4 *__restrict__ sbox,
+                                                      const float4 *__restrict__ sbox, int CT,
                                                       int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
-                                                      int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent,
-                                                      uint32_t *__restrict__ bwd_ent, uint32_t *__restrict__ bwd_aux,
-                                                      int32_t *__restrict__ bend, uint8_t *__restrict__ emask) {
-    constexpr int NK = kBwdCls + kSubKeys;  // count slots: classes, then (sub k, flag-free / flagged)
-    __shared__ uint32_t s_tot[NK], s_off[NK], s_w[kWavesPerBlock][NK];
-    const int c = blockIdx.x;
-    const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid >> 6;
+                                                      int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent) {
+    const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
+    const int lane = threadIdx.x & (kWave - 1);
+    if (c >= ncells) return;
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
     const int64_t base = (int64_t)kSubPerCell * b;
-    if (tid < NK) s_tot[tid] = 0u;
-    __syncthreads();
-    // ---- pass 1: masks and sizes
-    if (b < e) {
+    if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
         const float ctr[2] = {0.5f * (bx.x + bx.z), 0.5f * (bx.y + bx.w)};  // = cell_center
         float4 sb[kSubPerCell];
         for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
         const float qc = (float)(kQCut * (1.0 + 1e-4));
-        for (int j0 = b; j0 < e; j0 += kBlock) {  // (whole waves: the ballots below)
-            const int j = j0 + tid;
-            const bool valid = j < e;
-            const uint32_t ent = valid ? entries[j] : kUnsafe;
-            uint32_t mask = 0u;
-            if (valid && !(ent & kUnsafe)) {  // (the tile fallback cells hold kUnsafe entries only)
-                const uint32_t id = ent & kIdMask;
-                const float2 mm = gmean[id];
-                const float4 cc = gcon[id];
-                float sh[2] = {0.0f, 0.0f};
-                if (ent & kGeneral) {
-                    sh[0] = wrap_shift_f(mm.x - ctr[0]);
-                    sh[1] = wrap_shift_f(mm.y - ctr[1]);
-                }
-                const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
-                const float ic0 = 1.0f / cc.x, ic2 = 1.0f / cc.z;
-                for (int k = 0; k < kSubPerCell; ++k) {
-                    const float4 q = sb[k];
-                    if (!(q.x <= q.z)) continue;  // empty sub-cell
-                    const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(q.x), fabsf(q.z)));
-                    const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(q.y), fabsf(q.w)));
-                    if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y,
-                                           cc.z, ic0, ic2, qc))
-                        mask |= 1u << k;
+        for (int j0 = b; j0 < e; j0 += kWave) {
+            const int j = j0 + lane;
+            uint32_t mask = 0u, ent = 0u;
+            if (j < e) {
+                ent = entries[j];
+                if (!(ent & kUnsafe)) {
+                    const uint32_t id = ent & kIdMask;
+                    const float2 mm = gmean[id];
+                    const float4 cc = gcon[id];
+                    float sh[2] = {0.0f, 0.0f};
+                    if (ent & kGeneral) {
+                        sh[0] = wrap_shift_f(mm.x - ctr[0]);
+                        sh[1] = wrap_shift_f(mm.y - ctr[1]);
+                    }
+                    const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
+                    const float ic0 = 1.0f / cc.x, ic2 = 1.0f / cc.z;
+                    for (int k = 0; k < kSubPerCell; ++k) {
+                        const float4 q = sb[k];
+                        if (!(q.x <= q.z)) continue;  // empty sub-cell
+                        const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(q.x), fabsf(q.z)));
+                        const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(q.y), fabsf(q.w)));
+                        if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y,
+                                               cc.z, ic0, ic2, qc))
+                            mask |= 1u << k;
+                    }
                 }
             }
-            if (valid) emask[j] = (uint8_t)mask;
             const bool ff = j < m_;
-            const int cls = valid ? bwd_class(ent, mask, ff) : -1;
-            // one LDS add per (wave, class) and per (wave, sub key)
-            const uint64_t peers = class_peers(cls);
-            if (cls >= 0 && (peers & ((1ull << lane) - 1ull)) == 0ull) atomicAdd(&s_tot[cls], (uint32_t)__popcll(peers));
-            uint64_t kb[kSubKeys];
-            const uint32_t mine = sub_key_ballots(valid, mask, ff, lane, kb);
-            if (lane < kSubKeys && mine) atomicAdd(&s_tot[kBwdCls + lane], mine);
+            for (int k = 0; k < kSubPerCell; ++k) {
+                const bool hit = (mask >> k) & 1u;
+                const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
+                if (hit) {
+                    const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
+                    // flag-free entries precede the flagged ones in the cell list, so once a group
+                    // holds a flagged entry the flag-free count is final -- this group's own
+                    // flag-free hits included: the region fills [flag-free | flagged] in order
+                    const uint32_t nffk = nff[k] + (uint32_t)__popcll(bf);
+                    const int64_t o = base + (int64_t)k * n + (ff ? nff[k] : nffk + nfl[k]) + below;
+                    sub_ent[o] = ent;
+                }
+                nff[k] += (uint32_t)__popcll(bf);
+                nfl[k] += (uint32_t)__popcll(bl);
+            }
         }
     }
-    __syncthreads();
-    if (tid == 0) {
-        uint32_t o = (uint32_t)b;
-        for (int q = 0; q < kBwdCls; ++q) { s_off[q] = o; o += s_tot[q]; }
-        bend[c] = (int32_t)o;
+    if (lane == 0)
         for (int k = 0; k < kSubPerCell; ++k) {
-            const int64_t a = base + (int64_t)k * n;
-            const uint32_t nf = s_tot[kBwdCls + 2 * k], nl = s_tot[kBwdCls + 2 * k + 1];
-            s_off[kBwdCls + 2 * k] = (uint32_t)a;
-            s_off[kBwdCls + 2 * k + 1] = (uint32_t)(a + nf);
-            lbeg[c * kSubPerCell + k] = (int32_t)a;
-            lmid[c * kSubPerCell + k] = (int32_t)(a + nf);
-            lend[c * kSubPerCell + k] = (int32_t)(a + nf + nl);
+            const int a = (int)(base + (int64_t)k * n);
+            lbeg[c * kSubPerCell + k] = a;
+            lmid[c * kSubPerCell + k] = a + (int)nff[k];
+            lend[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);
         }
-    }
-    __syncthreads();
-    // ---- pass 2: stable writes, one chunk of kBlock entries at a time (positions = the class /
-    // list offset + the counts of the lower waves + the rank within the wave)
-    const uint64_t below = (1ull << lane) - 1ull;
-    for (int j0 = b; j0 < e; j0 += kBlock) {
-        const int j = j0 + tid;
-        const bool valid = j < e;
-        uint32_t ent = 0u, mask = 0u;
-        int cls = -1;
-        bool ff = false;
-        if (valid) {
-            ent = entries[j];
-            mask = emask[j];  // (written by this thread in pass 1)
-            ff = j < m_;
-            cls = bwd_class(ent, mask, ff);
-        }
-        // rank among the wave's lanes of the same class: the lanes agreeing on every class bit
-        const uint64_t peers = class_peers(cls);
-        uint64_t kb[kSubKeys];
-        const uint32_t mine = sub_key_ballots(valid, mask, ff, lane, kb);
-        if (lane < NK) s_w[w][lane] = 0u;  // (then this wave's counts: in order within the wave)
-        if (cls >= 0 && (peers & below) == 0ull) s_w[w][cls] = (uint32_t)__popcll(peers);
-        if (lane < kSubKeys) s_w[w][kBwdCls + lane] = mine;
-        __syncthreads();
-        if (cls >= 0) {
-            uint32_t o = s_off[cls] + (uint32_t)__popcll(peers & below);
-            for (int v = 0; v < w; ++v) o += s_w[v][cls];
-            bwd_ent[o] = ent;
-            bwd_aux[o] = (uint32_t)min(j - b, 0xffff) | (((ent & kUnsafe) ? 15u : mask) << 16);
-        }
-#pragma unroll
-        for (int q = 0; q < kSubKeys; ++q) {
-            if (!((kb[q] >> lane) & 1ull)) continue;
-            uint32_t o = s_off[kBwdCls + q] + (uint32_t)__popcll(kb[q] & below);
-            for (int v = 0; v < w; ++v) o += s_w[v][kBwdCls + q];
-            sub_ent[o] = ent;
-        }
-        __syncthreads();
-        if (tid < NK) {
-            uint32_t t = 0u;
-            for (int v = 0; v < kWavesPerBlock; ++v) t += s_w[v][tid];
-            s_off[tid] += t;
-        }
-        __syncthreads();
-    }
 }
 
 // Forward sub units per sub-cell (samples and entries both present): ceil(pairs / kSubPairs),
@@ -1637,7 +1547,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         char *gbuf = nullptr;
         uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
         uint32_t *sucnt, *suoff;  // sub units (D = 2)
-        uint8_t *emask;           // per cell-list entry: its sub-cell mask (k_sub_lists)
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
@@ -1660,7 +1569,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
         B.rvals = cb.take<uint32_t>(Rcap + 1);
         B.sucnt = cb.take<uint32_t>(nsub + 1); B.suoff = cb.take<uint32_t>(nsub + 1);
-        B.emask = cb.take<uint8_t>(nsub ? Ecap + 1 : 1);
         uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
         size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
         B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
@@ -1682,7 +1590,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             Carve::rebase(*q, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
-        Carve::rebase(B.emask, base);
         char *t = static_cast<char *>(B.tmp_b);
         Carve::rebase(t, base);
         B.tmp_b = t;
@@ -1727,8 +1634,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         }
     }
     if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries");
-    if (D == 2 && kSubPerCell * E >= (1LL << 31) - 64)
-        return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries for the sub lists (4 E >= 2^31)");
     if (R >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "num_rendered exceeds 2^31 (32-bit tile lists)");
     size_spec_put(P, N, D, E, R);
     if (E > B.Ecap || R > B.Rcap) {  // no speculation, or this call's lists do not fit it
@@ -1793,19 +1698,24 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, entries);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    if (nsub) {  // the forward's sub lists and the backward's bwd lists (D = 2)
+    k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
+                                                      cell_gend, fcnt, bcnt);
+    DGS_LAUNCH_CHECK(s, debug);
+    scan_excl<uint32_t>(ncells, fcnt, foff, bcnt, boff, static_cast<uint32_t *>(tmp_b), s);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
+                                                    boff, fwd_units, bwd_units, counters);
+    DGS_LAUNCH_CHECK(s, debug);
+    if (nsub) {  // the forward's sub lists and sub units (D = 2)
+        const unsigned wb = (unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave));
         const float2 *gmean = reinterpret_cast<const float2 *>(gbuf + L.o_gmean);
         const float4 *gcon = reinterpret_cast<const float4 *>(gbuf + L.o_gcon);
         int32_t *sub_lbeg = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lbeg);
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
-        int32_t *cell_bend = reinterpret_cast<int32_t *>(gbuf + L.o_cell_bend);
-        k_sub_lists<<<(unsigned)ncells, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
-                                                        cell_box, sub_box, sub_lbeg, sub_lmid, sub_lend, sub_ent,
-                                                        reinterpret_cast<uint32_t *>(gbuf + L.o_bwd_ent),
-                                                        reinterpret_cast<uint32_t *>(gbuf + L.o_bwd_aux), cell_bend,
-                                                        B.emask);
+        k_sub_lists<<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box,
+                                          sub_box, G.CT, sub_lbeg, sub_lmid, sub_lend, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);
         k_sub_ucnt<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, sub_send, sub_lbeg, sub_lend, B.sucnt);
         DGS_LAUNCH_CHECK(s, debug);
@@ -1814,15 +1724,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         k_sub_units<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, B.sucnt, B.suoff, fsub_units, counters);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    // forward / backward units over the cell lists (k_forward_t, k_forward_mx, k_backward; the
-    // D = 2 sub-cell kernels walk the sub units and the cells)
-    k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg, cell_gend, fcnt, bcnt);
-    DGS_LAUNCH_CHECK(s, debug);
-    scan_excl<uint32_t>(ncells, fcnt, foff, bcnt, boff, static_cast<uint32_t *>(tmp_b), s);
-    DGS_LAUNCH_CHECK(s, debug);
-    k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
-                                                    boff, fwd_units, bwd_units, counters);
-    DGS_LAUNCH_CHECK(s, debug);
 
     // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled) and the
     // call-time path's tables: its tile lists (the reference's point_list) and unit counts
@@ -1876,7 +1777,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_fsub_units = L0.o_fsub_units;
     h.o_sub_lbeg = L.o_sub_lbeg; h.o_sub_lmid = L.o_sub_lmid; h.o_sub_lend = L.o_sub_lend; h.o_sub_ent = L.o_sub_ent;
     h.fsub_cap = fsub_cap_of(D, N, ncells); h.esub_cap = esub_cap_of(D, E);
-    h.o_bwd_ent = L.o_bwd_ent; h.o_bwd_aux = L.o_bwd_aux; h.o_cell_bend = L.o_cell_bend;
     h.stamp = ++stamp_counter;
     k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
     DGS_LAUNCH_CHECK(s, debug);

@@ -216,9 +216,6 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
-#ifndef DGS_BWD_NOATOM
-#define DGS_BWD_NOATOM 0
-#endif
 #ifndef DGS_BWD_PIPE
 #define DGS_BWD_PIPE 1  // backward pair loop: the next batch of pair rows in flight during this one
 #endif
@@ -1021,17 +1018,11 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
     }
 }
 
-// Up to two sample ranges of a cell (sorted order): the whole cell, or at D = 2 the runs of the
-// sub-cells a backward unit visits.
-struct SRanges {
-    int n, a0, b0, a1, b1;
-};
-
 // The gradient sums of one lane's Gaussian (entry ent, row r, conic cr) over the samples
-// `rg` of `cell` (sorted order), finished into sm[D], sc[S], sv[CB].  The mode (fast /
+// [sb, se) of `cell` (sorted order), finished into sm[D], sc[S], sv[CB].  The mode (fast /
 // constant wrap shift / general) is chosen for the whole wave from its active lanes' flags.
 template <int FN, int D, int CB>
-__device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restrict__ srows, int cell, const SRanges &rg,
+__device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restrict__ srows, int cell, int sb, int se,
                                          uint32_t ent, bool active, const float (&r)[grow_stride<FN, D, CB>()],
                                          float4 cr, float (&sm)[2], float (&sc)[3], float (&sv)[CB]) {
     using Tr = Traits<FN, D>;
@@ -1048,8 +1039,7 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     for (int k = 0; k < NA; ++k) ra[k] = bc<V>(0.0f);
     float sh[2] = {0.0f, 0.0f};
     if (__any(active && unsafe)) {
-        for (int q = 0, qa = rg.a0, qb = rg.b0; q < rg.n; ++q, qa = rg.a1, qb = rg.b1)
-            bwd_loop<FN, D, CB, 2, V>(qa, qb, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, ra);
+        bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, ra);
     } else if (__any(active && wrap)) {
         if (active && wrap) {
             float ctr[2];
@@ -1057,11 +1047,9 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
 #pragma unroll
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
-        for (int q = 0, qa = rg.a0, qb = rg.b0; q < rg.n; ++q, qa = rg.a1, qb = rg.b1)
-            bwd_loop<FN, D, CB, 1, V>(qa, qb, srows, m, sh, c, &r[D], &r[B], false, false, ra);
+        bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     } else {
-        for (int q = 0, qa = rg.a0, qb = rg.b0; q < rg.n; ++q, qa = rg.a1, qb = rg.b1)
-            bwd_loop<FN, D, CB, 0, V>(qa, qb, srows, m, sh, c, &r[D], &r[B], false, false, ra);
+        bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     }
     if constexpr (bwd_mom<FN, D, CB>()) {
         float sum[kMomAcc];
@@ -1085,70 +1073,39 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     }
 }
 
-// The sub-cell sample boundaries of a cell (sorted by (cell, sub-cell)): sub-cell k's samples
-// are [Bd[k], Bd[k + 1]), Bd[0] / Bd[4] the cell's (empty sub-cells: zero-length).
-__device__ __forceinline__ void sub_bounds(const Bins &bins, int cell, int sb, int se, int (&Bd)[kSubPerCell + 1]) {
-    Bd[0] = sb;
-    Bd[kSubPerCell] = se;
-#pragma unroll
-    for (int k = kSubPerCell - 1; k >= 1; --k) {
-        const int a = sload(&bins.sub_sbeg[cell * kSubPerCell + k]), e = sload(&bins.sub_send[cell * kSubPerCell + k]);
-        Bd[k] = a < e ? a : Bd[k + 1];
-    }
-}
-
-// The samples a D = 2 backward unit visits: the sub-cells in `U` (wave-uniform union of its
-// entries' masks), consecutive ones merged into one range (an empty sub-cell never splits a run:
-// it has no samples between its neighbours'); at most two runs for 4 sub-cells.
-__device__ __forceinline__ SRanges sub_ranges(const int (&Bd)[kSubPerCell + 1], uint32_t U) {
-    SRanges rg{0, 0, 0, 0, 0};
-    int a = -1, b = -1;
-#pragma unroll
-    for (int k = 0; k < kSubPerCell; ++k) {
-        const int ss = Bd[k], se = Bd[k + 1];
-        if (ss >= se) continue;
-        if ((U >> k) & 1u) {
-            if (a < 0) a = ss;
-            b = se;
-        } else if (a >= 0) {
-            if (rg.n == 0) { rg.a0 = a; rg.b0 = b; } else { rg.a1 = a; rg.b1 = b; }
-            ++rg.n;
-            a = -1;
-        }
-    }
-    if (a >= 0) {
-        if (rg.n == 0) { rg.a0 = a; rg.b0 = b; } else { rg.a1 = a; rg.b1 = b; }
-        ++rg.n;
-    }
-    return rg;
-}
-
 // One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
-// conic cr), the samples `rg` wave-uniform; the lane's finished gradient in sm, sc, sv.
+// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane.
 template <int FN, int D, int CB>
-__device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows, int cell,
-                                         const SRanges &rg, bool active, uint32_t ent,
-                                         const float (&r)[grow_stride<FN, D, CB>()], float4 cr, float (&sm)[2],
-                                         float (&sc)[3], float (&sv)[CB]) {
-    bwd_sums<FN, D, CB>(bins, srows, cell, rg, ent, active, r, cr, sm, sc, sv);
-}
-
-// The lane's gradient straight to the global sums: one atomicAdd per component.
-template <int FN, int D, int CB>
-__device__ __forceinline__ void bwd_flush_global(float *__restrict__ acc, int P, int vrow0, int64_t id,
-                                                 const float (&sm)[2], const float (&sc)[3], const float (&sv)[CB]) {
+__device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows,
+                                         float *__restrict__ acc, int P, int vrow0, uint2 u,
+                                         uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
+                                         float4 cr, int lane) {
     constexpr int S = Traits<FN, D>::S;
+    const int cell = (int)u.x, eb = (int)u.y;
+    const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
+    const bool active = eb + lane < ee;
+    const int64_t id = ent & kIdMask;
+    const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+    float sm[2], sc[3], sv[CB];
+    bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, cr, sm, sc, sv);
+    if (active) {
 #pragma unroll
-    for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
+        for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
 #pragma unroll
-    for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
+        for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
 #pragma unroll
-    for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
+        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
+    }
 }
 
-// (b) Cell-list backward (D = 1): one wave per unit = (cell, <= 64 entries of the cell list)
-// against all the cell's samples (exact grid from the preprocess hint; grid-strided otherwise).
-// A persistent, software-pipelined form (rows of unit k + 1 in flight during unit k) measured
+// The lane's entry of unit u (clamped to the unit's last entry for padding lanes).
+__device__ __forceinline__ uint32_t bwd_entry(const Bins &bins, uint2 u, int lane) {
+    const int ee = min((int)u.y + kWave, sload(&bins.cell_gend[u.x]));
+    return bins.entries[min((int)u.y + lane, ee - 1)];
+}
+
+// One wave per unit (exact grid from the preprocess hint; grid-strided otherwise).  A
+// persistent, software-pipelined form (rows of unit k + 1 in flight during unit k) measured
 // 5-15 % slower: the hardware's dynamic wave dispatch balances the uneven units better.
 template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__ gbuf,  // (5 waves per SIMD: <= 96 VGPRs)
@@ -1165,104 +1122,10 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
     const int lane = threadIdx.x & (kWave - 1);
     for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         const uint2 u = sload(&bins.bwd_units[unit]);
-        const int cell = (int)u.x, eb = (int)u.y;
-        const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
-        const uint32_t ent = bins.entries[min(eb + lane, ee - 1)];  // (padding lanes: the unit's last entry)
-        const bool active = eb + lane < ee;
+        const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
         load_grow<RS>(grows, ent, r);
-        const SRanges rg{1, sload(&bins.cell_sbeg[cell]), sload(&bins.cell_send[cell]), 0, 0};
-        float sm[2], sc[3], sv[CB];
-        bwd_unit<FN, D, CB>(bins, srows, cell, rg, active, ent, r, bins.gcon[ent & kIdMask], sm, sc, sv);
-        // (DGS_BWD_NOATOM: timing experiment without the flush; the sums stay live)
-        if (active && (!DGS_BWD_NOATOM || __float_as_uint(sm[0] + sc[0] + sc[2] + sv[0]) == 0x7f800001u))
-            bwd_flush_global<FN, D, CB>(acc, P, vrow0, ent & kIdMask, sm, sc, sv);
-    }
-}
-
-// (b') Sub-cell backward (D = 2): one workgroup per cell; its waves take the units of the cell's
-// bwd list (64 entries grouped by sub-cell mask, visiting only the samples of the union of their
-// masks: sub_ranges) and store each finished gradient in the LDS slot of the entry's cell-list
-// position (one slot per (cell, Gaussian): plain stores); the workgroup then adds the slots to the
-// global sums in cell-list order, i.e. ascending Gaussian id over the gathered entries, so the
-// float atomics keep the cell lists' address runs (the grouped order scatters them: 2.3x the
-// 64-B atomic requests, measured 2x slower).  Positions past kBwdSlots go straight to the global
-// sums.  Slots left 0 (entries in no sub-cell, or no live pair) are not flushed.  Channel blocks
-// of more than 2 (more than 8 slots per entry) take k_backward over the cell lists.
-constexpr int kBwdSlots = 1536;
-template <int FN, int D, int CB>
-__global__ __launch_bounds__(kBlock, 4) void k_backward_c(const char *__restrict__ gbuf,
-                                                       const char *__restrict__ sbuf,
-                                                       const float *__restrict__ grows,
-                                                       const float *__restrict__ srows,
-                                                       float *__restrict__ acc, int P, int vrow0,
-                                                       const uint32_t *__restrict__ dirty) {
-    static_assert(D == 2 && D + Traits<FN, D>::S + CB <= 8, "sub-cell backward: D = 2, <= 8 gradient slots");
-    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
-    constexpr int RS = grow_stride<FN, D, CB>(), S = Traits<FN, D>::S, NV = D + S + CB;
-    __shared__ float slots[NV][kBwdSlots];
-    const Bins bins = resolve(gbuf, sbuf);
-    const int ncells = sload(&bins.h->ncells);
-    const int lane = threadIdx.x & (kWave - 1);
-    const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    for (int cb = block_unit_index(); cb < ncells; cb += gridDim.x) {
-        const int cell = cb;
-        const int gb = sload(&bins.cell_gbeg[cell]), ge = sload(&bins.cell_gend[cell]);
-        const int be = sload(&bins.cell_bend[cell]);
-        const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
-        if (be <= gb || se <= sb) continue;  // (workgroup-uniform)
-        int Bd[kSubPerCell + 1];
-        sub_bounds(bins, cell, sb, se, Bd);
-        const int ns = min(ge - gb, kBwdSlots);
-        for (int q = threadIdx.x; q < ns; q += kBlock)
-#pragma unroll
-            for (int k = 0; k < NV; ++k) slots[k][q] = 0.0f;
-        __syncthreads();
-        for (int eb = gb + w * kWave; eb < be; eb += kBlock) {
-            const int ee = min(eb + kWave, be);
-            const int kk = min(eb + lane, ee - 1);  // (padding lanes: the unit's last entry)
-            const uint32_t ent = bins.bwd_ent[kk], aux = bins.bwd_aux[kk];
-            const bool active = eb + lane < ee;
-            uint32_t U = 0u;
-#pragma unroll
-            for (int k = 0; k < kSubPerCell; ++k)
-                if (__ballot(active && ((aux >> (16 + k)) & 1u))) U |= 1u << k;
-            const SRanges rg = sub_ranges(Bd, U);
-            float r[RS];
-            load_grow<RS>(grows, ent, r);
-            float sm[2], sc[3], sv[CB];
-            bwd_unit<FN, D, CB>(bins, srows, cell, rg, active, ent, r, bins.gcon[ent & kIdMask], sm, sc, sv);
-            const int pos = (int)(aux & 0xffffu);
-            if (active) {
-                if (pos < kBwdSlots) {
-#pragma unroll
-                    for (int d = 0; d < D; ++d) slots[d][pos] = sm[d];
-#pragma unroll
-                    for (int k = 0; k < S; ++k) slots[D + k][pos] = sc[k];
-#pragma unroll
-                    for (int ch = 0; ch < CB; ++ch) slots[D + S + ch][pos] = sv[ch];
-                } else {
-                    bwd_flush_global<FN, D, CB>(acc, P, vrow0, ent & kIdMask, sm, sc, sv);
-                }
-            }
-        }
-        __syncthreads();
-        for (int q = threadIdx.x; q < ns; q += kBlock) {  // cell-list order: the entries' id runs
-            float x[NV];
-            bool any = false;
-#pragma unroll
-            for (int k = 0; k < NV; ++k) {
-                x[k] = slots[k][q];
-                any = any || x[k] != 0.0f;
-            }
-            if (!any || (DGS_BWD_NOATOM && __float_as_uint(x[0] + x[2]) != 0x7f800001u)) continue;
-            const int64_t id = bins.entries[gb + q] & kIdMask;
-#pragma unroll
-            for (int k = 0; k < D + S; ++k) atomicAdd(acc + (int64_t)k * P + id, x[k]);
-#pragma unroll
-            for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, x[D + S + ch]);
-        }
-        __syncthreads();
+        bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane);
     }
 }
 
@@ -1551,14 +1414,7 @@ static int run_backward(const Call &a) {
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s);
-            if constexpr (D == 2 && D + S + CB <= 8) {  // one workgroup per cell (grid-strided past 2^20 cells)
-                UnitHint h;
-                const int64_t ncells = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &h) ? h.ncells : 65536;
-                const unsigned nb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ncells, 1 << 20));
-                k_backward_c<FN, D, CB><<<nb, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
-            } else {
-                k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
-            }
+            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
