@@ -442,7 +442,8 @@ struct Geom {
     int D, T, n, CT, ncells;
     int grid[2];
     float off[2];
-    double fs;  // fine cell size = 0.51f / n
+    double fs;   // fine cell size = 0.51f / n
+    double ifs;  // 1 / fs (the binning's cell indices multiply by it: no fp64 divisions)
 };
 
 __device__ inline uint32_t sample_cell(const Geom &G, const float *s) {

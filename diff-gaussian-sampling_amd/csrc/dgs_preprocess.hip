@@ -222,7 +222,7 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         int h[2] = {0, 0};
         const int lim[2] = {home_w, home_h};
         for (int d = 0; d < D; ++d) {
-            const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
+            const double u = ((double)m[d] - (double)G.off[d]) * G.ifs;
             int v = (u == u) ? (int)floor(fmin(fmax(u, -1.0), (double)lim[d])) : 0;
             h[d] = v < 0 ? 0 : (v >= lim[d] ? lim[d] - 1 : v);
         }
@@ -314,8 +314,8 @@ __device__ inline bool axis_setup(const Geom &G, const Cut &k, int d, int tcd, i
     ks = (int)klo;  // e < 0.5 and a tile narrower than 1: at most one k
     const double dl = k.md[d] - 2.0 * klo - k.e[d] - k.epsx[d];
     const double dh = k.md[d] - 2.0 * klo + k.e[d] + k.epsx[d];
-    const int lo = (int)floor(fmax((dl - o) / G.fs - kCellSlack, -1.0));
-    const int hi = (int)floor(fmin((dh - o) / G.fs + kCellSlack, (double)G.n));
+    const int lo = (int)floor(fmax((dl - o) * G.ifs - kCellSlack, -1.0));
+    const int hi = (int)floor(fmin((dh - o) * G.ifs + kCellSlack, (double)G.n));
     flo = lo < 0 ? 0 : lo;
     fhi = hi > G.n - 1 ? G.n - 1 : hi;
     return flo <= fhi;
@@ -356,8 +356,8 @@ __device__ inline void row_cols(const Geom &G, const Cut &k, int tc0, int ks0, d
     const double o0 = tc0 * (double)kTile;
     const double A = k.md[0] - o0 - slack - k.epsx[0] - 2.0 * ks0;
     const double B = k.md[0] - o0 + slack + k.epsx[0] - 2.0 * ks0;
-    const double fa = ceil((A - (xu + tol)) / G.fs - 1.0 - 1e-9);
-    const double fb2 = floor((B - (xl - tol)) / G.fs + 1e-9);
+    const double fa = ceil((A - (xu + tol)) * G.ifs - 1.0 - 1e-9);
+    const double fb2 = floor((B - (xl - tol)) * G.ifs + 1e-9);
     if (fa > (double)fxl) fxl = fa > (double)G.n ? G.n : (int)fa;
     if (fb2 < (double)fxh) fxh = fb2 < -1.0 ? -1 : (int)fb2;
 }
@@ -384,9 +384,9 @@ __device__ inline int gather_reach(const Geom &G, const float *m, float r, const
     const int lim[2] = {G.grid[0] * G.n, G.grid[1] * G.n};
     int reach = 0;
     for (int d = 0; d < 2; ++d) {
-        const double u = ((double)m[d] - (double)G.off[d]) / G.fs;
+        const double u = ((double)m[d] - (double)G.off[d]) * G.ifs;
         if (!(u >= 0.0 && u < (double)lim[d])) return 0;  // (the home cell is clamped)
-        reach = max(reach, (int)ceil(k.e[d] / G.fs + 2.0));
+        reach = max(reach, (int)ceil(k.e[d] * G.ifs + 2.0));
     }
     return reach <= kGatherReach ? reach : 0;
 }
@@ -486,7 +486,7 @@ __device__ inline bool local_rows(const Geom &G, const float *m, float r, const 
     // match enumerate_fine bit for bit (it skips exactly these visits and emits all others); the
     // margins of the cut cover the rounding either way.
     const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
-    const double BS = (double)kTile, slack = kCellSlack * G.fs, ifs = 1.0 / G.fs;
+    const double BS = (double)kTile, slack = kCellSlack * G.fs, ifs = G.ifs;
     // (widened by a cell: every tile axis_setup can give a cell is among them)
     const double wx = k.e[0] + slack + k.epsx[0] + G.fs;
     const int ta = max(max(kr.x0, 0), (int)floor((k.md[0] - wx) / BS));
@@ -612,7 +612,7 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
             const Cut k = gauss_cut(G, m, c);
             reach = gather_reach(G, m, r, c, k);
             if (reach > 0) {
-                const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) / G.fs);
+                const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) * G.ifs);
                 if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
             }
             enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, (uint32_t)i,
@@ -929,12 +929,15 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                         sh[1] = wrap_shift_f(mm.y - ctr[1]);
                     }
                     const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
-                    const float ic0 = 1.0f / cc.x, ic2 = 1.0f / cc.z;
+                    // (approximate reciprocals: they only place the edge minima, which are then
+                    // evaluated exactly at feasible points; rounding margins from the cell box,
+                    // which holds every sub-cell box)
+                    const float ic0 = __builtin_amdgcn_rcpf(cc.x), ic2 = __builtin_amdgcn_rcpf(cc.z);
+                    const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(bx.x), fabsf(bx.z)));
+                    const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(bx.y), fabsf(bx.w)));
                     for (int k = 0; k < kSubPerCell; ++k) {
                         const float4 q = sb[k];
                         if (!(q.x <= q.z)) continue;  // empty sub-cell
-                        const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(q.x), fabsf(q.z)));
-                        const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(q.y), fabsf(q.w)));
                         if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y,
                                                cc.z, ic0, ic2, qc))
                             mask |= 1u << k;
@@ -1398,6 +1401,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     if (ncells64 >= (1LL << 30)) return fail(DGS_ERR_ARG, "too many fine cells");
     G.ncells = (int)ncells64;
     G.fs = (double)kTile / G.n;
+    G.ifs = 1.0 / G.fs;
     const int ncells = G.ncells;
     const int home_w = G.grid[0] * G.n, home_h = D == 2 ? G.grid[1] * G.n : 1;
 
