@@ -45,7 +45,10 @@ constexpr int kFwdUnit = kWave;
 // backward keeps the cell lists: their one flush per (cell, Gaussian), in ascending-id runs, is
 // what the float atomics allow.
 constexpr int kSubPerCell = 4;
-constexpr int kSubPairs = 24;
+#ifndef DGS_SUB_PAIRS
+#define DGS_SUB_PAIRS 24
+#endif
+constexpr int kSubPairs = DGS_SUB_PAIRS;
 constexpr int kBlock = 256;
 constexpr int kWavesPerBlock = kBlock / kWave;
 
