@@ -233,7 +233,9 @@ def bench_sample(args, world, rank, dev, torch, dist):
         # domains alternate (interior / boundary points); inputs generated before the clock starts
         med = lambda xs: sorted(xs)[len(xs) // 2]  # noqa: E731
         fresh = [torch.rand(N, D, device=dev) * 2.0 - 1.0 for _ in range(args.pre_reps + 1)]
-        other = samples + 0.25  # a second domain of the same density (another grid offset)
+        # a second sampler's points: an independent draw over the same domain (another grid
+        # offset, the same density and binning cost)
+        other = torch.rand(N, D, device=dev, generator=torch.Generator(device=dev).manual_seed(77)) * 2.0 - 1.0
         pats = {"preprocess_resampled_ms": [fresh[i] for i in range(args.pre_reps + 1)],
                 "preprocess_alternating_ms": [samples if i % 2 == 0 else other for i in range(2 * args.pre_reps + 2)]}
         for key, seq in pats.items():
