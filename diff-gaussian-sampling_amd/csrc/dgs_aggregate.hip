@@ -439,6 +439,8 @@ struct AggArgs {
     float *arows;                           // backward scratch: a of every row [P][L]
     float *dfeat, *dq, *dkeys, *dfreq, *ddt;
     const int32_t *order;  // optional row order (spatial, from dgs_agg_preprocess); NULL = 0..P-1
+    float *strows;         // transposed backward (dgs_agg_backward_tr): st = transform dL of every row [P][L]
+    float4 *ct;            // ... and per slot (c, te, row as int bits, 0) for the per-row gather
     int expt;              // profiling experiments (DGS_AGG_EXPT): bit 0 skips the scatter, bit 1 the
                            // distance-transform terms -- results are then wrong; 0 in production
 };
@@ -965,7 +967,10 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
 // Backward, L and K <= 64 (NB = max(L, K) rounded up).  Per-wave LDS: the staged rows, the
 // batch's (neighbour, dcw * fac, te), st[64], and the shared-array partials: every value is
 // first summed over the lane quartet (l, l^16, l^32, l^48) and kept by lanes 0..15 (NV x 16).
-template <int NB, bool COMBO, bool PIPE>
+// TR (dgs_agg_backward_tr): instead of scattering the neighbours' feature / key gradients with
+// float atomics, every slot's two factors (c, te) and its row go to A.ct in slot order (16-byte
+// coalesced stores) and every row's st to A.strows; k_agg_tgather then sums them per neighbour.
+template <int NB, bool COMBO, bool PIPE, bool TR>
 __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G) {
     extern __shared__ float lds[];
     const int lane = threadIdx.x & (kWave - 1);
@@ -1011,6 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             float v = 0.0f;
             for (int k = 0; k < L; ++k) v += A.transform[lane * L + k] * g[k];
             st[lane] = v;
+            if constexpr (TR) A.strows[(int64_t)i * L + lane] = v;
         }
         // this lane's factor in the scatter: st[t] for a feature lane, q[t - L] for a key lane
         wave_sync_lds();
@@ -1137,7 +1143,9 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             }
             // neighbour gradients (aggregate_neighbors.cu:296-319), a whole neighbour row
             // (dfeat row, then dkeys row) per G2 lanes of one atomic instruction
-            if (!(A.expt & 1)) {
+            if constexpr (TR) {
+                if (s < end) A.ct[s] = make_float4(c, te, __int_as_float(i), 0.0f);
+            } else if (!(A.expt & 1)) {
                 sc[lane] = c;
                 ste[lane] = te;
                 wave_sync_lds();
@@ -1219,6 +1227,98 @@ __global__ __launch_bounds__(kBlock) void k_agg_dtrans(int P, int L, const float
         float acc = 0.0f;
         for (int64_t i = r0; i < r1; ++i) acc += arows[i * L + j] * dL[i * L + k];
         atomicAdd(&dtrans[e], acc);
+    }
+}
+
+// Transposition keys: slot s names neighbour j = indices[s] (P for index -1: sorted last, in
+// no row's range); value s.
+__global__ void k_agg_tkeys(int64_t n, int P, const int64_t *__restrict__ indices, uint32_t *__restrict__ keys,
+                            uint32_t *__restrict__ vals) {
+    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= n) return;
+    const int64_t j = indices[s];
+    keys[s] = (j >= 0 && j < P) ? (uint32_t)j : (uint32_t)P;
+    vals[s] = (uint32_t)s;
+}
+
+// tstart[j] = first sorted position whose key is >= j, j in [0, P] (int32: length < 2^31).
+__global__ void k_agg_tstart(int P, int64_t n, const uint32_t *__restrict__ keys, int32_t *__restrict__ tstart) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j > P) return;
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if (keys[mid] < (uint32_t)j) lo = mid + 1;
+        else hi = mid;
+    }
+    tstart[j] = (int32_t)lo;
+}
+
+// Per-neighbour sum of the feature / key gradients (the transposed form of
+// aggregate_neighbors.cu:303 and 315): for row j, over its incoming slots (i -> j) in slot order,
+//   dL/dfeatures[j] = sum c * st_i,   dL/dkeys[j] = sum te * q_i
+// (c = dcw * factor, te = sum over the features of summed_transform * embedded, both from the slot's
+// row pass).  One wave per row (spatial order: the rows i of neighbouring j share L2), GR lanes per
+// slot (L + K <= GR: feature lanes, then key lanes), 64 / GR slots per step; a batch's 64 slot
+// records are staged in LDS while the next batch's load.  No atomics: each gradient row is
+// written once, in a fixed order.
+template <int GR>
+__global__ __launch_bounds__(kBlock) void k_agg_tgather(int P, int L, int K, const int32_t *__restrict__ tstart,
+                                                        const uint32_t *__restrict__ tslot,
+                                                        const float4 *__restrict__ ct,
+                                                        const float *__restrict__ strows,
+                                                        const float *__restrict__ queries,
+                                                        const int32_t *__restrict__ order, float *__restrict__ dfeat,
+                                                        float *__restrict__ dkeys) {
+    constexpr int SPP = kWave / GR;
+    __shared__ float4 srec[kWavesPerBlock][kWave];
+    const int lane = threadIdx.x & (kWave - 1);
+    float4 *rec = srec[threadIdx.x >> 6];
+    const int sub = lane / GR, t = lane - sub * GR;
+    const bool fl = t < L, kl = !fl && t < L + K;
+    const int stride = gridDim.x * kWavesPerBlock;
+    for (int w = wave_unit_index(P); w < P; w += stride) {
+        const int j = order ? order[w] : w;
+        const int kb = tstart[j], ke = tstart[j + 1];
+        float acc = 0.0f;
+        float4 nxt = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (kb + lane < ke) nxt = ct[tslot[kb + lane]];
+        for (int k0 = kb; k0 < ke; k0 += kWave) {
+            const int nb = min(kWave, ke - k0);
+            rec[lane] = nxt;
+            wave_sync_lds();
+            if (k0 + kWave + lane < ke) nxt = ct[tslot[k0 + kWave + lane]];  // next batch in flight
+            int b = 0;
+            for (; b + 8 * SPP <= nb; b += 8 * SPP) {
+                float4 e[8];
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) e[u] = rec[b + u * SPP + sub];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int64_t i = __float_as_int(e[u].z);
+                    v[u] = fl ? strows[i * L + t] : (kl ? queries[i * K + (t - L)] : 0.0f);
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc = fmaf(fl ? e[u].x : e[u].y, v[u], acc);
+            }
+            for (; b < nb; b += SPP) {
+                const int sl = b + sub;
+                if (sl < nb) {
+                    const float4 e = rec[sl];
+                    const int64_t i = __float_as_int(e.z);
+                    const float v = fl ? strows[i * L + t] : (kl ? queries[i * K + (t - L)] : 0.0f);
+                    acc = fmaf(fl ? e.x : e.y, v, acc);
+                }
+            }
+            wave_sync_lds();
+        }
+        if constexpr (SPP >= 4) acc += __shfl_xor(acc, 16);
+        if constexpr (SPP >= 2) acc += __shfl_xor(acc, 32);
+        if (sub == 0) {
+            if (fl) dfeat[(int64_t)j * L + t] = acc;
+            else if (kl) dkeys[(int64_t)j * K + (t - L)] = acc;
+        }
     }
 }
 
@@ -1383,18 +1483,23 @@ extern "C" int dgs_agg_forward(int P, int D, int L, int K, int E, const float *f
     return DGS_OK;
 }
 
-extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features, const float *transform,
-                                const float *queries, const float *keys, const float *frequencies,
-                                const float *distance_transform, const int64_t *indices, const int64_t *ranges,
-                                const float *dists, const float *densities, const float *weights,
-                                const float *embeddings, const float *factors, const float *inv_total,
-                                const int32_t *row_order, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
-                                float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
-                                void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
+static int agg_backward_impl(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                             const float *queries, const float *keys, const float *frequencies,
+                             const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                             const float *dists, const float *densities, const float *weights,
+                             const float *embeddings, const float *factors, const float *inv_total,
+                             const int32_t *row_order, const int32_t *tstart, const uint32_t *tslot, int64_t length,
+                             const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                             float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
+                             void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
     int rc = agg_check(P, D, L, K, E);
     if (rc) return rc;
-    if (workspace_bytes < dgs_agg_workspace_size(P, L) || (!workspace && P > 0))
+    const bool tr = tstart != nullptr;
+    const size_t need = tr ? dgs_agg_workspace_size_tr(P, L, length) : dgs_agg_workspace_size(P, L);
+    if (workspace_bytes < need || (!workspace && P > 0))
         return fail(DGS_ERR_ARG, "dgs_agg_backward: workspace smaller than dgs_agg_workspace_size");
+    if (tr && (L + K > kWave || !tslot || length < 0 || length >= ((int64_t)1 << 31)))
+        return fail(DGS_ERR_ARG, "dgs_agg_backward_tr: needs L + K <= 64, tslot and 0 <= length < 2^31");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int F = (E - 1) / D / 2;
     const int NV = 2 * E + F;
@@ -1405,10 +1510,12 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     const bool pipe = staged && L <= 16 && K <= 16 && G.vf && G.vk && !std::getenv("DGS_AGG_NOPIPE");
     if (lds > 160 * 1024) return fail(DGS_ERR_ARG, "aggregate backward: distance_transform too long for LDS");
     auto zero = [&](float *p, size_t n) { return n ? hipMemsetAsync(p, 0, sizeof(float) * n, s) : hipSuccess; };
-    DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
+    if (!tr) {  // (the transposed path writes every row of these)
+        DGS_TRY_HIP(zero(dL_dfeatures, (size_t)P * L));
+        DGS_TRY_HIP(zero(dL_dkeys, (size_t)P * K));
+    }
     DGS_TRY_HIP(zero(dL_dtransform, (size_t)L * L));
     DGS_TRY_HIP(zero(dL_dqueries, (size_t)P * K));
-    DGS_TRY_HIP(zero(dL_dkeys, (size_t)P * K));
     DGS_TRY_HIP(zero(dL_dfrequencies, (size_t)F));
     DGS_TRY_HIP(zero(dL_ddistance_transform, 2 * (size_t)E));
     if (P == 0) return DGS_OK;
@@ -1422,22 +1529,33 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
     A.dL = dL_dout, A.arows = static_cast<float *>(workspace);
     A.dfeat = dL_dfeatures, A.dq = dL_dqueries, A.dkeys = dL_dkeys, A.dfreq = dL_dfrequencies;
     A.ddt = dL_ddistance_transform, A.order = row_order;
+    if (tr) {
+        A.strows = A.arows + (size_t)P * L;
+        const size_t ct_off = ((sizeof(float) * 2 * (size_t)P * L + 15) / 16) * 16;
+        A.ct = reinterpret_cast<float4 *>(static_cast<char *>(workspace) + ct_off);
+    }
     if (const char *e = getenv("DGS_AGG_EXPT")) A.expt = atoi(e);
     // few enough waves that each flushes its shared-array partials after many rows
     const unsigned nb = std::min(agg_row_blocks(P), 2048u);
     if (staged) {
         const bool combo = D * F <= kWave;
+#define DGS_AGG_BWD(NB_, CO_, PI_)                                                  \
+    do {                                                                            \
+        if (tr) k_agg_backward_s<NB_, CO_, PI_, true><<<nb, kBlock, lds, s>>>(A, G);  \
+        else k_agg_backward_s<NB_, CO_, PI_, false><<<nb, kBlock, lds, s>>>(A, G);    \
+    } while (0)
         switch (agg_nb(std::max(std::max(L, K), 1)) * 2 + (combo ? 1 : 0)) {
         case 33:
-            if (pipe) k_agg_backward_s<16, true, true><<<nb, kBlock, lds, s>>>(A, G);
-            else k_agg_backward_s<16, true, false><<<nb, kBlock, lds, s>>>(A, G);
+            if (pipe) DGS_AGG_BWD(16, true, true);
+            else DGS_AGG_BWD(16, true, false);
             break;
-        case 32: k_agg_backward_s<16, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 65: k_agg_backward_s<32, true, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 64: k_agg_backward_s<32, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        case 129: k_agg_backward_s<64, true, false><<<nb, kBlock, lds, s>>>(A, G); break;
-        default: k_agg_backward_s<64, false, false><<<nb, kBlock, lds, s>>>(A, G); break;
+        case 32: DGS_AGG_BWD(16, false, false); break;
+        case 65: DGS_AGG_BWD(32, true, false); break;
+        case 64: DGS_AGG_BWD(32, false, false); break;
+        case 129: DGS_AGG_BWD(64, true, false); break;
+        default: DGS_AGG_BWD(64, false, false); break;
         }
+#undef DGS_AGG_BWD
     } else {
         switch (agg_nb(std::min(std::max(std::max(L, K), 1), 64))) {
         case 16: k_agg_backward<16><<<nb, kBlock, lds, s>>>(A); break;
@@ -1446,10 +1564,89 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
         }
     }
     DGS_LAUNCH_CHECK(s, debug);
+    if (tr && L + K > 0) {
+        const unsigned gb = agg_row_blocks(P);
+        const int gr = L + K <= 16 ? 16 : (L + K <= 32 ? 32 : 64);
+        if (gr == 16)
+            k_agg_tgather<16><<<gb, kBlock, 0, s>>>(P, L, K, tstart, tslot, A.ct, A.strows, queries, row_order,
+                                                    dL_dfeatures, dL_dkeys);
+        else if (gr == 32)
+            k_agg_tgather<32><<<gb, kBlock, 0, s>>>(P, L, K, tstart, tslot, A.ct, A.strows, queries, row_order,
+                                                    dL_dfeatures, dL_dkeys);
+        else
+            k_agg_tgather<64><<<gb, kBlock, 0, s>>>(P, L, K, tstart, tslot, A.ct, A.strows, queries, row_order,
+                                                    dL_dfeatures, dL_dkeys);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     if (L > 0) {
         const unsigned tb = (unsigned)std::max<int64_t>(1, std::min<int64_t>(2048, ((int64_t)P + 255) / 256));
         k_agg_dtrans<<<tb, kBlock, 0, s>>>(P, L, A.arows, dL_dout, dL_dtransform);
         DGS_LAUNCH_CHECK(s, debug);
     }
+    return DGS_OK;
+}
+
+extern "C" size_t dgs_agg_workspace_size_tr(int P, int L, int64_t length) {
+    const size_t rows = ((sizeof(float) * 2 * (size_t)std::max(P, 0) * std::max(L, 0) + 15) / 16) * 16;
+    return rows + 16 * (size_t)std::max<int64_t>(length, 0) + 256;
+}
+
+extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                                const float *queries, const float *keys, const float *frequencies,
+                                const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                                const float *dists, const float *densities, const float *weights,
+                                const float *embeddings, const float *factors, const float *inv_total,
+                                const int32_t *row_order, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                                float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
+                                void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
+    return agg_backward_impl(P, D, L, K, E, features, transform, queries, keys, frequencies, distance_transform,
+                             indices, ranges, dists, densities, weights, embeddings, factors, inv_total, row_order,
+                             nullptr, nullptr, 0, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
+                             dL_dfrequencies, dL_ddistance_transform, workspace, workspace_bytes, stream, debug);
+}
+
+extern "C" int dgs_agg_backward_tr(int P, int D, int L, int K, int E, const float *features, const float *transform,
+                                   const float *queries, const float *keys, const float *frequencies,
+                                   const float *distance_transform, const int64_t *indices, const int64_t *ranges,
+                                   const float *dists, const float *densities, const float *weights,
+                                   const float *embeddings, const float *factors, const float *inv_total,
+                                   const int32_t *row_order, const int32_t *tstart, const uint32_t *tslot,
+                                   int64_t length, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform,
+                                   float *dL_dqueries, float *dL_dkeys, float *dL_dfrequencies,
+                                   float *dL_ddistance_transform, void *workspace, size_t workspace_bytes,
+                                   dgs_stream_t stream, int debug) {
+    if (!tstart) return fail(DGS_ERR_ARG, "dgs_agg_backward_tr: tstart is NULL");
+    return agg_backward_impl(P, D, L, K, E, features, transform, queries, keys, frequencies, distance_transform,
+                             indices, ranges, dists, densities, weights, embeddings, factors, inv_total, row_order,
+                             tstart, tslot, length, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
+                             dL_dfrequencies, dL_ddistance_transform, workspace, workspace_bytes, stream, debug);
+}
+
+extern "C" int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, int32_t *tstart, uint32_t *tslot,
+                                 dgs_alloc_fn alloc, void *alloc_ctx, dgs_stream_t stream, int debug) {
+    if (P < 0 || length < 0 || length >= ((int64_t)1 << 31) || !tstart || (!tslot && length > 0) || !alloc)
+        return fail(DGS_ERR_ARG, "dgs_agg_transpose: bad arguments (length must be < 2^31)");
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (length == 0) {
+        DGS_TRY_HIP(hipMemsetAsync(tstart, 0, sizeof(int32_t) * ((size_t)P + 1), s));
+        return DGS_OK;
+    }
+    auto scratch = [&](size_t n) { return alloc(alloc_ctx, DGS_BUF_SCRATCH, std::max<size_t>(n, 16)); };
+    uint32_t *keys = static_cast<uint32_t *>(scratch(4 * (size_t)length));
+    uint32_t *keys_s = static_cast<uint32_t *>(scratch(4 * (size_t)length));
+    uint32_t *vals = static_cast<uint32_t *>(scratch(4 * (size_t)length));
+    if (!keys || !keys_s || !vals) return fail(DGS_ERR_ALLOC, "dgs_agg_transpose: scratch allocation failed");
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) <= (unsigned long long)P) ++bits;
+    size_t tb = 0;
+    DGS_TRY_HIP(onesweep_pairs<uint32_t>(nullptr, tb, keys, keys_s, vals, tslot, (size_t)length, 0u, (unsigned)bits, s));
+    void *tmp = scratch(tb);
+    if (!tmp) return fail(DGS_ERR_ALLOC, "dgs_agg_transpose: scratch allocation failed");
+    k_agg_tkeys<<<agg_elem_blocks(length), kBlock, 0, s>>>(length, P, indices, keys, vals);
+    DGS_LAUNCH_CHECK(s, debug);
+    DGS_TRY_HIP(onesweep_pairs<uint32_t>(tmp, tb, keys, keys_s, vals, tslot, (size_t)length, 0u, (unsigned)bits, s));
+    DGS_LAUNCH_CHECK(s, debug);
+    k_agg_tstart<<<agg_elem_blocks((int64_t)P + 1), kBlock, 0, s>>>(P, length, keys_s, tstart);
+    DGS_LAUNCH_CHECK(s, debug);
     return DGS_OK;
 }

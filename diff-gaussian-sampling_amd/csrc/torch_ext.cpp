@@ -391,35 +391,72 @@ std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_
 
 // ---- neighbour aggregation (aggregate_neighbors.h:11-47) --------------------------------
 
-// Spatial row order of the last few preprocess_aggregate calls, keyed by the indices buffer
-// they returned.  Only a scheduling hint (any permutation of 0..P-1 gives identical results),
-// so a stale entry whose key was reused by another tensor of the same P costs speed at most.
-struct OrderEntry {
+// Per preprocess_aggregate call: the spatial row order (a scheduling hint: any permutation of
+// 0..P-1 gives identical results, so a stale entry whose key was reused by another tensor of the
+// same P costs speed at most) and the transposed lists of dgs_agg_transpose (results depend on
+// them: used only while the very indices tensor they were built from is alive and unmodified --
+// a weak reference to it and its version counter).
+using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+struct AggEntry {
     const void *indices;
     int64_t P, length;
     Tensor order;
+    WeakImpl impl;
+    int64_t version;
+    Tensor tstart, tslot;  // undefined: not built
 };
-std::mutex g_order_mu;
-std::vector<OrderEntry> g_orders;
+std::mutex g_agg_mu;
+std::vector<AggEntry> g_agg;
 
-void order_put(const Tensor &indices, int64_t P, const Tensor &order) {
-    std::lock_guard<std::mutex> lk(g_order_mu);
-    for (auto it = g_orders.begin(); it != g_orders.end(); ++it)
-        if (it->indices == indices.data_ptr()) {
-            g_orders.erase(it);
-            break;
-        }
-    g_orders.push_back({indices.data_ptr(), P, indices.numel(), order});
-    if (g_orders.size() > 4) g_orders.erase(g_orders.begin());
+void agg_put(const Tensor &indices, int64_t P, const Tensor &order, const Tensor &tstart, const Tensor &tslot) {
+    std::lock_guard<std::mutex> lk(g_agg_mu);
+    for (auto it = g_agg.begin(); it != g_agg.end();)
+        if (it->indices == indices.data_ptr() || it->impl.expired()) it = g_agg.erase(it);
+        else ++it;
+    g_agg.push_back({indices.data_ptr(), P, indices.numel(), order, WeakImpl(indices.getIntrusivePtr()),
+                     (int64_t)indices._version(), tstart, tslot});
+    if (g_agg.size() > 2) g_agg.erase(g_agg.begin());
 }
 
 const int32_t *order_get(const Tensor &indices, int64_t P) {
-    std::lock_guard<std::mutex> lk(g_order_mu);
-    for (const auto &e : g_orders)
+    std::lock_guard<std::mutex> lk(g_agg_mu);
+    for (const auto &e : g_agg)
         if (e.indices == indices.data_ptr() && e.P == P && e.length == indices.numel() &&
             e.order.device() == indices.device())
             return e.order.data_ptr<int32_t>();
     return nullptr;
+}
+
+// The transposed lists built from exactly this indices tensor (same object, not modified since).
+bool transpose_get(const Tensor &indices, int64_t P, Tensor &tstart, Tensor &tslot) {
+    std::lock_guard<std::mutex> lk(g_agg_mu);
+    for (const auto &e : g_agg) {
+        if (!e.tstart.defined() || e.P != P || e.length != indices.numel()) continue;
+        const auto sp = e.impl.lock();
+        if (sp.get() == indices.unsafeGetTensorImpl() && e.version == (int64_t)indices._version()) {
+            tstart = e.tstart;
+            tslot = e.tslot;
+            return true;
+        }
+    }
+    return false;
+}
+
+bool transpose_enabled() {
+    const char *e = std::getenv("DGS_AGG_TRANSPOSE");
+    return !(e && e[0] == '0');
+}
+
+// dgs_agg_transpose into fresh tensors.
+void build_transpose(const Tensor &indices, int64_t P, Tensor &tstart, Tensor &tslot, bool debug) {
+    const int64_t length = indices.numel();
+    tstart = torch::empty({P + 1}, indices.options().dtype(torch::kInt32));
+    tslot = torch::empty({std::max<int64_t>(length, 1)}, indices.options().dtype(torch::kInt32));
+    AllocCtx ctx{indices.device()};
+    check(dgs_agg_transpose((int)P, length, indices.data_ptr<int64_t>(), tstart.data_ptr<int32_t>(),
+                            reinterpret_cast<uint32_t *>(tslot.data_ptr<int32_t>()), alloc_cb, &ctx,
+                            as_dgs(cur_stream()), debug ? 1 : 0),
+          "preprocess_aggregate (transpose)");
 }
 
 Tensor i64(const Tensor &t, const char *name) {
@@ -454,7 +491,12 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessC
         return ctx.bufs[which].view(st).narrow(0, 0, length * (shape.size() > 1 ? shape[1] : 1)).view(shape);
     };
     Tensor indices = view(DGS_BUF_AGG_INDICES, torch::kInt64, {length});
-    if (length > 0) order_put(indices, P, order);
+    if (length > 0) {
+        // the transposed lists for the backward's per-row gather (dgs_agg_backward_tr)
+        Tensor tstart, tslot;
+        if (transpose_enabled() && length < ((int64_t)1 << 31)) build_transpose(indices, P, tstart, tslot, debug);
+        agg_put(indices, P, order, tstart, tslot);
+    }
     return std::make_tuple(indices, ranges, view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
                            view(DGS_BUF_AGG_DENSITIES, torch::kFloat32, {length}), inv_total);
 }
@@ -526,6 +568,27 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
     Tensor dkeys = torch::zeros(a.keys.sizes(), a.features.options());
     Tensor dfreq = torch::zeros(a.freq.sizes(), a.features.options());
     Tensor ddt = torch::zeros(a.dt.sizes(), a.features.options());
+    const int64_t length = a.indices.numel();
+    Tensor tstart, tslot;
+    const bool tr = a.P > 0 && a.L + a.K <= 64 && length < ((int64_t)1 << 31) && transpose_enabled();
+    if (tr && !transpose_get(a.indices, a.P, tstart, tslot))  // indices not from preprocess_aggregate
+        build_transpose(a.indices, a.P, tstart, tslot, debug);
+    if (tr) {
+        const size_t ws = dgs_agg_workspace_size_tr(a.P, a.L, length);
+        Tensor work = torch::empty({(int64_t)ws}, a.features.options().dtype(torch::kUInt8));
+        check(dgs_agg_backward_tr(a.P, a.D, a.L, a.K, a.E, a.features.data_ptr<float>(), a.transform.data_ptr<float>(),
+                                  a.queries.data_ptr<float>(), a.keys.data_ptr<float>(), a.freq.data_ptr<float>(),
+                                  a.dt.data_ptr<float>(), a.indices.data_ptr<int64_t>(), a.ranges.data_ptr<int64_t>(),
+                                  a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), weights.data_ptr<float>(),
+                                  embeddings.data_ptr<float>(), factors.data_ptr<float>(), a.inv_total.data_ptr<float>(),
+                                  order_get(a.indices, a.P), tstart.data_ptr<int32_t>(),
+                                  reinterpret_cast<const uint32_t *>(tslot.data_ptr<int32_t>()), length,
+                                  dL.data_ptr<float>(), dfeat.data_ptr<float>(), dtrans.data_ptr<float>(),
+                                  dq.data_ptr<float>(), dkeys.data_ptr<float>(), dfreq.data_ptr<float>(),
+                                  ddt.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),
+              "aggregate_neighbors_backward");
+        return std::make_tuple(dfeat, dtrans, dq, dkeys, dfreq, ddt);
+    }
     const size_t ws = dgs_agg_workspace_size(a.P, a.L);
     Tensor work = torch::empty({(int64_t)ws}, a.features.options().dtype(torch::kUInt8));
     check(dgs_agg_backward(a.P, a.D, a.L, a.K, a.E, a.features.data_ptr<float>(), a.transform.data_ptr<float>(),

@@ -209,3 +209,63 @@ def test_aggregate_many_frequencies(dgs, oracle):
     distance-transform gradients."""
     means, conics, radii, fe = agg_problem(P=300, D=2, L=8, K=8, F=33, seed=99)
     _run(dgs, oracle, means, conics, radii, fe)
+
+
+def _bwd(dgs, fe, pre, fwd, g, env, monkeypatch):
+    monkeypatch.setenv("DGS_AGG_TRANSPOSE", env)
+    idx, rg, X, dn, inv = pre
+    t = [_cuda(fe[k]) for k in AGG_FEATURES]
+    return dgs._C.aggregate_neighbors_backward(*t, idx, rg, X, dn, *fwd[:3], inv, g, False)
+
+
+@pytest.mark.parametrize("L,K", [(16, 16), (8, 4), (40, 20), (6, 5)])
+def test_aggregate_transposed_backward(dgs, oracle, monkeypatch, L, K):
+    """The feature / key gradients as a per-neighbour gather over the transposed lists
+    (dgs_agg_transpose + dgs_agg_backward_tr, the default for L + K <= 64) against the float-atomic
+    scatter of the reference's form (DGS_AGG_TRANSPOSE=0) and the oracle's exact sums; the gather
+    sums in slot order, so two calls agree bit for bit."""
+    means, conics, radii, fe = agg_problem(P=1200, D=2, L=L, K=K, F=4, seed=110 + L, spread=0.5,
+                                           radius=(0.6, 1.0))
+    pre = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    t = [_cuda(fe[k]) for k in AGG_FEATURES]
+    fwd = dgs._C.aggregate_neighbors(*t, *pre[:4], pre[4], False)
+    g = _cuda(np.random.default_rng(7).normal(size=(1200, L)).astype(np.float32))
+    tr1 = _bwd(dgs, fe, pre, fwd, g, "1", monkeypatch)
+    tr2 = _bwd(dgs, fe, pre, fwd, g, "1", monkeypatch)
+    at = _bwd(dgs, fe, pre, fwd, g, "0", monkeypatch)
+    for name, a, b, c in zip(AGG_FEATURES, tr1, tr2, at):
+        if name in ("features", "keys"):
+            assert torch.equal(a, b), f"d/d{name}: transposed backward not repeatable"
+        close(a.cpu().numpy(), c.cpu().numpy(), 1e-5, 1e-5, f"d/d{name} transposed vs atomic")
+    args = [fe[k] for k in AGG_FEATURES]
+    idx_r, rg_r, X_r, dn_r, inv_r = oracle.agg_preprocess(means, conics, radii)
+    w_r, e_r, f_r, _ = oracle.agg_forward(*args, idx_r, rg_r, X_r, dn_r, inv_r)
+    ref = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g.cpu().numpy(), exact=True)
+    for name, a, b in zip(AGG_FEATURES, tr1, ref):
+        if name in ("features", "keys"):
+            close(a.cpu().numpy().reshape(b.shape), b, 1e-5, 1e-5, f"d/d{name}")
+
+
+def test_aggregate_transposed_lists_follow_the_indices(dgs, oracle):
+    """The transposed lists are cached per preprocess_aggregate result; indices changed in place
+    afterwards (or passed as another tensor) must not reuse them: slots set to -1 here must drop
+    out of the neighbours' gradients exactly as in the oracle given the same indices."""
+    means, conics, radii, fe = agg_problem(P=800, D=2, L=16, K=16, F=4, seed=120)
+    idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
+    t = [_cuda(fe[k]) for k in AGG_FEATURES]
+    fwd = dgs._C.aggregate_neighbors(*t, idx, rg, X, dn, inv, False)
+    g = np.random.default_rng(11).normal(size=(800, 16)).astype(np.float32)
+    dgs._C.aggregate_neighbors_backward(*t, idx, rg, X, dn, *fwd[:3], inv, _cuda(g), False)  # cache used
+    drop = torch.arange(0, idx.numel(), 7, device=idx.device)
+    idx[drop] = -1  # in place: the tensor's version moves on
+    got = dgs._C.aggregate_neighbors_backward(*t, idx, rg, X, dn, *fwd[:3], inv, _cuda(g), False)
+    got2 = dgs._C.aggregate_neighbors_backward(*t, idx.clone(), rg, X, dn, *fwd[:3], inv, _cuda(g), False)
+    args = [fe[k] for k in AGG_FEATURES]
+    idx_r = idx.cpu().numpy()
+    w, e, f = (x.cpu().numpy() for x in fwd[:3])
+    ref = oracle.agg_backward(*args, idx_r, rg.cpu().numpy(), X.cpu().numpy(), dn.cpu().numpy(), w, e, f,
+                              inv.cpu().numpy(), g, exact=True)
+    for name, a, a2, b in zip(AGG_FEATURES, got, got2, ref):
+        if name in ("features", "keys"):
+            close(a.cpu().numpy().reshape(b.shape), b, 1e-5, 1e-5, f"d/d{name} after the in-place change")
+            assert torch.equal(a, a2), f"d/d{name}: clone vs in-place tensor"
