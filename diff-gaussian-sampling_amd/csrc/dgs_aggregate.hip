@@ -440,7 +440,8 @@ struct AggArgs {
     float *dfeat, *dq, *dkeys, *dfreq, *ddt;
     const int32_t *order;  // optional row order (spatial, from dgs_agg_preprocess); NULL = 0..P-1
     float *strows;         // transposed backward (dgs_agg_backward_tr): st = transform dL of every row [P][L]
-    float4 *ct;            // ... and per slot (c, te, row as int bits, 0) for the per-row gather
+    float4 *ct;            // ... and per slot (c, te, row as int bits, 0) for the per-neighbour sum,
+    const int32_t *rstart; // at rstart[row] + (slot - the row's first slot): rows in spatial order
     int expt;              // profiling experiments (DGS_AGG_EXPT): bit 0 skips the scatter, bit 1 the
                            // distance-transform terms -- results are then wrong; 0 in production
 };
@@ -968,8 +969,9 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
 // batch's (neighbour, dcw * fac, te), st[64], and the shared-array partials: every value is
 // first summed over the lane quartet (l, l^16, l^32, l^48) and kept by lanes 0..15 (NV x 16).
 // TR (dgs_agg_backward_tr): instead of scattering the neighbours' feature / key gradients with
-// float atomics, every slot's two factors (c, te) and its row go to A.ct in slot order (16-byte
-// coalesced stores) and every row's st to A.strows; k_agg_tgather then sums them per neighbour.
+// float atomics, every slot's two factors (c, te) and its row go to A.ct (16-byte coalesced stores,
+// rows laid out in spatial order) and every row's st to A.strows; k_agg_tgather then sums them per
+// neighbour.
 template <int NB, bool COMBO, bool PIPE, bool TR>
 __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G) {
     extern __shared__ float lds[];
@@ -1144,7 +1146,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
             // neighbour gradients (aggregate_neighbors.cu:296-319), a whole neighbour row
             // (dfeat row, then dkeys row) per G2 lanes of one atomic instruction
             if constexpr (TR) {
-                if (s < end) A.ct[s] = make_float4(c, te, __int_as_float(i), 0.0f);
+                if (s < end) A.ct[A.rstart[i] + (s - start)] = make_float4(c, te, __int_as_float(i), 0.0f);
             } else if (!(A.expt & 1)) {
                 sc[lane] = c;
                 ste[lane] = te;
@@ -1230,15 +1232,44 @@ __global__ __launch_bounds__(kBlock) void k_agg_dtrans(int P, int L, const float
     }
 }
 
-// Transposition keys: slot s names neighbour j = indices[s] (P for index -1: sorted last, in
-// no row's range); value s.
-__global__ void k_agg_tkeys(int64_t n, int P, const int64_t *__restrict__ indices, uint32_t *__restrict__ keys,
-                            uint32_t *__restrict__ vals) {
-    const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= n) return;
-    const int64_t j = indices[s];
-    keys[s] = (j >= 0 && j < P) ? (uint32_t)j : (uint32_t)P;
-    vals[s] = (uint32_t)s;
+// Transposition keys, one wave per row (spatial order): slot s of row i names neighbour
+// j = indices[s] (key P for index -1: sorted last, in no row's range); its value is the slot's
+// position in the spatial-order record array, rstart[i] + (s - the row's first slot).  The
+// records of neighbouring rows are then near each other, and the per-neighbour sum, which visits
+// rows in spatial order, reads them from a moving window that stays in the last-level cache.
+__global__ __launch_bounds__(kBlock) void k_agg_tkeys(int P, const int64_t *__restrict__ indices,
+                                                      const int64_t *__restrict__ ranges,
+                                                      const int32_t *__restrict__ order,
+                                                      const int32_t *__restrict__ rstart, uint32_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ vals) {
+    const int lane = threadIdx.x & (kWave - 1);
+    const int stride = gridDim.x * kWavesPerBlock;
+    for (int w = wave_unit_index(P); w < P; w += stride) {
+        const int i = order ? order[w] : w;
+        const int64_t start = i == 0 ? 0 : ranges[i - 1], end = ranges[i];
+        const uint32_t r0 = (uint32_t)rstart[i];
+        for (int64_t s = start + lane; s < end; s += kWave) {
+            const int64_t j = indices[s];
+            keys[s] = (j >= 0 && j < P) ? (uint32_t)j : (uint32_t)P;
+            vals[s] = r0 + (uint32_t)(s - start);
+        }
+    }
+}
+
+// Row lengths in spatial order (the scan of these gives the rows' record offsets).
+__global__ void k_agg_rowlen(int P, const int64_t *__restrict__ ranges, const int32_t *__restrict__ order,
+                             int32_t *__restrict__ len) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= P) return;
+    const int i = order ? order[w] : w;
+    len[w] = (int32_t)(ranges[i] - (i == 0 ? 0 : ranges[i - 1]));
+}
+
+__global__ void k_agg_rowstart(int P, const int32_t *__restrict__ excl, const int32_t *__restrict__ order,
+                               int32_t *__restrict__ rstart) {
+    const int w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= P) return;
+    rstart[order ? order[w] : w] = excl[w];
 }
 
 // tstart[j] = first sorted position whose key is >= j, j in [0, P] (int32: length < 2^31).
@@ -1258,10 +1289,13 @@ __global__ void k_agg_tstart(int P, int64_t n, const uint32_t *__restrict__ keys
 // aggregate_neighbors.cu:303 and 315): for row j, over its incoming slots (i -> j) in slot order,
 //   dL/dfeatures[j] = sum c * st_i,   dL/dkeys[j] = sum te * q_i
 // (c = dcw * factor, te = sum over the features of summed_transform * embedded, both from the slot's
-// row pass).  One wave per row (spatial order: the rows i of neighbouring j share L2), GR lanes per
-// slot (L + K <= GR: feature lanes, then key lanes), 64 / GR slots per step; a batch's 64 slot
-// records are staged in LDS while the next batch's load.  No atomics: each gradient row is
-// written once, in a fixed order.
+// row pass).  One wave per row (spatial order: the rows i of neighbouring j share L2).  A batch's 64
+// slot records sit in LDS; GR lanes per slot (L + K <= GR: feature lanes, then key lanes), 64 / GR
+// slots per step, gather the slot's st_i / q_i row pieces (one 64-byte segment per 16 lanes).  The
+// batch pipeline: this batch's row loads are issued first, then the next batch's record (its slot
+// id came one batch earlier) and the slot id of the batch after, so the row loads' waits never wait
+// for the random record loads (vector-memory counters retire in issue order).  No atomics: every
+// gradient row is written once, in a fixed order.
 template <int GR>
 __global__ __launch_bounds__(kBlock) void k_agg_tgather(int P, int L, int K, const int32_t *__restrict__ tstart,
                                                         const uint32_t *__restrict__ tslot,
@@ -1270,48 +1304,54 @@ __global__ __launch_bounds__(kBlock) void k_agg_tgather(int P, int L, int K, con
                                                         const float *__restrict__ queries,
                                                         const int32_t *__restrict__ order, float *__restrict__ dfeat,
                                                         float *__restrict__ dkeys) {
-    constexpr int SPP = kWave / GR;
-    __shared__ float4 srec[kWavesPerBlock][kWave];
+    constexpr int SPP = kWave / GR, NS = kWave / SPP;  // steps per full batch
+    constexpr int CH = NS < 16 ? NS : 16, NCH = NS / CH;  // steps per chunk (registers), chunks
+    __shared__ float4 srec[kWavesPerBlock][2][kWave];
     const int lane = threadIdx.x & (kWave - 1);
-    float4 *rec = srec[threadIdx.x >> 6];
+    float4 (*rec)[kWave] = srec[threadIdx.x >> 6];
     const int sub = lane / GR, t = lane - sub * GR;
     const bool fl = t < L, kl = !fl && t < L + K;
+    const float *base = fl ? strows + t : queries + (t - L);
+    const int rs = fl ? L : K;
     const int stride = gridDim.x * kWavesPerBlock;
     for (int w = wave_unit_index(P); w < P; w += stride) {
         const int j = order ? order[w] : w;
         const int kb = tstart[j], ke = tstart[j + 1];
         float acc = 0.0f;
-        float4 nxt = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        if (kb + lane < ke) nxt = ct[tslot[kb + lane]];
+        // batch 0's record, batch 1's slot id
+        if (kb + lane < ke) rec[0][lane] = ct[tslot[kb + lane]];
+        uint32_t sid = (kb + kWave + lane < ke) ? tslot[kb + kWave + lane] : 0u;
+        wave_sync_lds();
+        int cur = 0;
         for (int k0 = kb; k0 < ke; k0 += kWave) {
             const int nb = min(kWave, ke - k0);
-            rec[lane] = nxt;
-            wave_sync_lds();
-            if (k0 + kWave + lane < ke) nxt = ct[tslot[k0 + kWave + lane]];  // next batch in flight
-            int b = 0;
-            for (; b + 8 * SPP <= nb; b += 8 * SPP) {
-                float4 e[8];
-                float v[8];
+            const bool more = k0 + kWave + lane < ke;
+            float4 nrec = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 #pragma unroll
-                for (int u = 0; u < 8; ++u) e[u] = rec[b + u * SPP + sub];
+            for (int ch = 0; ch < NCH; ++ch) {
+                if (ch * CH * SPP >= nb) break;
+                float2 e[CH];
+                float v[CH];
 #pragma unroll
-                for (int u = 0; u < 8; ++u) {
-                    const int64_t i = __float_as_int(e[u].z);
-                    v[u] = fl ? strows[i * L + t] : (kl ? queries[i * K + (t - L)] : 0.0f);
+                for (int u = 0; u < CH; ++u) {
+                    const float4 r = rec[cur][min((ch * CH + u) * SPP + sub, nb - 1)];
+                    e[u] = make_float2(fl ? r.x : r.y, r.z);
                 }
 #pragma unroll
-                for (int u = 0; u < 8; ++u) acc = fmaf(fl ? e[u].x : e[u].y, v[u], acc);
-            }
-            for (; b < nb; b += SPP) {
-                const int sl = b + sub;
-                if (sl < nb) {
-                    const float4 e = rec[sl];
-                    const int64_t i = __float_as_int(e.z);
-                    const float v = fl ? strows[i * L + t] : (kl ? queries[i * K + (t - L)] : 0.0f);
-                    acc = fmaf(fl ? e.x : e.y, v, acc);
+                for (int u = 0; u < CH; ++u) v[u] = (fl || kl) ? base[(int64_t)__float_as_int(e[u].y) * rs] : 0.0f;
+                if (ch == NCH - 1 || (ch + 1) * CH * SPP >= nb) {
+                    // the next batch's record and the slot id of the batch after, issued after
+                    // this batch's last row loads: their waits never wait for these
+                    if (more) nrec = ct[sid];
+                    sid = (k0 + 2 * kWave + lane < ke) ? tslot[k0 + 2 * kWave + lane] : 0u;
                 }
+#pragma unroll
+                for (int u = 0; u < CH; ++u)
+                    if ((ch * CH + u) * SPP + sub < nb) acc = fmaf(e[u].x, v[u], acc);
             }
+            if (more) rec[cur ^ 1][lane] = nrec;
             wave_sync_lds();
+            cur ^= 1;
         }
         if constexpr (SPP >= 4) acc += __shfl_xor(acc, 16);
         if constexpr (SPP >= 2) acc += __shfl_xor(acc, 32);
@@ -1488,8 +1528,8 @@ static int agg_backward_impl(int P, int D, int L, int K, int E, const float *fea
                              const float *distance_transform, const int64_t *indices, const int64_t *ranges,
                              const float *dists, const float *densities, const float *weights,
                              const float *embeddings, const float *factors, const float *inv_total,
-                             const int32_t *row_order, const int32_t *tstart, const uint32_t *tslot, int64_t length,
-                             const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
+                             const int32_t *row_order, const int32_t *tstart, const uint32_t *tslot,
+                             const int32_t *rstart, int64_t length, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
                              float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
                              void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
     int rc = agg_check(P, D, L, K, E);
@@ -1498,8 +1538,8 @@ static int agg_backward_impl(int P, int D, int L, int K, int E, const float *fea
     const size_t need = tr ? dgs_agg_workspace_size_tr(P, L, length) : dgs_agg_workspace_size(P, L);
     if (workspace_bytes < need || (!workspace && P > 0))
         return fail(DGS_ERR_ARG, "dgs_agg_backward: workspace smaller than dgs_agg_workspace_size");
-    if (tr && (L + K > kWave || !tslot || length < 0 || length >= ((int64_t)1 << 31)))
-        return fail(DGS_ERR_ARG, "dgs_agg_backward_tr: needs L + K <= 64, tslot and 0 <= length < 2^31");
+    if (tr && (L + K > kWave || !tslot || !rstart || length < 0 || length >= ((int64_t)1 << 31)))
+        return fail(DGS_ERR_ARG, "dgs_agg_backward_tr: needs L + K <= 64, tslot, rstart and 0 <= length < 2^31");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int F = (E - 1) / D / 2;
     const int NV = 2 * E + F;
@@ -1533,6 +1573,7 @@ static int agg_backward_impl(int P, int D, int L, int K, int E, const float *fea
         A.strows = A.arows + (size_t)P * L;
         const size_t ct_off = ((sizeof(float) * 2 * (size_t)P * L + 15) / 16) * 16;
         A.ct = reinterpret_cast<float4 *>(static_cast<char *>(workspace) + ct_off);
+        A.rstart = rstart;
     }
     if (const char *e = getenv("DGS_AGG_EXPT")) A.expt = atoi(e);
     // few enough waves that each flushes its shared-array partials after many rows
@@ -1601,7 +1642,7 @@ extern "C" int dgs_agg_backward(int P, int D, int L, int K, int E, const float *
                                 void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug) {
     return agg_backward_impl(P, D, L, K, E, features, transform, queries, keys, frequencies, distance_transform,
                              indices, ranges, dists, densities, weights, embeddings, factors, inv_total, row_order,
-                             nullptr, nullptr, 0, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
+                             nullptr, nullptr, nullptr, 0, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
                              dL_dfrequencies, dL_ddistance_transform, workspace, workspace_bytes, stream, debug);
 }
 
@@ -1611,27 +1652,38 @@ extern "C" int dgs_agg_backward_tr(int P, int D, int L, int K, int E, const floa
                                    const float *dists, const float *densities, const float *weights,
                                    const float *embeddings, const float *factors, const float *inv_total,
                                    const int32_t *row_order, const int32_t *tstart, const uint32_t *tslot,
-                                   int64_t length, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform,
+                                   const int32_t *rstart, int64_t length, const float *dL_dout, float *dL_dfeatures, float *dL_dtransform,
                                    float *dL_dqueries, float *dL_dkeys, float *dL_dfrequencies,
                                    float *dL_ddistance_transform, void *workspace, size_t workspace_bytes,
                                    dgs_stream_t stream, int debug) {
     if (!tstart) return fail(DGS_ERR_ARG, "dgs_agg_backward_tr: tstart is NULL");
     return agg_backward_impl(P, D, L, K, E, features, transform, queries, keys, frequencies, distance_transform,
                              indices, ranges, dists, densities, weights, embeddings, factors, inv_total, row_order,
-                             tstart, tslot, length, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
+                             tstart, tslot, rstart, length, dL_dout, dL_dfeatures, dL_dtransform, dL_dqueries, dL_dkeys,
                              dL_dfrequencies, dL_ddistance_transform, workspace, workspace_bytes, stream, debug);
 }
 
-extern "C" int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, int32_t *tstart, uint32_t *tslot,
+extern "C" int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, const int64_t *ranges,
+                                 const int32_t *row_order, int32_t *tstart, uint32_t *tslot, int32_t *rstart,
                                  dgs_alloc_fn alloc, void *alloc_ctx, dgs_stream_t stream, int debug) {
-    if (P < 0 || length < 0 || length >= ((int64_t)1 << 31) || !tstart || (!tslot && length > 0) || !alloc)
+    if (P < 0 || length < 0 || length >= ((int64_t)1 << 31) || !tstart || !rstart || !ranges ||
+        (!tslot && length > 0) || !alloc)
         return fail(DGS_ERR_ARG, "dgs_agg_transpose: bad arguments (length must be < 2^31)");
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0) return DGS_OK;
+    auto scratch = [&](size_t n) { return alloc(alloc_ctx, DGS_BUF_SCRATCH, std::max<size_t>(n, 16)); };
+    int32_t *len = static_cast<int32_t *>(scratch(4 * (size_t)P));
+    int32_t *excl = static_cast<int32_t *>(scratch(4 * (size_t)P));
+    int32_t *part = static_cast<int32_t *>(scratch(scan_scratch_bytes<int32_t>(P)));
+    if (!len || !excl || !part) return fail(DGS_ERR_ALLOC, "dgs_agg_transpose: scratch allocation failed");
+    k_agg_rowlen<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, ranges, row_order, len);
+    scan_excl<int32_t>(P, len, excl, nullptr, nullptr, part, s);
+    k_agg_rowstart<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, excl, row_order, rstart);
+    DGS_LAUNCH_CHECK(s, debug);
     if (length == 0) {
         DGS_TRY_HIP(hipMemsetAsync(tstart, 0, sizeof(int32_t) * ((size_t)P + 1), s));
         return DGS_OK;
     }
-    auto scratch = [&](size_t n) { return alloc(alloc_ctx, DGS_BUF_SCRATCH, std::max<size_t>(n, 16)); };
     uint32_t *keys = static_cast<uint32_t *>(scratch(4 * (size_t)length));
     uint32_t *keys_s = static_cast<uint32_t *>(scratch(4 * (size_t)length));
     uint32_t *vals = static_cast<uint32_t *>(scratch(4 * (size_t)length));
@@ -1642,7 +1694,7 @@ extern "C" int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, 
     DGS_TRY_HIP(onesweep_pairs<uint32_t>(nullptr, tb, keys, keys_s, vals, tslot, (size_t)length, 0u, (unsigned)bits, s));
     void *tmp = scratch(tb);
     if (!tmp) return fail(DGS_ERR_ALLOC, "dgs_agg_transpose: scratch allocation failed");
-    k_agg_tkeys<<<agg_elem_blocks(length), kBlock, 0, s>>>(length, P, indices, keys, vals);
+    k_agg_tkeys<<<agg_row_blocks(P), kBlock, 0, s>>>(P, indices, ranges, row_order, rstart, keys, vals);
     DGS_LAUNCH_CHECK(s, debug);
     DGS_TRY_HIP(onesweep_pairs<uint32_t>(tmp, tb, keys, keys_s, vals, tslot, (size_t)length, 0u, (unsigned)bits, s));
     DGS_LAUNCH_CHECK(s, debug);

@@ -403,18 +403,21 @@ struct AggEntry {
     Tensor order;
     WeakImpl impl;
     int64_t version;
-    Tensor tstart, tslot;  // undefined: not built
+    Tensor tstart, tslot, rstart;  // undefined: not built
+    Tensor ranges;                 // (the record layout follows the row lengths too)
+    int64_t ranges_version;
 };
 std::mutex g_agg_mu;
 std::vector<AggEntry> g_agg;
 
-void agg_put(const Tensor &indices, int64_t P, const Tensor &order, const Tensor &tstart, const Tensor &tslot) {
+void agg_put(const Tensor &indices, const Tensor &ranges, int64_t P, const Tensor &order, const Tensor &tstart,
+             const Tensor &tslot, const Tensor &rstart) {
     std::lock_guard<std::mutex> lk(g_agg_mu);
     for (auto it = g_agg.begin(); it != g_agg.end();)
         if (it->indices == indices.data_ptr() || it->impl.expired()) it = g_agg.erase(it);
         else ++it;
     g_agg.push_back({indices.data_ptr(), P, indices.numel(), order, WeakImpl(indices.getIntrusivePtr()),
-                     (int64_t)indices._version(), tstart, tslot});
+                     (int64_t)indices._version(), tstart, tslot, rstart, ranges, (int64_t)ranges._version()});
     if (g_agg.size() > 2) g_agg.erase(g_agg.begin());
 }
 
@@ -428,14 +431,17 @@ const int32_t *order_get(const Tensor &indices, int64_t P) {
 }
 
 // The transposed lists built from exactly this indices tensor (same object, not modified since).
-bool transpose_get(const Tensor &indices, int64_t P, Tensor &tstart, Tensor &tslot) {
+bool transpose_get(const Tensor &indices, const Tensor &ranges, int64_t P, Tensor &tstart, Tensor &tslot,
+                   Tensor &rstart) {
     std::lock_guard<std::mutex> lk(g_agg_mu);
     for (const auto &e : g_agg) {
         if (!e.tstart.defined() || e.P != P || e.length != indices.numel()) continue;
         const auto sp = e.impl.lock();
-        if (sp.get() == indices.unsafeGetTensorImpl() && e.version == (int64_t)indices._version()) {
+        if (sp.get() == indices.unsafeGetTensorImpl() && e.version == (int64_t)indices._version() &&
+            e.ranges.data_ptr() == ranges.data_ptr() && e.ranges_version == (int64_t)ranges._version()) {
             tstart = e.tstart;
             tslot = e.tslot;
+            rstart = e.rstart;
             return true;
         }
     }
@@ -448,14 +454,16 @@ bool transpose_enabled() {
 }
 
 // dgs_agg_transpose into fresh tensors.
-void build_transpose(const Tensor &indices, int64_t P, Tensor &tstart, Tensor &tslot, bool debug) {
+void build_transpose(const Tensor &indices, const Tensor &ranges, const int32_t *order, int64_t P, Tensor &tstart,
+                     Tensor &tslot, Tensor &rstart, bool debug) {
     const int64_t length = indices.numel();
     tstart = torch::empty({P + 1}, indices.options().dtype(torch::kInt32));
     tslot = torch::empty({std::max<int64_t>(length, 1)}, indices.options().dtype(torch::kInt32));
+    rstart = torch::empty({std::max<int64_t>(P, 1)}, indices.options().dtype(torch::kInt32));
     AllocCtx ctx{indices.device()};
-    check(dgs_agg_transpose((int)P, length, indices.data_ptr<int64_t>(), tstart.data_ptr<int32_t>(),
-                            reinterpret_cast<uint32_t *>(tslot.data_ptr<int32_t>()), alloc_cb, &ctx,
-                            as_dgs(cur_stream()), debug ? 1 : 0),
+    check(dgs_agg_transpose((int)P, length, indices.data_ptr<int64_t>(), ranges.data_ptr<int64_t>(), order,
+                            tstart.data_ptr<int32_t>(), reinterpret_cast<uint32_t *>(tslot.data_ptr<int32_t>()),
+                            rstart.data_ptr<int32_t>(), alloc_cb, &ctx, as_dgs(cur_stream()), debug ? 1 : 0),
           "preprocess_aggregate (transpose)");
 }
 
@@ -493,9 +501,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessC
     Tensor indices = view(DGS_BUF_AGG_INDICES, torch::kInt64, {length});
     if (length > 0) {
         // the transposed lists for the backward's per-row gather (dgs_agg_backward_tr)
-        Tensor tstart, tslot;
-        if (transpose_enabled() && length < ((int64_t)1 << 31)) build_transpose(indices, P, tstart, tslot, debug);
-        agg_put(indices, P, order, tstart, tslot);
+        Tensor tstart, tslot, rstart;
+        if (transpose_enabled() && length < ((int64_t)1 << 31))
+            build_transpose(indices, ranges, order.data_ptr<int32_t>(), P, tstart, tslot, rstart, debug);
+        agg_put(indices, ranges, P, order, tstart, tslot, rstart);
     }
     return std::make_tuple(indices, ranges, view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
                            view(DGS_BUF_AGG_DENSITIES, torch::kFloat32, {length}), inv_total);
@@ -569,10 +578,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
     Tensor dfreq = torch::zeros(a.freq.sizes(), a.features.options());
     Tensor ddt = torch::zeros(a.dt.sizes(), a.features.options());
     const int64_t length = a.indices.numel();
-    Tensor tstart, tslot;
+    Tensor tstart, tslot, rstart;
     const bool tr = a.P > 0 && a.L + a.K <= 64 && length < ((int64_t)1 << 31) && transpose_enabled();
-    if (tr && !transpose_get(a.indices, a.P, tstart, tslot))  // indices not from preprocess_aggregate
-        build_transpose(a.indices, a.P, tstart, tslot, debug);
+    if (tr && !transpose_get(a.indices, a.ranges, a.P, tstart, tslot, rstart))  // not from preprocess_aggregate
+        build_transpose(a.indices, a.ranges, order_get(a.indices, a.P), a.P, tstart, tslot, rstart, debug);
     if (tr) {
         const size_t ws = dgs_agg_workspace_size_tr(a.P, a.L, length);
         Tensor work = torch::empty({(int64_t)ws}, a.features.options().dtype(torch::kUInt8));
@@ -582,7 +591,8 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
                                   a.dists.data_ptr<float>(), a.densities.data_ptr<float>(), weights.data_ptr<float>(),
                                   embeddings.data_ptr<float>(), factors.data_ptr<float>(), a.inv_total.data_ptr<float>(),
                                   order_get(a.indices, a.P), tstart.data_ptr<int32_t>(),
-                                  reinterpret_cast<const uint32_t *>(tslot.data_ptr<int32_t>()), length,
+                                  reinterpret_cast<const uint32_t *>(tslot.data_ptr<int32_t>()),
+                                  rstart.data_ptr<int32_t>(), length,
                                   dL.data_ptr<float>(), dfeat.data_ptr<float>(), dtrans.data_ptr<float>(),
                                   dq.data_ptr<float>(), dkeys.data_ptr<float>(), dfreq.data_ptr<float>(),
                                   ddt.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),

@@ -247,19 +247,23 @@ int dgs_agg_backward(int P, int D, int L, int K, int E, const float *features,
                      void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug);
 
 /* The neighbour lists transposed (CSR -> CSC of the slot matrix): for every row j, the slots
- * (i -> j) that name j, in ascending slot order.  No reference counterpart: it turns the
- * reference's scatter of the neighbours' feature / key gradients (aggregate_neighbors.cu:
- * 303, 315 -- float atomics, here the float-atomic rate bounded the backward) into a per-row
- * gather, so the backward writes every gradient once.  tstart[P + 1]: out, row j's slots are
- * tslot[tstart[j] .. tstart[j + 1]); tslot[length]: out.  Slots with index -1 are left out.
- * Scratch (16 bytes per slot) through `alloc` (DGS_BUF_SCRATCH).  length < 2^31. */
-int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, int32_t *tstart, uint32_t *tslot,
+ * (i -> j) that name j, in ascending slot order: tslot[tstart[j] .. tstart[j + 1]) (slots with
+ * index -1 come after tstart[P]).  Each entry is the slot's position in a record array whose rows
+ * follow row_order (NULL = 0..P-1): row i's slots are at rstart[i] + 0, 1, ...  No reference
+ * counterpart: it turns the reference's scatter of the neighbours' feature / key gradients
+ * (aggregate_neighbors.cu:303, 315 -- float atomics, here the float-atomic rate bounded the
+ * backward) into a per-row sum, so the backward writes every gradient once.
+ * ranges / row_order: as from dgs_agg_preprocess.  tstart[P + 1], tslot[length], rstart[P]: out.
+ * Scratch (12 bytes per slot) through `alloc` (DGS_BUF_SCRATCH).  length < 2^31. */
+int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, const int64_t *ranges,
+                      const int32_t *row_order, int32_t *tstart, uint32_t *tslot, int32_t *rstart,
                       dgs_alloc_fn alloc, void *alloc_ctx, dgs_stream_t stream, int debug);
 
 /* Workspace bytes of dgs_agg_backward_tr (L + K <= 64; larger widths take dgs_agg_backward). */
 size_t dgs_agg_workspace_size_tr(int P, int L, int64_t length);
 
-/* dgs_agg_backward with the transposed lists of dgs_agg_transpose (same indices): identical
+/* dgs_agg_backward with the transposed lists of dgs_agg_transpose (same indices, ranges and
+ * row_order): identical
  * gradients up to float summation order, with no float atomics on the features / keys
  * gradients (each row sums its incoming slots in slot order: deterministic). */
 int dgs_agg_backward_tr(int P, int D, int L, int K, int E, const float *features,
@@ -268,8 +272,8 @@ int dgs_agg_backward_tr(int P, int D, int L, int K, int E, const float *features
                         const int64_t *indices, const int64_t *ranges, const float *dists,
                         const float *densities, const float *weights, const float *embeddings,
                         const float *factors, const float *inv_total, const int32_t *row_order,
-                        const int32_t *tstart, const uint32_t *tslot, int64_t length,
-                        const float *dL_dout,
+                        const int32_t *tstart, const uint32_t *tslot, const int32_t *rstart,
+                        int64_t length, const float *dL_dout,
                         float *dL_dfeatures, float *dL_dtransform, float *dL_dqueries,
                         float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
                         void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug);

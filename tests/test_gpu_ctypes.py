@@ -53,8 +53,10 @@ def test_ctypes_aggregate_matches_extension(dgs):
     g = torch.randn_like(fa[3])
     ga = dgs._C.aggregate_neighbors_backward(*t, *a[:4], *fa[:3], a[4], g, False)
     gb = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False)
-    for x, y in zip(ga, gb):
+    gc = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False, transposed=False)
+    for x, y, z in zip(ga, gb, gc):
         np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))
+        np.testing.assert_allclose(x.cpu().numpy(), z.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))
 
 
 def test_ctypes_multi_matches_extension(dgs):

@@ -187,6 +187,10 @@ _lib.dgs_agg_forward.argtypes = [_I] * 5 + [_P] * 11 + [_P] + [_P] * 4 + [_P, _I
 _lib.dgs_agg_backward.argtypes = [_I] * 5 + [_P] * 14 + [_P] + [_P] * 7 + [_P, _SZ, _P, _I]
 _lib.dgs_agg_workspace_size.restype = _SZ
 _lib.dgs_agg_workspace_size.argtypes = [_I, _I]
+_lib.dgs_agg_transpose.argtypes = [_I, _I64, _P, _P, _P, _P, _P, _P, ALLOC_FN, _P, _P, _I]
+_lib.dgs_agg_workspace_size_tr.restype = _SZ
+_lib.dgs_agg_workspace_size_tr.argtypes = [_I, _I, _I64]
+_lib.dgs_agg_backward_tr.argtypes = [_I] * 5 + [_P] * 14 + [_P] + [_P, _P, _P, _I64] + [_P] * 7 + [_P, _SZ, _P, _I]
 _orders = {}  # indices data_ptr -> (P, row order tensor): the scheduling hint of dgs_agg_preprocess
 
 
@@ -254,14 +258,37 @@ def aggregate_neighbors(features, transform, queries, keys, frequencies, distanc
 
 def aggregate_neighbors_backward(features, transform, queries, keys, frequencies, distance_transform, indices,
                                  ranges, dists, densities, weights, embeddings, factors, inv_total_densities,
-                                 dL_dneighbor_features, debug):
-    """aggregate_neighbors.h:31-47 -> the six gradients."""
+                                 dL_dneighbor_features, debug, transposed=True):
+    """aggregate_neighbors.h:31-47 -> the six gradients (transposed: dgs_agg_transpose +
+    dgs_agg_backward_tr, as the extension does for L + K <= 64; else dgs_agg_backward)."""
     f, T, q, k, fr, dt, X, dn, w, e, fa, inv, g = map(
         _f32, (features, transform, queries, keys, frequencies, distance_transform, dists, densities, weights,
                embeddings, factors, inv_total_densities, dL_dneighbor_features))
     idx, rg = _i64(indices), _i64(ranges)
     P, D, L, K, E = _agg_sizes(f, q, dt, X)
     outs = [torch.zeros_like(t) for t in (f, T, q, k, fr, dt)]
+    n = idx.numel()
+    if transposed and P > 0 and L + K <= 64:
+        # the transposed lists (dgs_agg_transpose), then the gather form of the backward
+        tstart = torch.empty(P + 1, dtype=torch.int32, device=f.device)
+        tslot = torch.empty(max(n, 1), dtype=torch.int32, device=f.device)
+        keep = []
+
+        def alloc(ctx, which, nbytes):
+            t = torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=f.device)
+            keep.append(t)
+            return t.data_ptr()
+
+        rstart = torch.empty(P, dtype=torch.int32, device=f.device)
+        order = _order(idx, P)
+        _check(_lib.dgs_agg_transpose(P, n, _ptr(idx), _ptr(rg), _ptr(order), _ptr(tstart), _ptr(tslot), _ptr(rstart),
+                                      ALLOC_FN(alloc), None, _stream(), int(bool(debug))))
+        ws = torch.empty(_lib.dgs_agg_workspace_size_tr(P, L, n), dtype=torch.uint8, device=f.device)
+        _check(_lib.dgs_agg_backward_tr(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt),
+                                        _ptr(idx), _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(e), _ptr(fa), _ptr(inv),
+                                        _ptr(order), _ptr(tstart), _ptr(tslot), _ptr(rstart), n, _ptr(g),
+                                        *[_ptr(o) for o in outs], _ptr(ws), ws.numel(), _stream(), int(bool(debug))))
+        return tuple(outs)
     ws = torch.empty(_lib.dgs_agg_workspace_size(P, L), dtype=torch.uint8, device=f.device)
     _check(_lib.dgs_agg_backward(P, D, L, K, E, _ptr(f), _ptr(T), _ptr(q), _ptr(k), _ptr(fr), _ptr(dt), _ptr(idx),
                                  _ptr(rg), _ptr(X), _ptr(dn), _ptr(w), _ptr(e), _ptr(fa), _ptr(inv),

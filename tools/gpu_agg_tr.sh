@@ -4,7 +4,7 @@ cd $GRAFT_REPO_ROOT
 T=${1:-r03t}
 O=gpurun_out/$T
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest tests/test_gpu_aggregate.py -x -v --timeout 200 --timeout-method thread > $O/agg_tests.log 2>&1 || { echo "agg tests failed"; tail -40 $O/agg_tests.log; exit 1; }
+timeout -k 10 400 python -u -m pytest tests/test_gpu_aggregate.py tests/test_gpu_ctypes.py -x -v --timeout 200 --timeout-method thread > $O/agg_tests.log 2>&1 || { echo "agg tests failed"; tail -40 $O/agg_tests.log; exit 1; }
 tail -1 $O/agg_tests.log
 timeout -k 10 300 python -u bench.py --op aggregate --steps 3 --warmup 1 --no-cpu > $O/agg.log 2>&1 || { echo agg failed; tail -5 $O/agg.log; exit 1; }
 tail -1 $O/agg.log
