@@ -629,6 +629,22 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
     # weights / embeddings / factors (12) and adds L + K floats into neighbour rows
     stream_b = 32.0 * Lnb + 4.0 * P * (3 * L + 3 * K)
     atomic_b = 4.0 * (L + K) * Lnb
+    if os.environ.get("DGS_AGG_TRANSPOSE", "1") != "0" and L + K <= 64:
+        # transposed backward: no float atomics on the neighbour rows; the row pass
+        # streams the slot arrays and stores one 16-byte record per slot, the per-neighbour sum
+        # reads the transposed slot ids (4 B) and the records (16 B, gathered): HBM-bound
+        rec_b = 36.0 * Lnb
+        roof_bwd = {"bound": "hbm", "kernel": "k_agg_backward_s + k_agg_tgather",
+                    "achieved": (stream_b + rec_b) / (b_ms * 1e-3) / 1e9, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": (stream_b + rec_b) / (b_ms * 1e-3) / 1e9 / PEAK_HBM_GBS,
+                    "bytes_basis": "slot streams 32 B + per-row terms, plus the 36 B per slot of the "
+                                   "transposed records (written, gathered, slot ids)", "traffic": None}
+    else:
+        # the atomic form is bound by the memory-side float-atomic rate (its added bytes)
+        roof_bwd = {"bound": "atomic", "kernel": "k_agg_backward_s",
+                    "achieved": atomic_b / (b_ms * 1e-3) / 1e9, "peak": PEAK_ATOMIC_GBS,
+                    "unit": "GB/s (float-atomic added bytes)",
+                    "frac": atomic_b / (b_ms * 1e-3) / 1e9 / PEAK_ATOMIC_GBS, "traffic": None}
     result = {
         "metric": "aggregated neighbour slots/sec (aggregate_neighbors fwd+bwd), 1M Gaussians",
         "value": Lnb * world / (ms_per_step / 1e3),
@@ -641,12 +657,7 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
         "preprocess_aggregate_ms": pre_ms,
         "preprocess_aggregate_first_call_ms": pre_times[0],
         "phases_ms": {"forward": f_ms, "backward": b_ms},
-        # the backward is bound by the memory-side float-atomic rate (its added bytes), not by
-        # HBM streaming: both are reported
-        "roofline": {"bound": "atomic", "kernel": "k_agg_backward_s",
-                     "achieved": atomic_b / (b_ms * 1e-3) / 1e9, "peak": PEAK_ATOMIC_GBS,
-                     "unit": "GB/s (float-atomic added bytes)",
-                     "frac": atomic_b / (b_ms * 1e-3) / 1e9 / PEAK_ATOMIC_GBS, "traffic": None},
+        "roofline": roof_bwd,
         # the forward: per slot it streams indices / dists / densities (20 B) and writes weights /
         # embeddings / factors (12 B), reads the neighbour's feature and key rows (4 (L + K) B,
         # mostly from cache: neighbours of adjacent rows coincide) and writes out once per row
