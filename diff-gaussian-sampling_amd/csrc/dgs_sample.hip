@@ -439,7 +439,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
 // list.  The pass's first 16 pair rows are loaded once per pass, before the group loop, and stay
 // in SGPRs for every group (no scalar load, hence no out-of-order lgkmcnt(0) wait, for them
 // inside the loop).  Arithmetic, order per lane and the reduce-scatter are those of (a).
-// The first HB blocks of 4 pair rows are hoisted (64 SGPRs: more spill into VGPR lanes and cost a
+// The first HB (DGS_FWD_HB = 2) blocks of 4 pair rows are hoisted (at 4 blocks, 64 SGPRs, the kernel spilled SGPRs into VGPR lanes: a
 // v_readlane per dword inside the loop); the pass's later blocks, needed by the larger sub-cells
 // only, are loaded where they are used.
 template <int FN, int D, int CB, int NPH, int HB, bool WRAP>
@@ -459,6 +459,12 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
     }
 }
 
+#ifndef DGS_FWD_UNROLL
+#define DGS_FWD_UNROLL 1  // sub-cell forward: list-walk unroll (register renaming instead of copies)
+#endif
+#ifndef DGS_FWD_HB
+#define DGS_FWD_HB 2  // sub-cell forward: blocks of 4 pair rows hoisted into SGPRs for the list walk (4: SGPR spills, 2.7 % slower)
+#endif
 #ifndef DGS_FWD_LDS
 #define DGS_FWD_LDS 0  // sub-cell forward: the pass's pair rows staged in LDS (else hoisted into SGPRs)
 #endif
@@ -552,6 +558,9 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
     uint32_t e_nxt = ents[min(eb + kWave + lane, last)];
     float r_cur[RS];
     load_grow<RS>(grows, e_cur, r_cur);
+#if DGS_FWD_UNROLL > 1
+#pragma unroll DGS_FWD_UNROLL
+#endif
     for (int g0 = eb; g0 < ee; g0 += kWave) {
         float r_nxt[RS];
         load_grow<RS>(grows, e_nxt, r_nxt);
@@ -574,7 +583,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
     using Tr = Traits<FN, D>;
     constexpr int U = Tr::U, UC = U * CB;
     constexpr int NP0 = 32 / UC, NPH = NP0 < kSubPairs ? NP0 : kSubPairs, NS = 2 * NPH;
-    constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL, HB = NB < 4 ? NB : 4;
+    constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL, HB = NB < DGS_FWD_HB ? NB : DGS_FWD_HB;
     static_assert(D == 2 && NPH >= 1 && NS * UC <= 64, "sub-cell form: D = 2, reduce-scatter width");
     const Bins bins = resolve(gbuf, sbuf);
     const float *__restrict__ fsrows = bins.fsrows;
