@@ -863,6 +863,9 @@ __global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, const int32_t *_
     if (lane == 0) box[c] = make_float4(clo[0], clo[1], chi[0], chi[1]);
 }
 
+#ifndef DGS_SUB_SLICE
+#define DGS_SUB_SLICE 1  // k_sub_lists: per-sub-row slices instead of per-sub-box minimisations
+#endif
 // Does the box [xa, xb] x [ya, yb] of displacements contain an X with X^T A X <= qcut?  fp32
 // with the reciprocals of c0 / c2 given (the sub-cell test runs once per entry and sub-cell).
 // Rounding moves the computed minimum by ~1e-6 relative; the callers' qcut has a 1e-4 margin and
@@ -935,6 +938,34 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                     const float ic0 = __builtin_amdgcn_rcpf(cc.x), ic2 = __builtin_amdgcn_rcpf(cc.z);
                     const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(bx.x), fabsf(bx.z)));
                     const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(bx.y), fabsf(bx.w)));
+#if DGS_SUB_SLICE
+                    // Per sub-row (the union of its two sub-boxes' sample y ranges) the ellipse's
+                    // slice is one X0 interval [xl, xu] (row_slice's construction in fp32); a
+                    // sub-box is hit when its X0 range meets it.  Two slices per entry instead of
+                    // four box minimisations.  The union band and the tolerances only widen the
+                    // lists (the cut itself sits 1 % outside the last live pair, kQCut).
+                    const float c0 = cc.x, c1 = cc.y, c2 = cc.z;
+                    const float det = c0 * c2 - c1 * c1;
+                    const float ex0 = __builtin_sqrtf(qc * c2 * __builtin_amdgcn_rcpf(det));
+                    const float ex1 = __builtin_sqrtf(qc * c0 * __builtin_amdgcn_rcpf(det));
+                    const float yu0 = -c1 * ex0 * ic2;
+#pragma unroll
+                    for (int r = 0; r < 2; ++r) {
+                        const float blo = fminf(sb[2 * r].y, sb[2 * r + 1].y), bhi = fmaxf(sb[2 * r].w, sb[2 * r + 1].w);
+                        const float ya = fmaxf(m1 - bhi - e1, -ex1), yb = fminf(m1 - blo + e1, ex1);
+                        if (!(ya <= yb)) continue;  // (also: both sub-boxes of the row empty)
+                        const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(-yu0, ya), yb);
+                        const float xu = (-c1 * yu + __builtin_sqrtf(fmaxf(qc * c0 - det * yu * yu, 0.0f))) * ic0;
+                        const float xl = (-c1 * yl - __builtin_sqrtf(fmaxf(qc * c0 - det * yl * yl, 0.0f))) * ic0;
+                        const float tol = 1e-5f * (1.0f + fabsf(xu) + fabsf(xl));
+#pragma unroll
+                        for (int h = 0; h < 2; ++h) {
+                            const float4 q = sb[2 * r + h];
+                            if (q.x <= q.z && m0 - q.z - e0 <= xu + tol && m0 - q.x + e0 >= xl - tol)
+                                mask |= 1u << (2 * r + h);
+                        }
+                    }
+#else
                     for (int k = 0; k < kSubPerCell; ++k) {
                         const float4 q = sb[k];
                         if (!(q.x <= q.z)) continue;  // empty sub-cell
@@ -942,6 +973,7 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                cc.z, ic0, ic2, qc))
                             mask |= 1u << k;
                     }
+#endif
                 }
             }
             const bool ff = j < m_;
