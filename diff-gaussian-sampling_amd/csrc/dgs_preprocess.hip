@@ -182,11 +182,16 @@ __global__ void k_identify(int64_t L, const KT *__restrict__ keys, uint32_t limi
 
 // ------------------------------------------------------------------- Gaussian binning
 // forward.cu:24-83 (radius, tiles touched) + the reference tile counts + spatial home key.
+// Also packs each Gaussian's mean, radius and conic into one 32-byte record (caller order,
+// coalesced): k_fine_count then gathers one record per Gaussian in internal order instead of
+// three scattered arrays.
 __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
-                             const float *__restrict__ covs, float *__restrict__ radii,
+                             const float *__restrict__ covs, const float *__restrict__ conics,
+                             float *__restrict__ radii,
                              uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
                              uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
-                             int home_w, int home_h, const uint8_t *__restrict__ present) {
+                             int home_w, int home_h, const uint8_t *__restrict__ present,
+                             float4 *__restrict__ grec) {
     __shared__ uint32_t hist[kHistBins];  // grid-strided, capped grid: see k_sample_cells
     const bool lds = G.T <= kHistBins;
     if (lds)
@@ -206,6 +211,12 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         radii[i] = r;
         touched[i] = t;
         ids[i] = (uint32_t)i;
+        {
+            const float c0 = conics[i * S], c1 = D == 2 ? conics[i * S + 1] : 0.0f;
+            const float c2 = D == 2 ? conics[i * S + 2] : 0.0f;
+            grec[2 * i] = make_float4(m[0], m[1], r, c0);
+            grec[2 * i + 1] = make_float4(c1, c2, 0.0f, 0.0f);
+        }
         if (!(r > 0.0f)) {
             home[i] = (uint32_t)home_w * (uint32_t)home_h;  // absent: after every home cell
             continue;
@@ -591,8 +602,7 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const in
 // (gather-path) Gaussians also their reach and local row ranges (k_gather reads them as
 // lrows[KR + dy][i]: coalesced over the contiguous id range of a home row), and the largest reach.
 __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
-                                                       const float *__restrict__ means, const float *__restrict__ conics,
-                                                       const float *__restrict__ radii, const int32_t *__restrict__ sbeg,
+                                                       const float4 *__restrict__ grec, const int32_t *__restrict__ sbeg,
                                                        const int32_t *__restrict__ send, const float4 *__restrict__ box,
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
@@ -601,10 +611,10 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
     int reach = 0;
     if (i < P) {
         const int64_t g = perm[i];
-        const float r = radii[g];
+        const float4 ga = grec[2 * g], gb2 = grec[2 * g + 1];  // (k_gauss_prep's record: one line)
+        const float r = ga.z;
         uint64_t n = 0;
-        float m[2], c[3];
-        load_gauss(G.D, means, conics, g, m, c);
+        const float m[2] = {ga.x, ga.y}, c[3] = {ga.w, gb2.x, gb2.y};
         // the one random gather of the Gaussians: internal-order copies for k_fine_fill / k_geo_pack
         igm[i] = make_float2(m[0], m[1]);
         igc[i] = make_float4(c[0], c[1], c[2], r);
@@ -1473,6 +1483,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     int32_t *rmax = ca.take<int32_t>(1);
     float2 *igm = ca.take<float2>(P);
     float4 *igc = ca.take<float4>(P);
+    float4 *grec = ca.take<float4>(2 * (size_t)P);
 
     // sort / scan temp storage: one piece sized for the largest phase-A primitive
     size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
@@ -1501,6 +1512,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(rmax, base);
         Carve::rebase(igm, base);
         Carve::rebase(igc, base);
+        Carve::rebase(grec, base);
         char *t = static_cast<char *>(tmp_a);
         Carve::rebase(t, base);
         tmp_a = t;
@@ -1551,14 +1563,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
-    k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, radii, touched, gtile,
-                                                home, gids, home_w, home_h, present);
+    k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, conics, radii, touched, gtile,
+                                                home, gids, home_w, home_h, present, grec);
     DGS_LAUNCH_CHECK(s, debug);
     tb = t_a;
     DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
-    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, means, conics, radii, cell_sbeg,
+    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, grec, cell_sbeg,
                                                 cell_send, cell_box, fcount, greach, lrows, rmax, igm, igc);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
