@@ -7,6 +7,7 @@ rect spans the whole grid (full range), det == 0 covariance (absent), a non-PD c
 sampler_impl.cu:169-177), D = 1 zero variance, and means far outside the sample domain
 (rect indices that are negative multiples of the grid: C's `%` wraps them to `grid`).
 """
+import math
 import numpy as np
 import torch
 
@@ -107,6 +108,29 @@ def seam_case(D=2, P=400, n=4000, C=1, seed=131):
         conics = torch.stack([covs[:, 2] / det, -covs[:, 1] / det, covs[:, 0] / det], 1).float()
     values = torch.randn(P, C, generator=g).float()
     return means, values, covs, conics, syn.samples(n, D, seed=seed + 1)
+
+
+def thin_case(P=6000, n=40000, C=1, seed=151):
+    """Thin rotated Gaussians (axis ratio up to 25, sigma_min down to 0.0008): cuts far longer
+    than the fine cells in one direction and narrower than a sub-cell in the other -- the sub-cell
+    lists' per-row slices (k_sub_lists) and the gather path's row ranges at their most anisotropic,
+    a quarter of the means within 0.05 of a torus seam."""
+    g = torch.Generator().manual_seed(seed)
+    means = torch.rand(P, 2, generator=g, dtype=torch.float64) * 2 - 1
+    edge = torch.rand(P, generator=g) < 0.25
+    means[edge, 0] = torch.where(means[edge, 0] < 0, -1.0, 1.0) * (1 - 0.05 * torch.rand(int(edge.sum()), generator=g,
+                                                                                          dtype=torch.float64))
+    s_min = 0.0008 + 0.002 * torch.rand(P, generator=g, dtype=torch.float64)
+    s_max = s_min * (1 + 24 * torch.rand(P, generator=g, dtype=torch.float64))
+    th = torch.rand(P, generator=g, dtype=torch.float64) * math.pi
+    c, sn = torch.cos(th), torch.sin(th)
+    a, b = s_max ** 2, s_min ** 2
+    xx, xy, yy = c * c * a + sn * sn * b, c * sn * (a - b), sn * sn * a + c * c * b
+    det = xx * yy - xy * xy
+    covs = torch.stack([xx, xy, yy], 1).float()
+    conics = torch.stack([yy / det, -xy / det, xx / det], 1).float()
+    values = torch.randn(P, C, generator=g).float()
+    return means.float(), values, covs, conics, syn.samples(n, 2, seed=seed + 1)
 
 
 def agg_problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0, radius=(0.3, 1.2), centre=0.0):

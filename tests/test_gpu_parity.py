@@ -84,6 +84,16 @@ def test_parity_small_gaussians_fine_cells(dgs, oracle, function):
 
 
 @pytest.mark.parametrize("function", FUNCS)
+def test_parity_thin_anisotropic(dgs, oracle, function):
+    """Thin rotated Gaussians near the seams (cases.thin_case): the sub-cell lists' slices and
+    the per-row cut ranges at high anisotropy, forward and backward against the oracle."""
+    means, values, covs, conics, samples = cases.thin_case()
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(samples.shape[0], K, 1, seed=152)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
+@pytest.mark.parametrize("function", FUNCS)
 def test_parity_edge_cases(dgs, oracle, function):
     """Torus wrap at +-1, full-range Gaussian, det == 0, non-PD conic, radius floor."""
     means, values, covs, conics, samples = cases.edge_case()
