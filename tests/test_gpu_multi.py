@@ -64,6 +64,13 @@ def test_multi_edge_and_seam(dgs, oracle, functions):
     _check(dgs, oracle, functions, *cases.seam_case(D=2, C=1), seed=41)
 
 
+@pytest.mark.parametrize("functions", [tuple(NAMES)])
+def test_multi_thin_anisotropic(dgs, oracle, functions):
+    """Thin rotated Gaussians (cases.thin_case): the fused moment-form backward and the fused
+    forward next to the reference-literal path of the ill-conditioned conics."""
+    _check(dgs, oracle, functions, *cases.thin_case(P=3000, n=20000), seed=51)
+
+
 def test_multi_order_and_fallback(dgs, oracle):
     """Outputs come back in the order asked; C > 1 (no fused kernel) runs the per-function
     kernels in turn and adds their gradients."""

@@ -83,13 +83,14 @@ def test_parity_small_gaussians_fine_cells(dgs, oracle, function):
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
-@pytest.mark.parametrize("function", FUNCS)
-def test_parity_thin_anisotropic(dgs, oracle, function):
+@pytest.mark.parametrize("function,C", [(f, 1) for f in FUNCS] + [("gaussian", 3), ("laplacian", 16)])
+def test_parity_thin_anisotropic(dgs, oracle, function, C):
     """Thin rotated Gaussians near the seams (cases.thin_case): the sub-cell lists' slices and
-    the per-row cut ranges at high anisotropy, forward and backward against the oracle."""
-    means, values, covs, conics, samples = cases.thin_case()
+    the per-row cut ranges at high anisotropy, forward and backward against the oracle; C = 3 and
+    16 take the lane-per-sample / matrix-core forwards and the literal backward terms."""
+    means, values, covs, conics, samples = cases.thin_case(C=C)
     K = syn.out_components(function, 2)
-    dL = syn.grad_out(samples.shape[0], K, 1, seed=152)
+    dL = syn.grad_out(samples.shape[0], K, C, seed=152)
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
