@@ -133,6 +133,23 @@ def thin_case(P=6000, n=40000, C=1, seed=151):
     return means.float(), values, covs, conics, syn.samples(n, 2, seed=seed + 1)
 
 
+def clustered_case(P=4000, n=30000, C=1, seed=161):
+    """Strongly non-uniform densities: 70 % of the samples in a blob of sigma 0.03 and a third of
+    the Gaussians around it (the fine cells are sized for the AVERAGE density, so the blob's cells
+    hold thousands of samples: many forward sub units and long backward sample walks per cell),
+    the rest uniform."""
+    g = torch.Generator().manual_seed(seed)
+    nb = int(0.7 * n)
+    blob = torch.tensor([0.3, -0.2], dtype=torch.float64) + 0.03 * torch.randn(nb, 2, generator=g, dtype=torch.float64)
+    rest = torch.rand(n - nb, 2, generator=g, dtype=torch.float64) * 2 - 1
+    samples = torch.cat([blob, rest]).clamp(-1.0, 0.999).float()
+    samples = samples[torch.randperm(n, generator=g)]
+    means, values, covs, conics = syn.gaussians(P, 2, C, seed=seed + 1)
+    k = P // 3
+    means[:k] = (torch.tensor([0.3, -0.2]) + 0.05 * torch.randn(k, 2, generator=g)).float()
+    return means, values, covs, conics, samples
+
+
 def agg_problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0, radius=(0.3, 1.2), centre=0.0):
     """aggregate_neighbors inputs (aggregate_neighbors.cu:323-475): means, conics, radii and the
     feature tensors.  Gaussians 0-2 have radius 0 (absent from every list); Gaussian 5 has a

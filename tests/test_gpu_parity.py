@@ -94,6 +94,16 @@ def test_parity_thin_anisotropic(dgs, oracle, function, C):
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
+@pytest.mark.parametrize("function,C", [("gaussian", 1), ("third", 1), ("derivative", 5)])
+def test_parity_clustered(dgs, oracle, function, C):
+    """A dense blob of samples and Gaussians in a uniform background (cases.clustered_case):
+    cells far above the target occupancy, many sub units per sub-cell."""
+    means, values, covs, conics, samples = cases.clustered_case(C=C)
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(samples.shape[0], K, C, seed=162)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
 @pytest.mark.parametrize("function", FUNCS)
 def test_parity_edge_cases(dgs, oracle, function):
     """Torus wrap at +-1, full-range Gaussian, det == 0, non-PD conic, radius floor."""
