@@ -42,7 +42,7 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a)).cuda()
 
 
-def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared_atol=1e-5):
+def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared_atol=1e-5, lit_scale=1.0):
     idx_r, rg_r, X_r, dn_r, inv_r = oracle.agg_preprocess(means, conics, radii)
     idx, rg, X, dn, inv = dgs._C.preprocess_aggregate(_cuda(means), _cuda(conics), _cuda(radii), False)
     torch.cuda.synchronize()
@@ -62,7 +62,8 @@ def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared
     close(f.cpu().numpy(), f_r, 1e-5, 1e-6, "factors")
     close(out.cpu().numpy(), out_r, 1e-5, 1e-6, "neighbor_features")
     out_lit = oracle.agg_forward(*args, idx_r, rg_r, X_r, dn_r, inv_r)[3]
-    close(out.cpu().numpy(), out_lit, LIT_RTOL, LIT_ATOL * 0.1, "neighbor_features vs the literal order")
+    close(out.cpu().numpy(), out_lit, LIT_RTOL * lit_scale, LIT_ATOL * 0.1 * lit_scale,
+          "neighbor_features vs the literal order")
     if not check_grads:
         return
     g = np.random.default_rng(seed).normal(size=out_r.shape).astype(np.float32)
@@ -76,8 +77,9 @@ def _run(dgs, oracle, means, conics, radii, fe, seed=5, check_grads=True, shared
     lit = oracle.agg_backward(*args, idx_r, rg_r, X_r, dn_r, w_r, e_r, f_r, inv_r, g)
     for name, a, b in zip(AGG_FEATURES, got, lit):
         shared = name in ("frequencies", "distance_transform")
-        tol = max(LIT_SHARED, 10 * shared_atol) if shared else LIT_RTOL
-        close(a.cpu().numpy().reshape(b.shape), b, tol, tol if shared else LIT_ATOL, f"d/d{name} vs the literal order")
+        tol = max(LIT_SHARED, 10 * shared_atol) if shared else LIT_RTOL * lit_scale
+        close(a.cpu().numpy().reshape(b.shape), b, tol, tol if shared else LIT_ATOL * lit_scale,
+              f"d/d{name} vs the literal order")
 
 
 @pytest.mark.parametrize("D", [1, 2])
@@ -269,3 +271,14 @@ def test_aggregate_transposed_lists_follow_the_indices(dgs, oracle):
         if name in ("features", "keys"):
             close(a.cpu().numpy().reshape(b.shape), b, 1e-5, 1e-5, f"d/d{name} after the in-place change")
             assert torch.equal(a, a2), f"d/d{name}: clone vs in-place tensor"
+
+
+def test_aggregate_long_rows_gradients(dgs, oracle):
+    """~2500 neighbours per row (beyond one wave's 2048-id sort: rows emitted in id windows) with
+    gradients: the transposed backward's per-neighbour sums run over as many incoming slots.
+    Against the exact sums the usual 1e-5; the bound against the reference's literal float order
+    is 3x the default: that order's own rounding grows with the row length (2.5x the rows the
+    default was set on, profiles/r02_agg_margins.json)."""
+    means, conics, radii, fe = agg_problem(P=2600, D=2, L=16, K=16, F=4, seed=42, spread=0.05,
+                                           radius=(0.8, 1.2))
+    _run(dgs, oracle, means, conics, radii, fe, shared_atol=3e-5, lit_scale=3.0)
