@@ -150,6 +150,29 @@ def clustered_case(P=4000, n=30000, C=1, seed=161):
     return means, values, covs, conics, samples
 
 
+def mixed_scales_case(P=3000, n=25000, C=1, seed=171):
+    """Scales from 1e-4 to 0.2 (log-uniform) with axis ratios up to 5 and random rotations: tiny
+    Gaussians under the radius floor, culled ones, and unculled ones whose cut exceeds half the
+    period (full-tile lists) in one problem; one sample in eight duplicated 4 times (zero-width
+    sub-cell boxes)."""
+    g = torch.Generator().manual_seed(seed)
+    means = torch.rand(P, 2, generator=g, dtype=torch.float64) * 2 - 1
+    s_min = 10 ** (-4 + 2.7 * torch.rand(P, generator=g, dtype=torch.float64))
+    s_max = s_min * (1 + 4 * torch.rand(P, generator=g, dtype=torch.float64))
+    th = torch.rand(P, generator=g, dtype=torch.float64) * math.pi
+    c, sn = torch.cos(th), torch.sin(th)
+    a, b = s_max ** 2, s_min ** 2
+    xx, xy, yy = c * c * a + sn * sn * b, c * sn * (a - b), sn * sn * a + c * c * b
+    det = xx * yy - xy * xy
+    covs = torch.stack([xx, xy, yy], 1).float()
+    conics = torch.stack([yy / det, -xy / det, xx / det], 1).float()
+    values = torch.randn(P, C, generator=g).float()
+    samples = syn.samples(n, 2, seed=seed + 1)
+    k = n // 8
+    samples[n - 4 * k:] = samples[:k].repeat(4, 1)
+    return means.float(), values, covs, conics, samples
+
+
 def agg_problem(P=120, D=2, L=6, K=5, F=3, seed=0, spread=1.0, radius=(0.3, 1.2), centre=0.0):
     """aggregate_neighbors inputs (aggregate_neighbors.cu:323-475): means, conics, radii and the
     feature tensors.  Gaussians 0-2 have radius 0 (absent from every list); Gaussian 5 has a

@@ -104,6 +104,16 @@ def test_parity_clustered(dgs, oracle, function, C):
     _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
 
 
+@pytest.mark.parametrize("function,C", [(f, 1) for f in FUNCS] + [("gaussian", 16)])
+def test_parity_mixed_scales(dgs, oracle, function, C):
+    """Scales over three decades, unculled and floor-radius Gaussians together, duplicated
+    samples (cases.mixed_scales_case)."""
+    means, values, covs, conics, samples = cases.mixed_scales_case(C=C)
+    K = syn.out_components(function, 2)
+    dL = syn.grad_out(samples.shape[0], K, C, seed=172)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+
+
 @pytest.mark.parametrize("function", FUNCS)
 def test_parity_edge_cases(dgs, oracle, function):
     """Torus wrap at +-1, full-range Gaussian, det == 0, non-PD conic, radius floor."""
