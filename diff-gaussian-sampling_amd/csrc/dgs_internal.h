@@ -20,7 +20,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 6;
+constexpr uint32_t kVersion = 7;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -99,6 +99,7 @@ struct Header {
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     int64_t fsub_cap, esub_cap;
+    uint32_t zero[4];  // always 0: the "inputs differ" word of calls whose inputs the caller vouches for
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");

@@ -406,11 +406,29 @@ __device__ inline int gather_reach(const Geom &G, const float *m, float r, const
 // order (sampler_impl.cu:94-124), restricted to non-empty cells that pass the exact cull.
 // skip_local: leave out the cells of the direct local tile visits (a regular Gaussian's:
 // k_gather makes them).
+// Per tile, whether its fallback cell holds samples, as bits in LDS (fbits; one block-wide pass:
+// enumerate_fine asks it for every tile a Gaussian visits).  NULL when the grid is too large.
+constexpr int kFbWords = 256;
+__device__ inline const uint32_t *fallback_bits(uint32_t *lds, const Geom &G, const int32_t *__restrict__ sbeg,
+                                                const int32_t *__restrict__ send) {
+    if (G.T > kFbWords * 32) return nullptr;
+    const int nw = (G.T + 31) >> 5;
+    for (int w = threadIdx.x; w < nw; w += blockDim.x) lds[w] = 0u;
+    __syncthreads();
+    for (int t = threadIdx.x; t < G.T; t += blockDim.x) {
+        const int64_t fb = (int64_t)t * G.CT + (G.CT - 1);
+        if (send[fb] > sbeg[fb]) atomicOr(&lds[t >> 5], 1u << (t & 31));
+    }
+    __syncthreads();
+    return lds;
+}
+
 template <class Emit>
 __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, const float *con, const Cut &k,
                                       bool skip_local, const int32_t *__restrict__ sbeg,
                                       const int32_t *__restrict__ send,
-                                      const float4 *__restrict__ box, uint32_t id, Emit emit) {
+                                      const float4 *__restrict__ box, const uint32_t *fbits, uint32_t id,
+                                      Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
     const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
@@ -474,7 +492,8 @@ __device__ inline void enumerate_fine(const Geom &G, const float *m, float r, co
                 }
             }
             const uint32_t fb = base + (uint32_t)(G.CT - 1);
-            if (send[fb] > sbeg[fb]) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
+            const bool fb_full = fbits ? ((fbits[key >> 5] >> (key & 31)) & 1u) != 0u : send[fb] > sbeg[fb];
+            if (fb_full) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
         }
 }
 
@@ -497,7 +516,7 @@ __device__ inline bool local_rows(const Geom &G, const float *m, float r, const 
     // match enumerate_fine bit for bit (it skips exactly these visits and emits all others); the
     // margins of the cut cover the rounding either way.
     const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
-    const double BS = (double)kTile, slack = kCellSlack * G.fs, ifs = G.ifs;
+    const double BS = (double)kTile, slack = kCellSlack * G.fs;
     // (widened by a cell: every tile axis_setup can give a cell is among them)
     const double wx = k.e[0] + slack + k.epsx[0] + G.fs;
     const int ta = max(max(kr.x0, 0), (int)floor((k.md[0] - wx) / BS));
@@ -511,35 +530,48 @@ __device__ inline bool local_rows(const Geom &G, const float *m, float r, const 
         xlo[t] = 1; xhi[t] = 0;
     }
     if (tb > ta + 1) return false;  // (wider than two tiles: not for this path)
-    const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
-    const double c0 = k.c0, c1 = k.c1, c2 = k.c2, det = c0 * c2 - c1 * c1;
-    const double e0 = sqrt(qc * c2 / det), ic0 = 1.0 / c0;
-    const double yu0 = -c1 * e0 / c2, yl0 = c1 * e0 / c2, qcc0 = qc * c0;
+    // The row slices in fp32 (fp64 sqrt / division sequences were most of this kernel's issue
+    // slots): coordinates relative to the tile origin, and margins that cover the fp32 rounding
+    // -- the slice ends' error is at most ~sqrt(8 eps) of the cut's half-width where the sqrt
+    // argument cancels (the ellipse's top and bottom), so tol = 2e-3 e0 + 1e-5 (1 + |x|) in
+    // displacement units, a few thousandths of a cell.  Extra cells only add exact zeros.
+    const float qc = (float)(kQCut * (1.0 + 1e-6));
+    const float c0 = (float)k.c0, c1 = (float)k.c1, c2 = (float)k.c2;
+    const float det = (float)(k.c0 * k.c2 - k.c1 * k.c1);
+    const float e0 = (float)sqrt((double)qc * k.c2 / (k.c0 * k.c2 - k.c1 * k.c1)), ic0 = 1.0f / c0;
+    const float yu0 = -c1 * e0 / c2, yl0 = c1 * e0 / c2, qcc0 = qc * c0;
+    const float fs = (float)G.fs, ifsf = (float)G.ifs, slackf = (float)slack;
+    const float e1 = (float)k.e[1], eps1 = (float)k.epsx[1] + 1e-6f, eps0 = (float)k.epsx[0] + 1e-6f;
+    const float tol0 = 2e-3f * e0 + 1e-5f;
+    float A0[2], B0[2];  // per tile of the x range: the tile-relative mean +- the margins
+    for (int t = 0; t < 2; ++t) {
+        const float md0 = (float)(k.md[0] - (ta + t) * BS);
+        A0[t] = md0 - slackf - eps0;
+        B0[t] = md0 + slackf + eps0;
+    }
     uint32_t written = 0u;  // bit KR + dy: row home_y + dy stored
     for (int ty = max(kr.y0, 0); ty < min(kr.y1, G.grid[1]); ++ty) {  // direct visits only
         int ks1, flo1, fhi1;
         if (!axis_setup(G, k, 1, ty, ks1, flo1, fhi1) || ks1 != 0) continue;
-        const double o1 = ty * BS;
+        const float md1 = (float)(k.md[1] - ty * BS);
         for (int fy = flo1; fy <= fhi1; ++fy) {
-            double ya = k.md[1] - (o1 + (fy + 1) * G.fs + slack) - k.epsx[1];
-            double yb = k.md[1] - (o1 + fy * G.fs - slack) + k.epsx[1];
-            ya = fmax(ya, -k.e[1]);
-            yb = fmin(yb, k.e[1]);
+            float ya = md1 - ((fy + 1) * fs + slackf) - eps1;
+            float yb = md1 - (fy * fs - slackf) + eps1;
+            ya = fmaxf(ya, -e1);
+            yb = fminf(yb, e1);
             if (ya > yb) continue;
-            const double yu = fmin(fmax(yu0, ya), yb), yl = fmin(fmax(yl0, ya), yb);
-            const double xu = (-c1 * yu + sqrt(fmax(qcc0 - det * yu * yu, 0.0))) * ic0;
-            const double xl = (-c1 * yl - sqrt(fmax(qcc0 - det * yl * yl, 0.0))) * ic0;
-            const double tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
+            const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(yl0, ya), yb);
+            const float xu = (-c1 * yu + sqrtf(fmaxf(qcc0 - det * yu * yu, 0.0f))) * ic0;
+            const float xl = (-c1 * yl - sqrtf(fmaxf(qcc0 - det * yl * yl, 0.0f))) * ic0;
+            const float tol = tol0 + 1e-5f * (fabsf(xu) + fabsf(xl));
             int lo = 0xffff, hi = 0;
             for (int t = 0; t < 2; ++t) {
                 if (xlo[t] > xhi[t]) continue;
                 const int tx = ta + t;
-                const double o0 = tx * BS;
-                const double A = k.md[0] - o0 - slack - k.epsx[0], B = k.md[0] - o0 + slack + k.epsx[0];
-                const double fa = ceil((A - (xu + tol)) * ifs - 1.0 - 1e-9);
-                const double fb = floor((B - (xl - tol)) * ifs + 1e-9);
-                const int fxl = fa > (double)xlo[t] ? (fa > (double)G.n ? G.n : (int)fa) : xlo[t];
-                const int fxh = fb < (double)xhi[t] ? (fb < -1.0 ? -1 : (int)fb) : xhi[t];
+                const float fa = ceilf((A0[t] - (xu + tol)) * ifsf - 1.0f - 1e-4f);
+                const float fb = floorf((B0[t] - (xl - tol)) * ifsf + 1e-4f);
+                const int fxl = fa > (float)xlo[t] ? (fa > (float)G.n ? G.n : (int)fa) : xlo[t];
+                const int fxh = fb < (float)xhi[t] ? (fb < -1.0f ? -1 : (int)fb) : xhi[t];
                 if (fxl > fxh) continue;
                 const int a = tx * G.n + fxl, b = tx * G.n + fxh;
                 if (lo > hi) { lo = a; hi = b; }
@@ -606,9 +638,13 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                                                        const int32_t *__restrict__ send, const float4 *__restrict__ box,
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
-                                                       float2 *__restrict__ igm, float4 *__restrict__ igc) {
+                                                       float2 *__restrict__ igm, float4 *__restrict__ igc,
+                                                       unsigned long long *__restrict__ nunsafe) {
+    __shared__ uint32_t fbl[kFbWords];
+    const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int reach = 0;
+    uint32_t nu = 0;  // kUnsafe entries (k_fine_fill emits the same ones): read back at the sync
     if (i < P) {
         const int64_t g = perm[i];
         const float4 ga = grec[2 * g], gb2 = grec[2 * g + 1];  // (k_gauss_prep's record: one line)
@@ -625,14 +661,20 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                 const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) * G.ifs);
                 if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
             }
-            enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, (uint32_t)i,
-                           [&](uint32_t, uint32_t) { ++n; });
+            enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, fbits, (uint32_t)i,
+                           [&](uint32_t, uint32_t v) { ++n; nu += (v & kUnsafe) ? 1u : 0u; });
         }
         counts[i] = n;
         greach[i] = (int8_t)reach;
     }
-    for (int off = kWave / 2; off > 0; off >>= 1) reach = max(reach, __shfl_xor(reach, off));
-    if ((threadIdx.x & (kWave - 1)) == 0 && reach > 0) atomicMax(rmax, reach);
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        reach = max(reach, __shfl_xor(reach, off));
+        nu += __shfl_xor(nu, off);
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0) {
+        if (reach > 0) atomicMax(rmax, reach);
+        if (nu) atomicAdd(nunsafe, (unsigned long long)nu);
+    }
 }
 
 // The block's Gaussians own one contiguous output range (offs is an exclusive scan in i
@@ -649,6 +691,8 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, KT *__restrict__ ekeys,
     uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
+    __shared__ uint32_t fbl[kFbWords];
+    const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
     const int64_t i = i0 + threadIdx.x;
     const int64_t ilast = min((int64_t)P, i0 + kFillBlock) - 1;
@@ -663,7 +707,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
         const Cut k = gauss_cut(G, m, c);
         const bool skip = greach[i] > 0;  // (k_fine_count's decision)
         uint64_t o = offs[i];
-        enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
+        enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, fbits, (uint32_t)i, [&](uint32_t cell, uint32_t val) {
             const uint32_t key = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
             if (stage) {
                 skey[o - base] = key;
@@ -824,12 +868,15 @@ __global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_
                          const uint64_t *__restrict__ toffs, const uint64_t *__restrict__ touched,
                          const int *__restrict__ dgrid, const float *__restrict__ doff,
                          const unsigned long long *__restrict__ eg, int64_t *__restrict__ out) {
+    // eg[0]: gathered entries, eg[1]: kUnsafe entries (k_fine_count)
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
     out[0] = P > 0 ? (int64_t)(toffs[P - 1] + touched[P - 1]) : 0;  // num_rendered (sampler_impl.cu:253-257)
     const int64_t es = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;  // sort-path entries
     out[1] = es + (int64_t)*eg;                                             // all entries
     out[4] = es;
-    out[5] = (int64_t)*eg;
+    out[5] = (int64_t)eg[0];
+    out[6] = (int64_t)eg[1];
+    out[7] = 0;
     // the device-computed tile grid (dgs_preprocess_auto): read back with the totals
     int32_t *g = reinterpret_cast<int32_t *>(out + 2);
     g[0] = dgrid ? dgrid[0] : 0;
@@ -897,14 +944,78 @@ __device__ inline bool box_hits_ellipse_f(float xa, float xb, float ya, float yb
     return best <= qcut;
 }
 
-// Sub lists (D = 2), one pass, one wave per cell.  For every entry of the cell list, the
-// sub-cells whose sample box its cut X^T A X <= kQCut meets, tested with the displacement the
-// forward uses: X = m - s, minus the entry's constant wrap shift for kGeneral entries
-// (wrap_shift_f of the mean minus the cell-box centre, exactly as k_forward_t forms it).  kUnsafe
-// entries get no sub-cell (the forward's tail pass adds them per cell).  Sub list k of the cell
-// has the region [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at
-// most every sub list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the
-// flag-free entries and [lmid, lend) the flagged ones.
+// The sub-cells of one cell a cell-list entry's cut X^T A X <= kQCut meets (bit k = sub-cell k),
+// tested with the displacement the forward uses: X = m - s, minus the entry's constant wrap
+// shift for kGeneral entries (wrap_shift_f of the mean minus the cell-box centre, exactly as
+// k_forward_t forms it).  kUnsafe entries get none (the forward's tail pass adds them per cell).
+__device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 *__restrict__ gmean,
+                                             const float4 *__restrict__ gcon, const float4 &bx, const float *ctr,
+                                             const float4 *sb) {
+    if (ent & kUnsafe) return 0u;
+    const uint32_t id = ent & kIdMask;
+    const float2 mm = gmean[id];
+    const float4 cc = gcon[id];
+    const float qc = (float)(kQCut * (1.0 + 1e-4));
+    float sh[2] = {0.0f, 0.0f};
+    if (ent & kGeneral) {
+        sh[0] = wrap_shift_f(mm.x - ctr[0]);
+        sh[1] = wrap_shift_f(mm.y - ctr[1]);
+    }
+    const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
+    // (approximate reciprocals: they only place the edge minima, which are then evaluated
+    // exactly at feasible points; rounding margins from the cell box, which holds every
+    // sub-cell box)
+    const float ic0 = __builtin_amdgcn_rcpf(cc.x), ic2 = __builtin_amdgcn_rcpf(cc.z);
+    const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(bx.x), fabsf(bx.z)));
+    const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(bx.y), fabsf(bx.w)));
+    uint32_t mask = 0u;
+#if DGS_SUB_SLICE
+    // Per sub-row (the union of its two sub-boxes' sample y ranges) the ellipse's slice is one
+    // X0 interval [xl, xu] (row_slice's construction in fp32); a sub-box is hit when its X0
+    // range meets it.  Two slices per entry instead of four box minimisations.  The union band
+    // and the tolerances only widen the lists (the cut itself sits 1 % outside the last live
+    // pair, kQCut).
+    const float c0 = cc.x, c1 = cc.y, c2 = cc.z;
+    const float det = c0 * c2 - c1 * c1;
+    const float ex0 = __builtin_sqrtf(qc * c2 * __builtin_amdgcn_rcpf(det));
+    const float ex1 = __builtin_sqrtf(qc * c0 * __builtin_amdgcn_rcpf(det));
+    const float yu0 = -c1 * ex0 * ic2;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+        const float blo = fminf(sb[2 * r].y, sb[2 * r + 1].y), bhi = fmaxf(sb[2 * r].w, sb[2 * r + 1].w);
+        const float ya = fmaxf(m1 - bhi - e1, -ex1), yb = fminf(m1 - blo + e1, ex1);
+        if (!(ya <= yb)) continue;  // (also: both sub-boxes of the row empty)
+        const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(-yu0, ya), yb);
+        const float xu = (-c1 * yu + __builtin_sqrtf(fmaxf(qc * c0 - det * yu * yu, 0.0f))) * ic0;
+        const float xl = (-c1 * yl - __builtin_sqrtf(fmaxf(qc * c0 - det * yl * yl, 0.0f))) * ic0;
+        const float tol = 1e-5f * (1.0f + fabsf(xu) + fabsf(xl));
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float4 q = sb[2 * r + h];
+            if (q.x <= q.z && m0 - q.z - e0 <= xu + tol && m0 - q.x + e0 >= xl - tol) mask |= 1u << (2 * r + h);
+        }
+    }
+#else
+    for (int k = 0; k < kSubPerCell; ++k) {
+        const float4 q = sb[k];
+        if (!(q.x <= q.z)) continue;  // empty sub-cell
+        if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y, cc.z, ic0,
+                               ic2, qc))
+            mask |= 1u << k;
+    }
+#endif
+    return mask;
+}
+
+// Sub lists (D = 2), one block per cell.  Sub list k of the cell has the region
+// [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
+// list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
+// entries and [lmid, lend) the flagged ones.  Phase 1: the block's 256 threads compute the
+// entries' sub-cell masks (independent per entry: the gathers of many entries in flight at
+// once) into LDS; phase 2: wave k compacts sub list k in order (ballots over the staged masks).
+// (Before: one wave per cell walked its list 64 entries at a time, two dependent memory round
+// trips per group with nothing else in flight.)
+constexpr int kSubStage = 2048;
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
                                                       const int32_t *__restrict__ gmid,
                                                       const int32_t *__restrict__ gend,
@@ -915,102 +1026,65 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float4 *__restrict__ sbox, int CT,
                                                       int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
                                                       int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent) {
-    const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
-    const int lane = threadIdx.x & (kWave - 1);
+    static_assert(kSubPerCell == kWavesPerBlock, "one wave per sub list");
+    __shared__ uint32_t sent[kSubStage];
+    __shared__ uint8_t smask[kSubStage];
+    const int c = block_unit_index();  // (XCD remap: neighbouring cells share Gaussians)
     if (c >= ncells) return;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int k = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // this wave's sub list
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
-    const int64_t base = (int64_t)kSubPerCell * b;
+    uint32_t nff = 0, nfl = 0;
+    const int64_t base = (int64_t)kSubPerCell * b + (int64_t)k * n;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
         const float ctr[2] = {0.5f * (bx.x + bx.z), 0.5f * (bx.y + bx.w)};  // = cell_center
         float4 sb[kSubPerCell];
-        for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
-        const float qc = (float)(kQCut * (1.0 + 1e-4));
-        for (int j0 = b; j0 < e; j0 += kWave) {
-            const int j = j0 + lane;
-            uint32_t mask = 0u, ent = 0u;
-            if (j < e) {
-                ent = entries[j];
-                if (!(ent & kUnsafe)) {
-                    const uint32_t id = ent & kIdMask;
-                    const float2 mm = gmean[id];
-                    const float4 cc = gcon[id];
-                    float sh[2] = {0.0f, 0.0f};
-                    if (ent & kGeneral) {
-                        sh[0] = wrap_shift_f(mm.x - ctr[0]);
-                        sh[1] = wrap_shift_f(mm.y - ctr[1]);
-                    }
-                    const float m0 = mm.x - sh[0], m1 = mm.y - sh[1];  // (exact: Sterbenz / even shifts)
-                    // (approximate reciprocals: they only place the edge minima, which are then
-                    // evaluated exactly at feasible points; rounding margins from the cell box,
-                    // which holds every sub-cell box)
-                    const float ic0 = __builtin_amdgcn_rcpf(cc.x), ic2 = __builtin_amdgcn_rcpf(cc.z);
-                    const float e0 = 1e-6f * (1.0f + fabsf(mm.x) + fmaxf(fabsf(bx.x), fabsf(bx.z)));
-                    const float e1 = 1e-6f * (1.0f + fabsf(mm.y) + fmaxf(fabsf(bx.y), fabsf(bx.w)));
-#if DGS_SUB_SLICE
-                    // Per sub-row (the union of its two sub-boxes' sample y ranges) the ellipse's
-                    // slice is one X0 interval [xl, xu] (row_slice's construction in fp32); a
-                    // sub-box is hit when its X0 range meets it.  Two slices per entry instead of
-                    // four box minimisations.  The union band and the tolerances only widen the
-                    // lists (the cut itself sits 1 % outside the last live pair, kQCut).
-                    const float c0 = cc.x, c1 = cc.y, c2 = cc.z;
-                    const float det = c0 * c2 - c1 * c1;
-                    const float ex0 = __builtin_sqrtf(qc * c2 * __builtin_amdgcn_rcpf(det));
-                    const float ex1 = __builtin_sqrtf(qc * c0 * __builtin_amdgcn_rcpf(det));
-                    const float yu0 = -c1 * ex0 * ic2;
 #pragma unroll
-                    for (int r = 0; r < 2; ++r) {
-                        const float blo = fminf(sb[2 * r].y, sb[2 * r + 1].y), bhi = fmaxf(sb[2 * r].w, sb[2 * r + 1].w);
-                        const float ya = fmaxf(m1 - bhi - e1, -ex1), yb = fminf(m1 - blo + e1, ex1);
-                        if (!(ya <= yb)) continue;  // (also: both sub-boxes of the row empty)
-                        const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(-yu0, ya), yb);
-                        const float xu = (-c1 * yu + __builtin_sqrtf(fmaxf(qc * c0 - det * yu * yu, 0.0f))) * ic0;
-                        const float xl = (-c1 * yl - __builtin_sqrtf(fmaxf(qc * c0 - det * yl * yl, 0.0f))) * ic0;
-                        const float tol = 1e-5f * (1.0f + fabsf(xu) + fabsf(xl));
-#pragma unroll
-                        for (int h = 0; h < 2; ++h) {
-                            const float4 q = sb[2 * r + h];
-                            if (q.x <= q.z && m0 - q.z - e0 <= xu + tol && m0 - q.x + e0 >= xl - tol)
-                                mask |= 1u << (2 * r + h);
-                        }
-                    }
-#else
-                    for (int k = 0; k < kSubPerCell; ++k) {
-                        const float4 q = sb[k];
-                        if (!(q.x <= q.z)) continue;  // empty sub-cell
-                        if (box_hits_ellipse_f(m0 - q.z - e0, m0 - q.x + e0, m1 - q.w - e1, m1 - q.y + e1, cc.x, cc.y,
-                                               cc.z, ic0, ic2, qc))
-                            mask |= 1u << k;
-                    }
-#endif
+        for (int q = 0; q < kSubPerCell; ++q) sb[q] = sbox[c * kSubPerCell + q];
+        for (int cs = b; cs < e; cs += kSubStage) {
+            const int ce = min(e, cs + kSubStage);
+            // phase 1: two entries per thread and pass, both gathers in flight
+            for (int j = cs + (int)threadIdx.x; j < ce; j += 2 * kBlock) {
+                const int j2 = j + kBlock;
+                const uint32_t ea = entries[j];
+                const uint32_t eb = j2 < ce ? entries[j2] : kUnsafe;
+                const uint32_t ma = sub_mask(ea, gmean, gcon, bx, ctr, sb);
+                const uint32_t mb = sub_mask(eb, gmean, gcon, bx, ctr, sb);
+                sent[j - cs] = ea;
+                smask[j - cs] = (uint8_t)ma;
+                if (j2 < ce) {
+                    sent[j2 - cs] = eb;
+                    smask[j2 - cs] = (uint8_t)mb;
                 }
             }
-            const bool ff = j < m_;
-            for (int k = 0; k < kSubPerCell; ++k) {
-                const bool hit = (mask >> k) & 1u;
+            __syncthreads();
+            // phase 2: sub list k in cell-list order
+            for (int j0 = cs; j0 < ce; j0 += kWave) {
+                const int j = j0 + lane;
+                const bool hit = j < ce && ((smask[j - cs] >> k) & 1u);
+                const bool ff = j < m_;
                 const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
                 if (hit) {
                     const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
                     // flag-free entries precede the flagged ones in the cell list, so once a group
                     // holds a flagged entry the flag-free count is final -- this group's own
                     // flag-free hits included: the region fills [flag-free | flagged] in order
-                    const uint32_t nffk = nff[k] + (uint32_t)__popcll(bf);
-                    const int64_t o = base + (int64_t)k * n + (ff ? nff[k] : nffk + nfl[k]) + below;
-                    sub_ent[o] = ent;
+                    const uint32_t nffk = nff + (uint32_t)__popcll(bf);
+                    sub_ent[base + (ff ? nff : nffk + nfl) + below] = sent[j - cs];
                 }
-                nff[k] += (uint32_t)__popcll(bf);
-                nfl[k] += (uint32_t)__popcll(bl);
+                nff += (uint32_t)__popcll(bf);
+                nfl += (uint32_t)__popcll(bl);
             }
+            __syncthreads();
         }
     }
-    if (lane == 0)
-        for (int k = 0; k < kSubPerCell; ++k) {
-            const int a = (int)(base + (int64_t)k * n);
-            lbeg[c * kSubPerCell + k] = a;
-            lmid[c * kSubPerCell + k] = a + (int)nff[k];
-            lend[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);
-        }
+    if (lane == 0) {
+        const int a = (int)base;
+        lbeg[c * kSubPerCell + k] = a;
+        lmid[c * kSubPerCell + k] = a + (int)nff;
+        lend[c * kSubPerCell + k] = a + (int)(nff + nfl);
+    }
 }
 
 // Forward sub units per sub-cell (samples and entries both present): ceil(pairs / kSubPairs),
@@ -1473,13 +1547,13 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *perm = ca.take<uint32_t>(P);
     uint64_t *touched = ca.take<uint64_t>(P), *fcount = ca.take<uint64_t>(P), *foffs = ca.take<uint64_t>(P);
     uint64_t *toffs = ca.take<uint64_t>(P);
-    int64_t *totals = ca.take<int64_t>(6);
+    int64_t *totals = ca.take<int64_t>(8);
     const int HK = home_w * home_h;  // (home cell keys; HK = absent)
     int8_t *greach = ca.take<int8_t>(P);
     uint32_t *lrows = ca.take<uint32_t>((size_t)kGatherRows * P);
     uint32_t *hstart = ca.take<uint32_t>((size_t)HK + 1), *gcnt = ca.take<uint32_t>(ncells);
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
-    unsigned long long *eg = ca.take<unsigned long long>(1);
+    unsigned long long *eg = ca.take<unsigned long long>(2);  // [gathered entries, kUnsafe entries]
     int32_t *rmax = ca.take<int32_t>(1);
     float2 *igm = ca.take<float2>(P);
     float4 *igc = ca.take<float4>(P);
@@ -1534,7 +1608,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(rbuf, (size_t)G.T * 8 + 8);
         zl.add(srbuf, (size_t)G.T * 8 + 8);
         zl.add(cnt2, sizeof(uint32_t) * kGatherRows * (size_t)ncells);
-        zl.add(eg, 8);
+        zl.add(eg, 16);
         zl.add(rmax, 4);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
@@ -1571,7 +1645,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                    hbits, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, grec, cell_sbeg,
-                                                cell_send, cell_box, fcount, greach, lrows, rmax, igm, igc);
+                                                cell_send, cell_box, fcount, greach, lrows, rmax, igm, igc, eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
                                                kWavesPerBlock - 1) / kWavesPerBlock);
@@ -1654,7 +1728,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
-    int64_t htot[6] = {0, 0, 0, 0, 0, 0};
+    int64_t htot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
     // the one host sync (num_rendered is a Python int): on an event right after the copy, so the
     // speculative phase B enqueued behind it keeps the GPU busy while the host reads the totals
@@ -1682,6 +1756,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         }
     }
     if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries");
+    // the D = 2 sub lists live at 4 gbeg + k n in sub_ent, addressed by int32 (sub_lbeg/lmid/lend)
+    if (nsub && kSubPerCell * E >= (1LL << 31) - 64)
+        return fail(DGS_ERR_ARG, "too many fine (Gaussian, cell) entries for the sub-cell lists (4 E >= 2^31)");
     if (R >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "num_rendered exceeds 2^31 (32-bit tile lists)");
     size_spec_put(P, N, D, E, R);
     if (E > B.Ecap || R > B.Rcap) {  // no speculation, or this call's lists do not fit it
@@ -1755,15 +1832,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                     boff, fwd_units, bwd_units, counters);
     DGS_LAUNCH_CHECK(s, debug);
     if (nsub) {  // the forward's sub lists and sub units (D = 2)
-        const unsigned wb = (unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave));
         const float2 *gmean = reinterpret_cast<const float2 *>(gbuf + L.o_gmean);
         const float4 *gcon = reinterpret_cast<const float4 *>(gbuf + L.o_gcon);
         int32_t *sub_lbeg = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lbeg);
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
-        k_sub_lists<<<wb, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box,
-                                          sub_box, G.CT, sub_lbeg, sub_lmid, sub_lend, sub_ent);
+        k_sub_lists<<<(unsigned)ncells, kBlock, 0, s>>>(ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon,
+                                                        cell_box, sub_box, G.CT, sub_lbeg, sub_lmid, sub_lend, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);
         k_sub_ucnt<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, sub_send, sub_lbeg, sub_lend, B.sucnt);
         DGS_LAUNCH_CHECK(s, debug);
@@ -1831,10 +1907,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
 
     // launch-size hint: the unit capacities (the exact counts stay on the device and the render
     // kernels grid-stride over them; surplus waves exit at once), so the binning needs no second
-    // host sync.  nunsafe = -1: unknown on the host (the tail pass checks the device counter).
+    // host sync.  nunsafe: the kUnsafe entry count k_fine_count read back at the sync (0: the
+    // forward's unsafe-only tail pass is not launched).
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
-    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = -1;
+    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6];
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R;

@@ -82,8 +82,14 @@ __host__ __device__ constexpr bool pair_rows() { return srow_stride<FN, D, CB>()
 
 template <int FN, int D, int CB>
 __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
-                               const DLs dls, int C, int cbase, float *__restrict__ rows) {
+                               const DLs dls, int C, int cbase, float *__restrict__ rows,
+                               float4 *__restrict__ acc_zero, int64_t acc_n4, uint32_t *__restrict__ flag_zero) {
     const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the gradient sums' zero-fill and the call's input-check word (k_verify runs next), folded
+    // into this launch (first channel block only)
+    if (flag_zero && j == 0) *flag_zero = 0u;
+    if (acc_zero)
+        for (int64_t k = j; k < acc_n4; k += (int64_t)gridDim.x * blockDim.x) acc_zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr bool PK = pair_rows<FN, D, CB>();
     if (j >= (PK ? (int64_t)(N + 1) / 2 * 2 : (int64_t)N)) return;
     constexpr int M = fn_mask(FN), RSS = srow_stride<FN, D, CB>();
@@ -1331,6 +1337,7 @@ static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_
 
 struct Call {
     int FN, P, D, N, C;
+    uint32_t opts;  // dgs_sample_flag bits
     const float *means, *values, *conics, *samples;
     DLs dls;
     const char *gb, *sb;
@@ -1350,11 +1357,23 @@ static RefCall ref_call(const Call &a, float *acc, const uint32_t *flag, int cba
                    a.P, a.N, a.C, cbase, R, a.s, a.debug};
 }
 
+// The word the render kernels test for "the call's inputs differ from the binned ones": the
+// call's own check word, or -- when the caller vouches for its inputs (DGS_SAMPLE_INPUTS_BINNED)
+// -- the binning header's always-zero word (no check, no call-time launches).
+static uint32_t *dirty_word(const Call &a, uint32_t *flag) {
+    if (!(a.opts & DGS_SAMPLE_INPUTS_BINNED)) return flag;
+    return reinterpret_cast<uint32_t *>(const_cast<char *>(a.gb) + offsetof(Header, zero));
+}
+
 template <int FN, int D, int CB>
 static int run_forward(const Call &a) {
     const WsLayout w = ws_layout(FN, a.P, D, a.N, a.C, false);
     float *grows = reinterpret_cast<float *>(a.ws);
-    uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
+    const bool binned = (a.opts & DGS_SAMPLE_INPUTS_BINNED) != 0;
+    // rows of an earlier call on this workspace (one channel block: the rows hold all of C)
+    const bool rows_valid = (a.opts & DGS_SAMPLE_ROWS_VALID) && a.C <= CB;
+    uint32_t *const check = reinterpret_cast<uint32_t *>(a.ws + w.flag);
+    uint32_t *const flag = dirty_word(a, check);
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false);
     const unsigned sub_blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false, kWavesPerBlock, true);
     constexpr bool T = fwd_transposed<FN, D, CB>(), MX = !T && fwd_mfma<FN, D, CB>();
@@ -1362,10 +1381,14 @@ static int run_forward(const Call &a) {
     hint.nunsafe = -1;
     const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
-                                                                   cbase == 0 ? flag : nullptr);
-        DGS_LAUNCH_CHECK(a.s, a.debug);
-        if (cbase == 0) {  // were the binned means / conics / samples passed? (device-side flag)
+        if (!rows_valid) {
+            k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
+                                                                       cbase == 0 && !binned ? flag : nullptr);
+            DGS_LAUNCH_CHECK(a.s, a.debug);
+        } else if (!binned) {
+            DGS_TRY_HIP(hipMemsetAsync(flag, 0, 4, a.s));
+        }
+        if (cbase == 0 && !binned) {  // were the binned means / conics / samples passed? (device-side flag)
             const int rc = verify_inputs(a.gb, a.sb, a.P, D, a.N, a.means, a.conics, a.samples, flag, a.s, a.debug);
             if (rc) return rc;
         }
@@ -1393,8 +1416,10 @@ static int run_forward(const Call &a) {
             }
         }
         // the call-time path (exits at once unless the inputs differ from the binned ones)
-        const int rc = ref_forward<FN, D, CB>(ref_call(a, nullptr, flag, cbase));
-        if (rc) return rc;
+        if (!binned) {
+            const int rc = ref_forward<FN, D, CB>(ref_call(a, nullptr, flag, cbase));
+            if (rc) return rc;
+        }
     }
     return DGS_OK;
 }
@@ -1405,29 +1430,37 @@ static int run_backward(const Call &a) {
     float *grows = reinterpret_cast<float *>(a.ws);
     float *srows = reinterpret_cast<float *>(a.ws + w.grows);
     float *acc = reinterpret_cast<float *>(a.ws + w.grows + w.srows);
-    uint32_t *flag = reinterpret_cast<uint32_t *>(a.ws + w.flag);
+    const bool binned = (a.opts & DGS_SAMPLE_INPUTS_BINNED) != 0;
+    const bool rows_valid = (a.opts & DGS_SAMPLE_ROWS_VALID) && a.C <= CB;
+    uint32_t *const check = reinterpret_cast<uint32_t *>(a.ws + w.flag);
+    uint32_t *const flag = dirty_word(a, check);
     constexpr int S = D * (D + 1) / 2;
-    DGS_TRY_HIP(hipMemsetAsync(acc, 0, w.acc, a.s));
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
     for (int cbase = 0; cbase < a.C; cbase += CB) {
-        k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
-                                                                   cbase == 0 ? flag : nullptr);
+        if (!rows_valid) {
+            k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
+                                                                       nullptr);
+            DGS_LAUNCH_CHECK(a.s, a.debug);
+        }
+        // sample rows (+ the zero-fill of the sums and of the check word, first block only)
+        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(
+            a.N, a.gb, a.sb, a.dls, a.C, cbase, srows, cbase == 0 ? reinterpret_cast<float4 *>(acc) : nullptr,
+            (int64_t)(w.acc / 16), cbase == 0 && !binned ? flag : nullptr);
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        if (cbase == 0) {
+        if (cbase == 0 && !binned) {
             const int rc = verify_inputs(a.gb, a.sb, a.P, D, a.N, a.means, a.conics, a.samples, flag, a.s, a.debug);
             if (rc) return rc;
         }
-        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(a.N, a.gb, a.sb, a.dls, a.C,
-                                                                      cbase, srows);
-        DGS_LAUNCH_CHECK(a.s, a.debug);
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s);
             k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
-        if (rc) return rc;
+        if (!binned) {
+            const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
+            if (rc) return rc;
+        }
     }
     if constexpr (D == 2 && CB == 1 && grow_stride<FN, D, CB>() >= 8) {
         if (a.C == 1) {  // the Gaussian-row region is free again: AoS rows there
@@ -1526,59 +1559,7 @@ extern "C" size_t dgs_sample_workspace_size(int function, int P, int D, int N, i
     return ws_layout(function, P, D, N, C, backward != 0).total;
 }
 
-extern "C" int dgs_sample_forward(int function, int P, int D, int N, int C, const float *means,
-                                  const float *values, const float *conics, const float *samples,
-                                  const void *binning, size_t binning_bytes,
-                                  const void *sample_binning, size_t sample_binning_bytes,
-                                  float *out, void *workspace, size_t workspace_bytes,
-                                  dgs_stream_t stream, int debug) {
-    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
-    const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 0);
-    int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
-                      sample_binning_bytes, need, workspace_bytes);
-    if (rc || P == 0 || N == 0 || C == 0) return rc;
-    Outs outs{{nullptr, nullptr, nullptr, nullptr}};
-    outs.p[function] = out;
-    Call a{function, P, D, N, C, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
-           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
-           binning_bytes, sample_binning_bytes, outs, nullptr, nullptr, nullptr,
-           static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
-    return dispatch(a, false);
-}
-
-extern "C" int dgs_sample_backward(int function, int P, int D, int N, int C, const float *means,
-                                   const float *values, const float *conics, const float *samples,
-                                   const float *dL_dout, const void *binning, size_t binning_bytes,
-                                   const void *sample_binning, size_t sample_binning_bytes,
-                                   float *dL_dmeans, float *dL_dvalues, float *dL_dconics,
-                                   void *workspace, size_t workspace_bytes, dgs_stream_t stream,
-                                   int debug) {
-    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
-    const size_t need = dgs_sample_workspace_size(function, P, D, N, C, 1);
-    int rc = validate(function, P, D, N, C, binning, binning_bytes, sample_binning,
-                      sample_binning_bytes, need, workspace_bytes);
-    if (rc) return rc;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (P == 0 || N == 0 || C == 0) {
-        // sample_points.cu:165-167: zero gradients
-        const int S = D * (D + 1) / 2;
-        if (P > 0) {
-            DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, sizeof(float) * (size_t)P * D, s));
-            DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, sizeof(float) * (size_t)P * S, s));
-            if (C > 0) DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, sizeof(float) * (size_t)P * C, s));
-        }
-        return DGS_OK;
-    }
-    DLs dls{{nullptr, nullptr, nullptr, nullptr}};
-    dls.p[function] = dL_dout;
-    Call a{function, P, D, N, C, means, values, conics, samples, dls,
-           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
-           binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
-           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
-    return dispatch(a, true);
-}
-
-// ------------------------------------------------------------------ fused functions
+// ------------------------------------------------------------------ entry points
 // One traversal of the pairs for every function of `mask` (bit f = dgs_function f): the
 // forward writes each function's output, the backward takes each function's dL and returns
 // the gradients of the summed loss.  A single-bit mask is the per-function path.
@@ -1594,33 +1575,108 @@ extern "C" size_t dgs_sample_workspace_size_multi(int mask, int P, int D, int N,
     return FN < 0 ? 256 : dgs_sample_workspace_size(FN, P, D, N, C, backward);
 }
 
-extern "C" int dgs_sample_forward_multi(int mask, int P, int D, int N, int C, const float *means,
-                                        const float *values, const float *conics, const float *samples,
-                                        const void *binning, size_t binning_bytes,
-                                        const void *sample_binning, size_t sample_binning_bytes,
-                                        float *const *outs, void *workspace, size_t workspace_bytes,
-                                        dgs_stream_t stream, int debug) {
+extern "C" int dgs_sample_forward_ex(int mask, int P, int D, int N, int C, const float *means,
+                                     const float *values, const float *conics, const float *samples,
+                                     const void *binning, size_t binning_bytes, const void *sample_binning,
+                                     size_t sample_binning_bytes, float *const *outs, void *workspace,
+                                     size_t workspace_bytes, const dgs_sample_options *opts, dgs_stream_t stream,
+                                     int debug) {
     const int FN = mask_code(mask);
     if (FN < 0) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
+    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 0);
+    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
+                      need, workspace_bytes);
+    if (rc || P == 0 || N == 0 || C == 0) return rc;
     Outs o{{nullptr, nullptr, nullptr, nullptr}};
     for (int f = 0; f < 4; ++f) {
         if (!(mask & (1 << f))) continue;
         if (!outs || !outs[f]) return fail(DGS_ERR_ARG, "missing output pointer for a function of the mask");
         o.p[f] = outs[f];
     }
-    if (!is_multi(FN))
-        return dgs_sample_forward(FN, P, D, N, C, means, values, conics, samples, binning, binning_bytes,
-                                  sample_binning, sample_binning_bytes, o.p[FN], workspace,
-                                  workspace_bytes, stream, debug);
-    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 0);
-    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
-                      need, workspace_bytes);
-    if (rc || P == 0 || N == 0 || C == 0) return rc;
-    Call a{FN, P, D, N, C, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
+    // (debug: always the device-side input check)
+    const uint32_t flags = opts && !debug ? opts->flags : 0u;
+    Call a{FN, P, D, N, C, flags, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
            binning_bytes, sample_binning_bytes, o, nullptr, nullptr, nullptr,
            static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
     return dispatch(a, false);
+}
+
+extern "C" int dgs_sample_backward_ex(int mask, int P, int D, int N, int C, const float *means,
+                                      const float *values, const float *conics, const float *samples,
+                                      const float *const *dL_douts, const void *binning, size_t binning_bytes,
+                                      const void *sample_binning, size_t sample_binning_bytes, float *dL_dmeans,
+                                      float *dL_dvalues, float *dL_dconics, void *workspace, size_t workspace_bytes,
+                                      const dgs_sample_options *opts, dgs_stream_t stream, int debug) {
+    const int FN = mask_code(mask);
+    if (FN < 0) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
+    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 1);
+    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
+                      need, workspace_bytes);
+    if (rc) return rc;
+    DLs d{{nullptr, nullptr, nullptr, nullptr}};
+    for (int f = 0; f < 4 && P > 0 && N > 0 && C > 0; ++f) {
+        if (!(mask & (1 << f))) continue;
+        if (!dL_douts || !dL_douts[f]) return fail(DGS_ERR_ARG, "missing dL_dout for a function of the mask");
+        d.p[f] = dL_douts[f];
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (P == 0 || N == 0 || C == 0) {
+        // sample_points.cu:165-167: zero gradients
+        const int S = D * (D + 1) / 2;
+        if (P > 0) {
+            DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, sizeof(float) * (size_t)P * D, s));
+            DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, sizeof(float) * (size_t)P * S, s));
+            if (C > 0) DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, sizeof(float) * (size_t)P * C, s));
+        }
+        return DGS_OK;
+    }
+    const uint32_t flags = opts && !debug ? opts->flags : 0u;
+    Call a{FN, P, D, N, C, flags, means, values, conics, samples, d,
+           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
+           binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
+           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
+    return dispatch(a, true);
+}
+
+extern "C" int dgs_sample_forward(int function, int P, int D, int N, int C, const float *means,
+                                  const float *values, const float *conics, const float *samples,
+                                  const void *binning, size_t binning_bytes,
+                                  const void *sample_binning, size_t sample_binning_bytes,
+                                  float *out, void *workspace, size_t workspace_bytes,
+                                  dgs_stream_t stream, int debug) {
+    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
+    float *outs[4] = {nullptr, nullptr, nullptr, nullptr};
+    outs[function] = out;
+    return dgs_sample_forward_ex(1 << function, P, D, N, C, means, values, conics, samples, binning, binning_bytes,
+                                 sample_binning, sample_binning_bytes, outs, workspace, workspace_bytes, nullptr,
+                                 stream, debug);
+}
+
+extern "C" int dgs_sample_backward(int function, int P, int D, int N, int C, const float *means,
+                                   const float *values, const float *conics, const float *samples,
+                                   const float *dL_dout, const void *binning, size_t binning_bytes,
+                                   const void *sample_binning, size_t sample_binning_bytes,
+                                   float *dL_dmeans, float *dL_dvalues, float *dL_dconics,
+                                   void *workspace, size_t workspace_bytes, dgs_stream_t stream,
+                                   int debug) {
+    if (function < 0 || function > 3) return fail(DGS_ERR_ARG, "unknown sampling function");
+    const float *dls[4] = {nullptr, nullptr, nullptr, nullptr};
+    dls[function] = dL_dout;
+    return dgs_sample_backward_ex(1 << function, P, D, N, C, means, values, conics, samples, dls, binning,
+                                  binning_bytes, sample_binning, sample_binning_bytes, dL_dmeans, dL_dvalues,
+                                  dL_dconics, workspace, workspace_bytes, nullptr, stream, debug);
+}
+
+extern "C" int dgs_sample_forward_multi(int mask, int P, int D, int N, int C, const float *means,
+                                        const float *values, const float *conics, const float *samples,
+                                        const void *binning, size_t binning_bytes,
+                                        const void *sample_binning, size_t sample_binning_bytes,
+                                        float *const *outs, void *workspace, size_t workspace_bytes,
+                                        dgs_stream_t stream, int debug) {
+    return dgs_sample_forward_ex(mask, P, D, N, C, means, values, conics, samples, binning, binning_bytes,
+                                 sample_binning, sample_binning_bytes, outs, workspace, workspace_bytes, nullptr,
+                                 stream, debug);
 }
 
 extern "C" int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float *means,
@@ -1630,36 +1686,9 @@ extern "C" int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, c
                                          size_t sample_binning_bytes, float *dL_dmeans,
                                          float *dL_dvalues, float *dL_dconics, void *workspace,
                                          size_t workspace_bytes, dgs_stream_t stream, int debug) {
-    const int FN = mask_code(mask);
-    if (FN < 0) return fail(DGS_ERR_ARG, "function mask must be in 1..15");
-    DLs d{{nullptr, nullptr, nullptr, nullptr}};
-    for (int f = 0; f < 4; ++f) {
-        if (!(mask & (1 << f))) continue;
-        if (!dL_douts || !dL_douts[f]) return fail(DGS_ERR_ARG, "missing dL_dout for a function of the mask");
-        d.p[f] = dL_douts[f];
-    }
-    if (!is_multi(FN))
-        return dgs_sample_backward(FN, P, D, N, C, means, values, conics, samples, d.p[FN], binning,
-                                   binning_bytes, sample_binning, sample_binning_bytes, dL_dmeans,
-                                   dL_dvalues, dL_dconics, workspace, workspace_bytes, stream, debug);
-    const size_t need = dgs_sample_workspace_size(FN, P, D, N, C, 1);
-    int rc = validate(FN, P, D, N, C, binning, binning_bytes, sample_binning, sample_binning_bytes,
-                      need, workspace_bytes);
-    if (rc) return rc;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (P == 0 || N == 0) {  // zero gradients (sample_points.cu:165-167)
-        if (P > 0) {
-            DGS_TRY_HIP(hipMemsetAsync(dL_dmeans, 0, sizeof(float) * (size_t)P * 2, s));
-            DGS_TRY_HIP(hipMemsetAsync(dL_dconics, 0, sizeof(float) * (size_t)P * 3, s));
-            DGS_TRY_HIP(hipMemsetAsync(dL_dvalues, 0, sizeof(float) * (size_t)P, s));
-        }
-        return DGS_OK;
-    }
-    Call a{FN, P, D, N, C, means, values, conics, samples, d,
-           static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
-           binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
-           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
-    return dispatch(a, true);
+    return dgs_sample_backward_ex(mask, P, D, N, C, means, values, conics, samples, dL_douts, binning,
+                                  binning_bytes, sample_binning, sample_binning_bytes, dL_dmeans, dL_dvalues,
+                                  dL_dconics, workspace, workspace_bytes, nullptr, stream, debug);
 }
 
 extern "C" int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics,

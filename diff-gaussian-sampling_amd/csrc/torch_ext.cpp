@@ -13,6 +13,8 @@
 #include <ATen/hip/HIPContext.h>
 #include <torch/extension.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <stdexcept>
 #include <tuple>
@@ -69,6 +71,90 @@ Tensor empty_u8(const torch::Device &dev) {
 
 using PreOut = std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
+// ---- per-step caches of the sampling calls (dgs_sample_options) ------------------------------
+// A tensor's identity: its TensorImpl (weakly held), data pointer and autograd version counter.
+// Same identity <=> same tensor object, not modified in place since (every in-place op bumps the
+// version; writes through .data or raw pointers do not: DGS_ALWAYS_VERIFY=1 or debug=True keep
+// the device-side comparison for code that does that).
+using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+struct TKey {
+    WeakImpl impl;
+    const void *ptr;
+    int64_t version;
+};
+TKey tkey(const Tensor &t) { return {WeakImpl(t.getIntrusivePtr()), t.data_ptr(), (int64_t)t._version()}; }
+bool same(const TKey &k, const Tensor &t) {
+    const auto sp = k.impl.lock();
+    return sp.get() == t.unsafeGetTensorImpl() && k.ptr == t.data_ptr() && k.version == (int64_t)t._version();
+}
+
+bool always_verify() {
+    static const bool on = [] {
+        const char *e = std::getenv("DGS_ALWAYS_VERIFY");
+        return e && e[0] && e[0] != '0';
+    }();
+    return on;
+}
+
+// What each binning was built from (preprocess): a forward / backward passing exactly those
+// means / conics / samples needs no device-side comparison (DGS_SAMPLE_INPUTS_BINNED).
+struct BinRecord {
+    TKey gb, means, conics, samples;
+};
+// The workspace of a forward whose Gaussian rows a later call on the same binning, function
+// mask and parameters reuses (DGS_SAMPLE_ROWS_VALID): the forward of a training step packs
+// them, its backward uses them (one pack per step instead of two).
+struct RowRecord {
+    TKey gb, means, values, conics;
+    int mask, C;
+    Tensor work;
+};
+std::mutex g_step_mu;
+std::vector<BinRecord> g_bins;
+std::vector<RowRecord> g_rows;
+
+void bins_put(const Tensor &gb, const Tensor &means, const Tensor &conics, const Tensor &samples) {
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    for (auto it = g_bins.begin(); it != g_bins.end();)
+        if (it->gb.impl.expired() || it->gb.ptr == gb.data_ptr()) it = g_bins.erase(it);
+        else ++it;
+    g_bins.push_back({tkey(gb), tkey(means), tkey(conics), tkey(samples)});
+    if (g_bins.size() > 8) g_bins.erase(g_bins.begin());
+}
+
+bool inputs_binned(const Tensor &gb, const Tensor &means, const Tensor &conics, const Tensor &samples) {
+    if (always_verify()) return false;
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    for (const auto &r : g_bins)
+        if (same(r.gb, gb)) return same(r.means, means) && same(r.conics, conics) && same(r.samples, samples);
+    return false;
+}
+
+// take = true: remove the record (a backward overwrites the rows).
+bool rows_get(const Tensor &gb, int mask, int C, const Tensor &means, const Tensor &values, const Tensor &conics,
+              size_t need, bool take, Tensor &work) {
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    for (auto it = g_rows.begin(); it != g_rows.end(); ++it) {
+        if (it->mask != mask || it->C != C || !same(it->gb, gb)) continue;
+        const bool ok = same(it->means, means) && same(it->values, values) && same(it->conics, conics) &&
+                        (size_t)it->work.numel() >= need;
+        if (ok) work = it->work;
+        if (take || !ok) g_rows.erase(it);
+        return ok;
+    }
+    return false;
+}
+
+void rows_put(const Tensor &gb, int mask, int C, const Tensor &means, const Tensor &values, const Tensor &conics,
+              const Tensor &work) {
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    for (auto it = g_rows.begin(); it != g_rows.end();)
+        if (it->gb.impl.expired() || (it->mask == mask && it->gb.ptr == gb.data_ptr())) it = g_rows.erase(it);
+        else ++it;
+    g_rows.push_back({tkey(gb), tkey(means), tkey(values), tkey(conics), mask, C, work});
+    if (g_rows.size() > 4) g_rows.erase(g_rows.begin());  // (the per-function path of a fused call keeps one per function)
+}
+
 PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Tensor &cov_in,
                        const Tensor &conics_in, const Tensor &samples_in, const std::vector<int> *grid_in,
                        const std::vector<float> *off_in, bool debug, const dgs_bin_options *opts = nullptr) {
@@ -100,6 +186,7 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
                   "preprocess_gaussians");
         }
     }
+    if (ctx.bufs[DGS_BUF_BINNING].numel() > 0) bins_put(ctx.bufs[DGS_BUF_BINNING], means_in, conics_in, samples_in);
     return std::make_tuple(rendered, ctx.bufs[DGS_BUF_BINNING], ctx.bufs[DGS_BUF_SAMPLE_BINNING],
                            ctx.bufs[DGS_BUF_RANGES], ctx.bufs[DGS_BUF_SAMPLE_RANGES], radii);
 }
@@ -138,62 +225,105 @@ PreOut PreprocessShardedCUDA(const Tensor &means, const Tensor &values, const Te
     return preprocess_impl(means, values, covariances, conics, samples, &grid, &offset, debug, &o);
 }
 
-Tensor sample_generic(int fn, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
-                      const Tensor &samples_in, const Tensor &binning_in, const Tensor &sbinning_in,
-                      bool debug) {
+std::vector<int64_t> out_shape(int fn, int64_t N, int64_t D, int64_t C) {
+    std::vector<int64_t> shape{N};
+    for (int k = 0; k < fn; ++k) shape.push_back(D);
+    shape.push_back(C);
+    return shape;
+}
+
+// The forward of every function of `mask` in one call (dgs_sample_forward_ex).  The call-time
+// inputs are compared with the binned ones on the host (object identity + version counters,
+// BinRecord) and, when any of means / values / conics requires a gradient, the workspace is
+// sized for the backward and kept for it with its packed Gaussian rows (RowRecord).
+void forward_mask(int mask, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
+                  const Tensor &samples_in, const Tensor &binning_in, const Tensor &sbinning_in, float *const *outs,
+                  bool debug) {
     const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
     const int C = (int)values.size(-1);
-    std::vector<int64_t> shape{N};
-    for (int k = 0; k < fn; ++k) shape.push_back(D);
-    shape.push_back(C);
-    Tensor out = torch::full(shape, 0.0, means.options());
-    if (P != 0 && N != 0) {
-        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-        const size_t ws = dgs_sample_workspace_size(fn, P, D, N, C, 0);
-        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
-        check(dgs_sample_forward(fn, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
-                                 conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(),
-                                 (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
-                                 out.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
-                                 debug ? 1 : 0),
-              "sample_gaussians");
-    }
+    if (P == 0 || N == 0) return;
+    const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+    dgs_sample_options o{};
+    if (inputs_binned(binning_in, means_in, conics_in, samples_in)) o.flags |= DGS_SAMPLE_INPUTS_BINNED;
+    const bool keep = means_in.requires_grad() || values_in.requires_grad() || conics_in.requires_grad();
+    const size_t ws = std::max(dgs_sample_workspace_size_multi(mask, P, D, N, C, 0),
+                               keep ? dgs_sample_workspace_size_multi(mask, P, D, N, C, 1) : (size_t)0);
+    Tensor work;
+    if (rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, false, work)) o.flags |= DGS_SAMPLE_ROWS_VALID;
+    else work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+    check(dgs_sample_forward_ex(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(), (size_t)gb.numel(),
+                                sb.data_ptr(), (size_t)sb.numel(), outs, work.data_ptr(), (size_t)work.numel(), &o,
+                                as_dgs(cur_stream()), debug ? 1 : 0),
+          "sample_gaussians");
+    if (keep && !(o.flags & DGS_SAMPLE_ROWS_VALID)) rows_put(binning_in, mask, C, means_in, values_in, conics_in, work);
+}
+
+Tensor sample_generic(int fn, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
+                      const Tensor &samples_in, const Tensor &binning_in, const Tensor &sbinning_in,
+                      bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples");
+    const int D = (int)means.size(-1);
+    Tensor out = torch::full(out_shape(fn, samples.size(0), D, values.size(-1)), 0.0, means.options());
+    float *outs[4] = {nullptr, nullptr, nullptr, nullptr};
+    outs[fn] = out.data_ptr<float>();
+    forward_mask(1 << fn, means_in, values_in, conics_in, samples_in, binning_in, sbinning_in, outs, debug);
     return out;
 }
 
 using Grads = std::tuple<Tensor, Tensor, Tensor>;
 
-Grads sample_backward_generic(int fn, const Tensor &means_in, const Tensor &values_in,
-                              const Tensor &conics_in, const Tensor &samples_in, const Tensor &dL_in,
-                              const Tensor &binning_in, const Tensor &sbinning_in, bool debug) {
+Grads backward_mask(int mask, const Tensor &means_in, const Tensor &values_in, const Tensor &conics_in,
+                    const Tensor &samples_in, const float *const *dls, const Tensor &binning_in,
+                    const Tensor &sbinning_in, bool debug) {
     const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
     const int C = (int)values.size(-1);
-    // dgs_sample_backward overwrites every gradient element; nothing to do -> zeros
+    // dgs_sample_backward_ex overwrites every gradient element; nothing to do -> zeros
     const auto alloc = [&](int64_t cols) {
         return N != 0 ? torch::empty({P, cols}, means.options()) : torch::zeros({P, cols}, means.options());
     };
     Tensor dmeans = alloc(D), dvalues = alloc(C), dconics = alloc(D * (D + 1) / 2);
     if (P != 0 && N != 0) {
-        const Tensor dL = f32(dL_in, "dL_dout_values");
-        int64_t K = 1;
-        for (int k = 0; k < fn; ++k) K *= D;
-        TORCH_CHECK(dL.numel() == (int64_t)N * K * C, "dL_dout has the wrong number of elements");
         const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-        const size_t ws = dgs_sample_workspace_size(fn, P, D, N, C, 1);
-        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
-        check(dgs_sample_backward(fn, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
-                                  conics.data_ptr<float>(), samples.data_ptr<float>(), dL.data_ptr<float>(),
-                                  gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
-                                  dmeans.data_ptr<float>(), dvalues.data_ptr<float>(),
-                                  dconics.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
-                                  debug ? 1 : 0),
+        dgs_sample_options o{};
+        if (inputs_binned(binning_in, means_in, conics_in, samples_in)) o.flags |= DGS_SAMPLE_INPUTS_BINNED;
+        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 1);
+        Tensor work;
+        if (rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, true, work)) o.flags |= DGS_SAMPLE_ROWS_VALID;
+        else work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
+        check(dgs_sample_backward_ex(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
+                                     conics.data_ptr<float>(), samples.data_ptr<float>(), dls, gb.data_ptr(),
+                                     (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), dmeans.data_ptr<float>(),
+                                     dvalues.data_ptr<float>(), dconics.data_ptr<float>(), work.data_ptr(),
+                                     (size_t)work.numel(), &o, as_dgs(cur_stream()), debug ? 1 : 0),
               "sample_gaussians_backward");
     }
     return std::make_tuple(dmeans, dvalues, dconics);
+}
+
+Grads sample_backward_generic(int fn, const Tensor &means_in, const Tensor &values_in,
+                              const Tensor &conics_in, const Tensor &samples_in, const Tensor &dL_in,
+                              const Tensor &binning_in, const Tensor &sbinning_in, bool debug) {
+    const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
+    const Tensor samples = f32(samples_in, "samples");
+    const int D = (int)means.size(-1);
+    const int64_t N = samples.size(0), C = values.size(-1);
+    Tensor dL;
+    const float *dls[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (means.size(0) != 0 && N != 0) {
+        dL = f32(dL_in, "dL_dout_values");
+        int64_t K = 1;
+        for (int k = 0; k < fn; ++k) K *= D;
+        TORCH_CHECK(dL.numel() == N * K * C, "dL_dout has the wrong number of elements");
+        dls[fn] = dL.data_ptr<float>();
+    }
+    return backward_mask(1 << fn, means_in, values_in, conics_in, samples_in, dls, binning_in, sbinning_in, debug);
 }
 
 #define DGS_FWD(NAME, FN)                                                                       \
@@ -246,33 +376,22 @@ std::vector<Tensor> SampleGaussiansMulti(const std::vector<int64_t> &functions, 
                                          const Tensor &sbinning_in, const bool debug) {
     const int mask = function_mask(functions);
     const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
-    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
-    const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
-    const int C = (int)values.size(-1);
+    f32(conics_in, "conics");
+    const Tensor samples = f32(samples_in, "samples");
+    const int D = (int)means.size(-1), C = (int)values.size(-1);
     std::vector<Tensor> outs;
     if (functions.size() == 1 || D != 2 || C != 1) {
         for (int64_t f : functions)
-            outs.push_back(sample_generic((int)f, means, values, conics, samples, binning_in, sbinning_in, debug));
+            outs.push_back(sample_generic((int)f, means_in, values_in, conics_in, samples_in, binning_in, sbinning_in,
+                                          debug));
         return outs;
     }
     float *ptr[4] = {nullptr, nullptr, nullptr, nullptr};
     for (int64_t f : functions) {
-        std::vector<int64_t> shape{N};
-        for (int k = 0; k < f; ++k) shape.push_back(D);
-        shape.push_back(C);
-        outs.push_back(torch::full(shape, 0.0, means.options()));
+        outs.push_back(torch::full(out_shape((int)f, samples.size(0), D, C), 0.0, means.options()));
         ptr[f] = outs.back().data_ptr<float>();
     }
-    if (P != 0 && N != 0) {
-        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 0);
-        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
-        check(dgs_sample_forward_multi(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
-                                       conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(),
-                                       (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), ptr,
-                                       work.data_ptr(), ws, as_dgs(cur_stream()), debug ? 1 : 0),
-              "sample_gaussians_multi");
-    }
+    forward_mask(mask, means_in, values_in, conics_in, samples_in, binning_in, sbinning_in, ptr, debug);
     return outs;
 }
 
@@ -283,46 +402,31 @@ Grads SampleGaussiansMultiBackward(const std::vector<int64_t> &functions, const 
     const int mask = function_mask(functions);
     TORCH_CHECK(dLs_in.size() == functions.size(), "one dL_dout per sampling function");
     const Tensor means = f32(means_in, "means"), values = f32(values_in, "values");
-    const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
+    const Tensor samples = f32(samples_in, "samples");
     const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
     const int C = (int)values.size(-1);
     if (functions.size() == 1 || D != 2 || C != 1) {
-        Grads g = sample_backward_generic((int)functions[0], means, values, conics, samples, dLs_in[0],
+        Grads g = sample_backward_generic((int)functions[0], means_in, values_in, conics_in, samples_in, dLs_in[0],
                                           binning_in, sbinning_in, debug);
         for (size_t i = 1; i < functions.size(); ++i) {
-            Grads h = sample_backward_generic((int)functions[i], means, values, conics, samples, dLs_in[i],
-                                              binning_in, sbinning_in, debug);
+            Grads h = sample_backward_generic((int)functions[i], means_in, values_in, conics_in, samples_in,
+                                              dLs_in[i], binning_in, sbinning_in, debug);
             std::get<0>(g).add_(std::get<0>(h));
             std::get<1>(g).add_(std::get<1>(h));
             std::get<2>(g).add_(std::get<2>(h));
         }
         return g;
     }
-    const auto alloc = [&](int64_t cols) {
-        return N != 0 ? torch::empty({P, cols}, means.options()) : torch::zeros({P, cols}, means.options());
-    };
-    Tensor dmeans = alloc(2), dvalues = alloc(1), dconics = alloc(3);
-    if (P != 0 && N != 0) {
-        std::vector<Tensor> dLs;
-        const float *ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+    std::vector<Tensor> dLs;
+    const float *ptr[4] = {nullptr, nullptr, nullptr, nullptr};
+    if (P != 0 && N != 0)
         for (size_t i = 0; i < functions.size(); ++i) {
             const int f = (int)functions[i];
             dLs.push_back(f32(dLs_in[i], "dL_dout_values"));
             TORCH_CHECK(dLs.back().numel() == (int64_t)N * (1 << f), "dL_dout has the wrong number of elements");
             ptr[f] = dLs.back().data_ptr<float>();
         }
-        const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 1);
-        Tensor work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
-        check(dgs_sample_backward_multi(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
-                                        conics.data_ptr<float>(), samples.data_ptr<float>(), ptr,
-                                        gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(),
-                                        dmeans.data_ptr<float>(), dvalues.data_ptr<float>(),
-                                        dconics.data_ptr<float>(), work.data_ptr(), ws, as_dgs(cur_stream()),
-                                        debug ? 1 : 0),
-              "sample_gaussians_multi_backward");
-    }
-    return std::make_tuple(dmeans, dvalues, dconics);
+    return backward_mask(mask, means_in, values_in, conics_in, samples_in, ptr, binning_in, sbinning_in, debug);
 }
 
 // Diagnostics: (W_cand, W_live) over the pairs the forward evaluates.
@@ -396,7 +500,6 @@ std::tuple<std::vector<int>, std::vector<float>> TileGrid(const Tensor &samples_
 // same P costs speed at most) and the transposed lists of dgs_agg_transpose (results depend on
 // them: used only while the very indices tensor they were built from is alive and unmodified --
 // a weak reference to it and its version counter).
-using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
 struct AggEntry {
     const void *indices;
     int64_t P, length;

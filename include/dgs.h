@@ -180,6 +180,39 @@ int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float 
                               float *dL_dconics, void *workspace, size_t workspace_bytes,
                               dgs_stream_t stream, int debug);
 
+/* Per-call options of dgs_sample_forward_ex / dgs_sample_backward_ex (not on the reference API;
+ * zero-initialise, then set what is wanted).  `flags` is a bit set of dgs_sample_flag:
+ *   DGS_SAMPLE_INPUTS_BINNED: the caller vouches that means, conics and samples are bitwise the
+ *     tensors the binning was built from (e.g. the same tensor objects, unmodified since: the
+ *     torch extension checks object identity and autograd version counters).  The call then
+ *     skips the device-side comparison with the binned copies and the call-time path of
+ *     dgs_reference.hip (forward.cu:136-145 reads the passed tensors; the comparison exists only
+ *     to detect a difference).  Wrong if the tensors were changed: leave it unset when unsure.
+ *   DGS_SAMPLE_ROWS_VALID: `workspace` comes from an earlier call on the same binning with the
+ *     same function mask, C <= 16 and the same means / conics / values (unmodified since), whose
+ *     Gaussian-row region (offset 0) the earlier call packed: the rows are reused, not repacked.
+ *     A forward followed by its backward shares one workspace of the backward's size this way.
+ *     A backward leaves the region overwritten (its finalize reuses it): never reuse after one. */
+enum dgs_sample_flag { DGS_SAMPLE_INPUTS_BINNED = 1, DGS_SAMPLE_ROWS_VALID = 2 };
+typedef struct dgs_sample_options {
+    uint32_t flags;
+} dgs_sample_options;
+
+/* The multi-function entry points with options (opts NULL = no flags).  mask as in
+ * dgs_sample_forward_multi (a single-bit mask is the per-function path, C any). */
+int dgs_sample_forward_ex(int mask, int P, int D, int N, int C, const float *means,
+                          const float *values, const float *conics, const float *samples,
+                          const void *binning, size_t binning_bytes, const void *sample_binning,
+                          size_t sample_binning_bytes, float *const *outs, void *workspace,
+                          size_t workspace_bytes, const dgs_sample_options *opts, dgs_stream_t stream,
+                          int debug);
+int dgs_sample_backward_ex(int mask, int P, int D, int N, int C, const float *means,
+                           const float *values, const float *conics, const float *samples,
+                           const float *const *dL_douts, const void *binning, size_t binning_bytes,
+                           const void *sample_binning, size_t sample_binning_bytes, float *dL_dmeans,
+                           float *dL_dvalues, float *dL_dconics, void *workspace, size_t workspace_bytes,
+                           const dgs_sample_options *opts, dgs_stream_t stream, int debug);
+
 /* Diagnostics (not on the reference API): counts, over the pairs the forward evaluates,
  * W_cand (candidate pairs after culling) and W_live (pairs with power >= thr, the survey's
  * live-pair count for thr = -104).  counts[0] = W_cand, counts[1] = W_live (host, syncs). */

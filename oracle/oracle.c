@@ -326,176 +326,17 @@ static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const
     (void)nt;
 }
 
-/* backward.cu:108-416 -- one pair's gradient contributions (literal formulas, including the
- * reference's D=1 third-derivative conic gradient at backward.cu:322-325). */
-static void bwd_pair(int fn, int D, int C, const float *X, const float *c, const float *v,
-                     const float *dL /* [K][C] of this sample */, float *gm, float *gv, float *gc) {
-    if (D == 1) {
-        float x1 = c[0] * X[0];
-        float power = fn == F_GAUSS ? (float)(-0.5 * c[0] * X[0] * X[0]) : (float)(-0.5 * x1 * X[0]);
-        if (power > 0.0) return;
-        float G = expf(power);
-        float dLdG = 0.0f;
-        for (int ch = 0; ch < C; ++ch) {
-            float d = dL[ch];
-            switch (fn) {
-            case F_GAUSS: gv[ch] += G * d; break;
-            case F_DERIV: gv[ch] += x1 * d * G; break;
-            case F_LAPL: { float gx = (x1 * x1 - c[0]) * d; gv[ch] += gx * G; } break;
-            default: { float gx = (float)((3.0 * c[0] * x1 - (double)(x1 * x1 * x1)) * d); gv[ch] += gx * G; }
-            }
-            dLdG += v[ch] * d;
-        }
-        switch (fn) {
-        case F_GAUSS: {
-            float gdx = G * X[0];
-            float dG = gdx * c[0];
-            float dLdx = dLdG * dG;
-            gm[0] += -dLdx;
-            gc[0] += (float)(-0.5 * gdx * X[0] * dLdG);
-        } break;
-        case F_DERIV: {
-            float dLdx = (x1 * x1 - c[0]) * dLdG * G;
-            gm[0] += -dLdx;
-            gc[0] += (float)(((double)X[0] - 0.5 * X[0] * X[0] * x1) * dLdG * G);
-        } break;
-        case F_LAPL: {
-            float dLdx = (float)(((double)(x1 * x1 * x1) - 3.0 * c[0] * x1) * dLdG * G);
-            float dVdc = (float)((2.0 * x1 * X[0] - 0.5 * (x1 * x1 - c[0]) * X[0] * X[0] - 1.0) * dLdG * G);
-            gm[0] += -dLdx;
-            gc[0] += dVdc;
-        } break;
-        default: {
-            float dLdx = (float)((6.0 * c[0] * x1 * x1 - (double)(x1 * x1 * x1 * x1) - 3.0 * c[0] * c[0]) * dLdG * G);
-            /* backward.cu:322-325: not the true derivative; reproduced literally */
-            float dVdc = (float)((2.0 * X[0] * X[0] - 2.0 * x1 * x1 * X[0] - 0.5 * (2.0 * X[0] * x1 - X[0]) * X[0] * X[0]
-                                  + 0.5 * (x1 * x1 - c[0]) * x1 * X[0] * X[0]) * dLdG * G);
-            gm[0] += -dLdx;
-            gc[0] += dVdc;
-        }
-        }
-        return;
-    }
-    float x1 = c[0] * X[0], x2 = c[2] * X[1];
-    float power;
-    if (fn == F_GAUSS)
-        power = (float)(-0.5 * (double)(c[0] * X[0] * X[0] + c[2] * X[1] * X[1]) - (double)(c[1] * X[0] * X[1]));
-    else
-        power = (float)(-0.5 * (double)(x1 * X[0] + x2 * X[1]) - (double)(c[1] * X[0] * X[1]));
-    if (power > 0.0) return;
-    float G = expf(power);
-    float a1 = x1 + c[1] * X[1], a2 = x2 + c[1] * X[0];
-    if (fn == F_GAUSS) {
-        float dLdG = 0.0f;
-        for (int ch = 0; ch < C; ++ch) { gv[ch] += G * dL[ch]; dLdG += v[ch] * dL[ch]; }
-        float gdx = G * X[0], gdy = G * X[1];
-        gm[0] += -dLdG * (gdx * c[0] + gdy * c[1]);
-        gm[1] += -dLdG * (gdx * c[1] + gdy * c[2]);
-        gc[0] += (float)(-0.5 * gdx * X[0] * dLdG);
-        gc[1] += -gdy * X[0] * dLdG;
-        gc[2] += (float)(-0.5 * gdy * X[1] * dLdG);
-        return;
-    }
-    if (fn == F_DERIV) {
-        float Gx = 0.0f, Gy = 0.0f;
-        for (int ch = 0; ch < C; ++ch) {
-            float dx = dL[ch], dy = dL[C + ch];
-            float gx = a1 * dx + a2 * dy;
-            gv[ch] += gx * G;
-            Gx += v[ch] * dx;
-            Gy += v[ch] * dy;
-        }
-        float gx = a1 * Gx + a2 * Gy;
-        float dLdx = ((a1 * a1 - c[0]) * Gx + (a1 * a2 - c[1]) * Gy) * G;
-        float dLdy = ((a2 * a2 - c[2]) * Gy + (a1 * a2 - c[1]) * Gx) * G;
-        gm[0] += -dLdx;
-        gm[1] += -dLdy;
-        gc[0] += (float)(((double)(X[0] * Gx) - 0.5 * X[0] * X[0] * gx) * G);
-        gc[1] += (X[1] * Gx + X[0] * Gy - X[0] * X[1] * gx) * G;
-        gc[2] += (float)(((double)(X[1] * Gy) - 0.5 * X[1] * X[1] * gx) * G);
-        return;
-    }
-    if (fn == F_LAPL) {
-        float dxx = a1 * a1 - c[0], dxy = a1 * a2 - c[1], dyy = a2 * a2 - c[2];
-        float Gxx = 0.0f, Gxy = 0.0f, Gyx = 0.0f, Gyy = 0.0f;
-        for (int ch = 0; ch < C; ++ch) {
-            float d0 = dL[ch], d1 = dL[C + ch], d2 = dL[2 * C + ch], d3 = dL[3 * C + ch];
-            float g = dxx * d0 + dxy * d1 + dxy * d2 + dyy * d3;
-            gv[ch] += g * G;
-            Gxx += v[ch] * d0; Gxy += v[ch] * d1; Gyx += v[ch] * d2; Gyy += v[ch] * d3;
-        }
-        float dLdx = (float)(((double)(a1 * a1 * a1) - 3.0 * c[0] * a1) * Gxx
-                             + (double)((a1 * a2 * a1 - c[1] * a1 - (c[1] * a1 + c[0] * a2)) * (Gxy + Gyx))
-                             + ((double)(a2 * a2 * a1 - c[2] * a1) - 2.0 * c[1] * a2) * Gyy) * G;
-        float dLdy = (float)(((double)(a1 * a1 * a2 - c[0] * a2) - 2.0 * c[1] * a1) * Gxx
-                             + (double)((a1 * a2 * a2 - c[1] * a2 - (c[2] * a1 + c[1] * a2)) * (Gxy + Gyx))
-                             + ((double)(a2 * a2 * a2) - 3.0 * c[2] * a2) * Gyy) * G;
-        gm[0] += -dLdx;
-        gm[1] += -dLdy;
-        float S = Gxy + Gyx;
-        float xx_cxx = (float)(-0.5 * dxx * X[0] * X[0] + 2.0 * a1 * X[0] - 1.0);
-        float xy_cxx = (float)(-0.5 * dxy * X[0] * X[0] + (double)(a2 * X[0]));
-        float yy_cxx = (float)(-0.5 * dyy * X[0] * X[0]);
-        float xx_cxy = (float)((double)(-dxx * X[0] * X[1]) + 2.0 * a1 * X[1]);
-        float xy_cxy = -dxy * X[0] * X[1] + a2 * X[1] + a1 * X[0] - 1.0f;
-        float yy_cxy = (float)((double)(-dyy * X[0] * X[1]) + 2.0 * a2 * X[0]);
-        float xx_cyy = (float)(-0.5 * dxx * X[1] * X[1]);
-        float xy_cyy = (float)(-0.5 * dxy * X[1] * X[1] + (double)(a1 * X[1]));
-        float yy_cyy = (float)(-0.5 * dyy * X[1] * X[1] + 2.0 * a2 * X[1] - 1.0);
-        gc[0] += (xx_cxx * Gxx + xy_cxx * S + yy_cxx * Gyy) * G;
-        gc[1] += (xx_cxy * Gxx + xy_cxy * S + yy_cxy * Gyy) * G;
-        gc[2] += (xx_cyy * Gxx + xy_cyy * S + yy_cyy * Gyy) * G;
-        return;
-    }
-    /* third, D == 2 (backward.cu:329-415) */
-    float dxxx = (float)(3.0 * c[0] * a1 - (double)(a1 * a1 * a1));
-    float dxxy = (float)(2.0 * c[1] * a1 - (double)(a1 * a1 * a2) + (double)(c[0] * a2));
-    float dxyy = (float)(2.0 * c[1] * a2 - (double)(a1 * a2 * a2) + (double)(c[2] * a1));
-    float dyyy = (float)(3.0 * c[2] * a2 - (double)(a2 * a2 * a2));
-    float Gk[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int ch = 0; ch < C; ++ch) {
-        const float *d = dL + ch;
-        float g = dxxx * d[0] + dxxy * d[C] + dxxy * d[2 * C] + dxyy * d[3 * C]
-                + dxxy * d[4 * C] + dxyy * d[5 * C] + dxyy * d[6 * C] + dyyy * d[7 * C];
-        gv[ch] += g * G;
-        for (int k = 0; k < 8; ++k) Gk[k] += v[ch] * d[k * C];
-    }
-    float S1 = Gk[1] + Gk[2] + Gk[4], S2 = Gk[3] + Gk[5] + Gk[6];
-    float xxy_dx = (float)(2.0 * a1 * a2 * c[0] + (double)(a1 * a1 * c[1]) - 3.0 * c[0] * c[1]);
-    float xyy_dx = (float)(2.0 * a1 * a2 * c[1] + (double)(a2 * a2 * c[0]) - (double)(c[2] * c[0]) - 2.0 * c[1] * c[1]);
-    /* left-to-right sum in double: each float term is promoted on its own */
-    float dLdx = (float)((((double)(dxxx * a1) - 3.0 * c[0] * c[0] + 3.0 * a1 * a1 * c[0]) * Gk[0]
-                          + (double)((dxxy * a1 + xxy_dx) * Gk[1]) + (double)((dxxy * a1 + xxy_dx) * Gk[2])
-                          + (double)((dxyy * a1 + xyy_dx) * Gk[3]) + (double)((dxxy * a1 + xxy_dx) * Gk[4])
-                          + (double)((dxyy * a1 + xyy_dx) * Gk[5]) + (double)((dxyy * a1 + xyy_dx) * Gk[6])
-                          + ((double)(dyyy * a1) - 3.0 * c[2] * c[1] + 3.0 * a2 * a2 * c[1]) * Gk[7]) * G);
-    float xxy_dy = (float)(2.0 * a1 * a2 * c[1] + (double)(a1 * a1 * c[2]) - (double)(c[0] * c[2]) - 2.0 * c[1] * c[1]);
-    float xyy_dy = (float)(2.0 * a1 * a2 * c[2] + (double)(a2 * a2 * c[1]) - 3.0 * c[2] * c[1]);
-    float dLdy = (float)((((double)(dxxx * a2) - 3.0 * c[0] * c[1] + 3.0 * a1 * a1 * c[1]) * Gk[0]
-                          + (double)((dxxy * a2 + xxy_dy) * Gk[1]) + (double)((dxxy * a2 + xxy_dy) * Gk[2])
-                          + (double)((dxyy * a2 + xyy_dy) * Gk[3]) + (double)((dxxy * a2 + xxy_dy) * Gk[4])
-                          + (double)((dxyy * a2 + xyy_dy) * Gk[5]) + (double)((dxyy * a2 + xyy_dy) * Gk[6])
-                          + ((double)(dyyy * a2) - 3.0 * c[2] * c[2] + 3.0 * a2 * a2 * c[2]) * Gk[7]) * G);
-    gm[0] += -dLdx;
-    gm[1] += -dLdy;
-    float X0 = X[0], X1 = X[1];
-    float v_cxx[4], v_cxy[4], v_cyy[4];
-    v_cxx[0] = (float)(-0.5 * dxxx * X0 * X0 + 3.0 * c[0] * X0 + 3.0 * a1 - 3.0 * a1 * a1 * X0);
-    v_cxx[1] = (float)(-0.5 * dxxy * X0 * X0 + 2.0 * c[1] * X0 - 2.0 * a1 * a2 * X0 + a2);
-    v_cxx[2] = (float)(-0.5 * dxyy * X0 * X0 - (double)(a2 * a2 * X0) + (double)(c[2] * X0));
-    v_cxx[3] = (float)(-0.5 * dyyy * X0 * X0);
-    v_cxy[0] = (float)((double)(-dxxx * X0 * X1) + 3.0 * c[0] * X1 - 3.0 * a1 * a1 * X1);
-    v_cxy[1] = (float)((double)(-dxxy * X0 * X1) + 2.0 * c[1] * X1 + 2.0 * a1 - 2.0 * a1 * a2 * X1 - (double)(a1 * a1 * X0) + (double)(c[0] * X0));
-    v_cxy[2] = (float)((double)(-dxyy * X0 * X1) + 2.0 * c[1] * X0 + 2.0 * a2 - (double)(a2 * a2 * X1) - 2.0 * a1 * a2 * X0 + (double)(c[2] * X1));
-    v_cxy[3] = (float)((double)(-dyyy * X0 * X1) + 3.0 * c[2] * X0 - 3.0 * a2 * a2 * X0);
-    v_cyy[0] = (float)(-0.5 * dxxx * X1 * X1);
-    v_cyy[1] = (float)(-0.5 * dxxy * X1 * X1 - (double)(a1 * a1 * X1) + (double)(c[0] * X1));
-    v_cyy[2] = (float)(-0.5 * dxyy * X1 * X1 + 2.0 * c[1] * X1 - 2.0 * a1 * a2 * X1 + a1);
-    v_cyy[3] = (float)(-0.5 * dyyy * X1 * X1 + 3.0 * c[2] * X1 + 3.0 * a2 - 3.0 * a2 * a2 * X1);
-    gc[0] += (v_cxx[0] * Gk[0] + v_cxx[1] * S1 + v_cxx[2] * S2 + v_cxx[3] * Gk[7]) * G;
-    gc[1] += (v_cxy[0] * Gk[0] + v_cxy[1] * S1 + v_cxy[2] * S2 + v_cxy[3] * Gk[7]) * G;
-    gc[2] += (v_cyy[0] * Gk[0] + v_cyy[1] * S1 + v_cyy[2] * S2 + v_cyy[3] * Gk[7]) * G;
-}
+/* backward.cu:108-416 (oracle_bwd_body.h): bwd_pair (float sums) and bwd_pair64 (exact sums) */
+#define BWD_T float
+#define BWD_FN(name) name
+#include "oracle_bwd_body.h"
+#undef BWD_T
+#undef BWD_FN
+#define BWD_T double
+#define BWD_FN(name) name##64
+#include "oracle_bwd_body.h"
+#undef BWD_T
+#undef BWD_FN
 
 static void displacement(int D, const float *m, const float *s, float *X) {
     for (int k = 0; k < D; ++k) X[k] = ref_wrap(m[k] - s[k]);
@@ -540,6 +381,29 @@ void orc_backward(const orc_bins *b, int fn, int C, const float *means, const fl
             float X[2];
             displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
             bwd_pair(fn, D, C, X, conics + (int64_t)g * S, values + (int64_t)g * C, dL,
+                     dmeans + (int64_t)g * D, dvalues + (int64_t)g * C, dconics + (int64_t)g * S);
+        }
+    }
+}
+
+/* orc_backward with exact (double) sums of the same float per-pair terms: the value around
+ * which every atomic order of the reference scatters; the GPU parity tests' gradient reference.  Grads are accumulated into dmeans[P][D], dvalues[P][C], dconics[P][S]
+ * (caller zero-initialises).  Only samples in `sub` contribute (NULL = all). */
+void orc_backward64(const orc_bins *b, int fn, int C, const float *means, const float *values,
+                    const float *conics, const float *samples, const float *dL_dout, double *dmeans,
+                    double *dvalues, double *dconics, int nsub, const int32_t *sub) {
+    const int D = b->D, S = D * (D + 1) / 2, K = out_comps(fn, D);
+    int count = sub ? nsub : b->N;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        const float *dL = dL_dout + (int64_t)sid * K * C;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            bwd_pair64(fn, D, C, X, conics + (int64_t)g * S, values + (int64_t)g * C, dL,
                      dmeans + (int64_t)g * D, dvalues + (int64_t)g * C, dconics + (int64_t)g * S);
         }
     }

@@ -44,6 +44,7 @@ def _load():
     lib.orc_tile_gaussians.restype = i64
     lib.orc_forward.argtypes = [P, i32, i32, P, P, P, P, P, i32, P]
     lib.orc_backward.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
+    lib.orc_backward64.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
     lib.orc_count_pairs.argtypes = [P, P, P, P, ctypes.c_double, i32, P, P, P]
     lib.orc_tile_grid.argtypes = [i32, i32, P, P, P]
     lib.orc_agg_counts.argtypes = [i32, i32, P, P, P]
@@ -148,7 +149,10 @@ class OracleBins:
                         _ptr(out), 0 if sub is None else len(sub), _ptr(sub))
         return out
 
-    def backward(self, function, values, conics, dL_dout, subset=None, samples=None, means=None):
+    def backward(self, function, values, conics, dL_dout, subset=None, samples=None, means=None, exact=False):
+        """backward.cu:26-106.  exact=False: the float sums in serial order (one of the reference's
+        atomic orders); exact=True: the same float per-pair terms summed in double (float64 arrays),
+        the value every atomic order scatters around -- the GPU parity tests' reference."""
         lib = _load()
         v = _f32(values)
         c = _f32(conics)
@@ -157,11 +161,12 @@ class OracleBins:
         C = v.shape[1]
         S = self.D * (self.D + 1) // 2
         dL = _f32(dL_dout).reshape(self.N, -1)
-        dm = np.zeros((self.P, self.D), np.float32)
-        dv = np.zeros((self.P, C), np.float32)
-        dc = np.zeros((self.P, S), np.float32)
+        ft = np.float64 if exact else np.float32
+        dm = np.zeros((self.P, self.D), ft)
+        dv = np.zeros((self.P, C), ft)
+        dc = np.zeros((self.P, S), ft)
         sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
-        lib.orc_backward(self._h, FUNCTIONS[function], C, _ptr(m), _ptr(v), _ptr(c), _ptr(s),
+        (lib.orc_backward64 if exact else lib.orc_backward)(self._h, FUNCTIONS[function], C, _ptr(m), _ptr(v), _ptr(c), _ptr(s),
                          _ptr(dL), _ptr(dm), _ptr(dv), _ptr(dc),
                          0 if sub is None else len(sub), _ptr(sub))
         return dm, dv, dc

@@ -3,9 +3,12 @@ oracle (oracle/oracle.c, the restatement of the reference), on identical seeded 
 
 Integer / index outputs (num_rendered, radii, reference-layout ranges) must be bit-identical.
 Floating-point outputs use the SURVEY 8c tolerance, per tensor:
-    |gpu - ref| <= RTOL * |ref| + ATOL * max|ref|,   RTOL = 1e-5, ATOL = 1e-6 (forward)
-and the same with ATOL = 1e-5 for gradients, whose reference order is atomic (nondeterministic)
-and whose terms cancel heavily (values ~ N(0,1), dL ~ N(0,1)).
+    |gpu - ref| <= RTOL * |ref| + ATOL * max|ref|,   RTOL = 1e-5, ATOL = 1e-6
+for the forward and for the gradients alike.  Gradients are compared with the oracle's exact sum
+of the reference's float per-pair terms (the reference adds them with float atomics in no fixed
+order): helpers.close_grad widens the bound only where the reference's own serial float order is
+further than half of it from that sum (dense clusters), to twice the reference's deviation.  Per-check margins are
+recorded when $DGS_MARGINS is set (profiles/r04_margins.json).
 """
 import numpy as np
 import pytest
@@ -13,13 +16,13 @@ import torch
 
 from diff_gaussian_sampling import synthetic as syn
 import cases
-from helpers import FUNCS, close, gpu_run, ref_ranges_bytes
+from helpers import FUNCS, close, close_grad, gpu_run, ref_ranges_bytes
 
 pytestmark = pytest.mark.gpu
 
 RTOL = 1e-5
 ATOL_FWD = 1e-6
-ATOL_BWD = 1e-5
+ATOL_BWD = 1e-6  # rtol 1e-5 + atol 1e-6 max|ref|
 
 
 def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=None,
@@ -53,11 +56,10 @@ def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL,
         got, ref_out = got[subset], ref_out[subset]
     attempt(close, got, ref_out, RTOL, atol_fwd, f"{function} forward")
     # backward
-    dm, dv, dc = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
-    gm, gv, gc = res["grads"]
-    attempt(close, gm, dm, RTOL, atol_bwd, f"{function} dL/dmeans")
-    attempt(close, gv, dv, RTOL, atol_bwd, f"{function} dL/dvalues")
-    attempt(close, gc, dc, RTOL, atol_bwd, f"{function} dL/dconics")
+    lit = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
+    ex = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
+    for got, e, l, name in zip(res["grads"], ex, lit, ("dmeans", "dvalues", "dconics")):
+        attempt(close_grad, got, e, l, RTOL, atol_bwd, f"{function} dL/d{name}")
     assert not errors, "\n".join(errors)
     return res, ob
 
