@@ -5,12 +5,17 @@
 
 Workload (BASELINE.json configs): 1M anisotropic 2-D Gaussians, C = 1.
   * N = 1: configs[2], the headline -- 1M Gaussians x 2M query points on one GPU.
-  * N > 1: configs[3] -- 1M Gaussians x 1M query points PER GPU (1M x 8M at N = 8), the query
-    points sharded, the Gaussians replicated (same seed on every rank), the tile grid the global
-    one (all-reduce MIN/MAX of the sample bounds, sample_points.cu:70-74), and ONE RCCL
-    all-reduce (sum) of the packed [dmeans | dvalues | dconics] gradients per step.
+  * N > 1: configs[3] -- 1M Gaussians x 1M query points PER GPU (1M x 8M at N = 8), the tile
+    grid the global one (all-reduce MIN/MAX of the sample bounds, sample_points.cu:70-74).  Two
+    ways to sum the per-Gaussian gradients:
+      --shard spatial (default): rank r's points are the strip r along y; the backward sends each
+        partial row to its owner rank only (one RCCL all-to-all, SupportExchange.reduce) and the
+        owners send their rows back to every rank that holds them (SupportExchange.push, an id
+        and a row all-to-all) -- both inside the timed step;
+      --shard dense: uniform points on every rank, ONE RCCL all-reduce (sum) of the packed
+        [dmeans | dvalues | dconics] gradients per step (the north star's formulation).
     `--weak` keeps 2M query points per GPU instead.
-One step = forward + backward through the autograd Function (+ the all-reduce for N > 1);
+One step = forward + backward through the autograd Function (+ the gradient exchange for N > 1);
 binning (preprocess) is timed separately, as the metric asks.
 
 `python bench.py --gpus N` without a torch.distributed environment starts the N ranks itself
@@ -257,7 +262,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
     if multi:  # one dL per function of the fused call
         dLm = [syn.grad_out(N, D ** FUNCS[f], C, seed=5 + 1000 * rank + 17 * i).to(dev).reshape(
             (N,) + (D,) * FUNCS[f] + (C,)) for i, f in enumerate(multi)]
-    ar_ev = []  # (start, end) events around the all-reduce, on its stream
+    ar_ev = []  # (start, end) events around the gradient sum, on its stream
+    push_ev = []  # (start, end) events around the spatial push
 
     def step(timed=False):
         for t in (means, values, conics):
@@ -280,6 +286,14 @@ def bench_sample(args, world, rank, dev, torch, dist):
             if timed:
                 e1.record()
                 ar_ev.append((e0, e1))
+            if spatial:  # the owners' rows to every rank their cut reaches (once per optimizer step)
+                if timed:
+                    p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    p0.record()
+                xchg.push([means, values, conics], means, conics)
+                if timed:
+                    p1.record()
+                    push_ev.append((p0, p1))
 
     for _ in range(args.warmup):
         step()
@@ -314,16 +328,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
     ms_per_step = elapsed * 1e3 / args.steps
     value = N * world / (ms_per_step / 1e3)
 
-    push_ms = 0.0
-    if spatial:  # the owners' rows to every rank their cut reaches: once per optimizer step
-        pushed = []
-        for _ in range(3):
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            xchg.push([means, values, conics], means, conics)
-            torch.cuda.synchronize()
-            pushed.append((time.perf_counter() - t0) * 1e3)
-        push_ms = sorted(pushed)[1]
+    push_ms = sum(a.elapsed_time(b) for a, b in push_ev) / len(push_ev) if push_ev else 0.0
     # ---- live-pair count (diagnostic kernel, outside the timed region)
     w_cand, w_live = dgs._C.count_pairs(means.detach(), conics.detach(), samples, gb, sb, -104.0)
     avg_f = fms / max(nf, 1)
@@ -383,7 +388,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
                                       else ", 1 RCCL all-reduce per step") if world > 1 else "")},
         "preprocess_ms": pre_ms,
         # the Physics-Informed-GS loop re-bins every step (means move): its step time
-        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms + push_ms,
+        "total_ms_per_step_incl_preprocess": ms_per_step + pre_ms,
         "preprocess_first_call_ms": pre_first_ms,
         **pre_extra,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
@@ -401,7 +406,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
                                                               else int(flat.numel() * 4)),
                                  "dense_allreduce_bytes": int(flat.numel() * 4),
                                  "exchange_setup_ms_once": xsetup_ms,
-                                 "push_ms": push_ms,
+                                 "push_ms_rank0_in_step": push_ms,
                                  "held_rows_rank0": int(xchg.held.sum()) if spatial else P,
                                  "w_cand_per_point_rank0": w_cand / N}
 
@@ -505,7 +510,14 @@ def bench_volume(args, world, rank, dev, torch, dist):
             fwd_ms.append(ev[0].elapsed_time(ev[1]))
             bwd_ms.append(ev[1].elapsed_time(ev[2]))
 
-    for _ in range(args.warmup):
+    # the first step also builds the transposed lists (at its backward, once per
+    # preprocess_aggregate: a loop that re-runs the neighbour search every step pays it per step)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    step(False)
+    torch.cuda.synchronize()
+    first_step_ms = (time.perf_counter() - t1) * 1e3
+    for _ in range(args.warmup - 1):
         step(False)
     torch.cuda.synchronize()
     if world > 1:
@@ -605,7 +617,14 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
             fwd_ms.append(ev[0].elapsed_time(ev[1]))
             bwd_ms.append(ev[1].elapsed_time(ev[2]))
 
-    for _ in range(args.warmup):
+    # the first step also builds the transposed lists (at its backward, once per
+    # preprocess_aggregate: a loop that re-runs the neighbour search every step pays it per step)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    step(False)
+    torch.cuda.synchronize()
+    first_step_ms = (time.perf_counter() - t1) * 1e3
+    for _ in range(args.warmup - 1):
         step(False)
     torch.cuda.synchronize()
     if world > 1:
@@ -656,6 +675,9 @@ def bench_aggregate(args, world, rank, dev, torch, dist):
                    "neighbour_slots": Lnb, "parallelism": f"replicas x{world}"},
         "preprocess_aggregate_ms": pre_ms,
         "preprocess_aggregate_first_call_ms": pre_times[0],
+        # the first fwd + bwd on new lists: + the transposition of the lists (built lazily at
+        # that backward); preprocess_aggregate + this is a re-binning loop's step
+        "first_step_ms_incl_transpose": first_step_ms,
         "phases_ms": {"forward": f_ms, "backward": b_ms},
         "roofline": roof_bwd,
         # the forward: per slot it streams indices / dists / densities (20 B) and writes weights /

@@ -534,9 +534,13 @@ const int32_t *order_get(const Tensor &indices, int64_t P) {
 }
 
 // The transposed lists built from exactly this indices tensor (same object, not modified since).
+// Entries whose indices tensor has died are dropped here too (they would pin their lists).
 bool transpose_get(const Tensor &indices, const Tensor &ranges, int64_t P, Tensor &tstart, Tensor &tslot,
                    Tensor &rstart) {
     std::lock_guard<std::mutex> lk(g_agg_mu);
+    for (auto it = g_agg.begin(); it != g_agg.end();)
+        if (it->impl.expired()) it = g_agg.erase(it);
+        else ++it;
     for (const auto &e : g_agg) {
         if (!e.tstart.defined() || e.P != P || e.length != indices.numel()) continue;
         const auto sp = e.impl.lock();
@@ -549,6 +553,24 @@ bool transpose_get(const Tensor &indices, const Tensor &ranges, int64_t P, Tenso
         }
     }
     return false;
+}
+
+// Keeps lists built at a backward call with the cache entry of the indices tensor they came from
+// (built lazily: forward-only users never pay for the transposition).
+void transpose_put(const Tensor &indices, const Tensor &ranges, int64_t P, const Tensor &tstart, const Tensor &tslot,
+                   const Tensor &rstart) {
+    std::lock_guard<std::mutex> lk(g_agg_mu);
+    for (auto &e : g_agg) {
+        if (e.P != P || e.length != indices.numel()) continue;
+        const auto sp = e.impl.lock();
+        if (sp.get() == indices.unsafeGetTensorImpl() && e.version == (int64_t)indices._version() &&
+            e.ranges.data_ptr() == ranges.data_ptr() && e.ranges_version == (int64_t)ranges._version()) {
+            e.tstart = tstart;
+            e.tslot = tslot;
+            e.rstart = rstart;
+            return;
+        }
+    }
 }
 
 bool transpose_enabled() {
@@ -602,13 +624,9 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsPreprocessC
         return ctx.bufs[which].view(st).narrow(0, 0, length * (shape.size() > 1 ? shape[1] : 1)).view(shape);
     };
     Tensor indices = view(DGS_BUF_AGG_INDICES, torch::kInt64, {length});
-    if (length > 0) {
-        // the transposed lists for the backward's per-row gather (dgs_agg_backward_tr)
-        Tensor tstart, tslot, rstart;
-        if (transpose_enabled() && length < ((int64_t)1 << 31))
-            build_transpose(indices, ranges, order.data_ptr<int32_t>(), P, tstart, tslot, rstart, debug);
-        agg_put(indices, ranges, P, order, tstart, tslot, rstart);
-    }
+    // (the transposed lists of the backward's per-row gather, dgs_agg_backward_tr, are built at
+    // the first backward on these lists and kept with this entry)
+    if (length > 0) agg_put(indices, ranges, P, order, Tensor(), Tensor(), Tensor());
     return std::make_tuple(indices, ranges, view(DGS_BUF_AGG_DISTS, torch::kFloat32, {length, D}),
                            view(DGS_BUF_AGG_DENSITIES, torch::kFloat32, {length}), inv_total);
 }
@@ -683,8 +701,10 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor> AggregateNeighborsBac
     const int64_t length = a.indices.numel();
     Tensor tstart, tslot, rstart;
     const bool tr = a.P > 0 && a.L + a.K <= 64 && length < ((int64_t)1 << 31) && transpose_enabled();
-    if (tr && !transpose_get(a.indices, a.ranges, a.P, tstart, tslot, rstart))  // not from preprocess_aggregate
+    if (tr && !transpose_get(a.indices, a.ranges, a.P, tstart, tslot, rstart)) {  // first backward on these lists
         build_transpose(a.indices, a.ranges, order_get(a.indices, a.P), a.P, tstart, tslot, rstart, debug);
+        transpose_put(a.indices, a.ranges, a.P, tstart, tslot, rstart);
+    }
     if (tr) {
         const size_t ws = dgs_agg_workspace_size_tr(a.P, a.L, length);
         Tensor work = torch::empty({(int64_t)ws}, a.features.options().dtype(torch::kUInt8));

@@ -154,6 +154,8 @@ def exchange_sets(means, conics, extents):
     dev = means.device
     ext = torch.as_tensor(extents).detach().double().cpu()
     W = ext.shape[0]
+    if W > 63:  # (the rank bits live in one int64 per Gaussian)
+        raise ValueError(f"exchange_sets: at most 63 ranks (got {W})")
     if means.is_cuda and W <= 32:
         mask, owner = _C.exchange_sets(means.detach(), conics.detach(), [float(v) for v in ext.reshape(-1)])
         return mask.long() & 0xFFFFFFFF, owner.long()
@@ -296,8 +298,14 @@ class SupportExchange:
             return 0
         mask, _ = exchange_sets(means, conics, self.extents)
         ids, send_n = self._by_rank(mask, torch.nonzero(self.owned).flatten())
-        out_splits = [int(v) for v in send_n.cpu()]
-        in_splits = self._counts_a2a(out_splits)
+        if dist.get_backend(self.group) == "gloo":
+            out_splits = [int(v) for v in send_n.cpu()]
+            in_splits = self._counts_a2a(out_splits)
+        else:  # the counts exchanged on the device, both read back in one host transfer
+            recv_n = torch.empty_like(send_n)
+            dist.all_to_all_single(recv_n, send_n, [1] * W, [1] * W, group=self.group)
+            n = torch.stack([send_n, recv_n]).cpu()
+            out_splits, in_splits = [int(v) for v in n[0]], [int(v) for v in n[1]]
         out_ids = list(torch.split(ids, out_splits))
         cols = [t.reshape(t.shape[0], -1) for t in tensors]
         F = sum(c.shape[1] for c in cols)
@@ -335,19 +343,28 @@ def shard_extents(samples, group=None):
     return torch.stack(out)
 
 
-def grid_and_box(samples, group=None):
+def grid_and_box(samples, group=None, strip=None):
     """(grid, offset) of the union of every rank's samples (global_tile_grid) and this rank's
-    own bounding box (lo[D], hi[D]), read back in ONE host transfer."""
+    own bounding box (lo[D], hi[D]), read back in ONE host transfer.  strip = (lo, hi) of this
+    rank along the sharding axis: also returns whether ANY rank's samples leave its strip (folded
+    into the MAX all-reduce, so every rank learns it together), else None."""
+    D = samples.shape[1]
     mn = samples.min(0).values
     mx = samples.max(0).values
     gmn, gmx = mn.clone(), mx.clone()
+    if strip is not None:
+        out = ((mn[D - 1] < strip[0]) | (mx[D - 1] > strip[1])).float().reshape(1)
+        gmx = torch.cat([gmx, out])
     if _world(group) > 1:
         dist.all_reduce(gmn, op=dist.ReduceOp.MIN, group=group)
         dist.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
-    grid = torch.ceil((gmx - gmn + 1e-6) / 0.51).to(torch.float32)
+    grid = torch.ceil((gmx[:D] - gmn + 1e-6) / 0.51).to(torch.float32)
     h = torch.stack([grid, gmn, mn, mx]).cpu()
-    return ([int(g) for g in h[0]], [float(o) for o in h[1]], [float(v) for v in h[2]],
-            [float(v) for v in h[3]])
+    res = ([int(g) for g in h[0]], [float(o) for o in h[1]], [float(v) for v in h[2]],
+           [float(v) for v in h[3]])
+    if strip is None:
+        return res
+    return res + (bool(gmx[D].item() > 0),)
 
 
 def pack_grads(grads):
@@ -413,14 +430,21 @@ class SpatialShardedGaussianSampler(ShardedGaussianSampler):
         W = _world(self.group)
         rank = dist.get_rank(self.group) if W > 1 else 0
         D = samples.shape[1]
-        grid, offset, lo, hi = grid_and_box(samples, self.group)
+        known = self.xchg.extents if self.xchg is not None else self.extents
+        strip = None
+        if known is not None:
+            e = torch.as_tensor(known).detach().double().cpu()[rank]
+            strip = (float(e[0]), float(e[1])) if samples.shape[0] else (-math.inf, math.inf)
+        # (an empty rank never leaves its strip)
+        grid, offset, lo, hi, *left = grid_and_box(samples, self.group, strip) if strip is not None else \
+            grid_and_box(samples, self.group)
+        if left and left[0]:  # raised on every rank together (no rank left waiting in a collective)
+            raise ValueError(f"rank {rank}: the samples of some rank leave its strip along the sharding axis "
+                             f"(this rank: [{lo[D - 1]}, {hi[D - 1]}] in [{strip[0]}, {strip[1]}]); pass "
+                             f"extents covering every call's points")
         if self.xchg is None:
             ext = self.extents if self.extents is not None else shard_extents(samples, self.group)
             self.xchg = SupportExchange(means, conics, ext, rank, self.group, self.debug)
-        e = self.xchg.extents[rank]
-        if samples.shape[0] and (lo[D - 1] < float(e[0]) or hi[D - 1] > float(e[1])):
-            raise ValueError(f"rank {rank}: samples leave the rank's strip [{float(e[0])}, {float(e[1])}] "
-                             f"along the sharding axis ([{lo[D - 1]}, {hi[D - 1]}])")
         area = 1.0
         for d in range(D):
             area *= max(hi[d] - lo[d], 0.0)

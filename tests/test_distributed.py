@@ -250,3 +250,43 @@ def test_support_halfwidth_bounds_the_live_pairs(oracle):
     live = -0.5 * q >= -104.0
     assert live.any()
     assert not np.any(live & (np.abs(X[..., 1]) > e[:, None]))
+
+
+def _strip_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import diff_gaussian_sampling.distributed as dd
+        from oracle_stub import OracleC
+        dd._C = OracleC()
+        means, values, covs, conics, samples, w = _spatial_problem()
+        order = torch.argsort(samples[:, 1])
+        shard = torch.tensor_split(order, world)[rank].sort().values
+        m, v, c = (t.clone().requires_grad_(True) for t in (means, values, conics))
+        sampler = dd.SpatialShardedGaussianSampler()
+        sampler.preprocess(m, v, covs, c, samples[shard])
+        moved = samples[shard].clone()
+        if rank == 1:  # only this rank's points leave its strip
+            moved[:, 1] -= 0.05
+        try:
+            sampler.preprocess(m, v, covs, c, moved)
+            raised = False
+        except ValueError:
+            raised = True
+        # a collective after the call: a rank that had not raised would be the only one here
+        flag = torch.tensor([int(raised)])
+        dist.all_reduce(flag)
+        np.savez(os.path.join(outdir, f"strip{rank}.npz"), raised=raised, total=int(flag))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_spatial_strip_violation_raises_on_every_rank(tmp_path):
+    """A later preprocess whose points leave one rank's strip raises ValueError on EVERY rank
+    (the check is folded into the grid all-reduce), so no rank waits alone in the backward's
+    all-to-all."""
+    world = 2
+    mp.spawn(_strip_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    for r in range(world):
+        z = np.load(tmp_path / f"strip{r}.npz")
+        assert bool(z["raised"]) and int(z["total"]) == world
