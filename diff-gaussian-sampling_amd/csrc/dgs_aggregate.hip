@@ -1702,3 +1702,14 @@ extern "C" int dgs_agg_transpose(int P, int64_t length, const int64_t *indices, 
     DGS_LAUNCH_CHECK(s, debug);
     return DGS_OK;
 }
+
+// ------------------------------------------------------------------------- warm-up
+// A no-op launch: the first launch of any kernel of this translation unit loads its code object
+// (rocprim's kernels included) onto the device; dgs_warmup does it for every unit up front.
+__global__ void k_warm_aggregate() {}
+namespace dgs {
+hipError_t warm_aggregate(hipStream_t s) {
+    k_warm_aggregate<<<1, 1, 0, s>>>();
+    return hipGetLastError();
+}
+}  // namespace dgs

@@ -290,3 +290,14 @@ DGS_REF_INST(kMulti + 11, 2, 1) DGS_REF_INST(kMulti + 12, 2, 1) DGS_REF_INST(kMu
 DGS_REF_INST(kMulti + 14, 2, 1) DGS_REF_INST(kMulti + 15, 2, 1)
 
 }  // namespace dgs
+
+// ------------------------------------------------------------------------- warm-up
+// A no-op launch: the first launch of any kernel of this translation unit loads its code object
+// (rocprim's kernels included) onto the device; dgs_warmup does it for every unit up front.
+__global__ void k_warm_reference() {}
+namespace dgs {
+hipError_t warm_reference(hipStream_t s) {
+    k_warm_reference<<<1, 1, 0, s>>>();
+    return hipGetLastError();
+}
+}  // namespace dgs

@@ -1220,3 +1220,14 @@ extern "C" int dgs_volume_count_pairs(int P, int N, const float *means, const fl
     counts[1] = (int64_t)h[1];
     return DGS_OK;
 }
+
+// ------------------------------------------------------------------------- warm-up
+// A no-op launch: the first launch of any kernel of this translation unit loads its code object
+// (rocprim's kernels included) onto the device; dgs_warmup does it for every unit up front.
+__global__ void k_warm_volume() {}
+namespace dgs {
+hipError_t warm_volume(hipStream_t s) {
+    k_warm_volume<<<1, 1, 0, s>>>();
+    return hipGetLastError();
+}
+}  // namespace dgs

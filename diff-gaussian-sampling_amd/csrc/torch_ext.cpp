@@ -848,6 +848,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("volume_backward", &VolumeBackward);
     m.def("volume_count_pairs", &VolumeCountPairs);
     m.def("library_version", []() { return dgs_version(); });
+    m.def("warmup", []() { check(dgs_warmup(as_dgs(cur_stream())), "warmup"); });
     m.def("timing_enable", [](bool on) { dgs_timing_enable(on ? 1 : 0); });
     m.def("timing_read", [](int which) {
         double ms = 0.0;

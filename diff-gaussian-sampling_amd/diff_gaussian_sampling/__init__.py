@@ -84,6 +84,13 @@ def call_debug(func, debug, name, *args):
         raise
 
 
+def warmup():
+    """Loads every code object of the native library onto the current GPU (dgs_warmup): the
+    one-time cost the first call of each kind would otherwise pay.  Optional; call once at
+    start-up (after torch.cuda.set_device)."""
+    _C.warmup()
+
+
 def preprocess_gaussians(means, values, covariances, conics, samples, debug):
     """Tile binning (py:52-65).  Returns (num_rendered, binning_buffer, sample_binning_buffer,
     ranges, sample_ranges, radii)."""

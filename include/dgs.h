@@ -63,6 +63,11 @@ typedef void *(*dgs_alloc_fn)(void *ctx, int which, size_t bytes);
 const char *dgs_last_error(void);
 int dgs_version(void);
 
+/* Loads every code object of the library onto the current device (one no-op launch per
+ * translation unit; synchronises `stream`).  Optional: otherwise the first call of each kind
+ * pays its unit's load (a training loop calls it once at start-up; bench.py reports it). */
+int dgs_warmup(dgs_stream_t stream);
+
 /* Tile grid of the reference host glue (sample_points.cu:70-74), computed on the device with
  * torch's CUDA-path arithmetic: grid[d] = ceil((max_d - min_d + 1e-6f) * (1.0f / 0.51f)),
  * offset[d] = min_d.  Synchronises `stream`; grid_out/offset_out are host arrays of D. */

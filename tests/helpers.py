@@ -54,16 +54,13 @@ def margin_of(got, ref, rtol, atol_frac):
 
 def close_grad(got, exact, literal, rtol, atol_frac, what=""):
     """A gradient against the oracle's exact sum of the reference's float per-pair terms
-    (OracleBins.backward(exact=True)).  The reference adds those terms with float atomics in no
-    fixed order; `literal` is one such order (the oracle's serial float sums).  The bound is the
-    SURVEY 8c tolerance, widened only where the reference's own serial order is further than half
-    of it from the exact sum (dense clusters: thousands of cancelling terms per Gaussian): then
-    the GPU must stay within twice the reference's own deviation."""
-    m_ref = margin_of(literal, exact, rtol, atol_frac)
-    _record_margin(what + " [reference serial order vs exact]", m_ref, rtol, atol_frac, int(np.size(exact)))
-    _record_margin(what + " [vs exact, 8c bound]", margin_of(got, exact, rtol, atol_frac), rtol, atol_frac,
-                   int(np.size(exact)))
-    close(got, exact, rtol, atol_frac * max(1.0, 2.0 * m_ref), what)
+    (OracleBins.backward(exact=True)) at the given tolerance.  The reference adds those terms with
+    float atomics in no fixed order; `literal` is one such order (the oracle's serial float sums),
+    whose distance from the exact sum -- the reference's own run-to-run spread -- is recorded next
+    to the GPU's (profiles/r04_margins.json) as the evidence for a case's stated bound."""
+    _record_margin(what + " [reference serial order vs exact]", margin_of(literal, exact, rtol, atol_frac), rtol,
+                   atol_frac, int(np.size(exact)))
+    close(got, exact, rtol, atol_frac, what)
 
 
 def gpu_run(C_mod, function, means, values, covs, conics, samples, dL=None, debug=False):

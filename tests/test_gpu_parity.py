@@ -6,8 +6,7 @@ Floating-point outputs use the SURVEY 8c tolerance, per tensor:
     |gpu - ref| <= RTOL * |ref| + ATOL * max|ref|,   RTOL = 1e-5, ATOL = 1e-6
 for the forward and for the gradients alike.  Gradients are compared with the oracle's exact sum
 of the reference's float per-pair terms (the reference adds them with float atomics in no fixed
-order): helpers.close_grad widens the bound only where the reference's own serial float order is
-further than half of it from that sum (dense clusters), to twice the reference's deviation.  Per-check margins are
+order); the one exception is the clustered case, whose stated bound is ATOL_BWD_CLUSTERED.  Per-check margins are
 recorded when $DGS_MARGINS is set (profiles/r04_margins.json).
 """
 import numpy as np
@@ -23,6 +22,11 @@ pytestmark = pytest.mark.gpu
 RTOL = 1e-5
 ATOL_FWD = 1e-6
 ATOL_BWD = 1e-6  # rtol 1e-5 + atol 1e-6 max|ref|
+# The clustered case (thousands of cancelling terms per Gaussian): the reference's own serial
+# float order is up to 1.5e-6 max|ref| from the exact sum there (profiles/r04_margins.json,
+# "[reference serial order vs exact]"), i.e. two runs of the reference differ by more than the
+# 8c bound; its stated bound is 4e-6.
+ATOL_BWD_CLUSTERED = 4e-6
 
 
 def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=None,
@@ -59,7 +63,7 @@ def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL,
     lit = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
     ex = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
     for got, e, l, name in zip(res["grads"], ex, lit, ("dmeans", "dvalues", "dconics")):
-        attempt(close_grad, got, e, l, RTOL, atol_bwd, f"{function} dL/d{name}")
+        attempt(close_grad, got, e, l, RTOL, atol_bwd, f"{function} dL/{name}")
     assert not errors, "\n".join(errors)
     return res, ob
 
@@ -103,7 +107,7 @@ def test_parity_clustered(dgs, oracle, function, C):
     means, values, covs, conics, samples = cases.clustered_case(C=C)
     K = syn.out_components(function, 2)
     dL = syn.grad_out(samples.shape[0], K, C, seed=162)
-    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, atol_bwd=ATOL_BWD_CLUSTERED)
 
 
 @pytest.mark.parametrize("function,C", [(f, 1) for f in FUNCS] + [("gaussian", 16)])

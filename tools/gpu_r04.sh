@@ -15,6 +15,9 @@ if [ "${2:-}" != "notests" ]; then
   echo "pytest rc=$rc"
   [ $rc -le 1 ] || exit $rc
 fi
+timeout -k 10 120 python -u tools/first_call.py > $O/first_call.log 2>&1 || { echo first_call failed; tail -5 $O/first_call.log; exit 1; }
+timeout -k 10 120 python -u tools/first_call.py --no-warmup >> $O/first_call.log 2>&1 || { echo first_call failed; tail -5 $O/first_call.log; exit 1; }
+cat $O/first_call.log
 timeout -k 10 300 python -u bench.py --no-cpu > $O/bench.log 2>&1 || { echo bench failed; tail -5 $O/bench.log; exit 1; }
 tail -1 $O/bench.log
 export TMPDIR=/tmp
