@@ -122,6 +122,8 @@ def main():
                          "(distributed.SupportExchange, SURVEY 8f f3); dense = uniform points on "
                          "every rank and one all-reduce of every gradient")
     ap.add_argument("--C", type=int, default=1)
+    ap.add_argument("--aniso", type=float, default=1.0,
+                    help="axis ratios U[1, aniso] at the headline's areas (thin Gaussians: 25)")
     ap.add_argument("--grid", type=int, default=0,
                     help="query points on a regular g x g lattice instead of uniform (SURVEY 8d config 5: 4096)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baselines")
@@ -136,6 +138,10 @@ def main():
                     help="sample: the headline (default); aggregate: aggregate_neighbors at SURVEY "
                          "config 5 (P = 1M, K = L = 16, F = 4), one GPU or N replicas")
     ap.add_argument("--cpu-rows", type=int, default=20000, help="aggregate CPU-baseline rows")
+    ap.add_argument("--calltime", action="store_true",
+                    help="also time fwd + bwd after an in-place step on the means WITHOUT re-binning: the "
+                         "call-time path (the reference's whole tile pair set, dgs_reference.hip), next to "
+                         "re-binning + the binned step")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -179,7 +185,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
     N = args.N if args.N is not None else (2_000_000 if (world == 1 or args.weak) else 1_000_000)
     fn = args.function
     K = D ** FUNCS[fn]
-    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, D, C, seed=0))
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, D, C, seed=0, aniso=args.aniso))
     if args.grid:
         g = args.grid
         allpts = syn.grid_samples(g, D)
@@ -369,6 +375,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
     workload = (f"{P // 1000}k Gaussians x {N // 1000}k query points per GPU"
                 + (f" ({args.grid}^2 lattice)" if args.grid else "")
                 + f", D=2, C={C}, function={fname}, fwd+bwd"
+                + (f", axis ratios U[1, {args.aniso:g}]" if args.aniso > 1 else "")
                 + ((", spatial strips + sparse gradient exchange" if spatial else ", RCCL all-reduce of grads")
                    if world > 1 else ""))
     result = {
@@ -400,6 +407,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
         **pre_extra,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
+        "entries": dict(zip(("num_rendered", "fine_entries", "literal_path_entries", "fine_cells"),
+                            dgs._C.binning_info(gb, sb))),
         "roofline": roofline,
         "hbm": hbm,
         "cpu_baseline": None,
@@ -417,6 +426,35 @@ def bench_sample(args, world, rank, dev, torch, dist):
                                  "held_rows_rank0": int(xchg.held.sum()) if spatial else P,
                                  "w_cand_per_point_rank0": w_cand / N}
 
+    if args.calltime and world == 1 and not multi:
+        # an optimizer-like in-place step on the means (1/10 of the mean spacing), then sampling
+        # with the stale binning: every call compares its inputs with the binned copies and takes
+        # the reference's own pair set (forward.cu:119-162 over every tile pair, W_ref ~ 2.3e11 at
+        # the headline), as the reference would.  Against: re-binning, then the binned step.
+        m_keep = means.detach().clone()
+        with torch.no_grad():
+            step_m = torch.randn(means.shape, generator=torch.Generator().manual_seed(9)).to(dev) * (0.1 * 2.0 / P ** 0.5)
+            means.add_(step_m)
+        ct = []
+        for k in range(3):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            step()
+            torch.cuda.synchronize()
+            ct.append((time.perf_counter() - t0) * 1e3)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        R, gb, sb, rg, srg, _ = dgs._C.preprocess_gaussians(means.detach(), values.detach(), covs, conics.detach(),
+                                                             samples, False)
+        step()
+        torch.cuda.synchronize()
+        rebin_ms = (time.perf_counter() - t0) * 1e3
+        with torch.no_grad():
+            means.copy_(m_keep)
+        result["calltime"] = {"ms_per_step_stale_binning": sorted(ct)[1],
+                              "ms_rebin_plus_step": rebin_ms,
+                              "note": "fwd + bwd after an in-place means update without re-preprocess (the "
+                                      "reference's tile pair set, evaluated on the GPU) vs preprocess + fwd + bwd"}
     if rank == 0 and world == 1 and not args.no_cpu and not multi:
         cpu_baselines(result, means.detach().cpu(), values.detach().cpu(), covs.cpu(),
                       conics.detach().cpu(), samples.cpu(), dL.cpu(), fn, w_live, N, args, torch)

@@ -513,6 +513,7 @@ struct UnitHint {
     int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
     int64_t R;        // num_rendered (sizes the call-time path's backward grid)
+    int64_t E;        // fine (Gaussian, cell) entries
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);

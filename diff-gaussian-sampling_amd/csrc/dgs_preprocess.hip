@@ -851,31 +851,6 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
     }
 }
 
-// Final per-cell list sizes: the gathered entries, then the sorted path's unflagged and flagged
-// half-cells (hb/he over the sorted keys cell << 1 | flag).
-__global__ void k_cell_tot(int ncells, const uint32_t *__restrict__ cnt2, const int32_t *__restrict__ hb,
-                           const int32_t *__restrict__ he, uint32_t *__restrict__ gcnt, uint32_t *__restrict__ tot) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncells) return;
-    uint32_t g = 0;
-    for (int q = 0; q < kGatherRows; ++q) g += cnt2[(int64_t)c * kGatherRows + q];
-    gcnt[c] = g;
-    tot[c] = g + (uint32_t)(he[2 * c] - hb[2 * c]) + (uint32_t)(he[2 * c + 1] - hb[2 * c + 1]);
-}
-
-// [gbeg, gmid, gend) of each cell from the scanned sizes: gathered + unflagged, then flagged.
-__global__ void k_cell_layout(int ncells, const uint32_t *__restrict__ gcnt, const int32_t *__restrict__ hb,
-                              const int32_t *__restrict__ he, const uint32_t *__restrict__ coff,
-                              int32_t *__restrict__ gbeg, int32_t *__restrict__ gmid, int32_t *__restrict__ gend) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncells) return;
-    const int32_t b = (int32_t)coff[c];
-    const int32_t mid = b + (int32_t)gcnt[c] + (he[2 * c] - hb[2 * c]);
-    gbeg[c] = b;
-    gmid[c] = mid;
-    gend[c] = mid + (he[2 * c + 1] - hb[2 * c + 1]);
-}
-
 // The sorted path's half-cells copied behind each cell's gathered entries (one wave per cell).
 __global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32_t *__restrict__ gcnt,
                                                         const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
@@ -890,27 +865,6 @@ __global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32
     const int32_t du = gbeg[c] + (int32_t)gcnt[c], df = gmid[c];
     for (int32_t k = lane; k < u1 - u0; k += kWave) entries[du + k] = svals[u0 + k];
     for (int32_t k = lane; k < f1 - f0; k += kWave) entries[df + k] = svals[f0 + k];
-}
-
-__global__ void k_totals(int P, const uint64_t *__restrict__ offs, const uint64_t *__restrict__ counts,
-                         const uint64_t *__restrict__ toffs, const uint64_t *__restrict__ touched,
-                         const int *__restrict__ dgrid, const float *__restrict__ doff,
-                         const unsigned long long *__restrict__ eg, int64_t *__restrict__ out) {
-    // eg[0]: gathered entries, eg[1]: kUnsafe entries (k_fine_count)
-    if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    out[0] = P > 0 ? (int64_t)(toffs[P - 1] + touched[P - 1]) : 0;  // num_rendered (sampler_impl.cu:253-257)
-    const int64_t es = P > 0 ? (int64_t)(offs[P - 1] + counts[P - 1]) : 0;  // sort-path entries
-    out[1] = es + (int64_t)*eg;                                             // all entries
-    out[4] = es;
-    out[5] = (int64_t)eg[0];
-    out[6] = (int64_t)eg[1];
-    out[7] = 0;
-    // the device-computed tile grid (dgs_preprocess_auto): read back with the totals
-    int32_t *g = reinterpret_cast<int32_t *>(out + 2);
-    g[0] = dgrid ? dgrid[0] : 0;
-    g[1] = dgrid ? dgrid[1] : 0;
-    g[2] = doff ? __float_as_int(doff[0]) : 0;
-    g[3] = doff ? __float_as_int(doff[1]) : 0;
 }
 
 // D = 2: the bounding boxes of a cell's four sub-cells and of the cell (their union), one wave
@@ -1099,57 +1053,8 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
         }
 }
 
-// Forward sub units per sub-cell (samples and entries both present): ceil(pairs / kSubPairs),
-// pair-aligned.
-__global__ void k_sub_ucnt(int nsub, const int32_t *__restrict__ ssbeg, const int32_t *__restrict__ ssend,
-                           const int32_t *__restrict__ lbeg, const int32_t *__restrict__ lend,
-                           uint32_t *__restrict__ ucnt) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nsub) return;
-    const int ns = ssend[k] - ssbeg[k];
-    const int npairs = ((ssend[k] + 1) >> 1) - (ssbeg[k] >> 1);
-    ucnt[k] = ns > 0 && lend[k] > lbeg[k] ? (uint32_t)((npairs + kSubPairs - 1) / kSubPairs) : 0u;
-}
-
-__global__ void k_sub_units(int nsub, const int32_t *__restrict__ ssbeg, const uint32_t *__restrict__ ucnt,
-                            const uint32_t *__restrict__ uoff, uint2 *__restrict__ units,
-                            int32_t *__restrict__ counters) {
-    const int k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= nsub) return;
-    for (uint32_t b = 0; b < ucnt[k]; ++b)
-        units[uoff[k] + b] = make_uint2((uint32_t)k, (uint32_t)(ssbeg[k] & ~1) + b * 2u * kSubPairs);
-    if (k == nsub - 1) counters[kNumFwdSubUnits] = (int32_t)(uoff[k] + ucnt[k]);
-}
-
-// ----------------------------------------------------------------------- work units
-__global__ void k_unit_counts(int ncells, const int32_t *__restrict__ sbeg,
-                              const int32_t *__restrict__ send, const int32_t *__restrict__ gbeg,
-                              const int32_t *__restrict__ gend, uint32_t *__restrict__ fcnt,
-                              uint32_t *__restrict__ bcnt) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncells) return;
-    const int ns = send[c] - sbeg[c], ng = gend[c] - gbeg[c];
-    const int npairs = ((send[c] + 1) >> 1) - (sbeg[c] >> 1);
-    fcnt[c] = ns > 0 && ng > 0 ? (uint32_t)((npairs + kFwdUnit / 2 - 1) / (kFwdUnit / 2)) : 0u;
-    bcnt[c] = ns > 0 ? (uint32_t)((ng + kWave - 1) / kWave) : 0u;
-}
-
-__global__ void k_unit_fill(int ncells, const int32_t *__restrict__ sbeg,
-                            const int32_t *__restrict__ gbeg, const uint32_t *__restrict__ fcnt,
-                            const uint32_t *__restrict__ bcnt, const uint32_t *__restrict__ foff,
-                            const uint32_t *__restrict__ boff, uint2 *__restrict__ funits,
-                            uint2 *__restrict__ bunits, int32_t *__restrict__ counters) {
-    const int c = blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= ncells) return;
-    for (uint32_t b = 0; b < fcnt[c]; ++b)
-        funits[foff[c] + b] = make_uint2((uint32_t)c, (uint32_t)(sbeg[c] & ~1) + b * kFwdUnit);
-    for (uint32_t b = 0; b < bcnt[c]; ++b)
-        bunits[boff[c] + b] = make_uint2((uint32_t)c, (uint32_t)gbeg[c] + b * kWave);
-    if (c == ncells - 1) {
-        counters[kNumFwdUnits] = (int32_t)(foff[c] + fcnt[c]);
-        counters[kNumBwdUnits] = (int32_t)(boff[c] + bcnt[c]);
-    }
-}
+// (The per-cell list sizes and layout, the forward / backward work units and the forward sub
+// units are each one fused_scan launch in preprocess_body: counts -> scan -> outputs.)
 
 // duplicateWithKeys (sampler_impl.cu:54-129) without the 64-bit key: every Gaussian writes
 // its tiles, in the reference's order, at its scan offset (caller id order); a stable sort by
@@ -1284,7 +1189,7 @@ __global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, cons
 
 // Zero-fills up to kZeroMax word-aligned regions in one launch (each hipMemsetAsync is a launch
 // of its own, ~5 us of GPU time even for a few bytes; the binning needs eleven).
-constexpr int kZeroMax = 12;
+constexpr int kZeroMax = 20;
 struct ZeroSpec {
     uint32_t *p[kZeroMax];
     int64_t n[kZeroMax];  // words
@@ -1587,17 +1492,17 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     float2 *igm = ca.take<float2>(P);
     float4 *igc = ca.take<float4>(P);
     float4 *grec = ca.take<float4>(2 * (size_t)P);
+    unsigned long long *fscan_a = ca.take<unsigned long long>(fused_scan_state_words(P, 2, 8));
 
     // sort / scan temp storage: one piece sized for the largest phase-A primitive
-    size_t t_ssort = 0, t_hsort = 0, t_scan = 0;
+    size_t t_ssort = 0, t_hsort = 0;
     const int sbits = bit_length((uint64_t)ncells * kSubPerCell);  // (cell, sub-cell) keys
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_ssort, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0,
                                     sbits, s));
     DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
                                                    perm, P, 0, hbits, s));
-    t_scan = scan_scratch_bytes<uint64_t>(P);
-    const size_t t_a = std::max(std::max(t_ssort, t_hsort), t_scan);
+    const size_t t_a = std::max(t_ssort, t_hsort);
     void *tmp_a = ca.take<char>(t_a);
     {
         char *base = S.get<char>(ca.off);
@@ -1616,6 +1521,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(igm, base);
         Carve::rebase(igc, base);
         Carve::rebase(grec, base);
+        Carve::rebase(fscan_a, base);
         char *t = static_cast<char *>(tmp_a);
         Carve::rebase(t, base);
         tmp_a = t;
@@ -1638,6 +1544,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(srbuf, (size_t)G.T * 8 + 8);
         zl.add(cnt2, sizeof(uint32_t) * kGatherRows * (size_t)ncells);
         zl.add(eg, 16);
+        zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
         zl.add(rmax, 4);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
@@ -1684,10 +1591,35 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         k_gather<false><<<gather_blocks, kBlock, 0, s>>>(G, P, greach, lrows, hstart, rmax, cnt2, eg, nullptr, nullptr);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    scan_excl<uint64_t>(P, fcount, foffs, touched, toffs, static_cast<uint64_t *>(tmp_a), s);
-    DGS_LAUNCH_CHECK(s, debug);
-    k_totals<<<1, 64, 0, s>>>(P, foffs, fcount, toffs, touched, dgrid, doff, eg, totals);
-    DGS_LAUNCH_CHECK(s, debug);
+    {  // sort-path entry offsets and the reference's tile-list offsets (sampler_impl.cu:253), then
+       // the totals read back at the sync: R (num_rendered), E, the device grid (k_bounds_final)
+       // and the gathered / kUnsafe entry counts of k_gather / k_fine_count (eg[0], eg[1])
+        const uint64_t *fc = fcount, *tc = touched;
+        uint64_t *fo = foffs, *to = toffs;
+        const unsigned long long *egc = eg;
+        int64_t *tot = totals;
+        const int *dg = dgrid;
+        const float *dof = doff;
+        DGS_TRY_HIP((fused_scan<2, 8>(
+            (int64_t)P, fscan_a,
+            [=] __device__(int64_t i, uint64_t *x) { x[0] = fc[i]; x[1] = tc[i]; },
+            [=] __device__(int64_t i, const uint64_t *, const uint64_t *ex) { fo[i] = ex[0]; to[i] = ex[1]; },
+            [=] __device__(const uint64_t *t) {
+                tot[0] = (int64_t)t[1];                   // num_rendered (sampler_impl.cu:253-257)
+                tot[1] = (int64_t)t[0] + (int64_t)egc[0];  // all entries
+                tot[4] = (int64_t)t[0];                   // sort-path entries
+                tot[5] = (int64_t)egc[0];
+                tot[6] = (int64_t)egc[1];
+                tot[7] = 0;
+                int32_t *g = reinterpret_cast<int32_t *>(tot + 2);
+                g[0] = dg ? dg[0] : 0;
+                g[1] = dg ? dg[1] : 0;
+                g[2] = dof ? __float_as_int(dof[0]) : 0;
+                g[3] = dof ? __float_as_int(dof[1]) : 0;
+            },
+            s)));
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     // ---- Gaussian-side buffer and phase-B scratch for capacities (Ecap, Rcap).  Set up BEFORE
     // the host sync with the previous call's sizes (+1/8) when known, so the allocations and the
     // E-independent launches (k_geo_pack, the zero-fills) overlap the sync; redone after it only
@@ -1696,8 +1628,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int64_t Ecap = -1, Rcap = -1, bwd_cap = 0;
         Layout L;
         char *gbuf = nullptr;
-        uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *fcnt, *bcnt, *foff, *boff, *rkeys, *rkeys_sorted, *rvals;
-        uint32_t *sucnt, *suoff;  // sub units (D = 2)
+        uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *rkeys, *rkeys_sorted, *rvals;
+        unsigned long long *fs_cells, *fs_units, *fs_sub;  // fused_scan states (zeroed with phase B)
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
@@ -1714,14 +1646,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve cb;
         B.ekeys = cb.take<uint32_t>(Ecap + 1); B.evals = cb.take<uint32_t>(Ecap + 1);
         B.ekeys_sorted = cb.take<uint32_t>(Ecap + 1); B.svals = cb.take<uint32_t>(Ecap + 1);
-        B.fcnt = cb.take<uint32_t>(ncells); B.bcnt = cb.take<uint32_t>(ncells);
         B.hbeg = cb.take<int32_t>(2 * (size_t)ncells); B.hend = cb.take<int32_t>(2 * (size_t)ncells);
-        B.foff = cb.take<uint32_t>(ncells); B.boff = cb.take<uint32_t>(ncells);
         B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
         B.rvals = cb.take<uint32_t>(Rcap + 1);
-        B.sucnt = cb.take<uint32_t>(nsub + 1); B.suoff = cb.take<uint32_t>(nsub + 1);
+        B.fs_cells = cb.take<unsigned long long>(fused_scan_state_words(ncells, 1, 1));
+        B.fs_units = cb.take<unsigned long long>(fused_scan_state_words(ncells, 2, 1));
+        B.fs_sub = cb.take<unsigned long long>(fused_scan_state_words(std::max(nsub, 1), 1, 1));
         uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
-        size_t t_esort = 0, t_cscan = 0, t_rsort = 0;
+        size_t t_esort = 0, t_rsort = 0;
         B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
         DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_rsort, B.rkeys, B.rkeys_sorted, B.rvals, rlist, (int)Rcap, 0,
                                         B.rbits, s));
@@ -1731,14 +1663,13 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                    B.ebits, s)
                           : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s));
-        t_cscan = scan_scratch_bytes<uint32_t>(ncells);
-        B.t_b = std::max(std::max(std::max(t_esort, t_cscan), t_rsort), scan_scratch_bytes<uint32_t>(std::max(nsub, 1)));
+        B.t_b = std::max(t_esort, t_rsort);
         B.tmp_b = cb.take<char>(B.t_b);
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
-        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.fcnt, &B.bcnt, &B.foff, &B.boff,
-                             &B.rkeys, &B.rkeys_sorted, &B.rvals, &B.sucnt, &B.suoff})
+        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.rkeys, &B.rkeys_sorted, &B.rvals})
             Carve::rebase(*q, base);
+        for (unsigned long long **q : {&B.fs_cells, &B.fs_units, &B.fs_sub}) Carve::rebase(*q, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
         char *t = static_cast<char *>(B.tmp_b);
@@ -1748,6 +1679,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.gbuf + B.L.o_counts, 16);
         zl.add(B.hbeg, sizeof(int32_t) * 2 * (size_t)ncells);
         zl.add(B.hend, sizeof(int32_t) * 2 * (size_t)ncells);
+        zl.add(B.fs_cells, 8 * fused_scan_state_words(ncells, 1, 1));
+        zl.add(B.fs_units, 8 * fused_scan_state_words(ncells, 2, 1));
+        zl.add(B.fs_sub, 8 * fused_scan_state_words(std::max(nsub, 1), 1, 1));
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
         k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc,
@@ -1804,7 +1738,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *entries = reinterpret_cast<uint32_t *>(gbuf + L.o_entries);
     uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
     uint32_t *ekeys = B.ekeys, *evals = B.evals, *ekeys_sorted = B.ekeys_sorted, *svals = B.svals;
-    uint32_t *fcnt = B.fcnt, *bcnt = B.bcnt, *foff = B.foff, *boff = B.boff;
     uint32_t *rkeys = B.rkeys, *rkeys_sorted = B.rkeys_sorted, *rvals = B.rvals;
     int32_t *hbeg = B.hbeg, *hend = B.hend;
     uint32_t *rlist = reinterpret_cast<uint32_t *>(gbuf + L.o_rlist);
@@ -1836,12 +1769,29 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    k_cell_tot<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cnt2, hbeg, hend, gcnt, fcnt);
-    DGS_LAUNCH_CHECK(s, debug);
-    scan_excl<uint32_t>(ncells, fcnt, foff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
-    DGS_LAUNCH_CHECK(s, debug);
-    k_cell_layout<<<grid_for(ncells), kBlock, 0, s>>>(ncells, gcnt, hbeg, hend, foff, cell_gbeg, cell_gmid, cell_gend);
-    DGS_LAUNCH_CHECK(s, debug);
+    {  // per cell: [gathered (ascending id) + sorted unflagged | sorted flagged] = [gbeg, gmid, gend)
+        const uint32_t *c2 = cnt2;
+        const int32_t *hb = hbeg, *he = hend;
+        uint32_t *gc = gcnt;
+        int32_t *gb_ = cell_gbeg, *gm_ = cell_gmid, *ge_ = cell_gend;
+        DGS_TRY_HIP((fused_scan<1, 1>(
+            (int64_t)ncells, B.fs_cells,
+            [=] __device__(int64_t c, uint64_t *x) {
+                uint32_t g = 0;
+                for (int q = 0; q < kGatherRows; ++q) g += c2[c * kGatherRows + q];
+                gc[c] = g;
+                x[0] = g + (uint32_t)(he[2 * c] - hb[2 * c]) + (uint32_t)(he[2 * c + 1] - hb[2 * c + 1]);
+            },
+            [=] __device__(int64_t c, const uint64_t *, const uint64_t *ex) {
+                const int32_t b = (int32_t)ex[0];
+                const int32_t mid = b + (int32_t)gc[c] + (he[2 * c] - hb[2 * c]);
+                gb_[c] = b;
+                gm_[c] = mid;
+                ge_[c] = mid + (he[2 * c + 1] - hb[2 * c + 1]);
+            },
+            [=] __device__(const uint64_t *) {}, s)));
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     if (D == 2 && E > Es) {
         k_gather<true><<<gather_blocks, kBlock, 0, s>>>(G, P, greach, lrows, hstart, rmax, cnt2, nullptr, cell_gbeg,
                                                         entries);
@@ -1852,14 +1802,31 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, entries);
         DGS_LAUNCH_CHECK(s, debug);
     }
-    k_unit_counts<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_send, cell_gbeg,
-                                                      cell_gend, fcnt, bcnt);
-    DGS_LAUNCH_CHECK(s, debug);
-    scan_excl<uint32_t>(ncells, fcnt, foff, bcnt, boff, static_cast<uint32_t *>(tmp_b), s);
-    DGS_LAUNCH_CHECK(s, debug);
-    k_unit_fill<<<grid_for(ncells), kBlock, 0, s>>>(ncells, cell_sbeg, cell_gbeg, fcnt, bcnt, foff,
-                                                    boff, fwd_units, bwd_units, counters);
-    DGS_LAUNCH_CHECK(s, debug);
+    {  // work units: forward (cell, 64 pair-aligned samples), backward (cell, 64 list entries)
+        const int32_t *sb_ = cell_sbeg, *se_ = cell_send, *gb_ = cell_gbeg, *ge_ = cell_gend;
+        uint2 *fu = fwd_units, *bu = bwd_units;
+        int32_t *cnt = counters;
+        DGS_TRY_HIP((fused_scan<2, 1>(
+            (int64_t)ncells, B.fs_units,
+            [=] __device__(int64_t c, uint64_t *x) {
+                const int ns = se_[c] - sb_[c], ng = ge_[c] - gb_[c];
+                const int npairs = ((se_[c] + 1) >> 1) - (sb_[c] >> 1);
+                x[0] = ns > 0 && ng > 0 ? (uint64_t)((npairs + kFwdUnit / 2 - 1) / (kFwdUnit / 2)) : 0u;
+                x[1] = ns > 0 ? (uint64_t)((ng + kWave - 1) / kWave) : 0u;
+            },
+            [=] __device__(int64_t c, const uint64_t *x, const uint64_t *ex) {
+                for (uint32_t b = 0; b < (uint32_t)x[0]; ++b)
+                    fu[ex[0] + b] = make_uint2((uint32_t)c, (uint32_t)(sb_[c] & ~1) + b * kFwdUnit);
+                for (uint32_t b = 0; b < (uint32_t)x[1]; ++b)
+                    bu[ex[1] + b] = make_uint2((uint32_t)c, (uint32_t)gb_[c] + b * kWave);
+            },
+            [=] __device__(const uint64_t *t) {
+                cnt[kNumFwdUnits] = (int32_t)t[0];
+                cnt[kNumBwdUnits] = (int32_t)t[1];
+            },
+            s)));
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     if (nsub) {  // the forward's sub lists and sub units (D = 2)
         const float2 *gmean = reinterpret_cast<const float2 *>(gbuf + L.o_gmean);
         const float4 *gcon = reinterpret_cast<const float4 *>(gbuf + L.o_gcon);
@@ -1871,11 +1838,22 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box, sub_box, G.CT, sub_lbeg, sub_lmid,
             sub_lend, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);
-        k_sub_ucnt<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, sub_send, sub_lbeg, sub_lend, B.sucnt);
-        DGS_LAUNCH_CHECK(s, debug);
-        scan_excl<uint32_t>(nsub, B.sucnt, B.suoff, nullptr, nullptr, static_cast<uint32_t *>(tmp_b), s);
-        DGS_LAUNCH_CHECK(s, debug);
-        k_sub_units<<<grid_for(nsub), kBlock, 0, s>>>(nsub, sub_sbeg, B.sucnt, B.suoff, fsub_units, counters);
+        // forward sub units per sub-cell with samples and entries: (sub-cell, kSubPairs pairs)
+        const int32_t *ssb = sub_sbeg, *sse = sub_send, *slb = sub_lbeg, *sle = sub_lend;
+        uint2 *su = fsub_units;
+        int32_t *cnt = counters;
+        DGS_TRY_HIP((fused_scan<1, 1>(
+            (int64_t)nsub, B.fs_sub,
+            [=] __device__(int64_t k, uint64_t *x) {
+                const int ns = sse[k] - ssb[k];
+                const int npairs = ((sse[k] + 1) >> 1) - (ssb[k] >> 1);
+                x[0] = ns > 0 && sle[k] > slb[k] ? (uint64_t)((npairs + kSubPairs - 1) / kSubPairs) : 0u;
+            },
+            [=] __device__(int64_t k, const uint64_t *x, const uint64_t *ex) {
+                for (uint32_t b = 0; b < (uint32_t)x[0]; ++b)
+                    su[ex[0] + b] = make_uint2((uint32_t)k, (uint32_t)(ssb[k] & ~1) + b * 2u * kSubPairs);
+            },
+            [=] __device__(const uint64_t *t) { cnt[kNumFwdSubUnits] = (int32_t)t[0]; }, s)));
         DGS_LAUNCH_CHECK(s, debug);
     }
 
@@ -1944,7 +1922,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6];
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
-    uh.P = P; uh.D = D; uh.N = N; uh.R = R;
+    uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E;
     hint_put(uh);
     return DGS_OK;
 }
@@ -2065,6 +2043,19 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     return rc;
 }
 
+
+extern "C" int dgs_binning_info(const void *binning, size_t binning_bytes, const void *sample_binning,
+                                size_t sample_binning_bytes, int64_t *out) {
+    UnitHint h;
+    if (!out) return fail(DGS_ERR_ARG, "dgs_binning_info: out required");
+    if (!hint_get(binning, binning_bytes, sample_binning, sample_binning_bytes, &h))
+        return fail(DGS_ERR_BUFFER, "dgs_binning_info: buffers not binned by this process");
+    out[0] = h.R;
+    out[1] = h.E;
+    out[2] = h.nunsafe;
+    out[3] = h.ncells;
+    return DGS_OK;
+}
 
 extern "C" int dgs_exchange_sets(int P, int D, const float *means, const float *conics, int W,
                                  const double *extents, uint32_t *mask_out, int32_t *owner_out,

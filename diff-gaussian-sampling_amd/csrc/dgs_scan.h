@@ -129,4 +129,108 @@ static void scan_excl(int64_t n, const T *a, T *ao, const T *b, T *bo, T *part, 
     k_scan_down<T><<<(unsigned)nt, kBlock, 0, s>>>(n, a, ao, b, bo, part, inclusive);
 }
 
+// ---- single-pass exclusive scan with decoupled look-back, fused with its producer and consumer
+// A chain "per-element counts -> exclusive scan -> per-element outputs" in ONE launch (the
+// three-kernel scan above plus the two kernels around it were five launches of ~5 us each, most
+// of their time launch overhead at the binning's sizes).  Tiles of kBlock * ITEMS elements are
+// taken in ticket order (atomic counter), so every tile's predecessors are running or done and
+// the look-back always terminates; wave 0 looks back 64 tiles at a time.  NA (1 or 2) arrays of
+// unsigned counts are scanned side by side.  ITEMS = 1 where the consumer does real work per
+// element (unit lists), more where it is a plain store.
+//   prod(i, v[NA])            : the counts of element i
+//   cons(i, v[NA], excl[NA])  : the outputs of element i given its exclusive prefixes
+//   last(total[NA])           : once, by the block holding element n - 1 (totals, counters)
+// state: fused_scan_state_words(n, NA, ITEMS) 64-bit words, ZERO-FILLED before the launch.
+constexpr uint64_t kFuseAgg = 1ull << 62, kFusePre = 2ull << 62, kFuseVal = (1ull << 62) - 1;
+
+static inline int64_t fused_scan_tiles(int64_t n, int items) { return (n + (int64_t)kBlock * items - 1) / ((int64_t)kBlock * items); }
+static inline size_t fused_scan_state_words(int64_t n, int NA, int items) {
+    return 1 + (size_t)NA * std::max<int64_t>(fused_scan_tiles(n, items), 1);
+}
+
+template <int NA, int ITEMS, class Prod, class Cons, class Last>
+__global__ __launch_bounds__(kBlock) void k_fused_scan(int64_t n, unsigned long long *__restrict__ state, Prod prod,
+                                                       Cons cons, Last last) {
+    __shared__ int tile_s;
+    __shared__ uint64_t pre_s[NA], tot_s[NA];
+    if (threadIdx.x == 0) tile_s = (int)atomicAdd(reinterpret_cast<unsigned int *>(state), 1u);
+    __syncthreads();
+    const int tile = tile_s;
+    unsigned long long *st = state + 1;
+    const int64_t i0 = ((int64_t)tile * kBlock + threadIdx.x) * ITEMS;  // blocked: ITEMS per thread
+    uint64_t v[ITEMS][NA], sum[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) sum[a] = 0;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        uint64_t x[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) x[a] = 0;
+        if (i0 + k < n) prod(i0 + k, x);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            v[k][a] = x[a];
+            sum[a] += x[a];
+        }
+    }
+    uint64_t excl[NA], agg[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) excl[a] = block_excl_scan<uint64_t>(sum[a], agg[a]);
+    if (threadIdx.x < kWave) {  // wave 0: publish the aggregate, look back, publish the prefix
+        const int lane = threadIdx.x;
+#pragma unroll
+        for (int a = 0; a < NA; ++a) {
+            if (lane == 0)
+                __hip_atomic_store(&st[(int64_t)tile * NA + a], (tile == 0 ? kFusePre : kFuseAgg) | agg[a],
+                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+            uint64_t pre = 0;
+            for (int j = tile - 1; j >= 0; j -= kWave) {
+                const int jj = j - lane;  // lane 0 = the nearest predecessor
+                uint64_t w = kFusePre;    // (before tile 0: a zero prefix)
+                if (jj >= 0)
+                    do {
+                        w = __hip_atomic_load(&st[(int64_t)jj * NA + a], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                    } while ((w & ~kFuseVal) == 0);
+                const uint64_t pm = __ballot((w & kFusePre) != 0);
+                const int stop = pm ? __builtin_ctzll(pm) : kWave;  // lanes <= stop contribute
+                uint64_t c = lane <= stop ? (w & kFuseVal) : 0;
+#pragma unroll
+                for (int off = kWave / 2; off > 0; off >>= 1) c += __shfl_xor(c, off);
+                pre += c;
+                if (pm) break;
+            }
+            if (lane == 0) {
+                if (tile > 0)
+                    __hip_atomic_store(&st[(int64_t)tile * NA + a], kFusePre | (pre + agg[a]), __ATOMIC_RELEASE,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                pre_s[a] = pre;
+                tot_s[a] = pre + agg[a];
+            }
+        }
+    }
+    __syncthreads();
+    uint64_t run[NA];
+#pragma unroll
+    for (int a = 0; a < NA; ++a) run[a] = pre_s[a] + excl[a];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        if (i0 + k < n) cons(i0 + k, v[k], run);
+#pragma unroll
+        for (int a = 0; a < NA; ++a) run[a] += v[k][a];
+    }
+    if (n > 0 && (int64_t)tile == (n - 1) / ((int64_t)kBlock * ITEMS) && threadIdx.x == 0) {
+        uint64_t t[NA];
+#pragma unroll
+        for (int a = 0; a < NA; ++a) t[a] = tot_s[a];
+        last(t);
+    }
+}
+
+template <int NA, int ITEMS, class Prod, class Cons, class Last>
+static hipError_t fused_scan(int64_t n, unsigned long long *state, Prod prod, Cons cons, Last last, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    k_fused_scan<NA, ITEMS><<<(unsigned)fused_scan_tiles(n, ITEMS), kBlock, 0, s>>>(n, state, prod, cons, last);
+    return hipGetLastError();
+}
+
 }  // namespace dgs

@@ -72,20 +72,25 @@ Tensor empty_u8(const torch::Device &dev) {
 using PreOut = std::tuple<int64_t, Tensor, Tensor, Tensor, Tensor, Tensor>;
 
 // ---- per-step caches of the sampling calls (dgs_sample_options) ------------------------------
-// A tensor's identity: its TensorImpl (weakly held), data pointer and autograd version counter.
-// Same identity <=> same tensor object, not modified in place since (every in-place op bumps the
-// version; writes through .data or raw pointers do not: DGS_ALWAYS_VERIFY=1 or debug=True keep
-// the device-side comparison for code that does that).
+// A tensor's identity: its storage (weakly held), data pointer, element count and autograd
+// version.  A tensor and its .detach() share storage and version counter, so they are the same
+// here; every in-place op through either bumps the shared version.  Writes that bypass the
+// counter (through .data, or raw pointers) are not seen: DGS_ALWAYS_VERIFY=1 or debug=True keep
+// the device-side comparison for code that does that.
 using WeakImpl = c10::weak_intrusive_ptr<c10::TensorImpl, c10::UndefinedTensorImpl>;
+using WeakStorage = c10::weak_intrusive_ptr<c10::StorageImpl>;
 struct TKey {
-    WeakImpl impl;
+    WeakStorage storage;
     const void *ptr;
-    int64_t version;
+    int64_t numel, version;
 };
-TKey tkey(const Tensor &t) { return {WeakImpl(t.getIntrusivePtr()), t.data_ptr(), (int64_t)t._version()}; }
+TKey tkey(const Tensor &t) {
+    return {t.storage().getWeakStorageImpl(), t.data_ptr(), t.numel(), (int64_t)t._version()};
+}
 bool same(const TKey &k, const Tensor &t) {
-    const auto sp = k.impl.lock();
-    return sp.get() == t.unsafeGetTensorImpl() && k.ptr == t.data_ptr() && k.version == (int64_t)t._version();
+    const auto sp = k.storage.lock();
+    return sp && sp.get() == t.storage().unsafeGetStorageImpl() && k.ptr == t.data_ptr() && k.numel == t.numel() &&
+           k.version == (int64_t)t._version();
 }
 
 bool always_verify() {
@@ -116,7 +121,7 @@ std::vector<RowRecord> g_rows;
 void bins_put(const Tensor &gb, const Tensor &means, const Tensor &conics, const Tensor &samples) {
     std::lock_guard<std::mutex> lk(g_step_mu);
     for (auto it = g_bins.begin(); it != g_bins.end();)
-        if (it->gb.impl.expired() || it->gb.ptr == gb.data_ptr()) it = g_bins.erase(it);
+        if (it->gb.storage.expired() || it->gb.ptr == gb.data_ptr()) it = g_bins.erase(it);
         else ++it;
     g_bins.push_back({tkey(gb), tkey(means), tkey(conics), tkey(samples)});
     if (g_bins.size() > 8) g_bins.erase(g_bins.begin());
@@ -149,7 +154,7 @@ void rows_put(const Tensor &gb, int mask, int C, const Tensor &means, const Tens
               const Tensor &work) {
     std::lock_guard<std::mutex> lk(g_step_mu);
     for (auto it = g_rows.begin(); it != g_rows.end();)
-        if (it->gb.impl.expired() || (it->mask == mask && it->gb.ptr == gb.data_ptr())) it = g_rows.erase(it);
+        if (it->gb.storage.expired() || (it->mask == mask && it->gb.ptr == gb.data_ptr())) it = g_rows.erase(it);
         else ++it;
     g_rows.push_back({tkey(gb), tkey(means), tkey(values), tkey(conics), mask, C, work});
     if (g_rows.size() > 4) g_rows.erase(g_rows.begin());  // (the per-function path of a fused call keeps one per function)
@@ -448,6 +453,14 @@ std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &co
               "count_pairs");
     }
     return std::make_tuple(counts[0], counts[1]);
+}
+
+// (R, E, kUnsafe entries, fine cells) of a binning (dgs_binning_info).
+std::tuple<int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
+    const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
+    int64_t o[4] = {0, 0, 0, 0};
+    check(dgs_binning_info(gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), o), "binning_info");
+    return std::make_tuple(o[0], o[1], o[2], o[3]);
 }
 
 // Whether forward / backward with these tensors take the binned path (dgs_inputs_match).
@@ -843,6 +856,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("tile_grid", &TileGrid);
     m.def("exchange_sets", &ExchangeSets);
     m.def("inputs_match", &InputsMatch);
+    m.def("binning_info", &BinningInfo);
     m.def("volume_preprocess", &VolumePreprocess);
     m.def("volume_forward", &VolumeForward);
     m.def("volume_backward", &VolumeBackward);

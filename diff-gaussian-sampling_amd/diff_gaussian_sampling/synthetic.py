@@ -21,11 +21,16 @@ def _gen(seed):
     return g
 
 
-def gaussians(P, D=2, C=1, seed=0, scale=1.0):
-    """Returns float32 CPU tensors (means, values, covariances, conics)."""
+def gaussians(P, D=2, C=1, seed=0, scale=1.0, aniso=1.0):
+    """Returns float32 CPU tensors (means, values, covariances, conics).  aniso > 1 (D = 2):
+    per-Gaussian axis ratios sigma_0 / sigma_1 ~ U[1, aniso] (seed + 6) at the same area
+    sigma_0 sigma_1 (the thin-Gaussian workload of bench.py --aniso)."""
     means = torch.rand(P, D, generator=_gen(seed), dtype=torch.float64) * 2.0 - 1.0
     h = 2.0 / (max(P, 1) ** (1.0 / D)) * scale
     sig = h * (0.5 + torch.rand(P, D, generator=_gen(seed + 1), dtype=torch.float64))
+    if D == 2 and aniso > 1.0:
+        ratio = 1.0 + (aniso - 1.0) * torch.rand(P, generator=_gen(seed + 6), dtype=torch.float64)
+        sig = sig * torch.stack([ratio.sqrt(), 1.0 / ratio.sqrt()], -1)
     if D == 1:
         var = sig[:, 0] ** 2
         cov = var[:, None]

@@ -227,6 +227,14 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
                     int64_t *counts, void *workspace, size_t workspace_bytes,
                     dgs_stream_t stream);
 
+/* Diagnostics (not on the reference API): host-known facts of a binning this process made (no
+ * device work): out[0] = num_rendered R, out[1] = fine (Gaussian, cell) entries E, out[2] = the
+ * entries that take the reference-literal per-pair path (kUnsafe: conics that are not
+ * well-conditioned positive definite, wrap breakpoints, fallback cells), out[3] = fine cells.
+ * DGS_ERR_BUFFER for buffers this process did not bin. */
+int dgs_binning_info(const void *binning, size_t binning_bytes, const void *sample_binning,
+                     size_t sample_binning_bytes, int64_t *out);
+
 /* Diagnostic: do means / conics / samples equal (bitwise) the tensors the binning was built
  * from?  *match = 1: forward / backward take the binned fine-cell path; 0: they take the
  * call-time path (the reference reads these tensors at every call, forward.cu:136-145,
