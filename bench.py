@@ -407,7 +407,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
         **pre_extra,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
-        "entries": dict(zip(("num_rendered", "fine_entries", "literal_path_entries", "fine_cells"),
+        "entries": dict(zip(("num_rendered", "fine_entries", "literal_path_entries", "fine_cells", "thin_entries"),
                             dgs._C.binning_info(gb, sb))),
         "roofline": roofline,
         "hbm": hbm,

@@ -24,9 +24,12 @@ constexpr uint32_t kVersion = 7;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
-constexpr uint32_t kUnsafe = 0x40000000u;   // conic not well-conditioned PD: reference-literal power
-constexpr uint32_t kSlow = kGeneral | kUnsafe;
-constexpr uint32_t kIdMask = 0x3fffffffu;
+constexpr uint32_t kUnsafe = 0x40000000u;   // conic not positive definite, a wrap breakpoint in the
+                                            // cell, or a fallback cell: the per-pair literal path
+constexpr uint32_t kThin = 0x20000000u;     // positive definite but ill-conditioned (rho^2 >= 0.82):
+                                            // packed, with the exponent in the reference's order
+constexpr uint32_t kSlow = kGeneral | kUnsafe | kThin;
+constexpr uint32_t kIdMask = 0x1fffffffu;
 constexpr int64_t kMaxGaussians = (int64_t)kIdMask;
 // Culling threshold on q = X^T A X.  power = -q/2 < -105 makes expf(power) exactly +0 in
 // fp32 (e^-105 < half of the smallest subnormal), so every forward and backward term of such
@@ -359,11 +362,19 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
 // Positive definite with rho^2 < 0.82 (D = 2), or c0 >= 0 (D = 1); every other conic takes the
 // reference-literal power evaluation with its `power > 0 -> skip` rule (forward.cu:228).  The
 // headline's Gaussians (axis ratio <= 3: rho <= 0.8) are all on the fast paths.
+// Not positive definite (or not finite): kUnsafe, the per-pair literal path with the exact wrap.
 __host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float c2f) {
     const double c0 = c0f, c1 = c1f, c2 = c2f;
     if (D == 1) return !(c0 >= 0.0 && c0 < INFINITY);
-    return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
-             c1 * c1 < 0.82 * c0 * c2);
+    return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY && c1 * c1 < c0 * c2);
+}
+// Positive definite but ill-conditioned, rho^2 = c1^2 / (c0 c2) >= 0.82 (D = 2): kThin.  The
+// fast paths' own operation order is not within the tolerance there (above); these entries keep
+// the packed fast kernels but evaluate the exponent in the reference's order (lit_prob).
+__host__ __device__ inline bool conic_thin(int D, float c0f, float c1f, float c2f) {
+    if (D != 2 || conic_unsafe(D, c0f, c1f, c2f)) return false;
+    const double c0 = c0f, c1 = c1f, c2 = c2f;
+    return !(c1 * c1 < 0.82 * c0 * c2);
 }
 
 __host__ __device__ inline int wrap_tile(int x, int g) { return x < 0 ? (g + (x % g)) : (x % g); }
@@ -510,7 +521,8 @@ struct UnitHint {
     const void *gbuf, *sbuf;
     size_t gbytes, sbytes;
     int64_t nfwd, nbwd, nfsub, ncells;
-    int64_t nunsafe;  // entries with a not-well-conditioned conic (the forward's tail pass)
+    int64_t nunsafe;  // kUnsafe entries (the forward's tail pass)
+    int64_t nthin;    // kThin entries (the forward's thin pass)
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
     int64_t R;        // num_rendered (sizes the call-time path's backward grid)
     int64_t E;        // fine (Gaussian, cell) entries

@@ -386,7 +386,9 @@ __device__ __forceinline__ bool visit_local(const Geom &G, const Cut &k, const i
 // per-Gaussian enumeration and the entry sort.  Returns the reach in cells, 0 if not regular.
 constexpr int kGatherReach = 6, kGatherRows = 2 * kGatherReach + 1;
 __device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k) {
-    if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2])) return 0;
+    if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2]) ||
+        conic_thin(2, con[0], con[1], con[2]))
+        return 0;
     if (!(k.e[0] + 3.0 * G.fs < 0.9 && k.e[1] + 3.0 * G.fs < 0.9)) return 0;
     // every tile visited at most once (a rect wider than the grid visits a tile repeatedly,
     // which the enumeration reproduces entry by entry)
@@ -431,7 +433,8 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
                                       Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
-    const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
+    const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
+                           : conic_thin(D, con[0], con[1], con[2]) ? kThin : 0u;
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             const uint32_t key = key_of(D, x, y, G.grid);
@@ -664,12 +667,12 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
                                                        float2 *__restrict__ igm, float4 *__restrict__ igc,
-                                                       unsigned long long *__restrict__ nunsafe) {
+                                                       unsigned long long *__restrict__ nflag) {
     __shared__ uint32_t fbl[kFbWords];
     const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int reach = 0;
-    uint32_t nu = 0;  // kUnsafe entries (k_fine_fill emits the same ones): read back at the sync
+    uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
     if (i < P) {
         const int64_t g = perm[i];
         const float4 ga = grec[2 * g], gb2 = grec[2 * g + 1];  // (k_gauss_prep's record: one line)
@@ -686,7 +689,11 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                 const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) * G.ifs);
                 if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
             }
-            const auto count = [&](uint32_t, uint32_t v) { ++n; nu += (v & kUnsafe) ? 1u : 0u; };
+            const auto count = [&](uint32_t, uint32_t v) {
+                ++n;
+                nu += (v & kUnsafe) ? 1u : 0u;
+                nt += (v & kThin) ? 1u : 0u;
+            };
             if (!(reach > 0 && fallback_only(G, m, r, sbeg, send, fbits, (uint32_t)i, count)))
                 enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, fbits, (uint32_t)i, count);
         }
@@ -696,10 +703,12 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
     for (int off = kWave / 2; off > 0; off >>= 1) {
         reach = max(reach, __shfl_xor(reach, off));
         nu += __shfl_xor(nu, off);
+        nt += __shfl_xor(nt, off);
     }
     if ((threadIdx.x & (kWave - 1)) == 0) {
         if (reach > 0) atomicMax(rmax, reach);
-        if (nu) atomicAdd(nunsafe, (unsigned long long)nu);
+        if (nu) atomicAdd(&nflag[0], (unsigned long long)nu);
+        if (nt) atomicAdd(&nflag[1], (unsigned long long)nt);
     }
 }
 
@@ -1429,7 +1438,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                            const uint8_t *present = nullptr, double sample_area = 0.0) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
-    if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^30 - 1)");
+    if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^29 - 1)");
     *num_rendered = 0;
     if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
     if (!grid || !grid_offset) return fail(DGS_ERR_ARG, "dgs_preprocess: grid/offset required");
@@ -1487,7 +1496,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *lrows = ca.take<uint32_t>((size_t)kGatherRows * P);
     uint32_t *hstart = ca.take<uint32_t>((size_t)HK + 1), *gcnt = ca.take<uint32_t>(ncells);
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
-    unsigned long long *eg = ca.take<unsigned long long>(2);  // [gathered entries, kUnsafe entries]
+    unsigned long long *eg = ca.take<unsigned long long>(4);  // [gathered, kUnsafe, kThin entries, -]
     int32_t *rmax = ca.take<int32_t>(1);
     float2 *igm = ca.take<float2>(P);
     float4 *igc = ca.take<float4>(P);
@@ -1543,7 +1552,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(rbuf, (size_t)G.T * 8 + 8);
         zl.add(srbuf, (size_t)G.T * 8 + 8);
         zl.add(cnt2, sizeof(uint32_t) * kGatherRows * (size_t)ncells);
-        zl.add(eg, 16);
+        zl.add(eg, 32);
         zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
         zl.add(rmax, 4);
         DGS_TRY_HIP(zl.launch(s));
@@ -1610,7 +1619,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                 tot[4] = (int64_t)t[0];                   // sort-path entries
                 tot[5] = (int64_t)egc[0];
                 tot[6] = (int64_t)egc[1];
-                tot[7] = 0;
+                tot[7] = (int64_t)egc[2];
                 int32_t *g = reinterpret_cast<int32_t *>(tot + 2);
                 g[0] = dg ? dg[0] : 0;
                 g[1] = dg ? dg[1] : 0;
@@ -1919,7 +1928,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // forward's unsafe-only tail pass is not launched).
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
-    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6];
+    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6]; uh.nthin = htot[7];
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E;
@@ -2054,6 +2063,7 @@ extern "C" int dgs_binning_info(const void *binning, size_t binning_bytes, const
     out[1] = h.E;
     out[2] = h.nunsafe;
     out[3] = h.ncells;
+    out[4] = h.nthin;
     return DGS_OK;
 }
 

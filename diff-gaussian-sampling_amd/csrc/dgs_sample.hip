@@ -175,6 +175,29 @@ __device__ __forceinline__ f2 general_prob(f2 *X, const float *c, const float *k
     return f2{Ga, Gb};
 }
 
+// kThin entries (D = 2): the reference's exponent in its own operation order -- float products
+// (c0 X0) X0, (c2 X1) X1, (c1 X0) X1 without contraction, their sum, then -0.5 a - b rounded once
+// (forward.cu:227 et seq.; the FMA below is that single rounding since -0.5 a is exact) -- and its
+// `power > 0 -> skip` rule; exp2 of power * log2(e).  Packed like the fast path: the flagged
+// groups that hold such an entry take this form for all their lanes.
+template <typename V>
+__device__ __forceinline__ V lit_prob(const V *X, const float *c) {
+    DGS_NO_CONTRACT
+    const V t0 = (bc<V>(c[0]) * X[0]) * X[0];
+    const V t1 = (bc<V>(c[2]) * X[1]) * X[1];
+    const V b = (bc<V>(c[1]) * X[0]) * X[1];
+    const V a = t0 + t1;
+    const V p = vfma(bc<V>(-0.5f), a, -b);
+    V G = vexp2(p * kLog2e);
+    if constexpr (sizeof(V) == 4) {
+        G = p > 0.0f ? 0.0f : G;
+    } else {
+        G.x = p.x > 0.0f ? 0.0f : G.x;
+        G.y = p.y > 0.0f ? 0.0f : G.y;
+    }
+    return G;
+}
+
 // Raw conic of a Gaussian row (FN != gaussian keeps it in the row).
 template <int FN, int D, int RS>
 __device__ __forceinline__ void row_conic(const float (&r)[RS], float *c) {
@@ -243,26 +266,31 @@ __host__ __device__ constexpr bool fwd_transposed() {
 // WRAP: some lane's entry crosses the torus seam.  Its wrap (forward.cu:149-157) is a
 // constant even shift over the cell (preprocess sends the other seam entries to the general
 // path), subtracted exactly: sh = 0 for every other lane.
-template <int FN, int D, int CB, bool WRAP>
+// LIT: kThin entries in the group -- the exponent from the raw conic `cl` in the reference's
+// order (lit_prob) for every lane.
+template <int FN, int D, int CB, bool WRAP, bool LIT = false>
 __device__ __forceinline__ void fwd_t_pair(const float *pr, const float *m, const float *sh, const float *c,
-                                           const float *kk, const float *v, f2 (&acc)[Traits<FN, D>::U][CB]) {
+                                           const float *kk, const float *v, f2 (&acc)[Traits<FN, D>::U][CB],
+                                           const float *cl = nullptr) {
     f2 X[2] = {m[0] - f2{pr[0], pr[1]}, D == 2 ? m[1] - f2{pr[2], pr[3]} : bc<f2>(0.0f)};
     if constexpr (WRAP) {
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
     }
-    const f2 G = fast_prob<D, f2>(X, kk);
+    f2 G;
+    if constexpr (LIT && D == 2) G = lit_prob<f2>(X, cl);
+    else G = fast_prob<D, f2>(X, kk);
     fwd_terms<FN, D, CB, f2>(X, c, G, v, acc);
 }
 
 // s_waitcnt lgkmcnt(0) (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
 #define DGS_WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
 
-template <int FN, int D, int CB, int NP, bool WRAP, bool FULL>
+template <int FN, int D, int CB, int NP, bool WRAP, bool FULL, bool LIT = false>
 __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, int p0, int np,
                                             const float *m, const float *sh, const float *c,
                                             const float *kk, const float *v,
-                                            f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
+                                            f2 (&acc)[NP][Traits<FN, D>::U][CB], const float *cl = nullptr) {
     constexpr int LW = 16;  // (x8 loads measured 6x slower: the unrolled pass stopped interleaving)
     constexpr int PRF = 2 * D, PPL = LW / PRF;  // floats per pair row, pairs per s_load_dwordx16
     if constexpr (FULL) {
@@ -283,7 +311,7 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < PPL; ++j)
-                fwd_t_pair<FN, D, CB, WRAP>(&cur.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
+                fwd_t_pair<FN, D, CB, WRAP, LIT>(&cur.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
             __builtin_amdgcn_sched_barrier(0);
             if (b + 1 < NB) cur = nxt;
         }
@@ -294,7 +322,7 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
             const F32s<LW> sr = sload_f<LW>(fsrows + (int64_t)(p0 + q) * PRF);
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
-                if (q + j < NP) fwd_t_pair<FN, D, CB, WRAP>(&sr.v[j * PRF], m, sh, c, kk, v, acc[q + j]);
+                if (q + j < NP) fwd_t_pair<FN, D, CB, WRAP, LIT>(&sr.v[j * PRF], m, sh, c, kk, v, acc[q + j], cl);
             }
         }
     }
@@ -320,8 +348,8 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
     // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0.  Flagged
     // groups zero the whole row (an unsafe conic may overflow); a padding lane of a flag-free
     // group holds a copy of a well-conditioned row (finite terms), so zero values suffice.
-    if constexpr (FLAGGED) {
-        if (!active || (ent & kUnsafe)) {
+    if constexpr (FLAGGED) {  // (kUnsafe: the tail pass; kThin: the thin pass, k_forward_s<..., true>)
+        if (!active || (ent & (kUnsafe | kThin))) {
 #pragma unroll
             for (int k = 0; k < RS; ++k) r[k] = 0.0f;
         }
@@ -336,7 +364,7 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     float sh[2] = {0.0f, 0.0f};  // the lane's constant wrap shift (kGeneral entries)
     if constexpr (FLAGGED) {
-        if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
+        if (active && (ent & (kGeneral | kUnsafe | kThin)) == kGeneral) {
 #pragma unroll
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
@@ -448,10 +476,11 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
 // The first HB (DGS_FWD_HB = 2) blocks of 4 pair rows are hoisted (at 4 blocks, 64 SGPRs, the kernel spilled SGPRs into VGPR lanes: a
 // v_readlane per dword inside the loop); the pass's later blocks, needed by the larger sub-cells
 // only, are loaded where they are used.
-template <int FN, int D, int CB, int NPH, int HB, bool WRAP>
+template <int FN, int D, int CB, int NPH, int HB, bool WRAP, bool LIT = false>
 __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const float *__restrict__ prow, int np,
                                             const float *m, const float *sh, const float *c, const float *kk,
-                                            const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+                                            const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB],
+                                            const float *cl = nullptr) {
     constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -461,7 +490,8 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
         else t = sload_f<16>(prow + (int64_t)b * PPL * PRF);
 #pragma unroll
         for (int j = 0; j < PPL; ++j)
-            if (b * PPL + j < NPH) fwd_t_pair<FN, D, CB, WRAP>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
+            if (b * PPL + j < NPH)
+                fwd_t_pair<FN, D, CB, WRAP, LIT>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
     }
 }
 
@@ -519,14 +549,18 @@ __device__ __forceinline__ void fwd_l_pairs(uint32_t slot, int np, const float *
     }
 }
 
-template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
+// THIN (the thin pass): only the kThin lanes, with the literal-order exponent; otherwise every
+// lane but the kUnsafe (tail pass) and kThin (thin pass) ones, with the fast exponent.
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED, bool THIN>
 __device__ __forceinline__ void fwd_s_group(const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
                                             float (&r)[grow_stride<FN, D, CB>()],
                                             uint32_t ent, bool active, int np, const float *ctr,
-                                            f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+                                            const float4 *__restrict__ gcon, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
     constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    bool on = active;
     if constexpr (FLAGGED) {
-        if (!active || (ent & kUnsafe)) {
+        on = THIN ? active && (ent & kThin) : active && !(ent & (kUnsafe | kThin));
+        if (!on) {
 #pragma unroll
             for (int k = 0; k < RS; ++k) r[k] = 0.0f;
         }
@@ -541,19 +575,28 @@ __device__ __forceinline__ void fwd_s_group(const F32s<16> (&hr)[HB], const floa
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     float sh[2] = {0.0f, 0.0f};
     if constexpr (FLAGGED) {
-        if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
+        if (on && (ent & kGeneral)) {
 #pragma unroll
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
     }
-    if constexpr (DGS_FWD_LDS)
+    if constexpr (THIN) {
+        float cl[3] = {0.0f, 0.0f, 0.0f};
+        if (on) {
+            const float4 q = gcon[ent & kIdMask];
+            cl[0] = q.x; cl[1] = q.y; cl[2] = q.z;
+        }
+        fwd_s_pairs<FN, D, CB, NPH, HB, FLAGGED, true>(hr, prow, np, m, sh, c, &r[D], &r[B], acc, cl);
+    } else if constexpr (DGS_FWD_LDS) {
         fwd_l_pairs<FN, D, CB, NPH, FLAGGED>(slot, np, m, sh, c, &r[D], &r[B], acc);
-    else
+    } else {
         fwd_s_pairs<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, np, m, sh, c, &r[D], &r[B], acc);
+    }
 }
 
-template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED, bool THIN>
 __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, const float *__restrict__ grows,
+                                             const float4 *__restrict__ gcon,
                                              const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
                                              int eb, int ee, int np, int lane,
                                              const float *ctr, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
@@ -571,7 +614,8 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
         float r_nxt[RS];
         load_grow<RS>(grows, e_nxt, r_nxt);
         const uint32_t e_nn = ents[min(g0 + 2 * kWave + lane, last)];
-        fwd_s_group<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr, acc);
+        fwd_s_group<FN, D, CB, NPH, HB, FLAGGED, THIN>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr, gcon,
+                                                       acc);
 #pragma unroll
         for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
         e_cur = e_nxt;
@@ -579,7 +623,10 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
     }
 }
 
-template <int FN, int D, int CB>
+// THIN = true: the thin pass -- per sub unit only the flagged part of the sub list, only its kThin
+// entries (the literal-order exponent, lit_prob), added onto the main pass's output.  Launched
+// only when the binning saw kThin entries.
+template <int FN, int D, int CB, bool THIN>
 __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
                                                       const float *__restrict__ grows,
@@ -606,6 +653,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
         const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
         const int hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
         const int gb = sload(&bins.sub_lbeg[sc]), gm = sload(&bins.sub_lmid[sc]), ge = sload(&bins.sub_lend[sc]);
+        if (THIN && gm == ge) continue;  // (no flagged entry in this sub list)
         float ctr[2];
         cell_center<D>(bins, cell, ctr);
         for (int ps = sb; ps < hi; ps += NS) {
@@ -627,9 +675,12 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
 #pragma unroll
                     for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
             constexpr int HBX = DGS_FWD_LDS ? 1 : HB;
-            fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
+            if constexpr (!THIN)
+                fwd_s_groups<FN, D, CB, NPH, HBX, false, false>(bins.sub_ent, grows, bins.gcon, hr, prow, slot, gb, gm, np,
+                                                                lane, ctr, acc);
             if (gm < ge)
-                fwd_s_groups<FN, D, CB, NPH, HBX, true>(bins.sub_ent, grows, hr, prow, slot, gm, ge, np, lane, ctr, acc);
+                fwd_s_groups<FN, D, CB, NPH, HBX, true, THIN>(bins.sub_ent, grows, bins.gcon, hr, prow, slot, gm, ge, np,
+                                                              lane, ctr, acc);
             float x[64];
 #pragma unroll
             for (int i = 0; i < 64; ++i) x[i] = 0.0f;
@@ -646,7 +697,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
             const int slot = lane / UC, comp = lane - slot * UC;
             const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
             if (lane < NS * UC && j >= lo && j < hi && ch < nch) {
-                store_unique<FN, D, false>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
+                store_unique<FN, D, THIN>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
             }
         }
     }
@@ -696,11 +747,12 @@ __device__ __forceinline__ void fwd_accumulate(const Bins &bins, const float *__
         if (!(e & kSlow)) {
             G = fast_prob<D, float>(X, &r[D]);
         } else {
-            if (e & kUnsafe) {
+            const bool lit = (e & (kUnsafe | kThin)) != 0;  // the reference-literal power
+            if (lit) {
                 const float4 cr = sload(&crows[id]);
                 c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
             }
-            G = general_prob<FN, D>(X, c, &r[D], (e & kGeneral) != 0, (e & kUnsafe) != 0);
+            G = general_prob<FN, D>(X, c, &r[D], (e & kGeneral) != 0, lit);
         }
         fwd_terms<FN, D, CB, float>(X, c, G, &r[B], acc);
     }
@@ -811,11 +863,18 @@ __device__ __forceinline__ void fwd_mx_groups(const Bins &bins, const float *__r
         for (int t = 0; t < 4; ++t) {
             bool act = e0 + 4 * t + kq < ee;
             float sh[2] = {0.0f, 0.0f};
+            bool thin = false;
+            float cl[3] = {0.0f, 0.0f, 0.0f};
             if constexpr (FLAGGED) {
                 act = act && !(ent[t] & kUnsafe);  // unsafe conics: the tail pass
                 if (act && (ent[t] & kGeneral)) {
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(hd[t][d] - ctr[d]);
+                }
+                thin = D == 2 && act && (ent[t] & kThin);  // the literal-order exponent (lit_prob)
+                if (thin) {
+                    const float4 q = bins.gcon[ent[t] & kIdMask];
+                    cl[0] = q.x; cl[1] = q.y; cl[2] = q.z;
                 }
             }
             float c[3];
@@ -828,7 +887,9 @@ __device__ __forceinline__ void fwd_mx_groups(const Bins &bins, const float *__r
                     X[0] = X[0] - sh[0];
                     if constexpr (D == 2) X[1] = X[1] - sh[1];
                 }
-                const float G = fast_prob<D, float>(X, &hd[t][D]);
+                float G;
+                if constexpr (FLAGGED && D == 2) G = thin ? lit_prob<float>(X, cl) : fast_prob<D, float>(X, &hd[t][D]);
+                else G = fast_prob<D, float>(X, &hd[t][D]);
                 float tu[U][1];
 #pragma unroll
                 for (int u = 0; u < U; ++u) tu[u][0] = 0.0f;
@@ -902,7 +963,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_mx(const char *__restrict__ 
 
 // ------------------------------------------------------------------ backward kernel
 // MODE 0: fast path; 1: plus the lane's constant torus-wrap shift sh (kGeneral entries);
-// 2: the fully general per-pair path (some lane has a kUnsafe entry).
+// 2: the fully general per-pair path (some lane has a kUnsafe entry); 3: mode 1 with the
+// exponent in the reference's order from the raw conic (some lane has a kThin entry, lit_prob).
 template <int FN, int D, int CB, int MODE, typename V>
 __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *sh,
                                            const float *c, const float *kk, const float *v,
@@ -914,11 +976,11 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) dl[a][ch] = srow[D + a * CB + ch];
     V X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : bc<V>(0.0f)};
-    if constexpr (MODE == 1) {
+    if constexpr (MODE == 1 || MODE == 3) {
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
     }
-    if constexpr (FN == 0 && D == 2 && CB == 1 && MODE != 2 && DGS_QFORM && DGS_VFACTOR) {
+    if constexpr (FN == 0 && D == 2 && CB == 1 && MODE < 2 && DGS_QFORM && DGS_VFACTOR) {
         // gaussian, C = 1: the exponent from the quadratic monomials q = (X0^2, X0 X1, X1^2)
         // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16
         const V q0 = X[0] * X[0], q1 = X[0] * X[1], q2 = X[1] * X[1];
@@ -934,6 +996,7 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
     }
     V G;
     if constexpr (MODE == 2) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
+    else if constexpr (MODE == 3 && D == 2) G = lit_prob<V>(X, c);
     else G = fast_prob<D, V>(X, kk);
     if constexpr (bwd_mom<FN, D, CB>()) bwd_mom_terms<FN, V>(X, c, G, &srow[D], acc);
     else bwd_terms<FN, D, CB, V>(X, c, G, v, dl, acc, acc + 2, acc + 2 + CB);
@@ -1044,7 +1107,7 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
     constexpr int B = Tr::GBASE;
     const bool wrap = (ent & kGeneral) != 0;
-    const bool unsafe = (ent & kUnsafe) != 0;
+    const bool unsafe = (ent & (kUnsafe | kThin)) != 0;  // (mode 2: the literal power for both)
     const float c[3] = {cr.x, cr.y, cr.z};
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     // register accumulators: [gm(2) gv(CB) gc(3)], or the kMomAcc sums of the moment form
@@ -1053,8 +1116,16 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
 #pragma unroll
     for (int k = 0; k < NA; ++k) ra[k] = bc<V>(0.0f);
     float sh[2] = {0.0f, 0.0f};
-    if (__any(active && unsafe)) {
+    if (__any(active && (ent & kUnsafe))) {
         bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, ra);
+    } else if (D == 2 && __any(active && (ent & kThin))) {
+        if (active && wrap) {
+            float ctr[2];
+            cell_center<D>(bins, cell, ctr);
+#pragma unroll
+            for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
+        }
+        bwd_loop<FN, D, CB, 3, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     } else if (__any(active && wrap)) {
         if (active && wrap) {
             float ctr[2];
@@ -1378,8 +1449,9 @@ static int run_forward(const Call &a) {
     const unsigned sub_blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false, kWavesPerBlock, true);
     constexpr bool T = fwd_transposed<FN, D, CB>(), MX = !T && fwd_mfma<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
-    hint.nunsafe = -1;
-    const bool has_unsafe = !hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) || hint.nunsafe != 0;
+    hint.nunsafe = hint.nthin = -1;
+    const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
+    const bool has_unsafe = !hinted || hint.nunsafe != 0, has_thin = !hinted || hint.nthin != 0;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         if (!rows_valid) {
             k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
@@ -1395,7 +1467,8 @@ static int run_forward(const Call &a) {
         {
             KernelTimer t(0, a.s);
             if constexpr (T && D == 2 && DGS_FWD_SUB)  // sub-cell lists (units from the sub-unit hint)
-                k_forward_s<FN, D, CB><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
+                k_forward_s<FN, D, CB, false><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
+                                                                              flag);
             else if constexpr (T)
                 k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else if constexpr (MX)
@@ -1405,6 +1478,13 @@ static int run_forward(const Call &a) {
                                                                           a.samples, a.outs, a.C, cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
+        if constexpr (T && D == 2) {
+            if (has_thin) {  // the kThin entries, packed with the literal-order exponent (the thin pass)
+                k_forward_s<FN, D, CB, true><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
+                                                                             flag);
+                DGS_LAUNCH_CHECK(a.s, a.debug);
+            }
+        }
         if constexpr (T || MX) {
             if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
                 // (grid-strided over a capped grid: it exits at once when the device-side

@@ -455,12 +455,12 @@ std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &co
     return std::make_tuple(counts[0], counts[1]);
 }
 
-// (R, E, kUnsafe entries, fine cells) of a binning (dgs_binning_info).
-std::tuple<int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
+// (R, E, literal-path entries, fine cells, thin entries) of a binning (dgs_binning_info).
+std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
     const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-    int64_t o[4] = {0, 0, 0, 0};
+    int64_t o[5] = {0, 0, 0, 0, 0};
     check(dgs_binning_info(gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), o), "binning_info");
-    return std::make_tuple(o[0], o[1], o[2], o[3]);
+    return std::make_tuple(o[0], o[1], o[2], o[3], o[4]);
 }
 
 // Whether forward / backward with these tensors take the binned path (dgs_inputs_match).

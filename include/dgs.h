@@ -229,9 +229,10 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
 
 /* Diagnostics (not on the reference API): host-known facts of a binning this process made (no
  * device work): out[0] = num_rendered R, out[1] = fine (Gaussian, cell) entries E, out[2] = the
- * entries that take the reference-literal per-pair path (kUnsafe: conics that are not
- * well-conditioned positive definite, wrap breakpoints, fallback cells), out[3] = fine cells.
- * DGS_ERR_BUFFER for buffers this process did not bin. */
+ * entries that take the reference-literal per-pair path (conics that are not positive definite,
+ * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = the entries of
+ * ill-conditioned positive-definite conics (rho^2 >= 0.82: the packed path with the exponent in
+ * the reference's order).  DGS_ERR_BUFFER for buffers this process did not bin. */
 int dgs_binning_info(const void *binning, size_t binning_bytes, const void *sample_binning,
                      size_t sample_binning_bytes, int64_t *out);
 
