@@ -434,6 +434,14 @@ __global__ void k_vol_verify(int P, int N, const uint32_t *__restrict__ m, const
     if (__any(diff) && (threadIdx.x & (kWave - 1)) == 0) *reinterpret_cast<volatile int *>(buf + h.o_flag) = 1;
 }
 
+// count_pairs: the flag word (or 1 for a stale buffer) into out
+__global__ void k_vol_flag_read(int P, int N, const char *buf, unsigned long long *out) {
+    const Hdr &h = *reinterpret_cast<const Hdr *>(buf);
+    if (threadIdx.x == 0)
+        out[0] = (h.magic != kVolMagic || h.P != P || h.N != N) ? 1ull
+                                                                : (unsigned long long)*reinterpret_cast<const volatile int *>(buf + h.o_flag);
+}
+
 __device__ inline bool vol_flagged(const char *buf, const Hdr &h) {
     return *reinterpret_cast<const volatile int *>(buf + h.o_flag) != 0;
 }
@@ -1206,16 +1214,19 @@ extern "C" int dgs_volume_count_pairs(int P, int N, const float *means, const fl
     if (N == 0 || P == 0) return DGS_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     unsigned long long *d = nullptr;
-    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&d), 16, s));
-    DGS_TRY_HIP(hipMemsetAsync(d, 0, 16, s));
+    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&d), 24, s));
+    DGS_TRY_HIP(hipMemsetAsync(d, 0, 24, s));
     if (int rc = vol_flag_reset_verify(P, N, means, conics, samples, binning, binning_bytes, s)) return rc;
     // values are not read in COUNT mode; conics stand in for the pointer
     k_vol_forward<0, 1, true><<<kVolFwdBlocks, kWave, 0, s>>>(static_cast<const char *>(binning), P, N, 1, 0, means,
                                                               conics, conics, samples, nullptr, d);
-    unsigned long long h[2] = {0, 0};
-    DGS_TRY_HIP(hipMemcpyAsync(h, d, 16, hipMemcpyDeviceToHost, s));
+    k_vol_flag_read<<<1, 64, 0, s>>>(P, N, static_cast<const char *>(binning), d + 2);
+    unsigned long long h[3] = {0, 0, 0};
+    DGS_TRY_HIP(hipMemcpyAsync(h, d, 24, hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipFreeAsync(d, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));
+    if (h[2])  // (the forward / backward write NaN instead; a count has no NaN)
+        return fail(DGS_ERR_BUFFER, "dgs_volume_count_pairs: inputs differ from the binned ones or stale buffer");
     counts[0] = (int64_t)h[0];
     counts[1] = (int64_t)h[1];
     return DGS_OK;

@@ -35,8 +35,10 @@ extern "C" {
  * Synchronises `stream` once (bounds, to size the grid).  forward/backward must be given the
  * same means, conics and samples (re-bin when they change): every forward / backward /
  * count_pairs call compares its tensors bitwise with the binned ones on the device (no sync)
- * and, on a difference, writes NaN to every output, as for a stale buffer.  The buffer holds
- * a flag word that these calls write. */
+ * and, on a difference, writes NaN to every output, as for a stale buffer (count_pairs
+ * returns DGS_ERR_BUFFER).  The buffer holds the flag word these calls reset and set, so the
+ * calls on one binning must be ordered (one stream, or events between streams): two
+ * concurrent calls could clear each other's flag. */
 int dgs_volume_preprocess(int P, int N, const float *means, const float *conics,
                           const float *samples, dgs_alloc_fn alloc, void *alloc_ctx,
                           dgs_stream_t stream, int debug);
@@ -59,7 +61,8 @@ int dgs_volume_backward(int function, int P, int N, int C, const float *means, c
                         size_t workspace_bytes, dgs_stream_t stream, int debug);
 
 /* Diagnostic (not on any reference API): counts[0] = pairs the forward evaluates (candidates
- * inside their own cut box), counts[1] = live pairs (G = expf(power) > 0).  Host, syncs. */
+ * inside their own cut box), counts[1] = live pairs (G = expf(power) > 0).  Host, syncs;
+ * DGS_ERR_BUFFER when the inputs differ from the binned ones. */
 int dgs_volume_count_pairs(int P, int N, const float *means, const float *conics, const float *samples,
                            const void *binning, size_t binning_bytes, int64_t *counts, dgs_stream_t stream);
 

@@ -175,6 +175,9 @@ def test_volume_changed_inputs_are_loud(dgs):
         assert torch.isnan(out).all(), which
         dm, dv, dc = _C.volume_backward(0, m2, values, c2, s2, buf, torch.ones_like(out), False)
         assert torch.isnan(dm).all() and torch.isnan(dc).all(), which
+        with pytest.raises(RuntimeError, match="differ from the binned"):  # a count has no NaN
+            _C.volume_count_pairs(m2, c2, s2, buf)
+    assert _C.volume_count_pairs(means, conics, s, buf)[1] > 0
     again = _C.volume_forward(0, means, values, conics, s, buf, False)  # the binned tensors: fine again
     assert torch.equal(again, ok)
 
