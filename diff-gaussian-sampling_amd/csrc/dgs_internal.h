@@ -20,7 +20,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 7;
+constexpr uint32_t kVersion = 8;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -62,7 +62,9 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 //   [gmean float2[P]][gcon float4[P]]  (means / conics in internal order, packed at binning)
 //   [mcopy float[P*D]][ccopy float[P*S]]  (the binned means / conics as passed, caller order)
 //   [rlist uint32[R]]  the reference's point_list: every tile's Gaussian ids, ascending
-//                      (sampler_impl.cu:265-283), the pair set of the call-time path
+//                      (sampler_impl.cu:265-283), the pair set of the call-time path -- built
+//                      at the binning's first call that may take that path (ensure_ref_lists)
+//   [rref uint2[P]]    per internal id: (tile-list offset, radius bits) for that build
 //   [rtab uint32[4][T+1]]  per tile: Gaussian-list start (rlist), sample start (sorted order),
 //                      and the prefix counts of the call-time path's forward / backward units
 // A cell's list is [gbeg, gend); its flag-free entries come first, [gbeg, gmid).
@@ -103,6 +105,7 @@ struct Header {
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     int64_t fsub_cap, esub_cap;
     uint32_t zero[4];  // always 0: the "inputs differ" word of calls whose inputs the caller vouches for
+    uint64_t o_rref;   // (rlist's inputs: uint2[P] per internal id)
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
@@ -115,7 +118,7 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
-    uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab;
+    uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab, o_rref;
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
@@ -151,6 +154,7 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_ccopy = o;     o = align_up(o + 4 * (size_t)P * S, 256);
     L.o_rlist = o;     o = align_up(o + 4 * (size_t)R + 64, 256);
     L.o_rtab = o;      o = align_up(o + 16 * ((size_t)T + 1), 256);
+    L.o_rref = o;      o = align_up(o + 8 * (size_t)P, 256);
     L.o_sub_lbeg = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
@@ -526,9 +530,16 @@ struct UnitHint {
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
     int64_t R;        // num_rendered (sizes the call-time path's backward grid)
     int64_t E;        // fine (Gaussian, cell) entries
+    Header hdr;       // the header preprocess wrote (ensure_ref_lists reads its geometry / offsets)
+    bool ref_built;   // rlist built (ensure_ref_lists), ref_done recorded after its build
+    hipEvent_t ref_done;
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);
+// The call-time path's tile lists (rlist) of a binning: built on `s` at the first call that may
+// take that path (any call not flagged DGS_SAMPLE_INPUTS_BINNED); later calls on another stream
+// wait for that build.  Buffers without a hint (not made by this process) are rebuilt per call.
+int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, hipStream_t s, int debug);
 
 // ---------------------------------------------------------------------------------------
 // Host-side error state

@@ -45,9 +45,18 @@ int check_hip(hipError_t e, const char *what) {
 // ------------------------------------------------------------------------ launch hints
 static std::mutex g_hint_mu;
 static std::unordered_map<const void *, UnitHint> g_hints;
+static void hint_drop(UnitHint &h) {  // (under g_hint_mu)
+    if (h.ref_done) (void)hipEventDestroy(h.ref_done);
+    h.ref_done = nullptr;
+}
 void hint_put(const UnitHint &h) {
     std::lock_guard<std::mutex> lk(g_hint_mu);
-    if (g_hints.size() > 4096) g_hints.clear();
+    if (g_hints.size() > 4096) {
+        for (auto &kv : g_hints) hint_drop(kv.second);
+        g_hints.clear();
+    }
+    auto it = g_hints.find(h.gbuf);
+    if (it != g_hints.end()) hint_drop(it->second);
     g_hints[h.gbuf] = h;
 }
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out) {
@@ -1069,16 +1078,20 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
 // its tiles, in the reference's order, at its scan offset (caller id order); a stable sort by
 // tile then yields the reference's point_list (ascending id per tile) -- the pair set of the
 // call-time path (dgs_reference.hip).
-__global__ void k_ref_keys(int P, Geom G, const float *__restrict__ means, const float *__restrict__ radii,
-                           const uint64_t *__restrict__ offs, uint32_t *__restrict__ keys,
-                           uint32_t *__restrict__ vals) {
-    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= P) return;
-    const float r = radii[g];
+// Run lazily (ensure_ref_lists) over the internal ids: the binned means (gmean), radius and
+// tile-list offset (rref) of caller id g = perm[i].
+__global__ void k_ref_keys(int P, Geom G, const float2 *__restrict__ gmean, const int32_t *__restrict__ perm,
+                           const uint2 *__restrict__ rref, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const uint2 rr = rref[i];
+    const float r = __uint_as_float(rr.y);
     if (!(r > 0.0f)) return;
-    const float m[2] = {means[g * G.D], G.D == 2 ? means[g * G.D + 1] : 0.0f};
+    const int64_t g = perm[i];
+    const float2 mm = gmean[i];
+    const float m[2] = {mm.x, mm.y};
     const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
-    uint64_t o = offs[g];
+    uint64_t o = rr.x;
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             keys[o] = key_of(G.D, x, y, G.grid);
@@ -1168,8 +1181,9 @@ __global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
 // Also stores perm (internal -> caller id) and its inverse back to back in gperm (one pass
 // over the permutation instead of two launches).
 __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float2 *__restrict__ igm,
-                           const float4 *__restrict__ igc, float2 *__restrict__ gmean,
-                           float4 *__restrict__ gcon, int32_t *__restrict__ gperm) {
+                           const float4 *__restrict__ igc, const uint64_t *__restrict__ toffs,
+                           float2 *__restrict__ gmean, float4 *__restrict__ gcon, int32_t *__restrict__ gperm,
+                           uint2 *__restrict__ rref) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -1178,6 +1192,8 @@ __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float
     gmean[i] = igm[i];  // (k_fine_count's internal-order copies: coalesced, no second gather)
     const float4 c = igc[i];
     gcon[i] = make_float4(c.x, c.y, c.z, 0.0f);
+    // (toffs < R < 2^31 when the binning succeeds; preprocess fails otherwise)
+    rref[i] = make_uint2((uint32_t)toffs[g], __float_as_uint(c.w));
 }
 
 // Forward sample pair rows in sorted order: pair p = samples 2p, 2p+1, field-interleaved
@@ -1637,13 +1653,13 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int64_t Ecap = -1, Rcap = -1, bwd_cap = 0;
         Layout L;
         char *gbuf = nullptr;
-        uint32_t *ekeys, *evals, *ekeys_sorted, *svals, *rkeys, *rkeys_sorted, *rvals;
+        uint32_t *ekeys, *evals, *ekeys_sorted, *svals;
         unsigned long long *fs_cells, *fs_units, *fs_sub;  // fused_scan states (zeroed with phase B)
         int32_t *hbeg, *hend;
         void *tmp_b;
         size_t t_b;
         bool k16;
-        int ebits, rbits;
+        int ebits;
     };
     auto setup_b = [&](int64_t Ecap, int64_t Rcap, PhaseB &B) -> int {
         B.Ecap = Ecap;
@@ -1656,27 +1672,21 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.ekeys = cb.take<uint32_t>(Ecap + 1); B.evals = cb.take<uint32_t>(Ecap + 1);
         B.ekeys_sorted = cb.take<uint32_t>(Ecap + 1); B.svals = cb.take<uint32_t>(Ecap + 1);
         B.hbeg = cb.take<int32_t>(2 * (size_t)ncells); B.hend = cb.take<int32_t>(2 * (size_t)ncells);
-        B.rkeys = cb.take<uint32_t>(Rcap + 1); B.rkeys_sorted = cb.take<uint32_t>(Rcap + 1);
-        B.rvals = cb.take<uint32_t>(Rcap + 1);
         B.fs_cells = cb.take<unsigned long long>(fused_scan_state_words(ncells, 1, 1));
         B.fs_units = cb.take<unsigned long long>(fused_scan_state_words(ncells, 2, 1));
         B.fs_sub = cb.take<unsigned long long>(fused_scan_state_words(std::max(nsub, 1), 1, 1));
-        uint32_t *rlist = reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rlist);
-        size_t t_esort = 0, t_rsort = 0;
-        B.rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
-        DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_rsort, B.rkeys, B.rkeys_sorted, B.rvals, rlist, (int)Rcap, 0,
-                                        B.rbits, s));
+        size_t t_esort = 0;
         B.ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
         B.k16 = B.ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
         DGS_TRY_HIP(B.k16 ? sort_entries<uint16_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s)
                           : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
                                                    B.ebits, s));
-        B.t_b = std::max(t_esort, t_rsort);
+        B.t_b = t_esort;
         B.tmp_b = cb.take<char>(B.t_b);
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
-        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals, &B.rkeys, &B.rkeys_sorted, &B.rvals})
+        for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals})
             Carve::rebase(*q, base);
         for (unsigned long long **q : {&B.fs_cells, &B.fs_units, &B.fs_sub}) Carve::rebase(*q, base);
         Carve::rebase(B.hbeg, base);
@@ -1693,10 +1703,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.fs_sub, 8 * fused_scan_state_words(std::max(nsub, 1), 1, 1));
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
-        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc,
+        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc, toffs,
                                                   reinterpret_cast<float2 *>(B.gbuf + B.L.o_gmean),
                                                   reinterpret_cast<float4 *>(B.gbuf + B.L.o_gcon),
-                                                  reinterpret_cast<int32_t *>(B.gbuf + B.L.o_perm));
+                                                  reinterpret_cast<int32_t *>(B.gbuf + B.L.o_perm),
+                                                  reinterpret_cast<uint2 *>(B.gbuf + B.L.o_rref));
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
@@ -1747,13 +1758,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *entries = reinterpret_cast<uint32_t *>(gbuf + L.o_entries);
     uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
     uint32_t *ekeys = B.ekeys, *evals = B.evals, *ekeys_sorted = B.ekeys_sorted, *svals = B.svals;
-    uint32_t *rkeys = B.rkeys, *rkeys_sorted = B.rkeys_sorted, *rvals = B.rvals;
     int32_t *hbeg = B.hbeg, *hend = B.hend;
-    uint32_t *rlist = reinterpret_cast<uint32_t *>(gbuf + L.o_rlist);
     void *tmp_b = B.tmp_b;
     const size_t t_b = B.t_b;
     const bool k16 = B.k16;
-    const int ebits = B.ebits, rbits = B.rbits;
+    const int ebits = B.ebits;
 
     // ---- cell lists: the sort path's entries (sorted by (cell, flag)), then per cell the
     // gathered local entries (ascending id), the sorted unflagged and the flagged ones
@@ -1867,18 +1876,12 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     }
 
     // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled) and the
-    // call-time path's tables: its tile lists (the reference's point_list) and unit counts
+    // call-time path's tables: per-tile list starts and unit counts (its tile lists -- the
+    // reference's point_list -- are sorted at the first call that may need them: ensure_ref_lists)
     k_ref_tables<<<1, 1024, 0, s>>>(G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf),
                                     reinterpret_cast<uint2 *>(srbuf),
                                     reinterpret_cast<uint32_t *>(gbuf + L.o_rtab));
     DGS_LAUNCH_CHECK(s, debug);
-    if (R > 0) {
-        k_ref_keys<<<grid_for(P), kBlock, 0, s>>>(P, G, means, radii, toffs, rkeys, rvals);
-        DGS_LAUNCH_CHECK(s, debug);
-        tb = t_b;
-        DGS_TRY_HIP(sort_pairs_onesweep(tmp_b, tb, rkeys, rkeys_sorted, rvals, rlist, (int)R, 0, rbits, s));
-        DGS_LAUNCH_CHECK(s, debug);
-    }
     {  // the binned tensors as passed (each forward / backward compares its inputs with them)
         const int S3 = D * (D + 1) / 2;
         CopySpec c{};
@@ -1912,7 +1915,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_sorted = L0.o_sorted; h.o_cell_sbeg = L0.o_cell_sbeg; h.o_cell_send = L0.o_cell_send;
     h.o_fwd_units = L0.o_fwd_units; h.o_cell_box = L0.o_cell_box; h.s_bytes = L0.s_bytes;
     h.o_gmean = L.o_gmean; h.o_gcon = L.o_gcon; h.o_fsrows = L0.o_fsrows;
-    h.o_mcopy = L.o_mcopy; h.o_ccopy = L.o_ccopy; h.o_rlist = L.o_rlist; h.o_rtab = L.o_rtab;
+    h.o_mcopy = L.o_mcopy; h.o_ccopy = L.o_ccopy; h.o_rlist = L.o_rlist; h.o_rtab = L.o_rtab; h.o_rref = L.o_rref;
     h.o_scopy = L0.o_scopy;
     h.o_sub_sbeg = L0.o_sub_sbeg; h.o_sub_send = L0.o_sub_send; h.o_sub_box = L0.o_sub_box;
     h.o_fsub_units = L0.o_fsub_units;
@@ -1932,7 +1935,81 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E;
+    uh.hdr = h;
+    uh.ref_built = false;
+    uh.ref_done = nullptr;
     hint_put(uh);
+    return DGS_OK;
+}
+// Sorts the call-time path's tile lists (see ensure_ref_lists in dgs_internal.h) of the binning
+// whose header is h: keys in caller-id order at the reference's scan offsets, then a stable sort
+// by tile (sampler_impl.cu:265-283).  Stream-ordered scratch.
+static int build_ref_lists(const Header &h, char *gbuf, hipStream_t s, int debug) {
+    const int64_t R = h.R, P = h.P;
+    if (R <= 0 || P <= 0) return DGS_OK;
+    Geom G{};
+    G.D = h.D; G.T = h.T; G.n = h.n; G.CT = h.CT; G.ncells = h.ncells;
+    G.grid[0] = h.grid[0]; G.grid[1] = h.grid[1];
+    G.off[0] = h.off[0]; G.off[1] = h.off[1];
+    G.fs = (double)kTile / h.n;
+    G.ifs = 1.0 / G.fs;
+    const int rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
+    uint32_t *rlist = reinterpret_cast<uint32_t *>(gbuf + h.o_rlist);
+    size_t tbytes = 0;
+    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, tbytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                    (const uint32_t *)nullptr, rlist, (int)R, 0, rbits, s));
+    const size_t kb = align_up(4 * (size_t)R, 256);
+    char *scr = nullptr;
+    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), 3 * kb + tbytes, s));
+    uint32_t *keys = reinterpret_cast<uint32_t *>(scr), *vals = reinterpret_cast<uint32_t *>(scr + kb);
+    uint32_t *keys_sorted = reinterpret_cast<uint32_t *>(scr + 2 * kb);
+    k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
+                                              reinterpret_cast<const int32_t *>(gbuf + h.o_perm),
+                                              reinterpret_cast<const uint2 *>(gbuf + h.o_rref), keys, vals);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = sort_pairs_onesweep(scr + 3 * kb, tbytes, keys, keys_sorted, vals, rlist, (int)R, 0, rbits, s);
+    const hipError_t f = hipFreeAsync(scr, s);
+    DGS_TRY_HIP(e);
+    DGS_TRY_HIP(f);
+    DGS_LAUNCH_CHECK(s, debug);
+    return DGS_OK;
+}
+
+static std::mutex g_ref_mu;  // one build per binning, whichever stream asks first
+
+int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, hipStream_t s, int debug) {
+    std::lock_guard<std::mutex> lk(g_ref_mu);
+    UnitHint h;
+    if (!hint_get(gbuf, gbytes, sbuf, sbytes, &h)) {  // a foreign buffer: its header, then a build
+        Header hd;
+        DGS_TRY_HIP(hipMemcpyAsync(&hd, gbuf, sizeof(hd), hipMemcpyDeviceToHost, s));
+        DGS_TRY_HIP(hipStreamSynchronize(s));
+        if (hd.magic != kMagic || hd.version != kVersion || hd.g_bytes > gbytes || hd.R < 0 ||
+            hd.R >= (1LL << 31))
+            return DGS_OK;  // (not a binning: the render kernels' own header check makes it loud)
+        return build_ref_lists(hd, static_cast<char *>(const_cast<void *>(gbuf)), s, debug);
+    }
+    if (h.ref_built) {
+        if (h.ref_done) DGS_TRY_HIP(hipStreamWaitEvent(s, h.ref_done, 0));
+        return DGS_OK;
+    }
+    if (int rc = build_ref_lists(h.hdr, static_cast<char *>(const_cast<void *>(gbuf)), s, debug)) return rc;
+    hipEvent_t ev = nullptr;
+    DGS_TRY_HIP(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (hipEventRecord(ev, s) != hipSuccess) {
+        (void)hipEventDestroy(ev);
+        return fail(DGS_ERR_HIP, "ensure_ref_lists: event record failed");
+    }
+    std::lock_guard<std::mutex> hl(g_hint_mu);
+    auto it = g_hints.find(gbuf);
+    if (it != g_hints.end() && it->second.hdr.stamp == h.hdr.stamp) {
+        hint_drop(it->second);
+        it->second.ref_built = true;
+        it->second.ref_done = ev;
+    } else {
+        (void)hipEventDestroy(ev);  // (re-binned meanwhile)
+    }
     return DGS_OK;
 }
 }  // namespace dgs

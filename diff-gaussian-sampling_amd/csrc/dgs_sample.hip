@@ -1452,6 +1452,8 @@ static int run_forward(const Call &a) {
     hint.nunsafe = hint.nthin = -1;
     const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
     const bool has_unsafe = !hinted || hint.nunsafe != 0, has_thin = !hinted || hint.nthin != 0;
+    if (!binned)  // (the call-time path's tile lists, at the binning's first such call)
+        if (int rc = ensure_ref_lists(a.gb, a.gbytes, a.sb, a.sbytes, a.s, a.debug)) return rc;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         if (!rows_valid) {
             k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
@@ -1516,6 +1518,8 @@ static int run_backward(const Call &a) {
     uint32_t *const flag = dirty_word(a, check);
     constexpr int S = D * (D + 1) / 2;
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
+    if (!binned)
+        if (int rc = ensure_ref_lists(a.gb, a.gbytes, a.sb, a.sbytes, a.s, a.debug)) return rc;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
         if (!rows_valid) {
             k_pack_gauss<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, a.values, a.C, cbase, grows,
