@@ -25,6 +25,7 @@
 #include <vector>
 
 #include "dgs_internal.h"
+#include "dgs_radix.h"
 #include "dgs_scan.h"
 
 namespace dgs {
@@ -1244,25 +1245,9 @@ struct ZeroList {
 
 static inline unsigned grid_for(int64_t n) { return (unsigned)((n + kBlock - 1) / kBlock); }
 
-// Every sort of the binning is a stable LSD radix sort of (key, u32 value) pairs on rocprim's
-// onesweep algorithm, called directly (rocprim::detail::radix_sort_onesweep_impl, the branch
-// rocprim::radix_sort_pairs takes for large inputs).  The public entry also instantiates a block
-// sort and a merge sort for small inputs: ~250 more kernels in this code object, whose load is
-// most of the first call's time.  Below 2^20 items rocprim would otherwise pick those (24
-// launches, ~170 us for the 1M home keys against ~25 us here).  Entry keys are u16 when every
-// (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per entry and pass).
-template <typename KT>
-static hipError_t sort_entries(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
-                               const uint32_t *vin, uint32_t *vout, int64_t n, int bits, hipStream_t s) {
-    return onesweep_pairs<KT>(tmp, bytes, reinterpret_cast<const KT *>(kin), reinterpret_cast<KT *>(kout), vin,
-                              vout, (size_t)n, 0u, (unsigned)bits, s);
-}
-
-static hipError_t sort_pairs_onesweep(void *tmp, size_t &bytes, const uint32_t *kin, uint32_t *kout,
-                                      const uint32_t *vin, uint32_t *vout, int n, int b0, int b1,
-                                      hipStream_t s) {
-    return onesweep_pairs<uint32_t>(tmp, bytes, kin, kout, vin, vout, (size_t)n, (unsigned)b0, (unsigned)b1, s);
-}
+// Every sort of the binning is dgs_radix.h's stable LSD radix sort of (key, u32 value) pairs.
+// Entry keys are u16 when every (cell, flag) key fits 16 bits (6 instead of 8 bytes moved per
+// entry and place).
 
 // Chooses the fine subdivision: about 120 samples per fine cell on average (two forward
 // waves per cell), capped so that cells stay reasonably large for sparse sample sets.
@@ -1519,16 +1504,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     float4 *grec = ca.take<float4>(2 * (size_t)P);
     unsigned long long *fscan_a = ca.take<unsigned long long>(fused_scan_state_words(P, 2, 8));
 
-    // sort / scan temp storage: one piece sized for the largest phase-A primitive
-    size_t t_ssort = 0, t_hsort = 0;
+    // the two phase-A sorts' scratch (each with its own zero-filled head: see dgs_radix.h)
     const int sbits = bit_length((uint64_t)ncells * kSubPerCell);  // (cell, sub-cell) keys
     const int hbits = bit_length((uint64_t)home_w * (uint64_t)home_h);  // absent key = home_w * home_h
-    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_ssort, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0,
-                                    sbits, s));
-    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, t_hsort, home, home_sorted, gids,
-                                                   perm, P, 0, hbits, s));
-    const size_t t_a = std::max(t_ssort, t_hsort);
-    void *tmp_a = ca.take<char>(t_a);
+    const RadixPlan plan_s = radix_plan(N, sbits), plan_h = radix_plan(P, hbits);
+    char *rs_s = ca.take<char>(plan_s.bytes), *rs_h = ca.take<char>(plan_h.bytes);
     {
         char *base = S.get<char>(ca.off);
         if (S.rc) return S.rc;
@@ -1547,9 +1527,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(igc, base);
         Carve::rebase(grec, base);
         Carve::rebase(fscan_a, base);
-        char *t = static_cast<char *>(tmp_a);
-        Carve::rebase(t, base);
-        tmp_a = t;
+        Carve::rebase(rs_s, base);
+        Carve::rebase(rs_h, base);
     }
 
     float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
@@ -1571,6 +1550,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(eg, 32);
         zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
         zl.add(rmax, 4);
+        zl.add(rs_s, plan_s.zero_bytes);
+        zl.add(rs_h, plan_h.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
     }
@@ -1578,8 +1559,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
     DGS_LAUNCH_CHECK(s, debug);
-    size_t tb = t_a;
-    DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, skeys, skeys_sorted, sids, (uint32_t *)sorted_sid, N, 0, sbits, s));
+    DGS_TRY_HIP(radix_sort<uint32_t>(plan_s, N, rs_s, skeys, skeys_sorted, sids, reinterpret_cast<uint32_t *>(sorted_sid),
+                                     s));
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 2);
     DGS_LAUNCH_CHECK(s, debug);
@@ -1601,9 +1582,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, conics, radii, touched, gtile,
                                                 home, gids, home_w, home_h, present, grec);
     DGS_LAUNCH_CHECK(s, debug);
-    tb = t_a;
-    DGS_TRY_HIP(sort_pairs_onesweep(tmp_a, tb, home, home_sorted, gids, perm, P, 0,
-                                                   hbits, s));
+    DGS_TRY_HIP(radix_sort<uint32_t>(plan_h, P, rs_h, home, home_sorted, gids, perm, s));
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, grec, cell_sbeg, cell_send, cell_box, fcount, greach,
                                                 lrows, rmax, igm, igc, eg + 1);
@@ -1656,8 +1635,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         uint32_t *ekeys, *evals, *ekeys_sorted, *svals;
         unsigned long long *fs_cells, *fs_units, *fs_sub;  // fused_scan states (zeroed with phase B)
         int32_t *hbeg, *hend;
-        void *tmp_b;
-        size_t t_b;
+        char *rs_e;  // the entry sort's scratch (zero head filled with phase B's regions)
+        RadixPlan plan_e;
         bool k16;
         int ebits;
     };
@@ -1675,15 +1654,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.fs_cells = cb.take<unsigned long long>(fused_scan_state_words(ncells, 1, 1));
         B.fs_units = cb.take<unsigned long long>(fused_scan_state_words(ncells, 2, 1));
         B.fs_sub = cb.take<unsigned long long>(fused_scan_state_words(std::max(nsub, 1), 1, 1));
-        size_t t_esort = 0;
         B.ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
         B.k16 = B.ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
-        DGS_TRY_HIP(B.k16 ? sort_entries<uint16_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
-                                                   B.ebits, s)
-                          : sort_entries<uint32_t>(nullptr, t_esort, B.ekeys, B.ekeys_sorted, B.evals, B.svals, Ecap,
-                                                   B.ebits, s));
-        B.t_b = t_esort;
-        B.tmp_b = cb.take<char>(B.t_b);
+        B.plan_e = radix_plan(Ecap, B.ebits);
+        B.rs_e = cb.take<char>(B.plan_e.bytes);
         char *base = S.get<char>(cb.off);
         if (S.rc) return S.rc;
         for (uint32_t **q : {&B.ekeys, &B.evals, &B.ekeys_sorted, &B.svals})
@@ -1691,9 +1665,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         for (unsigned long long **q : {&B.fs_cells, &B.fs_units, &B.fs_sub}) Carve::rebase(*q, base);
         Carve::rebase(B.hbeg, base);
         Carve::rebase(B.hend, base);
-        char *t = static_cast<char *>(B.tmp_b);
-        Carve::rebase(t, base);
-        B.tmp_b = t;
+        Carve::rebase(B.rs_e, base);
         ZeroList zl;
         zl.add(B.gbuf + B.L.o_counts, 16);
         zl.add(B.hbeg, sizeof(int32_t) * 2 * (size_t)ncells);
@@ -1701,6 +1673,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.fs_cells, 8 * fused_scan_state_words(ncells, 1, 1));
         zl.add(B.fs_units, 8 * fused_scan_state_words(ncells, 2, 1));
         zl.add(B.fs_sub, 8 * fused_scan_state_words(std::max(nsub, 1), 1, 1));
+        zl.add(B.rs_e, B.plan_e.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
         k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc, toffs,
@@ -1759,8 +1732,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint2 *bwd_units = reinterpret_cast<uint2 *>(gbuf + L.o_bwd_units);
     uint32_t *ekeys = B.ekeys, *evals = B.evals, *ekeys_sorted = B.ekeys_sorted, *svals = B.svals;
     int32_t *hbeg = B.hbeg, *hend = B.hend;
-    void *tmp_b = B.tmp_b;
-    const size_t t_b = B.t_b;
     const bool k16 = B.k16;
     const int ebits = B.ebits;
 
@@ -1776,9 +1747,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
                                                             fcount, greach, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
-        tb = t_b;
-        DGS_TRY_HIP(k16 ? sort_entries<uint16_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, svals, Es, ebits, s)
-                        : sort_entries<uint32_t>(tmp_b, tb, ekeys, ekeys_sorted, evals, svals, Es, ebits, s));
+        DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),
+                                               reinterpret_cast<uint16_t *>(ekeys_sorted), evals, svals, s)
+                        : radix_sort<uint32_t>(B.plan_e, Es, B.rs_e, ekeys, ekeys_sorted, evals, svals, s));
         DGS_LAUNCH_CHECK(s, debug);
         if (k16)
             k_identify<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(Es, reinterpret_cast<const uint16_t *>(ekeys_sorted),
@@ -1955,20 +1926,20 @@ static int build_ref_lists(const Header &h, char *gbuf, hipStream_t s, int debug
     G.ifs = 1.0 / G.fs;
     const int rbits = bit_length((uint64_t)(G.T > 1 ? G.T - 1 : 1));
     uint32_t *rlist = reinterpret_cast<uint32_t *>(gbuf + h.o_rlist);
-    size_t tbytes = 0;
-    DGS_TRY_HIP(sort_pairs_onesweep(nullptr, tbytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                    (const uint32_t *)nullptr, rlist, (int)R, 0, rbits, s));
+    const RadixPlan plan = radix_plan(R, rbits);
     const size_t kb = align_up(4 * (size_t)R, 256);
     char *scr = nullptr;
-    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), 3 * kb + tbytes, s));
+    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), 3 * kb + plan.bytes, s));
     uint32_t *keys = reinterpret_cast<uint32_t *>(scr), *vals = reinterpret_cast<uint32_t *>(scr + kb);
     uint32_t *keys_sorted = reinterpret_cast<uint32_t *>(scr + 2 * kb);
-    k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
-                                              reinterpret_cast<const int32_t *>(gbuf + h.o_perm),
-                                              reinterpret_cast<const uint2 *>(gbuf + h.o_rref), keys, vals);
-    hipError_t e = hipGetLastError();
-    if (e == hipSuccess)
-        e = sort_pairs_onesweep(scr + 3 * kb, tbytes, keys, keys_sorted, vals, rlist, (int)R, 0, rbits, s);
+    hipError_t e = hipMemsetAsync(scr + 3 * kb, 0, plan.zero_bytes, s);
+    if (e == hipSuccess) {
+        k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
+                                                  reinterpret_cast<const int32_t *>(gbuf + h.o_perm),
+                                                  reinterpret_cast<const uint2 *>(gbuf + h.o_rref), keys, vals);
+        e = hipGetLastError();
+    }
+    if (e == hipSuccess) e = radix_sort<uint32_t>(plan, R, scr + 3 * kb, keys, keys_sorted, vals, rlist, s);
     const hipError_t f = hipFreeAsync(scr, s);
     DGS_TRY_HIP(e);
     DGS_TRY_HIP(f);
@@ -2013,6 +1984,36 @@ int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t s
     return DGS_OK;
 }
 }  // namespace dgs
+
+// Test hook (not on the reference API, not in include/): the binning's radix sort on its own,
+// key_bytes 2 or 4, stream-ordered scratch.  tests/test_gpu_radix.py checks it against a stable
+// CPU argsort.
+extern "C" int dgs_test_radix_sort(int64_t n, int bits, int key_bytes, const void *kin, void *kout,
+                                   const uint32_t *vin, uint32_t *vout, dgs_stream_t stream) {
+    using namespace dgs;
+    if (n < 0 || bits < 1 || bits > (key_bytes == 2 ? 16 : 32) || (key_bytes != 2 && key_bytes != 4))
+        return fail(DGS_ERR_ARG, "dgs_test_radix_sort: bad arguments");
+    if (n == 0) return DGS_OK;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const RadixPlan plan = radix_plan(n, bits);
+    char *scr = nullptr;
+    DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), plan.bytes, s));
+    hipError_t e = hipMemsetAsync(scr, 0, plan.zero_bytes, s);
+    if (e == hipSuccess)
+        e = key_bytes == 2 ? radix_sort<uint16_t>(plan, n, scr, static_cast<const uint16_t *>(kin),
+                                                  static_cast<uint16_t *>(kout), vin, vout, s)
+                           : radix_sort<uint32_t>(plan, n, scr, static_cast<const uint32_t *>(kin),
+                                                  static_cast<uint32_t *>(kout), vin, vout, s);
+    uint32_t gave_up = 0;
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(&gave_up, scr + plan.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s);
+    const hipError_t f = hipFreeAsync(scr, s);
+    DGS_TRY_HIP(e);
+    DGS_TRY_HIP(f);
+    DGS_TRY_HIP(hipStreamSynchronize(s));
+    if (gave_up) return fail(DGS_ERR_HIP, "dgs_test_radix_sort: a look-back gave up");
+    return DGS_OK;
+}
 
 extern "C" int dgs_preprocess(int P, int D, int N, const float *means, const float *covariances,
                               const float *conics, const float *samples, const int *grid,

@@ -456,6 +456,24 @@ std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &co
 }
 
 // (R, E, literal-path entries, fine cells, thin entries) of a binning (dgs_binning_info).
+extern "C" int dgs_test_radix_sort(int64_t n, int bits, int key_bytes, const void *kin, void *kout,
+                                   const uint32_t *vin, uint32_t *vout, dgs_stream_t stream);
+
+// The binning's radix sort on its own (tests/test_gpu_radix.py): keys int16 / int32 (bit
+// patterns), values int32; returns the stably sorted pair.
+std::tuple<Tensor, Tensor> RadixSortTest(const Tensor &keys_in, const Tensor &vals_in, int64_t bits) {
+    TORCH_CHECK(keys_in.is_cuda() && vals_in.is_cuda(), "radix_sort_test: CUDA tensors");
+    TORCH_CHECK(keys_in.scalar_type() == at::kShort || keys_in.scalar_type() == at::kInt, "keys int16 / int32");
+    TORCH_CHECK(vals_in.scalar_type() == at::kInt && vals_in.numel() == keys_in.numel(), "values int32, same length");
+    const Tensor keys = keys_in.contiguous(), vals = vals_in.contiguous();
+    Tensor ko = torch::empty_like(keys), vo = torch::empty_like(vals);
+    check(dgs_test_radix_sort(keys.numel(), (int)bits, (int)keys.element_size(), keys.data_ptr(), ko.data_ptr(),
+                              reinterpret_cast<const uint32_t *>(vals.data_ptr<int32_t>()),
+                              reinterpret_cast<uint32_t *>(vo.data_ptr<int32_t>()), as_dgs(cur_stream())),
+          "radix_sort_test");
+    return std::make_tuple(ko, vo);
+}
+
 std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
     const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
     int64_t o[5] = {0, 0, 0, 0, 0};
@@ -857,6 +875,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("exchange_sets", &ExchangeSets);
     m.def("inputs_match", &InputsMatch);
     m.def("binning_info", &BinningInfo);
+    m.def("radix_sort_test", &RadixSortTest);
     m.def("volume_preprocess", &VolumePreprocess);
     m.def("volume_forward", &VolumeForward);
     m.def("volume_backward", &VolumeBackward);
