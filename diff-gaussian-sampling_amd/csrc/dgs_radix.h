@@ -13,7 +13,8 @@
 // in LDS order the items (wave chunks are contiguous: the order is wave, item, lane = index
 // order) -- publishes its per-digit counts, looks back per digit (one thread per digit) for
 // the exclusive prefix over earlier tiles, scatters the tile into LDS in digit order and
-// writes it out in runs of equal digits.
+// writes it out in runs of equal digits.  Look-back words are 8-byte {flag, count} granules
+// under relaxed agent-scope atomics, no fences (see k_fused_scan in dgs_scan.h).
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -155,7 +156,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
         tot += c;
     }
     unsigned long long *st = states + tile * kRsBins + tid;
-    __hip_atomic_store(st, (tile == 0 ? kRsPre : kRsAgg) | (unsigned long long)tot, __ATOMIC_RELEASE,
+    __hip_atomic_store(st, (tile == 0 ? kRsPre : kRsAgg) | (unsigned long long)tot, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
     const uint32_t tstart = rs_block_excl(tot, wsum);
     uint64_t pre = 0;
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
         uint32_t spins = 0;
         for (int64_t j = tile - 1; j >= 0;) {
             const unsigned long long v =
-                __hip_atomic_load(states + j * kRsBins + tid, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_load(states + j * kRsBins + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             if ((v & ~kRsVal) == 0ull) {  // not yet published: spin
                 if (++spins > (1u << 22)) {
                     atomicOr(err, 1u);
@@ -175,7 +176,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
             if (v & kRsPre) break;
             --j;
         }
-        __hip_atomic_store(st, kRsPre | (pre + tot), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st, kRsPre | (pre + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     s_tstart[tid] = tstart;
     s_delta[tid] = gbase + (uint32_t)pre - tstart;

@@ -980,11 +980,15 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
     }
-    if constexpr (FN == 0 && D == 2 && CB == 1 && MODE < 2 && DGS_QFORM && DGS_VFACTOR) {
+    if constexpr (FN == 0 && D == 2 && CB == 1 && MODE != 2 && DGS_QFORM && DGS_VFACTOR) {
         // gaussian, C = 1: the exponent from the quadratic monomials q = (X0^2, X0 X1, X1^2)
-        // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16
+        // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16 (mode 3:
+        // the exponent in the reference's order instead, the same moments)
         const V q0 = X[0] * X[0], q1 = X[0] * X[1], q2 = X[1] * X[1];
-        const V t = vexp2(vfma(bc<V>(kk[2]), q2, vfma(bc<V>(kk[1]), q1, kk[0] * q0))) * dl[0][0];
+        V e;
+        if constexpr (MODE == 3) e = lit_prob<V>(X, c);
+        else e = vexp2(vfma(bc<V>(kk[2]), q2, vfma(bc<V>(kk[1]), q1, kk[0] * q0)));
+        const V t = e * dl[0][0];
         V *gm = acc, *gv = acc + 2, *gc = acc + 3;
         gv[0] += t;
         gm[0] = vfma(t, X[0], gm[0]);

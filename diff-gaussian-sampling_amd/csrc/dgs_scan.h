@@ -134,7 +134,11 @@ static void scan_excl(int64_t n, const T *a, T *ao, const T *b, T *bo, T *part, 
 // three-kernel scan above plus the two kernels around it were five launches of ~5 us each, most
 // of their time launch overhead at the binning's sizes).  Tiles of kBlock * ITEMS elements are
 // taken in ticket order (atomic counter), so every tile's predecessors are running or done and
-// the look-back always terminates; wave 0 looks back 64 tiles at a time.  NA (1 or 2) arrays of
+// the look-back always terminates; wave 0 looks back 64 tiles at a time.  A look-back word is
+// one 8-byte {flag, value} granule written and polled with RELAXED agent-scope atomics (sc1
+// stores / loads, served past the non-coherent per-XCD L2s): the value travels in the flag's
+// own word, so no fence is needed -- an agent-scope release is a write-back of the XCD's whole
+// L2 and an acquire an L1 invalidate (MI355X_MICROARCH.md), and with them this scan took ~200 us.  NA (1 or 2) arrays of
 // unsigned counts are scanned side by side.  ITEMS = 1 where the consumer does real work per
 // element (unit lists), more where it is a plain store.
 //   prod(i, v[NA])            : the counts of element i
@@ -182,14 +186,14 @@ __global__ __launch_bounds__(kBlock) void k_fused_scan(int64_t n, unsigned long 
         for (int a = 0; a < NA; ++a) {
             if (lane == 0)
                 __hip_atomic_store(&st[(int64_t)tile * NA + a], (tile == 0 ? kFusePre : kFuseAgg) | agg[a],
-                                   __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             uint64_t pre = 0;
             for (int j = tile - 1; j >= 0; j -= kWave) {
                 const int jj = j - lane;  // lane 0 = the nearest predecessor
                 uint64_t w = kFusePre;    // (before tile 0: a zero prefix)
                 if (jj >= 0)
                     do {
-                        w = __hip_atomic_load(&st[(int64_t)jj * NA + a], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+                        w = __hip_atomic_load(&st[(int64_t)jj * NA + a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                     } while ((w & ~kFuseVal) == 0);
                 const uint64_t pm = __ballot((w & kFusePre) != 0);
                 const int stop = pm ? __builtin_ctzll(pm) : kWave;  // lanes <= stop contribute
@@ -201,7 +205,7 @@ __global__ __launch_bounds__(kBlock) void k_fused_scan(int64_t n, unsigned long 
             }
             if (lane == 0) {
                 if (tile > 0)
-                    __hip_atomic_store(&st[(int64_t)tile * NA + a], kFusePre | (pre + agg[a]), __ATOMIC_RELEASE,
+                    __hip_atomic_store(&st[(int64_t)tile * NA + a], kFusePre | (pre + agg[a]), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_AGENT);
                 pre_s[a] = pre;
                 tot_s[a] = pre + agg[a];

@@ -27,10 +27,11 @@ ap.add_argument("--N", type=int, default=2_000_000)
 ap.add_argument("--C", type=int, default=1)
 ap.add_argument("--function", default="gaussian", choices=FUNCS)
 ap.add_argument("--prep", type=int, default=0, help="extra (warm) preprocess calls, for profiles")
+ap.add_argument("--aniso", type=float, default=1.0, help="axis ratios U[1, aniso] (thin Gaussians)")
 a = ap.parse_args()
 dev = torch.device("cuda:0")
 D, fi = 2, FUNCS.index(a.function)
-means, values, covs, conics = (t.to(dev) for t in syn.gaussians(a.P, D, a.C, seed=0))
+means, values, covs, conics = (t.to(dev) for t in syn.gaussians(a.P, D, a.C, seed=0, aniso=a.aniso))
 samples = syn.samples(a.N, D, seed=4).to(dev)
 dL = syn.grad_out(a.N, D ** fi, a.C, seed=5).to(dev).reshape((a.N,) + (D,) * fi + (a.C,))
 R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(means, values, covs, conics, samples, False)
