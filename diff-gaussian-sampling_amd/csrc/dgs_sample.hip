@@ -1471,7 +1471,7 @@ static int run_forward(const Call &a) {
             if (rc) return rc;
         }
         {
-            KernelTimer t(0, a.s);
+            KernelTimer t(0, a.s);  // (the main pass and the thin / tail passes behind it)
             if constexpr (T && D == 2 && DGS_FWD_SUB)  // sub-cell lists (units from the sub-unit hint)
                 k_forward_s<FN, D, CB, false><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
                                                                               flag);
@@ -1482,23 +1482,23 @@ static int run_forward(const Call &a) {
             else
                 k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                           a.samples, a.outs, a.C, cbase, flag);
-        }
-        DGS_LAUNCH_CHECK(a.s, a.debug);
-        if constexpr (T && D == 2) {
-            if (has_thin) {  // the kThin entries, packed with the literal-order exponent (the thin pass)
-                k_forward_s<FN, D, CB, true><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
-                                                                             flag);
-                DGS_LAUNCH_CHECK(a.s, a.debug);
+            DGS_LAUNCH_CHECK(a.s, a.debug);
+            if constexpr (T && D == 2) {
+                if (has_thin) {  // the kThin entries, packed with the literal-order exponent (the thin pass)
+                    k_forward_s<FN, D, CB, true><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C,
+                                                                                 cbase, flag);
+                    DGS_LAUNCH_CHECK(a.s, a.debug);
+                }
             }
-        }
-        if constexpr (T || MX) {
-            if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
-                // (grid-strided over a capped grid: it exits at once when the device-side
-                // unsafe count is 0, which the host does not know without a sync)
-                const unsigned tb = hint.nunsafe > 0 ? blocks : std::min(blocks, 1024u);
-                k_forward<FN, D, CB, true><<<tb, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
-                                                                         a.samples, a.outs, a.C, cbase, flag);
-                DGS_LAUNCH_CHECK(a.s, a.debug);
+            if constexpr (T || MX) {
+                if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
+                    // (grid-strided over a capped grid: it exits at once when the device-side
+                    // unsafe count is 0, which the host does not know without a sync)
+                    const unsigned tb = hint.nunsafe > 0 ? blocks : std::min(blocks, 1024u);
+                    k_forward<FN, D, CB, true><<<tb, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.samples, a.outs, a.C,
+                                                                       cbase, flag);
+                    DGS_LAUNCH_CHECK(a.s, a.debug);
+                }
             }
         }
         // the call-time path (exits at once unless the inputs differ from the binned ones)
