@@ -668,6 +668,20 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const in
     if (lane == 0) box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
 }
 
+// DGS_FC_PROF builds (tuning only): per-phase wave-cycle sums of k_fine_count (s_memtime at
+// phase boundaries, lane 0 of each wave), read back with dgs_debug_fc_prof.
+#ifndef DGS_FC_PROF
+#define DGS_FC_PROF 0
+#endif
+#if DGS_FC_PROF
+__device__ unsigned long long g_fc_prof[8];
+#define FC_T(k) const uint64_t fc_t##k = __builtin_amdgcn_s_memtime()
+#define FC_ADD(a, b, slot) if ((threadIdx.x & 63) == 0) atomicAdd(&g_fc_prof[slot], (unsigned long long)(fc_t##b - fc_t##a))
+#else
+#define FC_T(k)
+#define FC_ADD(a, b, slot)
+#endif
+
 // Number of sort-path fine entries of each Gaussian (k_fine_fill writes them).  For the regular
 // (gather-path) Gaussians also their reach and local row ranges (k_gather reads them as
 // lrows[KR + dy][i]: coalesced over the contiguous id range of a home row), and the largest reach.
@@ -679,10 +693,13 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
                                                        float2 *__restrict__ igm, float4 *__restrict__ igc,
                                                        unsigned long long *__restrict__ nflag) {
     __shared__ uint32_t fbl[kFbWords];
+    FC_T(0);
     const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int reach = 0;
     uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
+    FC_T(1);
+    FC_ADD(0, 1, 0);
     if (i < P) {
         const int64_t g = perm[i];
         const float4 ga = grec[2 * g], gb2 = grec[2 * g + 1];  // (k_gauss_prep's record: one line)
@@ -692,13 +709,19 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
         // the one random gather of the Gaussians: internal-order copies for k_fine_fill / k_geo_pack
         igm[i] = make_float2(m[0], m[1]);
         igc[i] = make_float4(c[0], c[1], c[2], r);
+        FC_T(2);
+        FC_ADD(1, 2, 1);
         if (r > 0.0f) {
             const Cut k = gauss_cut(G, m, c);
             reach = gather_reach(G, m, r, c, k);
+            FC_T(3);
+            FC_ADD(2, 3, 2);
             if (reach > 0) {
                 const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) * G.ifs);
                 if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
             }
+            FC_T(4);
+            FC_ADD(3, 4, 3);
             const auto count = [&](uint32_t, uint32_t v) {
                 ++n;
                 nu += (v & kUnsafe) ? 1u : 0u;
@@ -706,10 +729,14 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
             };
             if (!(reach > 0 && fallback_only(G, m, r, sbeg, send, fbits, (uint32_t)i, count)))
                 enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, fbits, (uint32_t)i, count);
+            FC_T(5);
+            FC_ADD(4, 5, 4);
         }
         counts[i] = n;
         greach[i] = (int8_t)reach;
     }
+    FC_T(6);
+    FC_ADD(0, 6, 5);
     for (int off = kWave / 2; off > 0; off >>= 1) {
         reach = max(reach, __shfl_xor(reach, off));
         nu += __shfl_xor(nu, off);
@@ -1984,6 +2011,19 @@ int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t s
     return DGS_OK;
 }
 }  // namespace dgs
+
+// Tuning hook: k_fine_count's phase cycle sums of a DGS_FC_PROF build (reset after reading).
+extern "C" int dgs_debug_fc_prof(unsigned long long *out8) {
+#if DGS_FC_PROF
+    DGS_TRY_HIP(hipMemcpyFromSymbol(out8, HIP_SYMBOL(dgs::g_fc_prof), 64));
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    DGS_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dgs::g_fc_prof), z, 64));
+    return DGS_OK;
+#else
+    (void)out8;
+    return dgs::fail(DGS_ERR_ARG, "not a DGS_FC_PROF build");
+#endif
+}
 
 // Test hook (not on the reference API, not in include/): the binning's radix sort on its own,
 // key_bytes 2 or 4, stream-ordered scratch.  tests/test_gpu_radix.py checks it against a stable

@@ -474,6 +474,13 @@ std::tuple<Tensor, Tensor> RadixSortTest(const Tensor &keys_in, const Tensor &va
     return std::make_tuple(ko, vo);
 }
 
+extern "C" int dgs_debug_fc_prof(unsigned long long *out8);
+std::vector<int64_t> DebugFcProf() {
+    unsigned long long o[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    check(dgs_debug_fc_prof(o), "debug_fc_prof");
+    return std::vector<int64_t>(o, o + 8);
+}
+
 std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
     const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
     int64_t o[5] = {0, 0, 0, 0, 0};
@@ -876,6 +883,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("inputs_match", &InputsMatch);
     m.def("binning_info", &BinningInfo);
     m.def("radix_sort_test", &RadixSortTest);
+    m.def("debug_fc_prof", &DebugFcProf);
     m.def("volume_preprocess", &VolumePreprocess);
     m.def("volume_forward", &VolumeForward);
     m.def("volume_backward", &VolumeBackward);
