@@ -418,28 +418,30 @@ __device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float
 // order (sampler_impl.cu:94-124), restricted to non-empty cells that pass the exact cull.
 // skip_local: leave out the cells of the direct local tile visits (a regular Gaussian's:
 // k_gather makes them).
-// Per tile, whether its fallback cell holds samples, as bits in LDS (fbits; one block-wide pass:
-// enumerate_fine asks it for every tile a Gaussian visits).  NULL when the grid is too large.
-constexpr int kFbWords = 256;
-__device__ inline const uint32_t *fallback_bits(uint32_t *lds, const Geom &G, const int32_t *__restrict__ sbeg,
-                                                const int32_t *__restrict__ send) {
-    if (G.T > kFbWords * 32) return nullptr;
-    const int nw = (G.T + 31) >> 5;
-    for (int w = threadIdx.x; w < nw; w += blockDim.x) lds[w] = 0u;
-    __syncthreads();
-    for (int t = threadIdx.x; t < G.T; t += blockDim.x) {
-        const int64_t fb = (int64_t)t * G.CT + (G.CT - 1);
-        if (send[fb] > sbeg[fb]) atomicOr(&lds[t >> 5], 1u << (t & 31));
+// Per tile, whether its fallback cell holds samples: bits of fbg (set by k_sub_box /
+// k_cell_box, one word per 32 tiles).  The first 64 tiles' bits are preloaded into registers
+// (scalar loads, no LDS pass and no barrier: the usual grids have 4 x 4 tiles); later tiles
+// read fbg through the cache.
+struct FbBits {
+    uint64_t w;
+    const uint32_t *g;
+    __device__ __forceinline__ bool full(uint32_t key) const {
+        return key < 64u ? ((w >> key) & 1ull) != 0ull : ((g[key >> 5] >> (key & 31)) & 1u) != 0u;
     }
-    __syncthreads();
-    return lds;
+};
+__device__ __forceinline__ FbBits fb_load(const uint32_t *__restrict__ fbg, int T) {
+    FbBits b;
+    b.g = fbg;
+    const uint32_t lo = sload(&fbg[0]), hi = T > 32 ? sload(&fbg[1]) : 0u;
+    b.w = (uint64_t)lo | ((uint64_t)hi << 32);
+    return b;
 }
 
 template <class Emit>
 __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, float r, const float *con, const Cut &k,
                                       bool skip_local, const int32_t *__restrict__ sbeg,
                                       const int32_t *__restrict__ send,
-                                      const float4 *__restrict__ box, const uint32_t *fbits, uint32_t id,
+                                      const float4 *__restrict__ box, const FbBits &fbits, uint32_t id,
                                       Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
@@ -507,9 +509,7 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
                     }
                 }
             }
-            const uint32_t fb = base + (uint32_t)(G.CT - 1);
-            const bool fb_full = fbits ? ((fbits[key >> 5] >> (key & 31)) & 1u) != 0u : send[fb] > sbeg[fb];
-            if (fb_full) emit(fb, id | kUnsafe | kGeneral);  // whole tile: general path
+            if (fbits.full(key)) emit(base + (uint32_t)(G.CT - 1), id | kUnsafe | kGeneral);  // whole tile: general path
         }
 }
 
@@ -521,7 +521,7 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
 // why no tile of an inside rect has a shifted visit.
 template <class Emit>
 __device__ __forceinline__ bool fallback_only(const Geom &G, const float *m, float r, const int32_t *__restrict__ sbeg,
-                                              const int32_t *__restrict__ send, const uint32_t *fbits, uint32_t id,
+                                              const int32_t *__restrict__ send, const FbBits &fbits, uint32_t id,
                                               Emit emit) {
     const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
     if (kr.x0 < 0 || kr.y0 < 0 || kr.x1 > G.grid[0] || kr.y1 > G.grid[1]) return false;
@@ -529,8 +529,7 @@ __device__ __forceinline__ bool fallback_only(const Geom &G, const float *m, flo
         for (int x = kr.x0; x < kr.x1; ++x) {
             const uint32_t key = (uint32_t)(y * G.grid[0] + x);
             const uint32_t fb = key * (uint32_t)G.CT + (uint32_t)(G.CT - 1);
-            const bool full = fbits ? ((fbits[key >> 5] >> (key & 31)) & 1u) != 0u : send[fb] > sbeg[fb];
-            if (full) emit(fb, id | kUnsafe | kGeneral);
+            if (fbits.full(key)) emit(fb, id | kUnsafe | kGeneral);
         }
     return true;
 }
@@ -640,10 +639,19 @@ __device__ inline void load_gauss(int D, const float *__restrict__ means,
 
 // Bounding box of each cell's samples [min0 min1 max0 max1] (empty cells: unused).  One wave
 // per cell, lanes striding over the cell's samples in the packed sorted rows (k_fs_pack).
-__global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const int32_t *__restrict__ sbeg,
+// (Both box kernels also set the fallback-cell bits fbg: tile t's bit when its fallback cell,
+// cell t * CT + CT - 1, holds samples.)
+__device__ __forceinline__ void set_fb_bit(int c, int CT, bool nonempty, uint32_t *__restrict__ fbg) {
+    if (nonempty && c % CT == CT - 1) {
+        const int t = c / CT;
+        atomicOr(&fbg[t >> 5], 1u << (t & 31));
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, int CT, const int32_t *__restrict__ sbeg,
                                                      const int32_t *__restrict__ send,
                                                      const float *__restrict__ rows,
-                                                     float4 *__restrict__ box) {
+                                                     float4 *__restrict__ box, uint32_t *__restrict__ fbg) {
     const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
@@ -665,9 +673,32 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, const in
             hi[d] = fmaxf(hi[d], __shfl_xor(hi[d], off));
         }
     if (D == 1) { lo[1] = hi[1] = 0.0f; }
-    if (lane == 0) box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
+    if (lane == 0) {
+        box[c] = make_float4(lo[0], lo[1], hi[0], hi[1]);
+        set_fb_bit(c, CT, send[c] > sbeg[c], fbg);
+    }
 }
 
+// The Gaussians' records in internal order (k_gauss_prep's caller-order records gathered
+// through perm): igm = mean, igc = (conic, radius), read coalesced by k_fine_count / k_fine_fill
+// / k_geo_pack.  A kernel of its own: the random 32-byte gathers need many waves in flight
+// (in k_fine_count they were a dependent round trip at its 4 waves per SIMD).
+__global__ void k_gauss_permute(int P, const uint32_t *__restrict__ perm, const float4 *__restrict__ grec,
+                                float2 *__restrict__ igm, float4 *__restrict__ igc) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const int64_t g = perm[i];
+    const float4 ga = grec[2 * g], gb = grec[2 * g + 1];
+    igm[i] = make_float2(ga.x, ga.y);
+    igc[i] = make_float4(ga.w, gb.x, gb.y, ga.z);
+}
+
+// Number of sort-path fine entries of each Gaussian (k_fine_fill writes them).  For the regular
+// (gather-path) Gaussians also their reach and local row ranges (k_gather reads them as
+// lrows[KR + dy][i]: coalesced over the contiguous id range of a home row), and the largest
+// reach.  A regular Gaussian whose reference rect lies inside the grid counts its fallback
+// entries here; every other one (irr: the per-Gaussian enumeration, long and uneven loops) is
+// queued for k_fine_count_irr, so the waves here stay uniform.
 // DGS_FC_PROF builds (tuning only): per-phase wave-cycle sums of k_fine_count (s_memtime at
 // phase boundaries, lane 0 of each wave), read back with dgs_debug_fc_prof.
 #ifndef DGS_FC_PROF
@@ -682,33 +713,26 @@ __device__ unsigned long long g_fc_prof[8];
 #define FC_ADD(a, b, slot)
 #endif
 
-// Number of sort-path fine entries of each Gaussian (k_fine_fill writes them).  For the regular
-// (gather-path) Gaussians also their reach and local row ranges (k_gather reads them as
-// lrows[KR + dy][i]: coalesced over the contiguous id range of a home row), and the largest reach.
-__global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint32_t *__restrict__ perm,
-                                                       const float4 *__restrict__ grec, const int32_t *__restrict__ sbeg,
-                                                       const int32_t *__restrict__ send, const float4 *__restrict__ box,
+__global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const float2 *__restrict__ igm,
+                                                       const float4 *__restrict__ igc, const uint32_t *__restrict__ fbg,
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
-                                                       float2 *__restrict__ igm, float4 *__restrict__ igc,
+                                                       uint32_t *__restrict__ irr, uint32_t *__restrict__ nirr,
                                                        unsigned long long *__restrict__ nflag) {
-    __shared__ uint32_t fbl[kFbWords];
     FC_T(0);
-    const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
+    const FbBits fbits = fb_load(fbg, G.T);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int reach = 0;
-    uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
+    bool queue = false;
+    uint32_t nu = 0;  // kUnsafe entries (the regular Gaussians' fallback cells)
     FC_T(1);
     FC_ADD(0, 1, 0);
     if (i < P) {
-        const int64_t g = perm[i];
-        const float4 ga = grec[2 * g], gb2 = grec[2 * g + 1];  // (k_gauss_prep's record: one line)
-        const float r = ga.z;
+        const float2 mm = igm[i];
+        const float4 cc = igc[i];
+        const float r = cc.w;
         uint64_t n = 0;
-        const float m[2] = {ga.x, ga.y}, c[3] = {ga.w, gb2.x, gb2.y};
-        // the one random gather of the Gaussians: internal-order copies for k_fine_fill / k_geo_pack
-        igm[i] = make_float2(m[0], m[1]);
-        igc[i] = make_float4(c[0], c[1], c[2], r);
+        const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
         FC_T(2);
         FC_ADD(1, 2, 1);
         if (r > 0.0f) {
@@ -722,28 +746,68 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const uint
             }
             FC_T(4);
             FC_ADD(3, 4, 3);
-            const auto count = [&](uint32_t, uint32_t v) {
+            const auto count = [&](uint32_t, uint32_t v) {  // (fallback entries: kUnsafe)
                 ++n;
                 nu += (v & kUnsafe) ? 1u : 0u;
-                nt += (v & kThin) ? 1u : 0u;
             };
-            if (!(reach > 0 && fallback_only(G, m, r, sbeg, send, fbits, (uint32_t)i, count)))
-                enumerate_fine(G, m, r, c, k, reach > 0, sbeg, send, box, fbits, (uint32_t)i, count);
+            queue = !(reach > 0 && fallback_only(G, m, r, nullptr, nullptr, fbits, (uint32_t)i, count));
             FC_T(5);
             FC_ADD(4, 5, 4);
         }
         counts[i] = n;
         greach[i] = (int8_t)reach;
     }
-    FC_T(6);
-    FC_ADD(0, 6, 5);
+    // the wave's queued Gaussians take consecutive slots (one atomic per wave)
+    const uint64_t qm = __ballot(queue);
+    const int lane = threadIdx.x & (kWave - 1);
+    uint32_t qbase = 0;
+    if (qm) {
+        if (lane == 0) qbase = atomicAdd(nirr, (uint32_t)__popcll(qm));
+        qbase = __shfl(qbase, 0);
+        if (queue) irr[qbase + (uint32_t)__popcll(qm & ((1ull << lane) - 1ull))] = (uint32_t)i;
+    }
     for (int off = kWave / 2; off > 0; off >>= 1) {
         reach = max(reach, __shfl_xor(reach, off));
+        nu += __shfl_xor(nu, off);
+    }
+    if (lane == 0 && reach > 0) atomicMax(rmax, reach);
+    if (lane == 0 && nu) atomicAdd(&nflag[0], (unsigned long long)nu);
+    FC_T(6);
+    FC_ADD(0, 6, 5);
+}
+
+// The queued (irregular) Gaussians of k_fine_count: the per-Gaussian enumeration's count.
+// Grid-strided over the device-side queue length.
+__global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 *__restrict__ igm,
+                                                           const float4 *__restrict__ igc, const int32_t *__restrict__ sbeg,
+                                                           const int32_t *__restrict__ send, const float4 *__restrict__ box,
+                                                           const uint32_t *__restrict__ fbg, const int8_t *__restrict__ greach,
+                                                           const uint32_t *__restrict__ irr, const uint32_t *__restrict__ nirr,
+                                                           uint64_t *__restrict__ counts,
+                                                           unsigned long long *__restrict__ nflag) {
+    const FbBits fbits = fb_load(fbg, G.T);
+    const uint32_t nq = sload(nirr);
+    uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
+        const uint32_t i = irr[q];
+        const float2 mm = igm[i];
+        const float4 cc = igc[i];
+        const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
+        const Cut k = gauss_cut(G, m, c);
+        uint64_t n = 0;
+        const auto count = [&](uint32_t, uint32_t v) {
+            ++n;
+            nu += (v & kUnsafe) ? 1u : 0u;
+            nt += (v & kThin) ? 1u : 0u;
+        };
+        enumerate_fine(G, m, cc.w, c, k, greach[i] > 0, sbeg, send, box, fbits, i, count);
+        counts[i] = n;
+    }
+    for (int off = kWave / 2; off > 0; off >>= 1) {
         nu += __shfl_xor(nu, off);
         nt += __shfl_xor(nt, off);
     }
     if ((threadIdx.x & (kWave - 1)) == 0) {
-        if (reach > 0) atomicMax(rmax, reach);
         if (nu) atomicAdd(&nflag[0], (unsigned long long)nu);
         if (nt) atomicAdd(&nflag[1], (unsigned long long)nt);
     }
@@ -760,11 +824,10 @@ template <typename KT>
 __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     int P, Geom G, const float2 *__restrict__ igm, const float4 *__restrict__ igc, const int32_t *__restrict__ sbeg,
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
-    const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, KT *__restrict__ ekeys,
-    uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
+    const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, const uint32_t *__restrict__ fbg,
+    KT *__restrict__ ekeys, uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
-    __shared__ uint32_t fbl[kFbWords];
-    const uint32_t *fbits = fallback_bits(fbl, G, sbeg, send);
+    const FbBits fbits = fb_load(fbg, G.T);
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
     const int64_t i = i0 + threadIdx.x;
     const int64_t ilast = min((int64_t)P, i0 + kFillBlock) - 1;
@@ -915,10 +978,10 @@ __global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32
 
 // D = 2: the bounding boxes of a cell's four sub-cells and of the cell (their union), one wave
 // per cell.  Empty sub-cells get an empty box (+inf lo, -inf hi).
-__global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, const int32_t *__restrict__ ssbeg,
+__global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, int CT, const int32_t *__restrict__ ssbeg,
                                                     const int32_t *__restrict__ ssend,
                                                     const float *__restrict__ rows, float4 *__restrict__ sbox,
-                                                    float4 *__restrict__ box) {
+                                                    float4 *__restrict__ box, uint32_t *__restrict__ fbg) {
     const int c = blockIdx.x * (kBlock / kWave) + (threadIdx.x >> 6);
     const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
@@ -945,7 +1008,10 @@ __global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, const int32_t *_
         if (lane == 0) sbox[sc] = make_float4(lo[0], lo[1], hi[0], hi[1]);
         for (int d = 0; d < 2; ++d) { clo[d] = fminf(clo[d], lo[d]); chi[d] = fmaxf(chi[d], hi[d]); }
     }
-    if (lane == 0) box[c] = make_float4(clo[0], clo[1], chi[0], chi[1]);
+    if (lane == 0) {
+        box[c] = make_float4(clo[0], clo[1], chi[0], chi[1]);
+        set_fb_bit(c, CT, clo[0] <= chi[0], fbg);
+    }
 }
 
 #ifndef DGS_SUB_SLICE
@@ -1524,6 +1590,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *lrows = ca.take<uint32_t>((size_t)kGatherRows * P);
     uint32_t *hstart = ca.take<uint32_t>((size_t)HK + 1), *gcnt = ca.take<uint32_t>(ncells);
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
+    uint32_t *fbg = ca.take<uint32_t>((size_t)(G.T + 31) / 32 + 2);  // fallback-cell bits (+2: fb_load's words)
+    uint32_t *irr = ca.take<uint32_t>(P), *nirr = ca.take<uint32_t>(1);  // k_fine_count's queue
     unsigned long long *eg = ca.take<unsigned long long>(4);  // [gathered, kUnsafe, kThin entries, -]
     int32_t *rmax = ca.take<int32_t>(1);
     float2 *igm = ca.take<float2>(P);
@@ -1546,6 +1614,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(greach, base);
         Carve::rebase(lrows, base);
         Carve::rebase(cnt2, base);
+        Carve::rebase(fbg, base);
+        Carve::rebase(irr, base);
+        Carve::rebase(nirr, base);
         Carve::rebase(hstart, base);
         Carve::rebase(gcnt, base);
         Carve::rebase(eg, base);
@@ -1577,6 +1648,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(eg, 32);
         zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
         zl.add(rmax, 4);
+        zl.add(fbg, sizeof(uint32_t) * ((size_t)(G.T + 31) / 32 + 2));
+        zl.add(nirr, 4);
         zl.add(rs_s, plan_s.zero_bytes);
         zl.add(rs_h, plan_h.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
@@ -1599,10 +1672,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     DGS_LAUNCH_CHECK(s, debug);
     if (nsub)  // sub-cell boxes and the cell boxes (their union)
         k_sub_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
-            ncells, sub_sbeg, sub_send, fsrows, sub_box, cell_box);
+            ncells, G.CT, sub_sbeg, sub_send, fsrows, sub_box, cell_box, fbg);
     else
         k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
-            ncells, D, cell_sbeg, cell_send, fsrows, cell_box);
+            ncells, D, G.CT, cell_sbeg, cell_send, fsrows, cell_box, fbg);
     DGS_LAUNCH_CHECK(s, debug);
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
@@ -1611,8 +1684,12 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     DGS_LAUNCH_CHECK(s, debug);
     DGS_TRY_HIP(radix_sort<uint32_t>(plan_h, P, rs_h, home, home_sorted, gids, perm, s));
     DGS_LAUNCH_CHECK(s, debug);
-    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, perm, grec, cell_sbeg, cell_send, cell_box, fcount, greach,
-                                                lrows, rmax, igm, igc, eg + 1);
+    k_gauss_permute<<<grid_for(P), kBlock, 0, s>>>(P, perm, grec, igm, igc);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, igm, igc, fbg, fcount, greach, lrows, rmax, irr, nirr, eg + 1);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_fine_count_irr<<<std::min(grid_for(P), 2048u), kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg,
+                                                                     greach, irr, nirr, fcount, eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
                                                kWavesPerBlock - 1) / kWavesPerBlock);
@@ -1768,11 +1845,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
         if (k16)
             k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
-                                                            fcount, greach, reinterpret_cast<uint16_t *>(ekeys), evals,
-                                                            counters);
+                                                            fcount, greach, fbg, reinterpret_cast<uint16_t *>(ekeys),
+                                                            evals, counters);
         else
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
-                                                            fcount, greach, ekeys, evals, counters);
+                                                            fcount, greach, fbg, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),
                                                reinterpret_cast<uint16_t *>(ekeys_sorted), evals, svals, s)
