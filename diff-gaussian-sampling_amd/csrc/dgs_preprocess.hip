@@ -1042,13 +1042,21 @@ __device__ inline bool box_hits_ellipse_f(float xa, float xb, float ya, float yb
 // tested with the displacement the forward uses: X = m - s, minus the entry's constant wrap
 // shift for kGeneral entries (wrap_shift_f of the mean minus the cell-box centre, exactly as
 // k_forward_t forms it).  kUnsafe entries get none (the forward's tail pass adds them per cell).
-__device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 *__restrict__ gmean,
-                                             const float4 *__restrict__ gcon, const float4 &bx, const float *ctr,
-                                             const float4 *sb) {
+// (the entry's Gaussian, loaded a group ahead by k_sub_lists; zeros for kUnsafe entries)
+__device__ __forceinline__ void sub_row(uint32_t ent, const float2 *__restrict__ gmean, const float4 *__restrict__ gcon,
+                                        float2 &mm, float4 &cc) {
+    mm = make_float2(0.0f, 0.0f);
+    cc = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    if (!(ent & kUnsafe)) {
+        const uint32_t id = ent & kIdMask;
+        mm = gmean[id];
+        cc = gcon[id];
+    }
+}
+
+__device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 &mm, const float4 &cc, const float4 &bx,
+                                             const float *ctr, const float4 *sb) {
     if (ent & kUnsafe) return 0u;
-    const uint32_t id = ent & kIdMask;
-    const float2 mm = gmean[id];
-    const float4 cc = gcon[id];
     const float qc = (float)(kQCut * (1.0 + 1e-4));
     float sh[2] = {0.0f, 0.0f};
     if (ent & kGeneral) {
@@ -1105,8 +1113,9 @@ __device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 *__restr
 // sub-cells whose sample box its cut meets (sub_mask).  Sub list k of the cell has the region
 // [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
 // list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
-// entries and [lmid, lend) the flagged ones.  VALU-bound (the masks' slices); the next group's
-// entries and Gaussian rows are loaded while a group is tested.  (A block-per-cell form -- masks
+// entries and [lmid, lend) the flagged ones.  The next group's Gaussian rows and the one
+// after's entries are loaded while a group is tested (one stage: waves parked on the row
+// gathers half their cycles, PMC SQ_WAIT_ANY).  (A block-per-cell form -- masks
 // of the whole list in parallel into LDS, then one compacting wave per sub list -- was slower:
 // 235 against 182 us at the headline, the same math plus the LDS round trip.)
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
@@ -1131,12 +1140,22 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
         float4 sb[kSubPerCell];
 #pragma unroll
         for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
-        uint32_t ent_n = b + lane < e ? entries[b + lane] : kUnsafe;
+        // two-stage pipeline: group g + 1's Gaussians and group g + 2's entries are in flight
+        // while group g is tested
+        uint32_t ent_c = b + lane < e ? entries[b + lane] : kUnsafe;
+        uint32_t ent_n = b + kWave + lane < e ? entries[b + kWave + lane] : kUnsafe;
+        float2 mm_c;
+        float4 cc_c;
+        sub_row(ent_c, gmean, gcon, mm_c, cc_c);
         for (int j0 = b; j0 < e; j0 += kWave) {
             const int j = j0 + lane;
-            const uint32_t ent = ent_n;
-            ent_n = j + kWave < e ? entries[j + kWave] : kUnsafe;  // (next group's entry in flight)
-            const uint32_t mask = j < e ? sub_mask(ent, gmean, gcon, bx, ctr, sb) : 0u;
+            const uint32_t ent = ent_c;
+            const float2 mm = mm_c;
+            const float4 cc = cc_c;
+            ent_c = ent_n;
+            sub_row(ent_c, gmean, gcon, mm_c, cc_c);
+            ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
+            const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
             const bool ff = j < m_;
 #pragma unroll
             for (int k = 0; k < kSubPerCell; ++k) {
