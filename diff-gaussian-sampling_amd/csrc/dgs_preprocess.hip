@@ -70,6 +70,14 @@ bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, 
     return true;
 }
 
+// The binning's one host read-back target: 8 int64 of pinned host memory per host thread (the
+// calls of one thread are sequential; kept for the thread's lifetime).
+static int64_t *pinned_totals() {
+    static thread_local int64_t *p = nullptr;
+    if (!p && hipHostMalloc(reinterpret_cast<void **>(&p), 64, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    return p;
+}
+
 static int bit_length(uint64_t v) {
     int b = 0;
     while (v) { ++b; v >>= 1; }
@@ -144,15 +152,40 @@ static inline unsigned hist_grid(int64_t n) {
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kHistGrid));
 }
 
+// The digit histograms of a radix sort of the keys a producer kernel writes (dgs_radix.h's
+// k_rs_hist folded into the producer: one launch less per sort).  Per block in LDS, flushed once.
+struct RsHist {
+    uint32_t *g;  // global [places][256] (zero-filled), null: no histogram
+    int places;
+};
+static inline RsHist radix_hist(const RadixPlan &p, char *scratch) {  // (the plan's histograms)
+    return RsHist{p.places <= 4 ? reinterpret_cast<uint32_t *>(scratch) : nullptr, p.places};
+}
+__device__ __forceinline__ void rs_hist_zero(uint32_t *h, const RsHist &r) {
+    if (r.g)
+        for (int i = threadIdx.x; i < r.places * kRsBins; i += blockDim.x) h[i] = 0u;
+}
+__device__ __forceinline__ void rs_hist_add(uint32_t *h, const RsHist &r, uint32_t key) {
+    if (r.g)
+        for (int p = 0; p < r.places; ++p) atomicAdd(&h[p * kRsBins + rs_digit(key, p * kRsBits)], 1u);
+}
+__device__ __forceinline__ void rs_hist_flush(const uint32_t *h, const RsHist &r) {
+    if (r.g)
+        for (int i = threadIdx.x; i < r.places * kRsBins; i += blockDim.x)
+            if (h[i]) atomicAdd(&r.g[i], h[i]);
+}
+
 __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
                                uint32_t *__restrict__ keys, uint32_t *__restrict__ ids,
-                               uint32_t *__restrict__ tile_count) {
+                               uint32_t *__restrict__ tile_count, RsHist rh) {
     // grid-strided over a capped grid (kHistGrid blocks): the per-block LDS tile histogram is
     // flushed once, so the global same-address atomics on the few tile counters stay few
     __shared__ uint32_t hist[kHistBins];
+    __shared__ uint32_t dh[4 * kRsBins];
     const bool lds = G.T <= kHistBins;
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
+    rs_hist_zero(dh, rh);
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N;
          i += (int64_t)gridDim.x * blockDim.x) {
@@ -162,32 +195,47 @@ __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
             if (lds) atomicAdd(&hist[key], 1u);
             else atomicAdd(&tile_count[key], 1u);
         }
-        keys[i] = sample_cell_sub(G, s);  // (cell, sub-cell): cell ranges are keys >> 2
+        const uint32_t ck = sample_cell_sub(G, s);  // (cell, sub-cell): cell ranges are keys >> 2
+        keys[i] = ck;
         ids[i] = (uint32_t)i;
+        rs_hist_add(dh, rh, ck);
     }
     __syncthreads();
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x)
             if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
+    rs_hist_flush(dh, rh);
 }
 
 // identifyTileRanges (sampler_impl.cu:134-151) over sorted cell keys; keys >= limit ignored.
+// A second range set (beg2 non-null) over the same keys at another shift in the same launch
+// (the samples' cells and sub-cells).
 template <typename KT>
 __global__ void k_identify(int64_t L, const KT *__restrict__ keys, uint32_t limit,
-                           int32_t *__restrict__ beg, int32_t *__restrict__ end, int shift) {
+                           int32_t *__restrict__ beg, int32_t *__restrict__ end, int shift,
+                           uint32_t limit2 = 0, int32_t *__restrict__ beg2 = nullptr,
+                           int32_t *__restrict__ end2 = nullptr, int shift2 = 0) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L) return;
-    const uint32_t k = (uint32_t)keys[i] >> shift;
-    if (i == 0) {
-        if (k < limit) beg[k] = 0;
-    } else {
-        const uint32_t p = (uint32_t)keys[i - 1] >> shift;
-        if (k != p) {
-            if (p < limit) end[p] = (int32_t)i;
-            if (k < limit) beg[k] = (int32_t)i;
+    const uint32_t kr = (uint32_t)keys[i], pr = i > 0 ? (uint32_t)keys[i - 1] : 0u;
+#pragma unroll
+    for (int set = 0; set < 2; ++set) {
+        if (set == 1 && !beg2) break;
+        const int sh = set ? shift2 : shift;
+        const uint32_t lim = set ? limit2 : limit;
+        int32_t *b = set ? beg2 : beg, *e = set ? end2 : end;
+        const uint32_t k = kr >> sh;
+        if (i == 0) {
+            if (k < lim) b[k] = 0;
+        } else {
+            const uint32_t p = pr >> sh;
+            if (k != p) {
+                if (p < lim) e[p] = (int32_t)i;
+                if (k < lim) b[k] = (int32_t)i;
+            }
         }
+        if (i == L - 1 && k < lim) e[k] = (int32_t)L;
     }
-    if (i == L - 1 && k < limit) end[k] = (int32_t)L;
 }
 
 // ------------------------------------------------------------------- Gaussian binning
@@ -201,11 +249,13 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
                              uint64_t *__restrict__ touched, uint32_t *__restrict__ tile_count,
                              uint32_t *__restrict__ home, uint32_t *__restrict__ ids,
                              int home_w, int home_h, const uint8_t *__restrict__ present,
-                             float4 *__restrict__ grec) {
+                             float4 *__restrict__ grec, RsHist rh) {
     __shared__ uint32_t hist[kHistBins];  // grid-strided, capped grid: see k_sample_cells
+    __shared__ uint32_t dh[4 * kRsBins];  // (the home sort's digit counts)
     const bool lds = G.T <= kHistBins;
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x) hist[t] = 0;
+    rs_hist_zero(dh, rh);
     __syncthreads();
     const int D = G.D, S = D * (D + 1) / 2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < P;
@@ -229,6 +279,7 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         }
         if (!(r > 0.0f)) {
             home[i] = (uint32_t)home_w * (uint32_t)home_h;  // absent: after every home cell
+            rs_hist_add(dh, rh, (uint32_t)home_w * (uint32_t)home_h);
             continue;
         }
         const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
@@ -248,11 +299,13 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
             h[d] = v < 0 ? 0 : (v >= lim[d] ? lim[d] - 1 : v);
         }
         home[i] = (uint32_t)(h[1] * home_w + h[0]);
+        rs_hist_add(dh, rh, (uint32_t)(h[1] * home_w + h[0]));
     }
     __syncthreads();
     if (lds)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x)
             if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
+    rs_hist_flush(dh, rh);
 }
 
 // Does [xa, xb] x [ya, yb] contain an X with X^T A X <= qcut?  (convex quadratic: the
@@ -395,14 +448,14 @@ __device__ __forceinline__ bool visit_local(const Geom &G, const Cut &k, const i
 // entries are produced per cell by k_gather (no sort); everything else goes through the
 // per-Gaussian enumeration and the entry sort.  Returns the reach in cells, 0 if not regular.
 constexpr int kGatherReach = 6, kGatherRows = 2 * kGatherReach + 1;
-__device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k) {
+__device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k,
+                                            const KeyRect &kr) {
     if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2]) ||
         conic_thin(2, con[0], con[1], con[2]))
         return 0;
     if (!(k.e[0] + 3.0 * G.fs < 0.9 && k.e[1] + 3.0 * G.fs < 0.9)) return 0;
     // every tile visited at most once (a rect wider than the grid visits a tile repeatedly,
-    // which the enumeration reproduces entry by entry)
-    const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
+    // which the enumeration reproduces entry by entry); kr = ref_key_rect(2, m, r, ...)
     if (kr.x1 - kr.x0 > G.grid[0] || kr.y1 - kr.y0 > G.grid[1]) return 0;
     const int lim[2] = {G.grid[0] * G.n, G.grid[1] * G.n};
     int reach = 0;
@@ -520,10 +573,8 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
 // reaches no torus image of a tile within its rect (e < 0.5 while an image is 2 away), which is
 // why no tile of an inside rect has a shifted visit.
 template <class Emit>
-__device__ __forceinline__ bool fallback_only(const Geom &G, const float *m, float r, const int32_t *__restrict__ sbeg,
-                                              const int32_t *__restrict__ send, const FbBits &fbits, uint32_t id,
+__device__ __forceinline__ bool fallback_only(const Geom &G, const KeyRect &kr, const FbBits &fbits, uint32_t id,
                                               Emit emit) {
-    const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
     if (kr.x0 < 0 || kr.y0 < 0 || kr.x1 > G.grid[0] || kr.y1 > G.grid[1]) return false;
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
@@ -546,18 +597,18 @@ __device__ inline uint32_t cell_of(const Geom &G, int gx, int gy) {
 // order, each row's tiles in turn, so a row's range is merged in registers and stored once.
 // False if some row's cells are not one range (never for a convex cut; the Gaussian then stays
 // on the sort path).
-__device__ __forceinline__ bool local_rows(const Geom &G, const float *m, float r, const Cut &k, int home_y, int reach,
+__device__ __forceinline__ bool local_rows(const Geom &G, const KeyRect &kr, const Cut &k, int home_y, int reach,
                                   int64_t P, int64_t i, uint32_t *__restrict__ lrows) {
     // Per Gaussian: the x tiles its cut can reach as a direct local visit (at most two: the cut is
     // narrower than a tile) with their cell ranges, and the slice constants.  These need not
     // match enumerate_fine bit for bit (it skips exactly these visits and emits all others); the
     // margins of the cut cover the rounding either way.
-    const KeyRect kr = ref_key_rect(2, m, r, G.grid, G.off);
     const double BS = (double)kTile, slack = kCellSlack * G.fs;
-    // (widened by a cell: every tile axis_setup can give a cell is among them)
-    const double wx = k.e[0] + slack + k.epsx[0] + G.fs;
-    const int ta = max(max(kr.x0, 0), (int)floor((k.md[0] - wx) / BS));
-    const int tb = min(min(kr.x1, G.grid[0]) - 1, (int)floor((k.md[0] + wx) / BS));
+    // (widened by a cell: every tile axis_setup can give a cell is among them -- which also
+    // covers the rounding of the reciprocal multiply)
+    const double wx = k.e[0] + slack + k.epsx[0] + G.fs, iBS = 1.0 / BS;
+    const int ta = max(max(kr.x0, 0), (int)floor((k.md[0] - wx) * iBS));
+    const int tb = min(min(kr.x1, G.grid[0]) - 1, (int)floor((k.md[0] + wx) * iBS));
     int xlo[2] = {1, 1}, xhi[2] = {0, 0};  // cell ranges of tiles ta, ta + 1 (empty: lo > hi)
     for (int t = 0; t < 2; ++t) {
         const int tx = ta + t;
@@ -575,7 +626,9 @@ __device__ __forceinline__ bool local_rows(const Geom &G, const float *m, float 
     const float qc = (float)(kQCut * (1.0 + 1e-6));
     const float c0 = (float)k.c0, c1 = (float)k.c1, c2 = (float)k.c2;
     const float det = (float)(k.c0 * k.c2 - k.c1 * k.c1);
-    const float e0 = (float)sqrt((double)qc * k.c2 / (k.c0 * k.c2 - k.c1 * k.c1)), ic0 = 1.0f / c0;
+    // (e0: the cut's X0 half-width; k.e[0] exceeds sqrt(qc c2 / det) by ~5e-7 relative, which
+    // only widens the slices)
+    const float e0 = (float)k.e[0], ic0 = 1.0f / c0;
     const float yu0 = -c1 * e0 / c2, yl0 = c1 * e0 / c2, qcc0 = qc * c0;
     const float fs = (float)G.fs, ifsf = (float)G.ifs, slackf = (float)slack;
     const float e1 = (float)k.e[1], eps1 = (float)k.epsx[1] + 1e-6f, eps0 = (float)k.epsx[0] + 1e-6f;
@@ -598,8 +651,9 @@ __device__ __forceinline__ bool local_rows(const Geom &G, const float *m, float 
             yb = fminf(yb, e1);
             if (ya > yb) continue;
             const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(yl0, ya), yb);
-            const float xu = (-c1 * yu + sqrtf(fmaxf(qcc0 - det * yu * yu, 0.0f))) * ic0;
-            const float xl = (-c1 * yl - sqrtf(fmaxf(qcc0 - det * yl * yl, 0.0f))) * ic0;
+            // (v_sqrt_f32, ~1 ulp: far inside tol)
+            const float xu = (-c1 * yu + __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yu * yu, 0.0f))) * ic0;
+            const float xl = (-c1 * yl - __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yl * yl, 0.0f))) * ic0;
             const float tol = tol0 + 1e-5f * (fabsf(xu) + fabsf(xl));
             int lo = 0xffff, hi = 0;
             for (int t = 0; t < 2; ++t) {
@@ -737,12 +791,13 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
         FC_ADD(1, 2, 1);
         if (r > 0.0f) {
             const Cut k = gauss_cut(G, m, c);
-            reach = gather_reach(G, m, r, c, k);
+            const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
+            reach = gather_reach(G, m, r, c, k, kr);
             FC_T(3);
             FC_ADD(2, 3, 2);
             if (reach > 0) {
                 const int home_y = (int)floor(((double)m[1] - (double)G.off[1]) * G.ifs);
-                if (!local_rows(G, m, r, k, home_y, reach, P, i, lrows)) reach = 0;
+                if (!local_rows(G, kr, k, home_y, reach, P, i, lrows)) reach = 0;
             }
             FC_T(4);
             FC_ADD(3, 4, 3);
@@ -750,7 +805,7 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
                 ++n;
                 nu += (v & kUnsafe) ? 1u : 0u;
             };
-            queue = !(reach > 0 && fallback_only(G, m, r, nullptr, nullptr, fbits, (uint32_t)i, count));
+            queue = !(reach > 0 && fallback_only(G, kr, fbits, (uint32_t)i, count));
             FC_T(5);
             FC_ADD(4, 5, 4);
         }
@@ -854,7 +909,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
             nunsafe += (val & kUnsafe) ? 1u : 0u;
             ++o;
         };
-        if (!(skip && fallback_only(G, m, r, sbeg, send, fbits, (uint32_t)i, put)))
+        if (!(skip && fallback_only(G, ref_key_rect(2, m, r, G.grid, G.off), fbits, (uint32_t)i, put)))
             enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, fbits, (uint32_t)i, put);
     }
     if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
@@ -1216,11 +1271,11 @@ __global__ void k_ref_keys(int P, Geom G, const float2 *__restrict__ gmean, cons
 // Reference-layout ranges (identifyTileRanges semantics: empty tiles stay (0, 0)) for the
 // Gaussian and the sample lists, and the call-time path's per-tile tables (RefTab): list
 // starts and unit prefix counts.  One block; each thread scans a contiguous run of tiles.
-__global__ __launch_bounds__(1024) void k_ref_tables(int T, const uint32_t *__restrict__ gcnt,
-                                                     const uint32_t *__restrict__ scnt,
-                                                     uint2 *__restrict__ granges, uint2 *__restrict__ sranges,
-                                                     uint32_t *__restrict__ rtab) {
-    __shared__ uint4 part[1024];
+__device__ __forceinline__ void ref_tables_block(int T, const uint32_t *__restrict__ gcnt,
+                                                 const uint32_t *__restrict__ scnt,
+                                                 uint2 *__restrict__ granges, uint2 *__restrict__ sranges,
+                                                 uint32_t *__restrict__ rtab) {
+    __shared__ uint4 part[kBlock];
     const int nt = blockDim.x, t = threadIdx.x;
     const int per = (T + nt - 1) / nt, a = min(T, t * per), b = min(T, a + per);
     uint4 sum = make_uint4(0u, 0u, 0u, 0u);
@@ -1266,7 +1321,26 @@ struct CopySpec {
     int count;
 };
 
-__global__ void k_copy_multi(CopySpec c) {
+// The binning's last launch: block 0 the reference-layout ranges and the call-time tables
+// (ref_tables_block), the last block the headers of both buffers, every block its share of the
+// binned-tensor copies (three launches before).
+struct TailSpec {
+    int T;
+    const uint32_t *gcnt, *scnt;
+    uint2 *granges, *sranges;
+    uint32_t *rtab;
+    char *gbuf, *sbuf;
+};
+
+__global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts, Header h) {
+    if (blockIdx.x == 0) ref_tables_block(ts.T, ts.gcnt, ts.scnt, ts.granges, ts.sranges, ts.rtab);
+    if (blockIdx.x == gridDim.x - 1) {
+        const char *src = reinterpret_cast<const char *>(&h);
+        for (int i = threadIdx.x; i < (int)sizeof(Header); i += blockDim.x) {
+            ts.gbuf[i] = src[i];
+            ts.sbuf[i] = src[i];
+        }
+    }
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
     for (int r = 0; r < c.count; ++r) {
         int64_t done = 0;
@@ -1278,15 +1352,6 @@ __global__ void k_copy_multi(CopySpec c) {
             done = n4 << 2;
         }
         for (int64_t i = done + t; i < c.n[r]; i += st) c.dst[r][i] = c.src[r][i];
-    }
-}
-
-__global__ void k_write_header(Header h, char *gbuf, char *sbuf) {
-    const int i = threadIdx.x;
-    const char *src = reinterpret_cast<const char *>(&h);
-    if (i < (int)sizeof(Header)) {
-        gbuf[i] = src[i];
-        sbuf[i] = src[i];
     }
 }
 
@@ -1676,17 +1741,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     }
 
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
-    k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile);
+    k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile, radix_hist(plan_s, rs_s));
     DGS_LAUNCH_CHECK(s, debug);
     DGS_TRY_HIP(radix_sort<uint32_t>(plan_s, N, rs_s, skeys, skeys_sorted, sids, reinterpret_cast<uint32_t *>(sorted_sid),
-                                     s));
+                                     s, true));
     DGS_LAUNCH_CHECK(s, debug);
-    k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 2);
+    k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 2,
+                                                        (uint32_t)nsub, nsub ? sub_sbeg : nullptr, sub_send, 0);
     DGS_LAUNCH_CHECK(s, debug);
-    if (nsub) {
-        k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)nsub, sub_sbeg, sub_send, 0);
-        DGS_LAUNCH_CHECK(s, debug);
-    }
     k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
     DGS_LAUNCH_CHECK(s, debug);
     if (nsub)  // sub-cell boxes and the cell boxes (their union)
@@ -1699,9 +1761,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
     k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, conics, radii, touched, gtile,
-                                                home, gids, home_w, home_h, present, grec);
+                                                home, gids, home_w, home_h, present, grec, radix_hist(plan_h, rs_h));
     DGS_LAUNCH_CHECK(s, debug);
-    DGS_TRY_HIP(radix_sort<uint32_t>(plan_h, P, rs_h, home, home_sorted, gids, perm, s));
+    DGS_TRY_HIP(radix_sort<uint32_t>(plan_h, P, rs_h, home, home_sorted, gids, perm, s, true));
     DGS_LAUNCH_CHECK(s, debug);
     k_gauss_permute<<<grid_for(P), kBlock, 0, s>>>(P, perm, grec, igm, igc);
     DGS_LAUNCH_CHECK(s, debug);
@@ -1807,8 +1869,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
-    int64_t htot[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    DGS_TRY_HIP(hipMemcpyAsync(htot, totals, sizeof(htot), hipMemcpyDeviceToHost, s));
+    // (into pinned host memory: a copy to pageable memory is staged by the runtime, which held
+    // the stream ~28 us past the copy before the speculative phase-B work below could start)
+    int64_t *htot = pinned_totals();
+    if (!htot) return fail(DGS_ERR_ALLOC, "pinned host buffer allocation failed");
+    DGS_TRY_HIP(hipMemcpyAsync(htot, totals, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     // the one host sync (num_rendered is a Python int): on an event right after the copy, so the
     // speculative phase B enqueued behind it keeps the GPU busy while the host reads the totals
     hipEvent_t copied = nullptr;
@@ -1972,13 +2037,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // ---- reference-layout ranges (uint2 per tile + 8 slack bytes, zero-filled) and the
     // call-time path's tables: per-tile list starts and unit counts (its tile lists -- the
     // reference's point_list -- are sorted at the first call that may need them: ensure_ref_lists)
-    k_ref_tables<<<1, 1024, 0, s>>>(G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf),
-                                    reinterpret_cast<uint2 *>(srbuf),
-                                    reinterpret_cast<uint32_t *>(gbuf + L.o_rtab));
-    DGS_LAUNCH_CHECK(s, debug);
+    // (launched with the copies and the headers below: k_binning_tail)
+    CopySpec c{};
     {  // the binned tensors as passed (each forward / backward compares its inputs with them)
         const int S3 = D * (D + 1) / 2;
-        CopySpec c{};
         c.src[0] = reinterpret_cast<const uint32_t *>(means); c.dst[0] = reinterpret_cast<uint32_t *>(gbuf + L.o_mcopy);
         c.n[0] = (int64_t)P * D;
         c.src[1] = reinterpret_cast<const uint32_t *>(conics); c.dst[1] = reinterpret_cast<uint32_t *>(gbuf + L.o_ccopy);
@@ -1986,8 +2048,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         c.src[2] = reinterpret_cast<const uint32_t *>(samples); c.dst[2] = reinterpret_cast<uint32_t *>(sbuf + L0.o_scopy);
         c.n[2] = (int64_t)N * D;
         c.count = 3;
-        k_copy_multi<<<1024, kBlock, 0, s>>>(c);
-        DGS_LAUNCH_CHECK(s, debug);
     }
 
     // ---- headers
@@ -2016,7 +2076,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_sub_lbeg = L.o_sub_lbeg; h.o_sub_lmid = L.o_sub_lmid; h.o_sub_lend = L.o_sub_lend; h.o_sub_ent = L.o_sub_ent;
     h.fsub_cap = fsub_cap_of(D, N, ncells); h.esub_cap = esub_cap_of(D, E);
     h.stamp = ++stamp_counter;
-    k_write_header<<<1, kHeaderBytes, 0, s>>>(h, gbuf, sbuf);
+    const TailSpec ts{G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf), reinterpret_cast<uint2 *>(srbuf),
+                      reinterpret_cast<uint32_t *>(gbuf + L.o_rtab), gbuf, sbuf};
+    k_binning_tail<<<1024, kBlock, 0, s>>>(c, ts, h);
     DGS_LAUNCH_CHECK(s, debug);
 
     // launch-size hint: the unit capacities (the exact counts stay on the device and the render
@@ -2220,9 +2282,10 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // sample_points.cu:70-74 on the device (torch's CUDA arithmetic, k_bounds_final)
     const int nparts = (int)std::min<int64_t>(1024, grid_for(N));
-    float *part = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, align_up(sizeof(float) * 4 * nparts, 256)));
-    char *gb = static_cast<char *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, 256));
-    if (!part || !gb) return fail(DGS_ERR_ALLOC, "scratch allocation failed");
+    const size_t pbytes = align_up(sizeof(float) * 4 * nparts, 256);
+    float *part = static_cast<float *>(alloc(alloc_ctx, DGS_BUF_SCRATCH, pbytes + 256));
+    if (!part) return fail(DGS_ERR_ALLOC, "scratch allocation failed");
+    char *gb = reinterpret_cast<char *>(part) + pbytes;
     int *dgrid = reinterpret_cast<int *>(gb);
     float *doff = reinterpret_cast<float *>(gb + 16);
     k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, part);

@@ -203,9 +203,11 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
 // The sort of n <= p.n items: keys kin (KT) / values vin -> kout / vout, stable, over the key
 // bits the plan was made for.  scratch: p.bytes, its first p.zero_bytes zero-filled beforehand
 // (once: a plan's scratch serves one sort).  The look-back's give-up word is tickets[63].
+// hist_ready: the keys' producer has already added their digit counts into the plan's
+// histograms (radix_hist; dgs_preprocess.hip's RsHist), so the histogram launch is skipped.
 template <typename KT>
 static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const KT *kin, KT *kout,
-                             const uint32_t *vin, uint32_t *vout, hipStream_t s) {
+                             const uint32_t *vin, uint32_t *vout, hipStream_t s, bool hist_ready = false) {
     if (n <= 0) return hipSuccess;
     if (n > p.n) return hipErrorInvalidValue;
     uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
@@ -216,7 +218,7 @@ static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const
     KT *tk = reinterpret_cast<KT *>(scratch + p.o_tkeys);
     uint32_t *tv = reinterpret_cast<uint32_t *>(scratch + p.o_tvals);
     const unsigned hb = (unsigned)(tiles < 1024 ? tiles : 1024);
-    k_rs_hist<KT><<<hb, kRsThreads, 0, s>>>(n, kin, p.places, hist);
+    if (!hist_ready) k_rs_hist<KT><<<hb, kRsThreads, 0, s>>>(n, kin, p.places, hist);
     const KT *ki = kin;
     const uint32_t *vi = vin;
     for (int q = 0; q < p.places; ++q) {

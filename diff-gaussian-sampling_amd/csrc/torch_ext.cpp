@@ -167,7 +167,8 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     (void)values_in;
     const int P = (int)means.size(0), D = (int)means.size(-1), N = (int)samples.size(0);
-    Tensor radii = torch::full({P}, 0, means.options());
+    // (k_gauss_prep writes every radius when there is anything to bin; zeros otherwise)
+    Tensor radii = P != 0 && N != 0 ? torch::empty({P}, means.options()) : torch::full({P}, 0, means.options());
     AllocCtx ctx{means.device()};
     for (int i = 0; i < 4; ++i) ctx.bufs[i] = empty_u8(means.device());
     int64_t rendered = 0;

@@ -1,10 +1,13 @@
 """k_fine_count phase breakdown from a DGS_FC_PROF build (tuning only):
-DGS_EXTRA_CFLAGS=-DDGS_FC_PROF=1 python diff-gaussian-sampling_amd/build.py, then run this on a GPU."""
+tools/variant.sh fcprof -DDGS_FC_PROF=1, then on a GPU: python tools/fc_prof.py [ANISO] (it loads
+variants/fcprof)."""
 import json
 import os
 import sys
 
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "diff-gaussian-sampling_amd"))
+_root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, os.path.join(_root, "diff-gaussian-sampling_amd"))
+sys.path.insert(0, os.path.join(_root, "variants", os.environ.get("DGS_VARIANT", "fcprof")))
 import torch  # noqa: E402
 
 import diff_gaussian_sampling as dgs  # noqa: E402
@@ -24,5 +27,5 @@ for _ in range(reps):
 torch.cuda.synchronize()
 v = dgs._C.debug_fc_prof()
 waves = reps * ((P + 63) // 64)
-names = ["fallback_bits", "loads+copies", "cut+reach", "local_rows", "fallback/enumerate", "whole"]
-print(json.dumps({"aniso": aniso, "cycles_per_wave": {n: round(v[k] / waves) for k, n in enumerate(names)}}))
+names = ["fallback_bits", "loads", "cut+reach", "local_rows", "fallback_only+queue", "whole"]
+print(json.dumps({"lib": dgs._C.__file__, "aniso": aniso, "cycles_per_wave": {n: round(v[k] / waves) for k, n in enumerate(names)}}))
