@@ -239,6 +239,25 @@ __global__ void k_identify(int64_t L, const KT *__restrict__ keys, uint32_t limi
 }
 
 // ------------------------------------------------------------------- Gaussian binning
+// A Gaussian's reference rect (ref_key_rect) as four int16 in two words, computed once by
+// k_gauss_prep; a rect that does not fit int16 is stored as kRectNone and recomputed.
+constexpr uint32_t kRectNone = 0x80008000u;
+__device__ __forceinline__ uint2 rect_pack(const KeyRect &k) {
+    const bool fits = k.x0 > -32768 && k.x0 < 32768 && k.x1 > -32768 && k.x1 < 32768 && k.y0 > -32768 &&
+                      k.y0 < 32768 && k.y1 > -32768 && k.y1 < 32768;
+    if (!fits) return make_uint2(kRectNone, kRectNone);
+    return make_uint2(((uint32_t)k.x0 & 0xffffu) | ((uint32_t)k.x1 << 16), ((uint32_t)k.y0 & 0xffffu) | ((uint32_t)k.y1 << 16));
+}
+__device__ __forceinline__ KeyRect rect_get(uint2 p, int D, const float *m, float r, const Geom &G) {
+    if (p.x == kRectNone) return ref_key_rect(D, m, r, G.grid, G.off);
+    KeyRect k;
+    k.x0 = (int)(int16_t)(p.x & 0xffffu);
+    k.x1 = (int)(int16_t)(p.x >> 16);
+    k.y0 = (int)(int16_t)(p.y & 0xffffu);
+    k.y1 = (int)(int16_t)(p.y >> 16);
+    return k;
+}
+
 // forward.cu:24-83 (radius, tiles touched) + the reference tile counts + spatial home key.
 // Also packs each Gaussian's mean, radius and conic into one 32-byte record (caller order,
 // coalesced): k_fine_count then gathers one record per Gaussian in internal order instead of
@@ -271,18 +290,19 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         radii[i] = r;
         touched[i] = t;
         ids[i] = (uint32_t)i;
+        const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
         {
             const float c0 = conics[i * S], c1 = D == 2 ? conics[i * S + 1] : 0.0f;
             const float c2 = D == 2 ? conics[i * S + 2] : 0.0f;
+            const uint2 pk = rect_pack(kr);  // (k_fine_count / k_fine_fill reuse the rect)
             grec[2 * i] = make_float4(m[0], m[1], r, c0);
-            grec[2 * i + 1] = make_float4(c1, c2, 0.0f, 0.0f);
+            grec[2 * i + 1] = make_float4(c1, c2, __uint_as_float(pk.x), __uint_as_float(pk.y));
         }
         if (!(r > 0.0f)) {
             home[i] = (uint32_t)home_w * (uint32_t)home_h;  // absent: after every home cell
             rs_hist_add(dh, rh, (uint32_t)home_w * (uint32_t)home_h);
             continue;
         }
-        const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
         for (int y = kr.y0; y < kr.y1; ++y)
             for (int x = kr.x0; x < kr.x1; ++x) {
                 const uint32_t key = key_of(D, x, y, G.grid);
@@ -640,44 +660,55 @@ __device__ __forceinline__ bool local_rows(const Geom &G, const KeyRect &kr, con
         B0[t] = md0 + slackf + eps0;
     }
     uint32_t written = 0u;  // bit KR + dy: row home_y + dy stored
+    bool bad = false;       // (some row's cells are not one range, or a row is out of reach)
+    const bool v0t = xlo[0] <= xhi[0], v1t = xlo[1] <= xhi[1];
+    const float fn = (float)G.n;
     for (int ty = max(kr.y0, 0); ty < min(kr.y1, G.grid[1]); ++ty) {  // direct visits only
         int ks1, flo1, fhi1;
         if (!axis_setup(G, k, 1, ty, ks1, flo1, fhi1) || ks1 != 0) continue;
         const float md1 = (float)(k.md[1] - ty * BS);
+        // (the row body without branches: its divergent continues / breaks were a third of
+        // this kernel's instructions; partial stores of a Gaussian that ends up `bad` are never
+        // read -- k_gather reads rows only of Gaussians with a reach)
         for (int fy = flo1; fy <= fhi1; ++fy) {
-            float ya = md1 - ((fy + 1) * fs + slackf) - eps1;
-            float yb = md1 - (fy * fs - slackf) + eps1;
-            ya = fmaxf(ya, -e1);
-            yb = fminf(yb, e1);
-            if (ya > yb) continue;
+            const float ya = fmaxf(md1 - ((fy + 1) * fs + slackf) - eps1, -e1);
+            const float yb = fminf(md1 - (fy * fs - slackf) + eps1, e1);
+            const bool rowok = ya <= yb;
             const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(yl0, ya), yb);
             // (v_sqrt_f32, ~1 ulp: far inside tol)
             const float xu = (-c1 * yu + __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yu * yu, 0.0f))) * ic0;
             const float xl = (-c1 * yl - __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yl * yl, 0.0f))) * ic0;
             const float tol = tol0 + 1e-5f * (fabsf(xu) + fabsf(xl));
-            int lo = 0xffff, hi = 0;
+            int a[2], b[2];
+            bool v[2];
+#pragma unroll
             for (int t = 0; t < 2; ++t) {
-                if (xlo[t] > xhi[t]) continue;
-                const int tx = ta + t;
                 const float fa = ceilf((A0[t] - (xu + tol)) * ifsf - 1.0f - 1e-4f);
                 const float fb = floorf((B0[t] - (xl - tol)) * ifsf + 1e-4f);
-                const int fxl = fa > (float)xlo[t] ? (fa > (float)G.n ? G.n : (int)fa) : xlo[t];
-                const int fxh = fb < (float)xhi[t] ? (fb < -1.0f ? -1 : (int)fb) : xhi[t];
-                if (fxl > fxh) continue;
-                const int a = tx * G.n + fxl, b = tx * G.n + fxh;
-                if (lo > hi) { lo = a; hi = b; }
-                else if (a == hi + 1) hi = b;
-                else return false;
+                const int fxl = max(xlo[t], (int)fminf(fmaxf(fa, -1.0f), fn));
+                const int fxh = min(xhi[t], (int)fmaxf(fminf(fb, fn), -1.0f));
+                v[t] = (t == 0 ? v0t : v1t) && fxl <= fxh;
+                a[t] = (ta + t) * G.n + fxl;
+                b[t] = (ta + t) * G.n + fxh;
             }
-            if (lo > hi) continue;
+            const int lo = v[0] ? a[0] : a[1], hi = v[1] ? b[1] : b[0];
+            bad = bad || (rowok && v[0] && v[1] && a[1] != b[0] + 1);
             const int dy = ty * G.n + fy - home_y;
-            if (dy < -reach || dy > reach) return false;
-            lrows[(int64_t)(kGatherReach + dy) * P + i] = (uint32_t)lo | ((uint32_t)hi << 16);
-            written |= 1u << (kGatherReach + dy);
+            const bool put = rowok && (v[0] || v[1]);
+            const bool inr = dy >= -reach && dy <= reach;
+            bad = bad || (put && !inr);
+            if (put && inr) {
+                lrows[(int64_t)(kGatherReach + dy) * P + i] = (uint32_t)lo | ((uint32_t)hi << 16);
+                written |= 1u << (kGatherReach + dy);
+            }
         }
     }
-    for (int q = kGatherReach - reach; q <= kGatherReach + reach; ++q)
-        if (!((written >> q) & 1u)) lrows[(int64_t)q * P + i] = 0x0000ffffu;
+    if (bad) return false;
+    uint32_t *rp = lrows + i;
+#pragma unroll
+    for (int q = 0; q < kGatherRows; ++q)
+        if (q >= kGatherReach - reach && q <= kGatherReach + reach && !((written >> q) & 1u))
+            rp[(int64_t)q * P] = 0x0000ffffu;
     return true;
 }
 
@@ -738,13 +769,14 @@ __global__ __launch_bounds__(kBlock) void k_cell_box(int ncells, int D, int CT, 
 // / k_geo_pack.  A kernel of its own: the random 32-byte gathers need many waves in flight
 // (in k_fine_count they were a dependent round trip at its 4 waves per SIMD).
 __global__ void k_gauss_permute(int P, const uint32_t *__restrict__ perm, const float4 *__restrict__ grec,
-                                float2 *__restrict__ igm, float4 *__restrict__ igc) {
+                                float2 *__restrict__ igm, float4 *__restrict__ igc, uint2 *__restrict__ irect) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
     const float4 ga = grec[2 * g], gb = grec[2 * g + 1];
     igm[i] = make_float2(ga.x, ga.y);
     igc[i] = make_float4(ga.w, gb.x, gb.y, ga.z);
+    irect[i] = make_uint2(__float_as_uint(gb.z), __float_as_uint(gb.w));
 }
 
 // Number of sort-path fine entries of each Gaussian (k_fine_fill writes them).  For the regular
@@ -768,7 +800,8 @@ __device__ unsigned long long g_fc_prof[8];
 #endif
 
 __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const float2 *__restrict__ igm,
-                                                       const float4 *__restrict__ igc, const uint32_t *__restrict__ fbg,
+                                                       const float4 *__restrict__ igc, const uint2 *__restrict__ irect,
+                                                       const uint32_t *__restrict__ fbg,
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
                                                        uint32_t *__restrict__ irr, uint32_t *__restrict__ nirr,
@@ -791,7 +824,7 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
         FC_ADD(1, 2, 1);
         if (r > 0.0f) {
             const Cut k = gauss_cut(G, m, c);
-            const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
+            const KeyRect kr = rect_get(irect[i], G.D, m, r, G);
             reach = gather_reach(G, m, r, c, k, kr);
             FC_T(3);
             FC_ADD(2, 3, 2);
@@ -880,7 +913,8 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     int P, Geom G, const float2 *__restrict__ igm, const float4 *__restrict__ igc, const int32_t *__restrict__ sbeg,
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, const uint32_t *__restrict__ fbg,
-    KT *__restrict__ ekeys, uint32_t *__restrict__ evals, int32_t *__restrict__ counters) {
+    const uint2 *__restrict__ irect, KT *__restrict__ ekeys, uint32_t *__restrict__ evals,
+    int32_t *__restrict__ counters) {
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
     const FbBits fbits = fb_load(fbg, G.T);
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
@@ -909,7 +943,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
             nunsafe += (val & kUnsafe) ? 1u : 0u;
             ++o;
         };
-        if (!(skip && fallback_only(G, ref_key_rect(2, m, r, G.grid, G.off), fbits, (uint32_t)i, put)))
+        if (!(skip && fallback_only(G, rect_get(irect[i], 2, m, r, G), fbits, (uint32_t)i, put)))
             enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, fbits, (uint32_t)i, put);
     }
     if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
@@ -1676,6 +1710,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
     uint32_t *fbg = ca.take<uint32_t>((size_t)(G.T + 31) / 32 + 2);  // fallback-cell bits (+2: fb_load's words)
     uint32_t *irr = ca.take<uint32_t>(P), *nirr = ca.take<uint32_t>(1);  // k_fine_count's queue
+    uint2 *irect = ca.take<uint2>(P);  // reference rects in internal order
     unsigned long long *eg = ca.take<unsigned long long>(4);  // [gathered, kUnsafe, kThin entries, -]
     int32_t *rmax = ca.take<int32_t>(1);
     float2 *igm = ca.take<float2>(P);
@@ -1701,6 +1736,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(fbg, base);
         Carve::rebase(irr, base);
         Carve::rebase(nirr, base);
+        Carve::rebase(irect, base);
         Carve::rebase(hstart, base);
         Carve::rebase(gcnt, base);
         Carve::rebase(eg, base);
@@ -1765,9 +1801,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     DGS_LAUNCH_CHECK(s, debug);
     DGS_TRY_HIP(radix_sort<uint32_t>(plan_h, P, rs_h, home, home_sorted, gids, perm, s, true));
     DGS_LAUNCH_CHECK(s, debug);
-    k_gauss_permute<<<grid_for(P), kBlock, 0, s>>>(P, perm, grec, igm, igc);
+    k_gauss_permute<<<grid_for(P), kBlock, 0, s>>>(P, perm, grec, igm, igc, irect);
     DGS_LAUNCH_CHECK(s, debug);
-    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, igm, igc, fbg, fcount, greach, lrows, rmax, irr, nirr, eg + 1);
+    k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, igm, igc, irect, fbg, fcount, greach, lrows, rmax, irr, nirr,
+                                                eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count_irr<<<std::min(grid_for(P), 2048u), kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg,
                                                                      greach, irr, nirr, fcount, eg + 1);
@@ -1929,11 +1966,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
         if (k16)
             k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
-                                                            fcount, greach, fbg, reinterpret_cast<uint16_t *>(ekeys),
-                                                            evals, counters);
+                                                            fcount, greach, fbg, irect,
+                                                            reinterpret_cast<uint16_t *>(ekeys), evals, counters);
         else
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
-                                                            fcount, greach, fbg, ekeys, evals, counters);
+                                                            fcount, greach, fbg, irect, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
         DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),
                                                reinterpret_cast<uint16_t *>(ekeys_sorted), evals, svals, s)
