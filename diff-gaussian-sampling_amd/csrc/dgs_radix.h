@@ -24,8 +24,11 @@
 namespace dgs {
 
 constexpr int kRsBits = 8, kRsBins = 1 << kRsBits;
-constexpr int kRsThreads = 256, kRsWaves = kRsThreads / kWave, kRsItems = 16;
-constexpr int kRsTile = kRsThreads * kRsItems;  // 4096 items, each wave a contiguous 1024
+#ifndef DGS_RS_ITEMS
+#define DGS_RS_ITEMS 16
+#endif
+constexpr int kRsThreads = 256, kRsWaves = kRsThreads / kWave, kRsItems = DGS_RS_ITEMS;
+constexpr int kRsTile = kRsThreads * kRsItems;  // 4096 items (16 per thread), each wave a contiguous 1024
 static_assert(kRsThreads == kRsBins, "one thread per digit in the look-back");
 constexpr uint64_t kRsAgg = 1ull << 62, kRsPre = 2ull << 62, kRsVal = (1ull << 62) - 1;
 

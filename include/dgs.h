@@ -143,7 +143,11 @@ size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int b
 /* Forward: replaces SampleGaussians{,Derivative,Laplacian,Third}CUDA (sample_points.cu:100-143,
  * 198-296), CudaSampler::Sampler::forward (sampler_impl.cu:333-364) and FORWARD::render
  * (forward.cu:277-345).  out[N][K][C], K = D^function, must be zero-filled by the caller
- * (samples outside every tile stay 0, as in the reference). */
+ * (samples outside every tile stay 0, as in the reference).
+ * The first forward / backward of a binning that may take the call-time path (every call
+ * without DGS_SAMPLE_INPUTS_BINNED) also sorts that path's tile lists -- the reference's
+ * point_list, sampler_impl.cu:265-283 -- on `stream` (stream-ordered scratch); later calls on
+ * other streams wait for that sort.  A binning's calls otherwise only read it. */
 int dgs_sample_forward(int function, int P, int D, int N, int C, const float *means,
                        const float *values, const float *conics, const float *samples,
                        const void *binning, size_t binning_bytes, const void *sample_binning,
