@@ -64,7 +64,7 @@ constexpr int kWavesPerBlock = kBlock / kWave;
 //   [rlist uint32[R]]  the reference's point_list: every tile's Gaussian ids, ascending
 //                      (sampler_impl.cu:265-283), the pair set of the call-time path -- built
 //                      at the binning's first call that may take that path (ensure_ref_lists)
-//   [rref uint2[P]]    per internal id: (tile-list offset, radius bits) for that build
+//   [rref u32[P] f32[P]] tile-list offsets (caller order), radii (internal order) for that build
 //   [rtab uint32[4][T+1]]  per tile: Gaussian-list start (rlist), sample start (sorted order),
 //                      and the prefix counts of the call-time path's forward / backward units
 // A cell's list is [gbeg, gend); its flag-free entries come first, [gbeg, gmid).
@@ -105,7 +105,7 @@ struct Header {
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     int64_t fsub_cap, esub_cap;
     uint32_t zero[4];  // always 0: the "inputs differ" word of calls whose inputs the caller vouches for
-    uint64_t o_rref;   // (rlist's inputs: uint2[P] per internal id)
+    uint64_t o_rref;   // (rlist's inputs: tile-list offsets u32[P] by caller id, radii f32[P] by internal id)
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");

@@ -723,7 +723,7 @@ __device__ inline void load_gauss(int D, const float *__restrict__ means,
 }
 
 // Bounding box of each cell's samples [min0 min1 max0 max1] (empty cells: unused).  One wave
-// per cell, lanes striding over the cell's samples in the packed sorted rows (k_fs_pack).
+// per cell, lanes striding over the cell's samples in the packed sorted rows (FsRows).
 // (Both box kernels also set the fallback-cell bits fbg: tile t's bit when its fallback cell,
 // cell t * CT + CT - 1, holds samples.)
 __device__ __forceinline__ void set_fb_bit(int c, int CT, bool nonempty, uint32_t *__restrict__ fbg) {
@@ -1283,17 +1283,16 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
 // Run lazily (ensure_ref_lists) over the internal ids: the binned means (gmean), radius and
 // tile-list offset (rref) of caller id g = perm[i].
 __global__ void k_ref_keys(int P, Geom G, const float2 *__restrict__ gmean, const int32_t *__restrict__ perm,
-                           const uint2 *__restrict__ rref, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
+                           const uint32_t *__restrict__ rref, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
-    const uint2 rr = rref[i];
-    const float r = __uint_as_float(rr.y);
+    const float r = __uint_as_float(rref[P + i]);  // (radius, internal order)
     if (!(r > 0.0f)) return;
     const int64_t g = perm[i];
     const float2 mm = gmean[i];
     const float m[2] = {mm.x, mm.y};
     const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
-    uint64_t o = rr.x;
+    uint64_t o = rref[g];  // (tile-list offset, caller order)
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             keys[o] = key_of(G.D, x, y, G.grid);
@@ -1395,7 +1394,7 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
 __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float2 *__restrict__ igm,
                            const float4 *__restrict__ igc, const uint64_t *__restrict__ toffs,
                            float2 *__restrict__ gmean, float4 *__restrict__ gcon, int32_t *__restrict__ gperm,
-                           uint2 *__restrict__ rref) {
+                           uint32_t *__restrict__ rref) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -1404,25 +1403,27 @@ __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float
     gmean[i] = igm[i];  // (k_fine_count's internal-order copies: coalesced, no second gather)
     const float4 c = igc[i];
     gcon[i] = make_float4(c.x, c.y, c.z, 0.0f);
-    // (toffs < R < 2^31 when the binning succeeds; preprocess fails otherwise)
-    rref[i] = make_uint2((uint32_t)toffs[g], __float_as_uint(c.w));
+    // rlist's inputs (ensure_ref_lists): the tile-list offsets in caller order, copied coalesced
+    // (toffs < R < 2^31 when the binning succeeds; preprocess fails otherwise), then the radii
+    // in internal order
+    rref[i] = (uint32_t)toffs[i];
+    rref[P + i] = __float_as_uint(c.w);
 }
 
 // Forward sample pair rows in sorted order: pair p = samples 2p, 2p+1, field-interleaved
-// [s0 s0' (s1 s1')]; a missing second sample (odd N) is 0.
-__global__ void k_fs_pack(int N, int D, const int32_t *__restrict__ sorted, const float *__restrict__ samples,
-                          float *__restrict__ rows) {
-    const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= (int64_t)(N + 1) / 2 * 2) return;
-    float s[2] = {0.0f, 0.0f};
-    if (j < N) {
-        const int64_t sid = sorted[j];
-        s[0] = samples[sid * D];
-        if (D == 2) s[1] = samples[sid * D + 1];
+// [s0 s0' (s1 s1')]; a missing second sample (odd N) is 0 (zero-filled with phase A).  Written by
+// the sample sort's last place (FsRows: the payload of dgs_radix.h's Extra hook).
+struct FsRows {
+    const float *samples;
+    float *rows;
+    int D;
+    __device__ __forceinline__ void operator()(uint32_t j, uint32_t sid) const {
+        float *row = rows + (int64_t)(j >> 1) * (2 * D) + (j & 1);
+        row[0] = samples[(int64_t)sid * D];
+        if (D == 2) row[2] = samples[(int64_t)sid * D + 1];
     }
-    float *row = rows + (j >> 1) * (2 * D) + (j & 1);
-    for (int f = 0; f < D; ++f) row[2 * f] = s[f];
-}
+};
+
 
 // Zero-fills up to kZeroMax word-aligned regions in one launch (each hipMemsetAsync is a launch
 // of its own, ~5 us of GPU time even for a few bytes; the binning needs eleven).
@@ -1750,8 +1751,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     }
 
     float *fsrows = reinterpret_cast<float *>(sbuf + L0.o_fsrows);
-    {  // one launch for every zero-fill of phase A (k_fs_pack writes all of fsrows but its slack)
-        const size_t fs_written = (size_t)((N + 1) / 2 * 2) * D * 4;
+    {  // one launch for every zero-fill of phase A (the sample sort writes fsrows but its slack)
+        const size_t fs_written = (size_t)(N / 2 * 2) * D * 4;  // (the sort writes whole pairs; an odd N's last one from here)
         ZeroList zl;
         zl.add(stile, sizeof(uint32_t) * (G.T + 1));
         zl.add(gtile, sizeof(uint32_t) * (G.T + 1));
@@ -1780,12 +1781,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile, radix_hist(plan_s, rs_s));
     DGS_LAUNCH_CHECK(s, debug);
     DGS_TRY_HIP(radix_sort<uint32_t>(plan_s, N, rs_s, skeys, skeys_sorted, sids, reinterpret_cast<uint32_t *>(sorted_sid),
-                                     s, true));
+                                     s, true, FsRows{samples, fsrows, D}));
     DGS_LAUNCH_CHECK(s, debug);
     k_identify<uint32_t><<<grid_for(N), kBlock, 0, s>>>(N, skeys_sorted, (uint32_t)ncells, cell_sbeg, cell_send, 2,
                                                         (uint32_t)nsub, nsub ? sub_sbeg : nullptr, sub_send, 0);
-    DGS_LAUNCH_CHECK(s, debug);
-    k_fs_pack<<<grid_for((int64_t)N + 1), kBlock, 0, s>>>(N, D, sorted_sid, samples, fsrows);
     DGS_LAUNCH_CHECK(s, debug);
     if (nsub)  // sub-cell boxes and the cell boxes (their union)
         k_sub_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
@@ -1902,7 +1901,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                   reinterpret_cast<float2 *>(B.gbuf + B.L.o_gmean),
                                                   reinterpret_cast<float4 *>(B.gbuf + B.L.o_gcon),
                                                   reinterpret_cast<int32_t *>(B.gbuf + B.L.o_perm),
-                                                  reinterpret_cast<uint2 *>(B.gbuf + B.L.o_rref));
+                                                  reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rref));
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
@@ -2158,7 +2157,7 @@ static int build_ref_lists(const Header &h, char *gbuf, hipStream_t s, int debug
     if (e == hipSuccess) {
         k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
                                                   reinterpret_cast<const int32_t *>(gbuf + h.o_perm),
-                                                  reinterpret_cast<const uint2 *>(gbuf + h.o_rref), keys, vals);
+                                                  reinterpret_cast<const uint32_t *>(gbuf + h.o_rref), keys, vals);
         e = hipGetLastError();
     }
     if (e == hipSuccess) e = radix_sort<uint32_t>(plan, R, scr + 3 * kb, keys, keys_sorted, vals, rlist, s);

@@ -102,12 +102,19 @@ __device__ __forceinline__ uint32_t rs_block_excl(uint32_t x, uint32_t *wsum) {
 // place's tile counter (both zero before the launch).  grid = tiles.  A look-back that waits
 // implausibly long (a broken invariant, never expected) gives up and sets *err instead of
 // hanging the device.
-template <typename KT>
+// Extra: called as extra(position, value) for every item the pass writes (the last place of a
+// sort may scatter a payload gathered by value, e.g. the samples' pair rows); RsNone: nothing.
+struct RsNone {
+    __device__ __forceinline__ void operator()(uint32_t, uint32_t) const {}
+};
+
+template <typename KT, class Extra>
 __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__restrict__ kin, KT *__restrict__ kout,
                                                         const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
                                                         int shift, const uint32_t *__restrict__ hist,
                                                         unsigned long long *__restrict__ states,
-                                                        uint32_t *__restrict__ ticket, uint32_t *__restrict__ err) {
+                                                        uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
+                                                        Extra extra) {
     __shared__ uint32_t sk[kRsTile], sv[kRsTile];
     __shared__ uint32_t cnt[kRsWaves][kRsBins];
     __shared__ uint32_t s_tstart[kRsBins], s_delta[kRsBins];
@@ -198,8 +205,10 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
     for (int i = tid; i < cnt_tile; i += kRsThreads) {
         const uint32_t kk = sk[i];
         const uint32_t o = s_delta[rs_digit(kk, shift)] + (uint32_t)i;
+        const uint32_t v = sv[i];
         kout[o] = (KT)kk;
-        vout[o] = sv[i];
+        vout[o] = v;
+        extra(o, v);
     }
 }
 
@@ -208,9 +217,10 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
 // (once: a plan's scratch serves one sort).  The look-back's give-up word is tickets[63].
 // hist_ready: the keys' producer has already added their digit counts into the plan's
 // histograms (radix_hist; dgs_preprocess.hip's RsHist), so the histogram launch is skipped.
-template <typename KT>
+template <typename KT, class Extra = RsNone>
 static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const KT *kin, KT *kout,
-                             const uint32_t *vin, uint32_t *vout, hipStream_t s, bool hist_ready = false) {
+                             const uint32_t *vin, uint32_t *vout, hipStream_t s, bool hist_ready = false,
+                             Extra extra = Extra{}) {
     if (n <= 0) return hipSuccess;
     if (n > p.n) return hipErrorInvalidValue;
     uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
@@ -228,9 +238,14 @@ static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const
         const bool to_out = ((p.places - 1 - q) & 1) == 0;  // the last place writes kout / vout
         KT *ko = to_out ? kout : tk;
         uint32_t *vo = to_out ? vout : tv;
-        k_rs_pass<KT><<<(unsigned)tiles, kRsThreads, 0, s>>>(
-            n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, states + (size_t)q * p.tiles * kRsBins,
-            tickets + q, err);
+        if (q == p.places - 1)  // (the last place: the payload too)
+            k_rs_pass<KT, Extra><<<(unsigned)tiles, kRsThreads, 0, s>>>(
+                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, states + (size_t)q * p.tiles * kRsBins,
+                tickets + q, err, extra);
+        else
+            k_rs_pass<KT, RsNone><<<(unsigned)tiles, kRsThreads, 0, s>>>(
+                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, states + (size_t)q * p.tiles * kRsBins,
+                tickets + q, err, RsNone{});
         ki = ko;
         vi = vo;
     }
