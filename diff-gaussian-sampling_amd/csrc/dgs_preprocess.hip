@@ -932,7 +932,9 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
         const bool skip = greach[i] > 0;  // (k_fine_count's decision)
         uint64_t o = offs[i];
         const auto put = [&](uint32_t cell, uint32_t val) {
-            const uint32_t key = (cell << 1) | ((val & kSlow) ? 1u : 0u);  // flagged entries last in a cell
+            // (cell, class): flag-free, flagged, then the thin (kThin) ones last in a cell -- the
+            // forward's main and thin passes then meet few mixed groups; key >> 1 = (cell, flagged)
+            const uint32_t key = (cell << 2) | ((val & kSlow) ? 2u : 0u) | ((val & kThin) ? 1u : 0u);
             if (stage) {
                 skey[o - base] = key;
                 sval[o - base] = val;
@@ -1875,7 +1877,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         B.fs_cells = cb.take<unsigned long long>(fused_scan_state_words(ncells, 1, 1));
         B.fs_units = cb.take<unsigned long long>(fused_scan_state_words(ncells, 2, 1));
         B.fs_sub = cb.take<unsigned long long>(fused_scan_state_words(std::max(nsub, 1), 1, 1));
-        B.ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 1;  // + slow bit
+        B.ebits = bit_length((uint64_t)(ncells > 1 ? ncells - 1 : 1)) + 2;  // + slow and thin bits
         B.k16 = B.ebits <= 16;  // (cell, flag) keys in 16 bits: a u16-key sort
         B.plan_e = radix_plan(Ecap, B.ebits);
         B.rs_e = cb.take<char>(B.plan_e.bytes);
@@ -1977,9 +1979,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         if (k16)
             k_identify<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(Es, reinterpret_cast<const uint16_t *>(ekeys_sorted),
-                                                                 2u * (uint32_t)ncells, hbeg, hend, 0);
+                                                                 2u * (uint32_t)ncells, hbeg, hend, 1);
         else
-            k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 0);
+            k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 1);
         DGS_LAUNCH_CHECK(s, debug);
     }
     {  // per cell: [gathered (ascending id) + sorted unflagged | sorted flagged] = [gbeg, gmid, gend)

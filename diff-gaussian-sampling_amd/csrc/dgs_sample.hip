@@ -614,8 +614,18 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
         float r_nxt[RS];
         load_grow<RS>(grows, e_nxt, r_nxt);
         const uint32_t e_nn = ents[min(g0 + 2 * kWave + lane, last)];
-        fwd_s_group<FN, D, CB, NPH, HB, FLAGGED, THIN>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr, gcon,
-                                                       acc);
+        // flagged groups with no lane for this pass are skipped (the entry sort puts a cell's kThin
+        // entries after its other flagged ones, so the main and the thin pass share few groups)
+        bool work = true;
+        if constexpr (FLAGGED) {
+            const bool act = g0 + lane < ee;
+            work = __builtin_amdgcn_readfirstlane(
+                       (uint32_t)(__ballot(act && (THIN ? (e_cur & kThin) != 0 : (e_cur & (kUnsafe | kThin)) == 0)) !=
+                                  0ull)) != 0u;
+        }
+        if (work)
+            fwd_s_group<FN, D, CB, NPH, HB, FLAGGED, THIN>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr,
+                                                           gcon, acc);
 #pragma unroll
         for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
         e_cur = e_nxt;
