@@ -1200,15 +1200,19 @@ __device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 &mm, con
     return mask;
 }
 
-// Sub lists (D = 2), one pass, one wave per cell: for every entry of the cell list, the
+// Sub lists (D = 2), one block (4 waves) per cell: for every entry of the cell list, the
 // sub-cells whose sample box its cut meets (sub_mask).  Sub list k of the cell has the region
-// [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
-// list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
-// entries and [lmid, lend) the flagged ones.  The next group's Gaussian rows and the one
-// after's entries are loaded while a group is tested (one stage: waves parked on the row
-// gathers half their cycles, PMC SQ_WAIT_ANY).  (A block-per-cell form -- masks
-// of the whole list in parallel into LDS, then one compacting wave per sub list -- was slower:
-// 235 against 182 us at the headline, the same math plus the LDS round trip.)
+// [4 gbeg + k n, + n) (n = the cell list's length, its largest possible size; esub_cap = 4 E
+// covers every sub list of every cell); it is written in cell-list order, so [lbeg, lmid) holds
+// the flag-free entries and [lmid, lend) the flagged ones.  The list is walked in rounds of
+// kSlWaves x kSlGroups groups of 64 entries, each wave a contiguous run of groups: first every
+// wave tests its groups (masks and entries kept in registers) and counts its hits per sub list
+// and class, then one LDS exclusive scan over the waves places each wave's hits, then every wave
+// writes its hits in order.  (One wave per cell walked ~19 groups serially with ~3 waves per SIMD
+// resident: waves were parked on loads half their cycles.)  The flag-free entries precede the
+// flagged ones in a cell list, so when a round holds a flagged entry every flag-free one is
+// counted by the end of that round's scan.
+constexpr int kSlWaves = kWavesPerBlock, kSlGroups = 4;
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
                                                       const int32_t *__restrict__ gmid,
                                                       const int32_t *__restrict__ gend,
@@ -1219,11 +1223,12 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float4 *__restrict__ sbox, int CT,
                                                       int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
                                                       int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent) {
-    const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
-    const int lane = threadIdx.x & (kWave - 1);
+    __shared__ uint32_t scnt[kSlWaves][2 * kSubPerCell];
+    const int c = block_unit_index();  // (XCD remap: neighbouring cells share Gaussians)
     if (c >= ncells) return;
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};  // (block totals so far)
     const int64_t base = (int64_t)kSubPerCell * b;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
@@ -1231,42 +1236,76 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
         float4 sb[kSubPerCell];
 #pragma unroll
         for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
-        // two-stage pipeline: group g + 1's Gaussians and group g + 2's entries are in flight
-        // while group g is tested
-        uint32_t ent_c = b + lane < e ? entries[b + lane] : kUnsafe;
-        uint32_t ent_n = b + kWave + lane < e ? entries[b + kWave + lane] : kUnsafe;
-        float2 mm_c;
-        float4 cc_c;
-        sub_row(ent_c, gmean, gcon, mm_c, cc_c);
-        for (int j0 = b; j0 < e; j0 += kWave) {
-            const int j = j0 + lane;
-            const uint32_t ent = ent_c;
-            const float2 mm = mm_c;
-            const float4 cc = cc_c;
-            ent_c = ent_n;
-            sub_row(ent_c, gmean, gcon, mm_c, cc_c);
-            ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
-            const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
-            const bool ff = j < m_;
+        constexpr int RG = kSlWaves * kSlGroups * kWave;  // entries per round
+        for (int r0 = b; r0 < e; r0 += RG) {
+            // this wave's groups of the round: entries [r0 + w*G*64, +G*64)
+            const int w0 = r0 + w * kSlGroups * kWave;
+            uint32_t ent[kSlGroups], msk[kSlGroups];
+            float2 mm[kSlGroups];
+            float4 cc[kSlGroups];
+#pragma unroll
+            for (int g = 0; g < kSlGroups; ++g) {  // (all loads first: kSlGroups rows in flight)
+                const int j = w0 + g * kWave + lane;
+                ent[g] = j < e ? entries[j] : kUnsafe;
+            }
+#pragma unroll
+            for (int g = 0; g < kSlGroups; ++g) sub_row(ent[g], gmean, gcon, mm[g], cc[g]);
+            uint32_t cf[2 * kSubPerCell] = {0, 0, 0, 0, 0, 0, 0, 0};  // this wave's hits [ff k | fl k]
+#pragma unroll
+            for (int g = 0; g < kSlGroups; ++g) {
+                const int j = w0 + g * kWave + lane;
+                msk[g] = j < e ? sub_mask(ent[g], mm[g], cc[g], bx, ctr, sb) : 0u;
+                const bool ff = j < m_;
+#pragma unroll
+                for (int k = 0; k < kSubPerCell; ++k) {
+                    const bool hit = (msk[g] >> k) & 1u;
+                    cf[k] += (uint32_t)__popcll(__ballot(hit && ff));
+                    cf[kSubPerCell + k] += (uint32_t)__popcll(__ballot(hit && !ff));
+                }
+            }
+            if (lane == 0)
+#pragma unroll
+                for (int q = 0; q < 2 * kSubPerCell; ++q) scnt[w][q] = cf[q];
+            __syncthreads();
+            uint32_t pff[kSubPerCell], pfl[kSubPerCell], tff[kSubPerCell];  // this wave's offsets
 #pragma unroll
             for (int k = 0; k < kSubPerCell; ++k) {
-                const bool hit = (mask >> k) & 1u;
-                const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
-                if (hit) {
-                    const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
-                    // flag-free entries precede the flagged ones in the cell list, so once a group
-                    // holds a flagged entry the flag-free count is final -- this group's own
-                    // flag-free hits included: the region fills [flag-free | flagged] in order
-                    const uint32_t nffk = nff[k] + (uint32_t)__popcll(bf);
-                    const int64_t o = base + (int64_t)k * n + (ff ? nff[k] : nffk + nfl[k]) + below;
-                    sub_ent[o] = ent;
+                uint32_t a = 0, t = 0, fa = 0, ft = 0;
+#pragma unroll
+                for (int q = 0; q < kSlWaves; ++q) {
+                    const uint32_t x = scnt[q][k], y = scnt[q][kSubPerCell + k];
+                    a += q < w ? x : 0u;
+                    t += x;
+                    fa += q < w ? y : 0u;
+                    ft += y;
                 }
-                nff[k] += (uint32_t)__popcll(bf);
-                nfl[k] += (uint32_t)__popcll(bl);
+                pff[k] = nff[k] + a;
+                tff[k] = nff[k] + t;  // (every flag-free hit of the list up to this round)
+                pfl[k] = nfl[k] + fa;
+                nff[k] += t;
+                nfl[k] += ft;
+            }
+            __syncthreads();  // (scnt is rewritten next round)
+#pragma unroll
+            for (int g = 0; g < kSlGroups; ++g) {
+                const int j = w0 + g * kWave + lane;
+                const bool ff = j < m_;
+#pragma unroll
+                for (int k = 0; k < kSubPerCell; ++k) {
+                    const bool hit = (msk[g] >> k) & 1u;
+                    const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
+                    if (hit) {
+                        const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
+                        const int64_t o = base + (int64_t)k * n + (ff ? pff[k] : tff[k] + pfl[k]) + below;
+                        sub_ent[o] = ent[g];
+                    }
+                    pff[k] += (uint32_t)__popcll(bf);
+                    pfl[k] += (uint32_t)__popcll(bl);
+                }
             }
         }
     }
-    if (lane == 0)
+    if (threadIdx.x == 0)
         for (int k = 0; k < kSubPerCell; ++k) {
             const int a = (int)(base + (int64_t)k * n);
             lbeg[c * kSubPerCell + k] = a;
@@ -2049,7 +2088,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
-        k_sub_lists<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
+        k_sub_lists<<<(unsigned)ncells, kBlock, 0, s>>>(
             ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box, sub_box, G.CT, sub_lbeg, sub_lmid,
             sub_lend, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);
