@@ -29,6 +29,7 @@
 // and frequency gradients are per-lane LDS partials, flushed once per wave.
 
 #include <algorithm>
+#include <vector>
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
@@ -68,17 +69,40 @@ static inline float o2f(uint32_t o) {
 __device__ __forceinline__ float agg_r(float radius) { return (float)((double)radius * 0.2); }
 __device__ __forceinline__ bool agg_valid(float r) { return (double)r >= 1e-6; }
 
+// stats: kAggStatCopies copies of [rmax, min[2], max[2]] (order-preserving u32 codes), kAggStatStride
+// words apart; a wave reduces its lanes first and block b adds to copy b % 8 (one word takes only
+// ~88 atomic ops per us: one atomic per lane on five words was the kernel's whole cost).
+constexpr int kAggStatCopies = 8, kAggStatStride = 32;
 __global__ void k_agg_prep(int P, int D, const float *__restrict__ means, const float *__restrict__ radii,
-                           uint32_t *__restrict__ stats /* rmax, min[2], max[2] */) {
+                           uint32_t *__restrict__ stats) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
-    const float r = agg_r(radii[i]);
-    if (!agg_valid(r)) return;
-    atomicMax(&stats[0], f2o(r));
-    for (int d = 0; d < D; ++d) {
-        const float m = means[(int64_t)i * D + d];
-        atomicMin(&stats[1 + d], f2o(m));
-        atomicMax(&stats[3 + d], f2o(m));
+    uint32_t v[5] = {0u, 0xffffffffu, 0xffffffffu, 0u, 0u};
+    if (i < P) {
+        const float r = agg_r(radii[i]);
+        if (agg_valid(r)) {
+            v[0] = f2o(r);
+            for (int d = 0; d < D; ++d) {
+                const uint32_t m = f2o(means[(int64_t)i * D + d]);
+                v[1 + d] = m;
+                v[3 + d] = m;
+            }
+        }
+    }
+#pragma unroll
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        v[0] = max(v[0], (uint32_t)__shfl_xor((int)v[0], off));
+        for (int d = 0; d < 2; ++d) {
+            v[1 + d] = min(v[1 + d], (uint32_t)__shfl_xor((int)v[1 + d], off));
+            v[3 + d] = max(v[3 + d], (uint32_t)__shfl_xor((int)v[3 + d], off));
+        }
+    }
+    if ((threadIdx.x & (kWave - 1)) == 0 && v[0] != 0u) {
+        uint32_t *st = stats + (blockIdx.x & (kAggStatCopies - 1)) * kAggStatStride;
+        atomicMax(&st[0], v[0]);
+        for (int d = 0; d < D; ++d) {
+            atomicMin(&st[1 + d], v[1 + d]);
+            atomicMax(&st[3 + d], v[3 + d]);
+        }
     }
 }
 
@@ -1380,15 +1404,29 @@ extern "C" int dgs_agg_preprocess(int P, int D, const float *means, const float 
     if (P == 0) return DGS_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     auto scratch = [&](size_t n) { return alloc(alloc_ctx, DGS_BUF_SCRATCH, std::max<size_t>(n, 16)); };
-    uint32_t *stats = static_cast<uint32_t *>(scratch(64));
+    constexpr size_t kStatWords = (size_t)kAggStatCopies * kAggStatStride;
+    uint32_t *stats = static_cast<uint32_t *>(scratch(4 * kStatWords));
     if (!stats) return fail(DGS_ERR_ALLOC, "aggregate: scratch allocation failed");
-    static const uint32_t init[5] = {0u, 0xffffffffu, 0xffffffffu, 0u, 0u};
-    DGS_TRY_HIP(hipMemcpyAsync(stats, init, sizeof(init), hipMemcpyHostToDevice, s));
+    static const std::vector<uint32_t> init = [] {
+        std::vector<uint32_t> v(kStatWords, 0u);
+        for (int q = 0; q < kAggStatCopies; ++q) v[q * kAggStatStride + 1] = v[q * kAggStatStride + 2] = 0xffffffffu;
+        return v;
+    }();
+    DGS_TRY_HIP(hipMemcpyAsync(stats, init.data(), 4 * kStatWords, hipMemcpyHostToDevice, s));
     k_agg_prep<<<agg_elem_blocks(P), kBlock, 0, s>>>(P, D, means, radii, stats);
     DGS_LAUNCH_CHECK(s, debug);
-    uint32_t h[5];
-    DGS_TRY_HIP(hipMemcpyAsync(h, stats, sizeof(h), hipMemcpyDeviceToHost, s));
+    std::vector<uint32_t> hs(kStatWords);
+    DGS_TRY_HIP(hipMemcpyAsync(hs.data(), stats, 4 * kStatWords, hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));
+    uint32_t h[5] = {0u, 0xffffffffu, 0xffffffffu, 0u, 0u};
+    for (int q = 0; q < kAggStatCopies; ++q) {
+        const uint32_t *c = &hs[(size_t)q * kAggStatStride];
+        h[0] = std::max(h[0], c[0]);
+        for (int d = 0; d < 2; ++d) {
+            h[1 + d] = std::min(h[1 + d], c[1 + d]);
+            h[3 + d] = std::max(h[3 + d], c[3 + d]);
+        }
+    }
 
     AggGeom g;
     g.D = D;

@@ -152,6 +152,14 @@ static inline unsigned hist_grid(int64_t n) {
     return (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + kBlock - 1) / kBlock, kHistGrid));
 }
 
+// Same-address global atomics: one word sustains ~88 atomic ops per us (MI355X_MICROARCH.md,
+// 'dequeue'), so a counter that every wave or block of a large grid adds to (k_fine_count's
+// largest reach: 15.6k waves, 180 us) is kept in kShards copies, one per XCD (block b adds to
+// copy b % 8, its own lines), and the reader sums or maxes the copies.
+constexpr int kShards = 8;
+constexpr int kShard64 = 16, kShard32 = 32;  // copy strides in u64 / u32 words: 128 bytes (a line) per copy
+__device__ __forceinline__ int shard_of_block() { return (int)(blockIdx.x & (kShards - 1)); }
+
 // The digit histograms of a radix sort of the keys a producer kernel writes (dgs_radix.h's
 // k_rs_hist folded into the producer: one launch less per sort).  Per block in LDS, flushed once.
 struct RsHist {
@@ -170,9 +178,11 @@ __device__ __forceinline__ void rs_hist_add(uint32_t *h, const RsHist &r, uint32
         for (int p = 0; p < r.places; ++p) atomicAdd(&h[p * kRsBins + rs_digit(key, p * kRsBits)], 1u);
 }
 __device__ __forceinline__ void rs_hist_flush(const uint32_t *h, const RsHist &r) {
-    if (r.g)
+    if (r.g) {
+        uint32_t *g = r.g + (size_t)shard_of_block() * r.places * kRsBins;  // (dgs_radix.h: kRsHistCopies)
         for (int i = threadIdx.x; i < r.places * kRsBins; i += blockDim.x)
-            if (h[i]) atomicAdd(&r.g[i], h[i]);
+            if (h[i]) atomicAdd(&g[i], h[i]);
+    }
 }
 
 __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
@@ -193,7 +203,7 @@ __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
         const uint32_t key = ref_sample_key(G.D, s, G.grid, G.off);
         if (key < (uint32_t)G.T) {
             if (lds) atomicAdd(&hist[key], 1u);
-            else atomicAdd(&tile_count[key], 1u);
+            else atomicAdd(&tile_count[(size_t)shard_of_block() * (G.T + 1) + key], 1u);
         }
         const uint32_t ck = sample_cell_sub(G, s);  // (cell, sub-cell): cell ranges are keys >> 2
         keys[i] = ck;
@@ -201,9 +211,9 @@ __global__ void k_sample_cells(int N, Geom G, const float *__restrict__ samples,
         rs_hist_add(dh, rh, ck);
     }
     __syncthreads();
-    if (lds)
+    if (lds)  // (tile_count: kShards copies of T + 1 words)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x)
-            if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
+            if (hist[t]) atomicAdd(&tile_count[(size_t)shard_of_block() * (G.T + 1) + t], hist[t]);
     rs_hist_flush(dh, rh);
 }
 
@@ -308,7 +318,7 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
                 const uint32_t key = key_of(D, x, y, G.grid);
                 if (key < (uint32_t)G.T) {
                     if (lds) atomicAdd(&hist[key], 1u);
-                    else atomicAdd(&tile_count[key], 1u);
+                    else atomicAdd(&tile_count[(size_t)shard_of_block() * (G.T + 1) + key], 1u);
                 }
             }
         int h[2] = {0, 0};
@@ -322,9 +332,9 @@ __global__ void k_gauss_prep(int P, Geom G, const float *__restrict__ means,
         rs_hist_add(dh, rh, (uint32_t)(h[1] * home_w + h[0]));
     }
     __syncthreads();
-    if (lds)
+    if (lds)  // (tile_count: kShards copies of T + 1 words)
         for (int t = threadIdx.x; t < G.T; t += blockDim.x)
-            if (hist[t]) atomicAdd(&tile_count[t], hist[t]);
+            if (hist[t]) atomicAdd(&tile_count[(size_t)shard_of_block() * (G.T + 1) + t], hist[t]);
     rs_hist_flush(dh, rh);
 }
 
@@ -858,8 +868,14 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
         reach = max(reach, __shfl_xor(reach, off));
         nu += __shfl_xor(nu, off);
     }
-    if (lane == 0 && reach > 0) atomicMax(rmax, reach);
-    if (lane == 0 && nu) atomicAdd(&nflag[0], (unsigned long long)nu);
+    // one sharded atomic per block for the largest reach, one per wave for rare unsafe counts
+    __shared__ int bmax;
+    if (threadIdx.x == 0) bmax = 0;
+    __syncthreads();
+    if (lane == 0 && reach > 0) atomicMax(&bmax, reach);
+    __syncthreads();
+    if (threadIdx.x == 0 && bmax > 0) atomicMax(&rmax[shard_of_block() * kShard32], bmax);
+    if (lane == 0 && nu) atomicAdd(&nflag[shard_of_block() * kShard64], (unsigned long long)nu);
     FC_T(6);
     FC_ADD(0, 6, 5);
 }
@@ -895,9 +911,9 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
         nu += __shfl_xor(nu, off);
         nt += __shfl_xor(nt, off);
     }
-    if ((threadIdx.x & (kWave - 1)) == 0) {
-        if (nu) atomicAdd(&nflag[0], (unsigned long long)nu);
-        if (nt) atomicAdd(&nflag[1], (unsigned long long)nt);
+    if ((threadIdx.x & (kWave - 1)) == 0) {  // (sharded: see kShards)
+        if (nu) atomicAdd(&nflag[shard_of_block() * kShard64], (unsigned long long)nu);
+        if (nt) atomicAdd(&nflag[shard_of_block() * kShard64 + 1], (unsigned long long)nt);
     }
 }
 
@@ -948,7 +964,9 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
         if (!(skip && fallback_only(G, rect_get(irect[i], 2, m, r, G), fbits, (uint32_t)i, put)))
             enumerate_fine(G, m, r, c, k, skip, sbeg, send, box, fbits, (uint32_t)i, put);
     }
-    if (nunsafe) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
+    for (int off = kWave / 2; off > 0; off >>= 1) nunsafe += __shfl_xor(nunsafe, off);
+    if ((threadIdx.x & (kWave - 1)) == 0 && nunsafe)  // (one add per wave that has any)
+        atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nunsafe);
     if (stage) {
         __syncthreads();
         const int n = (int)(end - base);
@@ -993,7 +1011,9 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
     const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
     const int strip = wid / kGatherRows, q = wid - strip * kGatherRows, dy = q - kGatherReach;
     if (strip >= home_h * spr) return;
-    const int R = sload(rmax);
+    int R = 0;
+#pragma unroll
+    for (int q2 = 0; q2 < kShards; ++q2) R = max(R, sload(&rmax[q2 * kShard32]));
     const int gy = strip / spr, gx0 = (strip - gy * spr) * kStripW, nw = min(kStripW, home_w - gx0);
     const int hy = gy - dy;
     if (dy < -R || dy > R || hy < 0 || hy >= home_h) return;  // (cnt2 stays 0 there)
@@ -1047,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
         unsigned long long t = lane < nw ? cur : 0u;
 #pragma unroll
         for (int off = kWave / 2; off > 0; off >>= 1) t += __shfl_xor(t, off);
-        if (lane == 0 && t) atomicAdd(eg, t);
+        if (lane == 0 && t) atomicAdd(&eg[shard_of_block() * kShard64], t);  // (sharded: see kShards)
     }
 }
 
@@ -1200,19 +1220,15 @@ __device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 &mm, con
     return mask;
 }
 
-// Sub lists (D = 2), one block (4 waves) per cell: for every entry of the cell list, the
+// Sub lists (D = 2), one pass, one wave per cell: for every entry of the cell list, the
 // sub-cells whose sample box its cut meets (sub_mask).  Sub list k of the cell has the region
-// [4 gbeg + k n, + n) (n = the cell list's length, its largest possible size; esub_cap = 4 E
-// covers every sub list of every cell); it is written in cell-list order, so [lbeg, lmid) holds
-// the flag-free entries and [lmid, lend) the flagged ones.  The list is walked in rounds of
-// kSlWaves x kSlGroups groups of 64 entries, each wave a contiguous run of groups: first every
-// wave tests its groups (masks and entries kept in registers) and counts its hits per sub list
-// and class, then one LDS exclusive scan over the waves places each wave's hits, then every wave
-// writes its hits in order.  (One wave per cell walked ~19 groups serially with ~3 waves per SIMD
-// resident: waves were parked on loads half their cycles.)  The flag-free entries precede the
-// flagged ones in a cell list, so when a round holds a flagged entry every flag-free one is
-// counted by the end of that round's scan.
-constexpr int kSlWaves = kWavesPerBlock, kSlGroups = 4;
+// [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
+// list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
+// entries and [lmid, lend) the flagged ones.  The next group's Gaussian rows and the one
+// after's entries are loaded while a group is tested (one stage: waves parked on the row
+// gathers half their cycles, PMC SQ_WAIT_ANY).  (A block-per-cell form -- masks
+// of the whole list in parallel into LDS, then one compacting wave per sub list -- was slower:
+// 235 against 182 us at the headline, the same math plus the LDS round trip.)
 __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t *__restrict__ gbeg,
                                                       const int32_t *__restrict__ gmid,
                                                       const int32_t *__restrict__ gend,
@@ -1223,12 +1239,11 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float4 *__restrict__ sbox, int CT,
                                                       int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
                                                       int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent) {
-    __shared__ uint32_t scnt[kSlWaves][2 * kSubPerCell];
-    const int c = block_unit_index();  // (XCD remap: neighbouring cells share Gaussians)
+    const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
+    const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};  // (block totals so far)
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
     const int64_t base = (int64_t)kSubPerCell * b;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
@@ -1236,76 +1251,42 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
         float4 sb[kSubPerCell];
 #pragma unroll
         for (int k = 0; k < kSubPerCell; ++k) sb[k] = sbox[c * kSubPerCell + k];
-        constexpr int RG = kSlWaves * kSlGroups * kWave;  // entries per round
-        for (int r0 = b; r0 < e; r0 += RG) {
-            // this wave's groups of the round: entries [r0 + w*G*64, +G*64)
-            const int w0 = r0 + w * kSlGroups * kWave;
-            uint32_t ent[kSlGroups], msk[kSlGroups];
-            float2 mm[kSlGroups];
-            float4 cc[kSlGroups];
-#pragma unroll
-            for (int g = 0; g < kSlGroups; ++g) {  // (all loads first: kSlGroups rows in flight)
-                const int j = w0 + g * kWave + lane;
-                ent[g] = j < e ? entries[j] : kUnsafe;
-            }
-#pragma unroll
-            for (int g = 0; g < kSlGroups; ++g) sub_row(ent[g], gmean, gcon, mm[g], cc[g]);
-            uint32_t cf[2 * kSubPerCell] = {0, 0, 0, 0, 0, 0, 0, 0};  // this wave's hits [ff k | fl k]
-#pragma unroll
-            for (int g = 0; g < kSlGroups; ++g) {
-                const int j = w0 + g * kWave + lane;
-                msk[g] = j < e ? sub_mask(ent[g], mm[g], cc[g], bx, ctr, sb) : 0u;
-                const bool ff = j < m_;
-#pragma unroll
-                for (int k = 0; k < kSubPerCell; ++k) {
-                    const bool hit = (msk[g] >> k) & 1u;
-                    cf[k] += (uint32_t)__popcll(__ballot(hit && ff));
-                    cf[kSubPerCell + k] += (uint32_t)__popcll(__ballot(hit && !ff));
-                }
-            }
-            if (lane == 0)
-#pragma unroll
-                for (int q = 0; q < 2 * kSubPerCell; ++q) scnt[w][q] = cf[q];
-            __syncthreads();
-            uint32_t pff[kSubPerCell], pfl[kSubPerCell], tff[kSubPerCell];  // this wave's offsets
+        // two-stage pipeline: group g + 1's Gaussians and group g + 2's entries are in flight
+        // while group g is tested
+        uint32_t ent_c = b + lane < e ? entries[b + lane] : kUnsafe;
+        uint32_t ent_n = b + kWave + lane < e ? entries[b + kWave + lane] : kUnsafe;
+        float2 mm_c;
+        float4 cc_c;
+        sub_row(ent_c, gmean, gcon, mm_c, cc_c);
+        for (int j0 = b; j0 < e; j0 += kWave) {
+            const int j = j0 + lane;
+            const uint32_t ent = ent_c;
+            const float2 mm = mm_c;
+            const float4 cc = cc_c;
+            ent_c = ent_n;
+            sub_row(ent_c, gmean, gcon, mm_c, cc_c);
+            ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
+            const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
+            const bool ff = j < m_;
 #pragma unroll
             for (int k = 0; k < kSubPerCell; ++k) {
-                uint32_t a = 0, t = 0, fa = 0, ft = 0;
-#pragma unroll
-                for (int q = 0; q < kSlWaves; ++q) {
-                    const uint32_t x = scnt[q][k], y = scnt[q][kSubPerCell + k];
-                    a += q < w ? x : 0u;
-                    t += x;
-                    fa += q < w ? y : 0u;
-                    ft += y;
+                const bool hit = (mask >> k) & 1u;
+                const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
+                if (hit) {
+                    const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
+                    // flag-free entries precede the flagged ones in the cell list, so once a group
+                    // holds a flagged entry the flag-free count is final -- this group's own
+                    // flag-free hits included: the region fills [flag-free | flagged] in order
+                    const uint32_t nffk = nff[k] + (uint32_t)__popcll(bf);
+                    const int64_t o = base + (int64_t)k * n + (ff ? nff[k] : nffk + nfl[k]) + below;
+                    sub_ent[o] = ent;
                 }
-                pff[k] = nff[k] + a;
-                tff[k] = nff[k] + t;  // (every flag-free hit of the list up to this round)
-                pfl[k] = nfl[k] + fa;
-                nff[k] += t;
-                nfl[k] += ft;
-            }
-            __syncthreads();  // (scnt is rewritten next round)
-#pragma unroll
-            for (int g = 0; g < kSlGroups; ++g) {
-                const int j = w0 + g * kWave + lane;
-                const bool ff = j < m_;
-#pragma unroll
-                for (int k = 0; k < kSubPerCell; ++k) {
-                    const bool hit = (msk[g] >> k) & 1u;
-                    const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
-                    if (hit) {
-                        const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
-                        const int64_t o = base + (int64_t)k * n + (ff ? pff[k] : tff[k] + pfl[k]) + below;
-                        sub_ent[o] = ent[g];
-                    }
-                    pff[k] += (uint32_t)__popcll(bf);
-                    pfl[k] += (uint32_t)__popcll(bl);
-                }
+                nff[k] += (uint32_t)__popcll(bf);
+                nfl[k] += (uint32_t)__popcll(bl);
             }
         }
     }
-    if (threadIdx.x == 0)
+    if (lane == 0)
         for (int k = 0; k < kSubPerCell; ++k) {
             const int a = (int)(base + (int64_t)k * n);
             lbeg[c * kSubPerCell + k] = a;
@@ -1353,8 +1334,14 @@ __device__ __forceinline__ void ref_tables_block(int T, const uint32_t *__restri
     const int nt = blockDim.x, t = threadIdx.x;
     const int per = (T + nt - 1) / nt, a = min(T, t * per), b = min(T, a + per);
     uint4 sum = make_uint4(0u, 0u, 0u, 0u);
+    // gcnt / scnt: kShards copies of T + 1 counts
+    const auto tcount = [&](const uint32_t *cnt, int k) {
+        uint32_t v = 0;
+        for (int q = 0; q < kShards; ++q) v += cnt[(size_t)q * (T + 1) + k];
+        return v;
+    };
     for (int k = a; k < b; ++k) {
-        const uint32_t g = gcnt[k], sm = scnt[k];
+        const uint32_t g = tcount(gcnt, k), sm = tcount(scnt, k);
         sum.x += g;
         sum.y += sm;
         sum.z += g ? (sm + kRefUnit - 1) / kRefUnit : 0u;  // forward units: sample chunks of tiles with Gaussians
@@ -1373,7 +1360,7 @@ __device__ __forceinline__ void ref_tables_block(int T, const uint32_t *__restri
     uint32_t *tab[4] = {rtab + kRtGStart * (T + 1), rtab + kRtSStart * (T + 1), rtab + kRtFwdUnits * (T + 1),
                         rtab + kRtBwdUnits * (T + 1)};
     for (int k = a; k < b; ++k) {
-        const uint32_t g = gcnt[k], sm = scnt[k];
+        const uint32_t g = tcount(gcnt, k), sm = tcount(scnt, k);
         granges[k] = g ? make_uint2(acc[0], acc[0] + g) : make_uint2(0u, 0u);
         sranges[k] = sm ? make_uint2(acc[1], acc[1] + sm) : make_uint2(0u, 0u);
         for (int q = 0; q < 4; ++q) tab[q][k] = acc[q];
@@ -1739,7 +1726,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     Scratch S{alloc, alloc_ctx};
     Carve ca;
     uint32_t *skeys = ca.take<uint32_t>(N), *skeys_sorted = ca.take<uint32_t>(N), *sids = ca.take<uint32_t>(N);
-    uint32_t *stile = ca.take<uint32_t>(G.T + 1), *gtile = ca.take<uint32_t>(G.T + 1);
+    // (tile counts, largest reach and entry counts: kShards copies each, see kShards)
+    const size_t tcw = (size_t)kShards * (G.T + 1);
+    uint32_t *stile = ca.take<uint32_t>(tcw), *gtile = ca.take<uint32_t>(tcw);
     uint32_t *home = ca.take<uint32_t>(P), *home_sorted = ca.take<uint32_t>(P), *gids = ca.take<uint32_t>(P);
     uint32_t *perm = ca.take<uint32_t>(P);
     uint64_t *touched = ca.take<uint64_t>(P), *fcount = ca.take<uint64_t>(P), *foffs = ca.take<uint64_t>(P);
@@ -1753,8 +1742,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *fbg = ca.take<uint32_t>((size_t)(G.T + 31) / 32 + 2);  // fallback-cell bits (+2: fb_load's words)
     uint32_t *irr = ca.take<uint32_t>(P), *nirr = ca.take<uint32_t>(1);  // k_fine_count's queue
     uint2 *irect = ca.take<uint2>(P);  // reference rects in internal order
-    unsigned long long *eg = ca.take<unsigned long long>(4);  // [gathered, kUnsafe, kThin entries, -]
-    int32_t *rmax = ca.take<int32_t>(1);
+    unsigned long long *eg = ca.take<unsigned long long>(kShards * kShard64);  // per copy [gathered, kUnsafe, kThin entries]
+    int32_t *rmax = ca.take<int32_t>(kShards * kShard32);
     float2 *igm = ca.take<float2>(P);
     float4 *igc = ca.take<float4>(P);
     float4 *grec = ca.take<float4>(2 * (size_t)P);
@@ -1795,8 +1784,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     {  // one launch for every zero-fill of phase A (the sample sort writes fsrows but its slack)
         const size_t fs_written = (size_t)(N / 2 * 2) * D * 4;  // (the sort writes whole pairs; an odd N's last one from here)
         ZeroList zl;
-        zl.add(stile, sizeof(uint32_t) * (G.T + 1));
-        zl.add(gtile, sizeof(uint32_t) * (G.T + 1));
+        zl.add(stile, sizeof(uint32_t) * tcw);
+        zl.add(gtile, sizeof(uint32_t) * tcw);
         zl.add(cell_sbeg, sizeof(int32_t) * ncells);
         zl.add(cell_send, sizeof(int32_t) * ncells);
         if (nsub) {
@@ -1807,9 +1796,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(rbuf, (size_t)G.T * 8 + 8);
         zl.add(srbuf, (size_t)G.T * 8 + 8);
         zl.add(cnt2, sizeof(uint32_t) * kGatherRows * (size_t)ncells);
-        zl.add(eg, 32);
+        zl.add(eg, 8 * kShards * kShard64);
         zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
-        zl.add(rmax, 4);
+        zl.add(rmax, 4 * kShards * kShard32);
         zl.add(fbg, sizeof(uint32_t) * ((size_t)(G.T + 31) / 32 + 2));
         zl.add(nirr, 4);
         zl.add(rs_s, plan_s.zero_bytes);
@@ -1871,12 +1860,15 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             [=] __device__(int64_t i, uint64_t *x) { x[0] = fc[i]; x[1] = tc[i]; },
             [=] __device__(int64_t i, const uint64_t *, const uint64_t *ex) { fo[i] = ex[0]; to[i] = ex[1]; },
             [=] __device__(const uint64_t *t) {
-                tot[0] = (int64_t)t[1];                   // num_rendered (sampler_impl.cu:253-257)
-                tot[1] = (int64_t)t[0] + (int64_t)egc[0];  // all entries
-                tot[4] = (int64_t)t[0];                   // sort-path entries
-                tot[5] = (int64_t)egc[0];
-                tot[6] = (int64_t)egc[1];
-                tot[7] = (int64_t)egc[2];
+                unsigned long long ec[3] = {0, 0, 0};  // (the counters' copies)
+                for (int q = 0; q < kShards; ++q)
+                    for (int k = 0; k < 3; ++k) ec[k] += egc[q * kShard64 + k];
+                tot[0] = (int64_t)t[1];                  // num_rendered (sampler_impl.cu:253-257)
+                tot[1] = (int64_t)t[0] + (int64_t)ec[0];  // all entries
+                tot[4] = (int64_t)t[0];                  // sort-path entries
+                tot[5] = (int64_t)ec[0];
+                tot[6] = (int64_t)ec[1];
+                tot[7] = (int64_t)ec[2];
                 int32_t *g = reinterpret_cast<int32_t *>(tot + 2);
                 g[0] = dg ? dg[0] : 0;
                 g[1] = dg ? dg[1] : 0;
@@ -2088,7 +2080,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
-        k_sub_lists<<<(unsigned)ncells, kBlock, 0, s>>>(
+        k_sub_lists<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
             ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box, sub_box, G.CT, sub_lbeg, sub_lmid,
             sub_lend, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);

@@ -33,8 +33,11 @@ static_assert(kRsThreads == kRsBins, "one thread per digit in the look-back");
 constexpr uint64_t kRsAgg = 1ull << 62, kRsPre = 2ull << 62, kRsVal = (1ull << 62) - 1;
 
 // Host plan of one sort of n items over key bits [0, bits): scratch = [zeroed: histograms
-// u32[places][256], tickets u32[64], states u64[places][tiles][256]] [tmp keys u32[n]]
-// [tmp values u32[n]].  zero_bytes from the start must be zero before the sort.
+// u32[kRsHistCopies][places][256], tickets u32[64], states u64[places][tiles][256]] [tmp keys
+// u32[n]] [tmp values u32[n]].  zero_bytes from the start must be zero before the sort.  The
+// histograms are kept in one copy per XCD (block b adds to copy b % 8: one word takes only ~88
+// atomic adds per us) and summed by the passes.
+constexpr int kRsHistCopies = 8;
 struct RadixPlan {
     int64_t n = 0, tiles = 0;
     int places = 0;
@@ -46,7 +49,7 @@ inline RadixPlan radix_plan(int64_t n, int bits) {
     p.n = n;
     p.places = n > 0 ? (std::max(bits, 1) + kRsBits - 1) / kRsBits : 0;
     p.tiles = (n + kRsTile - 1) / kRsTile;
-    size_t o = align_up(4 * (size_t)p.places * kRsBins, 256);
+    size_t o = align_up(4 * (size_t)kRsHistCopies * p.places * kRsBins, 256);
     p.o_tickets = o;
     o += 256;
     p.o_states = o;
@@ -74,8 +77,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_hist(int64_t n, const KT *__r
         for (int p = 0; p < places; ++p) atomicAdd(&h[p * kRsBins + rs_digit(k, p * kRsBits)], 1u);
     }
     __syncthreads();
+    uint32_t *hc = hist + (size_t)(blockIdx.x & (kRsHistCopies - 1)) * places * kRsBins;
     for (int i = threadIdx.x; i < places * kRsBins; i += kRsThreads)
-        if (h[i]) atomicAdd(&hist[i], h[i]);
+        if (h[i]) atomicAdd(&hc[i], h[i]);
 }
 
 // exclusive scan over the block of one value per thread
@@ -111,7 +115,7 @@ struct RsNone {
 template <typename KT, class Extra>
 __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__restrict__ kin, KT *__restrict__ kout,
                                                         const uint32_t *__restrict__ vin, uint32_t *__restrict__ vout,
-                                                        int shift, const uint32_t *__restrict__ hist,
+                                                        int shift, const uint32_t *__restrict__ hist, int hstride,
                                                         unsigned long long *__restrict__ states,
                                                         uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
                                                         Extra extra) {
@@ -124,7 +128,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
     if (tid == 0) s_tile = (int)atomicAdd(ticket, 1u);
 #pragma unroll
     for (int q = 0; q < kRsWaves; ++q) cnt[q][tid] = 0u;
-    const uint32_t gcount = hist[tid];
+    uint32_t gcount = 0;  // (the histogram's copies, hstride words apart)
+#pragma unroll
+    for (int q = 0; q < kRsHistCopies; ++q) gcount += hist[q * hstride + tid];
     const uint32_t gbase = rs_block_excl(gcount, wsum);  // (its barriers also publish s_tile / cnt)
     const int64_t tile = s_tile;
     const int64_t base = tile * kRsTile;
@@ -240,12 +246,12 @@ static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const
         uint32_t *vo = to_out ? vout : tv;
         if (q == p.places - 1)  // (the last place: the payload too)
             k_rs_pass<KT, Extra><<<(unsigned)tiles, kRsThreads, 0, s>>>(
-                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, states + (size_t)q * p.tiles * kRsBins,
-                tickets + q, err, extra);
+                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, p.places * kRsBins,
+                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, extra);
         else
             k_rs_pass<KT, RsNone><<<(unsigned)tiles, kRsThreads, 0, s>>>(
-                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, states + (size_t)q * p.tiles * kRsBins,
-                tickets + q, err, RsNone{});
+                n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, p.places * kRsBins,
+                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, RsNone{});
         ki = ko;
         vi = vo;
     }
