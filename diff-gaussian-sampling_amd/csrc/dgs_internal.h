@@ -20,7 +20,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 8;
+constexpr uint32_t kVersion = 9;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -106,6 +106,12 @@ struct Header {
     int64_t fsub_cap, esub_cap;
     uint32_t zero[4];  // always 0: the "inputs differ" word of calls whose inputs the caller vouches for
     uint64_t o_rref;   // (rlist's inputs: tile-list offsets u32[P] by caller id, radii f32[P] by internal id)
+    // the sorted part of the cell lists (sort-path entries): per list position its Gaussian-major
+    // slot q (esum_q u32[E]), per cell where that part begins (cell_gsort i32[ncells]), per
+    // internal id its first slot (goff u32[P + 1]); the backward stores those entries' sums in
+    // slot order and k_bwd_esum adds them per Gaussian (no scattered atomics)
+    uint64_t o_esum_q, o_cell_gsort, o_goff;
+    int64_t Es;        // sort-path entries
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
@@ -118,7 +124,7 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
-    uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab, o_rref;
+    uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab, o_rref, o_esum_q, o_cell_gsort, o_goff;
     uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
@@ -155,6 +161,9 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_rlist = o;     o = align_up(o + 4 * (size_t)R + 64, 256);
     L.o_rtab = o;      o = align_up(o + 16 * ((size_t)T + 1), 256);
     L.o_rref = o;      o = align_up(o + 8 * (size_t)P, 256);
+    L.o_esum_q = o;    o = align_up(o + 4 * (size_t)E + 64, 256);
+    L.o_cell_gsort = o; o = align_up(o + 4 * (size_t)ncells, 256);
+    L.o_goff = o;      o = align_up(o + 4 * ((size_t)P + 1), 256);
     L.o_sub_lbeg = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
@@ -198,6 +207,8 @@ struct Bins {
     const uint2 *fsub_units;             // (sub-cell, pair-aligned first sample)
     const int32_t *sub_lbeg, *sub_lmid, *sub_lend;
     const uint32_t *sub_ent;             // sub lists: entries of the cell list, flagged last
+    const uint32_t *esum_q;              // sorted-part list position -> Gaussian-major slot
+    const int32_t *cell_gsort;           // first sorted-part position of each cell list
 };
 
 // Uniform (wave-invariant) loads through the constant address space: with a wave-uniform
@@ -255,6 +266,8 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.sub_lmid = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lmid));
     B.sub_lend = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lend));
     B.sub_ent = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_sub_ent));
+    B.esum_q = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_esum_q));
+    B.cell_gsort = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_cell_gsort));
     return B;
 }
 
@@ -530,6 +543,7 @@ struct UnitHint {
     int32_t P, D, N;  // the problem the buffers were built for (validate() checks calls against it)
     int64_t R;        // num_rendered (sizes the call-time path's backward grid)
     int64_t E;        // fine (Gaussian, cell) entries
+    int64_t Es;       // of which sort-path entries (the backward's slot sums)
     Header hdr;       // the header preprocess wrote (ensure_ref_lists reads its geometry / offsets)
     bool ref_built;   // rlist built (ensure_ref_lists), ref_done recorded after its build
     hipEvent_t ref_done;

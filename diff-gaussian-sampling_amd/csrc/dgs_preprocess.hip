@@ -1072,19 +1072,32 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
 }
 
 // The sorted path's half-cells copied behind each cell's gathered entries (one wave per cell).
+// sq: the sort's values, the entries' Gaussian-major positions q (k_fine_fill's order); the
+// entry itself is evals[q], and q is kept as the position's backward slot (esum_q).
 __global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32_t *__restrict__ gcnt,
                                                         const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
                                                         const int32_t *__restrict__ gbeg,
                                                         const int32_t *__restrict__ gmid,
-                                                        const uint32_t *__restrict__ svals,
-                                                        uint32_t *__restrict__ entries) {
+                                                        const uint32_t *__restrict__ sq,
+                                                        const uint32_t *__restrict__ evals,
+                                                        uint32_t *__restrict__ entries, uint32_t *__restrict__ esum_q,
+                                                        int32_t *__restrict__ gsort) {
     const int c = blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
     if (c >= ncells) return;
     const int lane = threadIdx.x & (kWave - 1);
     const int32_t u0 = hb[2 * c], u1 = he[2 * c], f0 = hb[2 * c + 1], f1 = he[2 * c + 1];
     const int32_t du = gbeg[c] + (int32_t)gcnt[c], df = gmid[c];
-    for (int32_t k = lane; k < u1 - u0; k += kWave) entries[du + k] = svals[u0 + k];
-    for (int32_t k = lane; k < f1 - f0; k += kWave) entries[df + k] = svals[f0 + k];
+    if (lane == 0) gsort[c] = du;
+    for (int32_t k = lane; k < u1 - u0; k += kWave) {
+        const uint32_t q = sq[u0 + k];
+        entries[du + k] = evals[q];
+        esum_q[du + k] = q;
+    }
+    for (int32_t k = lane; k < f1 - f0; k += kWave) {
+        const uint32_t q = sq[f0 + k];
+        entries[df + k] = evals[q];
+        esum_q[df + k] = q;
+    }
 }
 
 // D = 2: the bounding boxes of a cell's four sub-cells and of the cell (their union), one wave
@@ -1421,8 +1434,9 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
 // over the permutation instead of two launches).
 __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float2 *__restrict__ igm,
                            const float4 *__restrict__ igc, const uint64_t *__restrict__ toffs,
+                           const uint64_t *__restrict__ foffs, const uint64_t *__restrict__ fcount,
                            float2 *__restrict__ gmean, float4 *__restrict__ gcon, int32_t *__restrict__ gperm,
-                           uint32_t *__restrict__ rref) {
+                           uint32_t *__restrict__ rref, uint32_t *__restrict__ goff) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
     const int64_t g = perm[i];
@@ -1436,6 +1450,9 @@ __global__ void k_geo_pack(int P, const uint32_t *__restrict__ perm, const float
     // in internal order
     rref[i] = (uint32_t)toffs[i];
     rref[P + i] = __float_as_uint(c.w);
+    // the Gaussian-major slots of the sort-path entries (k_fine_fill's offsets; < 2^31)
+    goff[i] = (uint32_t)foffs[i];
+    if (i == P - 1) goff[P] = (uint32_t)(foffs[i] + fcount[i]);
 }
 
 // Forward sample pair rows in sorted order: pair p = samples 2p, 2p+1, field-interleaved
@@ -1930,11 +1947,12 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(B.rs_e, B.plan_e.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
         DGS_LAUNCH_CHECK(s, debug);
-        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc, toffs,
+        k_geo_pack<<<grid_for(P), kBlock, 0, s>>>(P, perm, igm, igc, toffs, foffs, fcount,
                                                   reinterpret_cast<float2 *>(B.gbuf + B.L.o_gmean),
                                                   reinterpret_cast<float4 *>(B.gbuf + B.L.o_gcon),
                                                   reinterpret_cast<int32_t *>(B.gbuf + B.L.o_perm),
-                                                  reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rref));
+                                                  reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_rref),
+                                                  reinterpret_cast<uint32_t *>(B.gbuf + B.L.o_goff));
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
@@ -2004,9 +2022,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
                                                             fcount, greach, fbg, irect, ekeys, evals, counters);
         DGS_LAUNCH_CHECK(s, debug);
+        // (values: the entries' positions q, for the backward's slots; k_copy_sorted gathers evals[q])
         DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),
-                                               reinterpret_cast<uint16_t *>(ekeys_sorted), evals, svals, s)
-                        : radix_sort<uint32_t>(B.plan_e, Es, B.rs_e, ekeys, ekeys_sorted, evals, svals, s));
+                                               reinterpret_cast<uint16_t *>(ekeys_sorted), nullptr, svals, s)
+                        : radix_sort<uint32_t>(B.plan_e, Es, B.rs_e, ekeys, ekeys_sorted, nullptr, svals, s));
         DGS_LAUNCH_CHECK(s, debug);
         if (k16)
             k_identify<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(Es, reinterpret_cast<const uint16_t *>(ekeys_sorted),
@@ -2045,7 +2064,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     }
     if (Es > 0) {
         k_copy_sorted<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
-            ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, entries);
+            ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, evals, entries,
+            reinterpret_cast<uint32_t *>(gbuf + L.o_esum_q), reinterpret_cast<int32_t *>(gbuf + L.o_cell_gsort));
         DGS_LAUNCH_CHECK(s, debug);
     }
     {  // work units: forward (cell, 64 pair-aligned samples), backward (cell, 64 list entries)
@@ -2139,6 +2159,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_fwd_units = L0.o_fwd_units; h.o_cell_box = L0.o_cell_box; h.s_bytes = L0.s_bytes;
     h.o_gmean = L.o_gmean; h.o_gcon = L.o_gcon; h.o_fsrows = L0.o_fsrows;
     h.o_mcopy = L.o_mcopy; h.o_ccopy = L.o_ccopy; h.o_rlist = L.o_rlist; h.o_rtab = L.o_rtab; h.o_rref = L.o_rref;
+    h.o_esum_q = L.o_esum_q; h.o_cell_gsort = L.o_cell_gsort; h.o_goff = L.o_goff; h.Es = Es;
     h.o_scopy = L0.o_scopy;
     h.o_sub_sbeg = L0.o_sub_sbeg; h.o_sub_send = L0.o_sub_send; h.o_sub_box = L0.o_sub_box;
     h.o_fsub_units = L0.o_fsub_units;
@@ -2159,7 +2180,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6]; uh.nthin = htot[7];
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
-    uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E;
+    uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E; uh.Es = Es;
     uh.hdr = h;
     uh.ref_built = false;
     uh.ref_done = nullptr;

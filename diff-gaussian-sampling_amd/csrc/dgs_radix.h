@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
         const int64_t i = cb + (int64_t)k * kWave;
         const bool ok = i < n;
         key[k] = ok ? (uint32_t)kin[i] : 0u;
-        val[k] = ok ? vin[i] : 0u;
+        val[k] = ok ? (vin ? vin[i] : (uint32_t)i) : 0u;  // (vin null: the values are the input positions)
     }
     const uint64_t lt = (1ull << lane) - 1ull;
 #pragma unroll
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
 }
 
 // The sort of n <= p.n items: keys kin (KT) / values vin -> kout / vout, stable, over the key
-// bits the plan was made for.  scratch: p.bytes, its first p.zero_bytes zero-filled beforehand
+// bits the plan was made for (vin null: the values are the input positions 0 .. n - 1).  scratch: p.bytes, its first p.zero_bytes zero-filled beforehand
 // (once: a plan's scratch serves one sort).  The look-back's give-up word is tickets[63].
 // hist_ready: the keys' producer has already added their digit counts into the plan's
 // histograms (radix_hist; dgs_preprocess.hip's RsHist), so the histogram launch is skipped.

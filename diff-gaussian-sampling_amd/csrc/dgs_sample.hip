@@ -1173,14 +1173,21 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     }
 }
 
+// The slot row width of a Gaussian's sums (k_bwd_esum): [dm(D) dc(S) dv(CB)] padded to 4 floats.
+template <int FN, int D, int CB>
+__host__ __device__ constexpr int esum_stride() {
+    return (D + Traits<FN, D>::S + CB + 3) / 4 * 4;
+}
+
 // One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
-// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane.
+// conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane
+// (a slot store for the sorted part, below).
 template <int FN, int D, int CB>
 __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restrict__ srows,
                                          float *__restrict__ acc, int P, int vrow0, uint2 u,
                                          uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
-                                         float4 cr, int lane) {
-    constexpr int S = Traits<FN, D>::S;
+                                         float4 cr, int lane, float *__restrict__ esums) {
+    constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
     const int cell = (int)u.x, eb = (int)u.y;
     const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
     const bool active = eb + lane < ee;
@@ -1188,7 +1195,23 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
     const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
     float sm[2], sc[3], sv[CB];
     bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, cr, sm, sc, sv);
-    if (active) {
+    // Sort-path entries (the sorted part of the list: scattered ids, one cache line per lane and
+    // atomic) store their sums in their Gaussian-major slot instead; k_bwd_esum adds them up.
+    const bool slot = esums != nullptr && eb + lane >= sload(&bins.cell_gsort[cell]);
+    if (active && slot) {
+        float row[SSW];
+#pragma unroll
+        for (int k = 0; k < SSW; ++k) row[k] = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) row[d] = sm[d];
+#pragma unroll
+        for (int k = 0; k < S; ++k) row[D + k] = sc[k];
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) row[D + S + ch] = sv[ch];
+        float4 *o = reinterpret_cast<float4 *>(esums + (int64_t)bins.esum_q[eb + lane] * SSW);
+#pragma unroll
+        for (int k = 0; k < SSW / 4; ++k) o[k] = make_float4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+    } else if (active) {
 #pragma unroll
         for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
 #pragma unroll
@@ -1213,7 +1236,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
                                                      const float *__restrict__ grows,
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0,
-                                                     const uint32_t *__restrict__ dirty) {
+                                                     const uint32_t *__restrict__ dirty, float *__restrict__ esums) {
     if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
     constexpr int RS = grow_stride<FN, D, CB>();
     const Bins bins = resolve(gbuf, sbuf);
@@ -1225,8 +1248,40 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
         const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
         load_grow<RS>(grows, ent, r);
-        bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane);
+        bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane, esums);
     }
+}
+
+// The sort-path entries' sums (k_backward's slots), per Gaussian in slot order -- its entries'
+// order of k_fine_fill -- added to the atomics' sums (plain adds: k_backward has finished).
+template <int FN, int D, int CB>
+__global__ void k_bwd_esum(int P, const char *__restrict__ gbuf, const float *__restrict__ esums,
+                           float *__restrict__ acc, int vrow0, const uint32_t *__restrict__ dirty) {
+    if (sload(dirty)) return;  // (k_backward wrote no slot)
+    constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= P) return;
+    const Header *h = reinterpret_cast<const Header *>(gbuf);
+    const uint32_t *goff = reinterpret_cast<const uint32_t *>(gbuf + h->o_goff);
+    const uint32_t q0 = goff[i], q1 = goff[i + 1];
+    if (q0 >= q1) return;
+    float sum[SSW];
+#pragma unroll
+    for (int k = 0; k < SSW; ++k) sum[k] = 0.0f;
+    for (uint32_t q = q0; q < q1; ++q) {
+        const float4 *rw = reinterpret_cast<const float4 *>(esums + (int64_t)q * SSW);
+#pragma unroll
+        for (int k = 0; k < SSW / 4; ++k) {
+            const float4 x = rw[k];
+            sum[4 * k] += x.x; sum[4 * k + 1] += x.y; sum[4 * k + 2] += x.z; sum[4 * k + 3] += x.w;
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) acc[(int64_t)d * P + i] += sum[d];
+#pragma unroll
+    for (int k = 0; k < S; ++k) acc[(int64_t)(D + k) * P + i] += sum[D + k];
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) acc[(int64_t)(vrow0 + ch) * P + i] += sum[D + S + ch];
 }
 
 // Internal (spatial) order -> caller order: thread = caller id g gathers its six sums from
@@ -1532,6 +1587,19 @@ static int run_backward(const Call &a) {
     uint32_t *const flag = dirty_word(a, check);
     constexpr int S = D * (D + 1) / 2;
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
+    // the sort-path entries' slots (one channel block: the sums of a multi-block C accumulate
+    // over the blocks, so those keep the atomics; buffers without a hint keep them too)
+    UnitHint hint;
+    const int64_t Es = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) ? hint.Es : 0;
+    struct SlotBuf {  // (stream-ordered; freed on every return)
+        float *p = nullptr;
+        hipStream_t s;
+        ~SlotBuf() { if (p) (void)hipFreeAsync(p, s); }
+    } slots{nullptr, a.s};
+    if (Es > 0 && a.C <= CB)
+        DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&slots.p),
+                                   sizeof(float) * esum_stride<FN, D, CB>() * (size_t)Es, a.s));
+    float *const esums = slots.p;
     if (!binned)
         if (int rc = ensure_ref_lists(a.gb, a.gbytes, a.sb, a.sbytes, a.s, a.debug)) return rc;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
@@ -1552,7 +1620,10 @@ static int run_backward(const Call &a) {
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s);
-            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag);
+            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag,
+                                                               esums);
+            if (esums)
+                k_bwd_esum<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, esums, acc, D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if (!binned) {
