@@ -1589,8 +1589,11 @@ static int run_backward(const Call &a) {
     const unsigned blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, true);
     // the sort-path entries' slots (one channel block: the sums of a multi-block C accumulate
     // over the blocks, so those keep the atomics; buffers without a hint keep them too)
+    // Only where the sort path holds a large share of the entries (thin fields: 70 %): at the
+    // headline (2 %) the slot pass costs more than the few scattered atomics it replaces.
     UnitHint hint;
-    const int64_t Es = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint) ? hint.Es : 0;
+    const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
+    const int64_t Es = hinted && 4 * hint.Es >= hint.E ? hint.Es : 0;
     struct SlotBuf {  // (stream-ordered; freed on every return)
         float *p = nullptr;
         hipStream_t s;

@@ -171,7 +171,17 @@ def test_spatial_sampler_two_ranks_real_C(dgs, oracle, tmp_path):
     _loop(dd.ShardedGaussianSampler(), m, v, c, samples.to(dev), w.to(dev), ADAM_STEPS, False)
     refp = {"m": m.detach().cpu().numpy(), "v": v.detach().cpu().numpy(), "c": c.detach().cpu().numpy()}
     assert not np.allclose(refp["m"], means.numpy())
+    # Adam divides each step by the gradient's running RMS, so where the exact gradient is at the
+    # float noise of two summation orders (|g| within the parity bound of 0) the two runs' updates
+    # may differ by up to the step size itself; there the check is that bound, elsewhere 2e-5
+    # (the first step's full gradient: the owned rows of the two ranks)
+    full = {k: sum(r[gk] for r in ranks) for k, gk in (("m", "gm"), ("v", "gv"), ("c", "gc"))}
     for r in ranks:
         h = r["held"]
         for k in ("m", "v", "c"):
-            np.testing.assert_allclose(r[k][h], refp[k][h], rtol=2e-5, atol=1e-6 * np.abs(refp[k]).max())
+            g = np.abs(full[k]).reshape(refp[k].shape)
+            noise = g <= 10 * ATOL_BWD * g.max()
+            a, b = r[k][h], refp[k][h]
+            nz = noise[h]
+            np.testing.assert_allclose(a[~nz], b[~nz], rtol=2e-5, atol=1e-6 * np.abs(refp[k]).max())
+            assert np.all(np.abs(a[nz] - b[nz]) <= 2 * ADAM_LR * ADAM_STEPS), k
