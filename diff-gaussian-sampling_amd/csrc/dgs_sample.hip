@@ -663,7 +663,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
         const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
         const int hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
         const int gb = sload(&bins.sub_lbeg[sc]), gm = sload(&bins.sub_lmid[sc]), ge = sload(&bins.sub_lend[sc]);
-        if (THIN && gm == ge) continue;  // (no flagged entry in this sub list)
+        // (the thin pass: a sub list's kThin entries are its last ones -- the entry sort's order --
+        // so a list whose last entry is not kThin has none)
+        if (THIN && (gm == ge || !(sload(&bins.sub_ent[ge - 1]) & kThin))) continue;
         float ctr[2];
         cell_center<D>(bins, cell, ctr);
         for (int ps = sb; ps < hi; ps += NS) {
