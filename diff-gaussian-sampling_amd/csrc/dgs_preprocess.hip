@@ -815,7 +815,7 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
                                                        uint64_t *__restrict__ counts, int8_t *__restrict__ greach,
                                                        uint32_t *__restrict__ lrows, int32_t *__restrict__ rmax,
                                                        uint32_t *__restrict__ irr, uint32_t *__restrict__ nirr,
-                                                       unsigned long long *__restrict__ nflag) {
+                                                       int qcap, unsigned long long *__restrict__ nflag) {
     FC_T(0);
     const FbBits fbits = fb_load(fbg, G.T);
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -860,9 +860,11 @@ __global__ __launch_bounds__(kBlock) void k_fine_count(int P, Geom G, const floa
     const int lane = threadIdx.x & (kWave - 1);
     uint32_t qbase = 0;
     if (qm) {
-        if (lane == 0) qbase = atomicAdd(nirr, (uint32_t)__popcll(qm));
+        // (the queue in kShards parts, one counter each: in thin fields most waves queue)
+        const int sh = shard_of_block();
+        if (lane == 0) qbase = atomicAdd(&nirr[sh * kShard32], (uint32_t)__popcll(qm));
         qbase = __shfl(qbase, 0);
-        if (queue) irr[qbase + (uint32_t)__popcll(qm & ((1ull << lane) - 1ull))] = (uint32_t)i;
+        if (queue) irr[(int64_t)sh * qcap + qbase + (uint32_t)__popcll(qm & ((1ull << lane) - 1ull))] = (uint32_t)i;
     }
     for (int off = kWave / 2; off > 0; off >>= 1) {
         reach = max(reach, __shfl_xor(reach, off));
@@ -887,13 +889,14 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
                                                            const int32_t *__restrict__ send, const float4 *__restrict__ box,
                                                            const uint32_t *__restrict__ fbg, const int8_t *__restrict__ greach,
                                                            const uint32_t *__restrict__ irr, const uint32_t *__restrict__ nirr,
-                                                           uint64_t *__restrict__ counts,
+                                                           int qcap, uint64_t *__restrict__ counts,
                                                            unsigned long long *__restrict__ nflag) {
     const FbBits fbits = fb_load(fbg, G.T);
-    const uint32_t nq = sload(nirr);
     uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < nq; q += gridDim.x * blockDim.x) {
-        const uint32_t i = irr[q];
+    for (int sh = 0; sh < kShards; ++sh)  // (the queue's parts)
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, nq = sload(&nirr[sh * kShard32]); q < nq;
+         q += gridDim.x * blockDim.x) {
+        const uint32_t i = irr[(int64_t)sh * qcap + q];
         const float2 mm = igm[i];
         const float4 cc = igc[i];
         const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
@@ -1072,32 +1075,25 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
 }
 
 // The sorted path's half-cells copied behind each cell's gathered entries (one wave per cell).
-// sq: the sort's values, the entries' Gaussian-major positions q (k_fine_fill's order); the
-// entry itself is evals[q], and q is kept as the position's backward slot (esum_q).
-__global__ __launch_bounds__(kBlock) void k_copy_sorted(int ncells, const uint32_t *__restrict__ gcnt,
-                                                        const int32_t *__restrict__ hb, const int32_t *__restrict__ he,
-                                                        const int32_t *__restrict__ gbeg,
-                                                        const int32_t *__restrict__ gmid,
-                                                        const uint32_t *__restrict__ sq,
-                                                        const uint32_t *__restrict__ evals,
-                                                        uint32_t *__restrict__ entries, uint32_t *__restrict__ esum_q,
-                                                        int32_t *__restrict__ gsort) {
-    const int c = blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6);
-    if (c >= ncells) return;
-    const int lane = threadIdx.x & (kWave - 1);
-    const int32_t u0 = hb[2 * c], u1 = he[2 * c], f0 = hb[2 * c + 1], f1 = he[2 * c + 1];
-    const int32_t du = gbeg[c] + (int32_t)gcnt[c], df = gmid[c];
-    if (lane == 0) gsort[c] = du;
-    for (int32_t k = lane; k < u1 - u0; k += kWave) {
-        const uint32_t q = sq[u0 + k];
-        entries[du + k] = evals[q];
-        esum_q[du + k] = q;
-    }
-    for (int32_t k = lane; k < f1 - f0; k += kWave) {
-        const uint32_t q = sq[f0 + k];
-        entries[df + k] = evals[q];
-        esum_q[df + k] = q;
-    }
+// The sorted path's entries copied behind each cell's gathered ones, one thread per sorted
+// position r: its key gives the cell and the class (key >> 1 = (cell, flagged)), hb the class's
+// first sorted position.  sq: the sort's values, the entries' Gaussian-major positions q
+// (k_fine_fill's order); the entry itself is evals[q], and q is kept as the list position's
+// backward slot (esum_q).
+template <typename KT>
+__global__ void k_copy_sorted(int64_t Es, const KT *__restrict__ keys, const uint32_t *__restrict__ sq,
+                              const uint32_t *__restrict__ evals, const int32_t *__restrict__ hb,
+                              const int32_t *__restrict__ gbeg, const int32_t *__restrict__ gmid,
+                              const uint32_t *__restrict__ gcnt, uint32_t *__restrict__ entries,
+                              uint32_t *__restrict__ esum_q) {
+    const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= Es) return;
+    const uint32_t key = (uint32_t)keys[r], c = key >> 2;
+    const bool fl = (key >> 1) & 1u;
+    const int64_t p = fl ? (int64_t)gmid[c] + (r - hb[2 * c + 1]) : (int64_t)gbeg[c] + gcnt[c] + (r - hb[2 * c]);
+    const uint32_t q = sq[r];
+    entries[p] = evals[q];
+    esum_q[p] = q;
 }
 
 // D = 2: the bounding boxes of a cell's four sub-cells and of the cell (their union), one wave
@@ -1757,7 +1753,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uint32_t *hstart = ca.take<uint32_t>((size_t)HK + 1), *gcnt = ca.take<uint32_t>(ncells);
     uint32_t *cnt2 = ca.take<uint32_t>((size_t)kGatherRows * ncells);
     uint32_t *fbg = ca.take<uint32_t>((size_t)(G.T + 31) / 32 + 2);  // fallback-cell bits (+2: fb_load's words)
-    uint32_t *irr = ca.take<uint32_t>(P), *nirr = ca.take<uint32_t>(1);  // k_fine_count's queue
+    // k_fine_count's queue: kShards parts of qcap ids (a part takes the blocks b = s mod kShards)
+    const int qcap = (int)((grid_for(P) + kShards - 1) / kShards) * kBlock;
+    uint32_t *irr = ca.take<uint32_t>((size_t)kShards * qcap), *nirr = ca.take<uint32_t>(kShards * kShard32);
     uint2 *irect = ca.take<uint2>(P);  // reference rects in internal order
     unsigned long long *eg = ca.take<unsigned long long>(kShards * kShard64);  // per copy [gathered, kUnsafe, kThin entries]
     int32_t *rmax = ca.take<int32_t>(kShards * kShard32);
@@ -1817,7 +1815,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(fscan_a, 8 * fused_scan_state_words(P, 2, 8));
         zl.add(rmax, 4 * kShards * kShard32);
         zl.add(fbg, sizeof(uint32_t) * ((size_t)(G.T + 31) / 32 + 2));
-        zl.add(nirr, 4);
+        zl.add(nirr, 4 * kShards * kShard32);
         zl.add(rs_s, plan_s.zero_bytes);
         zl.add(rs_h, plan_h.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
@@ -1850,10 +1848,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     k_gauss_permute<<<grid_for(P), kBlock, 0, s>>>(P, perm, grec, igm, igc, irect);
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count<<<grid_for(P), kBlock, 0, s>>>(P, G, igm, igc, irect, fbg, fcount, greach, lrows, rmax, irr, nirr,
-                                                eg + 1);
+                                                qcap, eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count_irr<<<std::min(grid_for(P), 2048u), kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg,
-                                                                     greach, irr, nirr, fcount, eg + 1);
+                                                                     greach, irr, nirr, qcap, fcount, eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
                                                kWavesPerBlock - 1) / kWavesPerBlock);
@@ -2039,6 +2037,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         const int32_t *hb = hbeg, *he = hend;
         uint32_t *gc = gcnt;
         int32_t *gb_ = cell_gbeg, *gm_ = cell_gmid, *ge_ = cell_gend;
+        int32_t *gs_ = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gsort);  // (where each sorted part begins)
         DGS_TRY_HIP((fused_scan<1, 1>(
             (int64_t)ncells, B.fs_cells,
             [=] __device__(int64_t c, uint64_t *x) {
@@ -2053,6 +2052,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                 gb_[c] = b;
                 gm_[c] = mid;
                 ge_[c] = mid + (he[2 * c + 1] - hb[2 * c + 1]);
+                gs_[c] = b + (int32_t)gc[c];
             },
             [=] __device__(const uint64_t *) {}, s)));
         DGS_LAUNCH_CHECK(s, debug);
@@ -2063,9 +2063,14 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
     }
     if (Es > 0) {
-        k_copy_sorted<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
-            ncells, gcnt, hbeg, hend, cell_gbeg, cell_gmid, svals, evals, entries,
-            reinterpret_cast<uint32_t *>(gbuf + L.o_esum_q), reinterpret_cast<int32_t *>(gbuf + L.o_cell_gsort));
+        uint32_t *eq = reinterpret_cast<uint32_t *>(gbuf + L.o_esum_q);
+        if (k16)
+            k_copy_sorted<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(
+                Es, reinterpret_cast<const uint16_t *>(ekeys_sorted), svals, evals, hbeg, cell_gbeg, cell_gmid, gcnt,
+                entries, eq);
+        else
+            k_copy_sorted<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, svals, evals, hbeg, cell_gbeg,
+                                                                    cell_gmid, gcnt, entries, eq);
         DGS_LAUNCH_CHECK(s, debug);
     }
     {  // work units: forward (cell, 64 pair-aligned samples), backward (cell, 64 list entries)

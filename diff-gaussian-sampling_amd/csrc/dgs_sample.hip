@@ -1256,21 +1256,28 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
 
 // The sort-path entries' sums (k_backward's slots), per Gaussian in slot order -- its entries'
 // order of k_fine_fill -- added to the atomics' sums (plain adds: k_backward has finished).
+// (kEsumLanes lanes per Gaussian stride over its slots, 32-byte rows side by side, then a
+// shuffle reduction: one thread per Gaussian walked ~24 rows serially in thin fields)
+constexpr int kEsumLanes = 8;
 template <int FN, int D, int CB>
 __global__ void k_bwd_esum(int P, const char *__restrict__ gbuf, const float *__restrict__ esums,
                            float *__restrict__ acc, int vrow0, const uint32_t *__restrict__ dirty) {
     if (sload(dirty)) return;  // (k_backward wrote no slot)
     constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= P) return;
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t i = t / kEsumLanes;
+    const int sub = (int)(t & (kEsumLanes - 1));
     const Header *h = reinterpret_cast<const Header *>(gbuf);
     const uint32_t *goff = reinterpret_cast<const uint32_t *>(gbuf + h->o_goff);
-    const uint32_t q0 = goff[i], q1 = goff[i + 1];
-    if (q0 >= q1) return;
+    uint32_t q0 = 0, q1 = 0;
+    if (i < P) {
+        q0 = goff[i];
+        q1 = goff[i + 1];
+    }
     float sum[SSW];
 #pragma unroll
     for (int k = 0; k < SSW; ++k) sum[k] = 0.0f;
-    for (uint32_t q = q0; q < q1; ++q) {
+    for (uint32_t q = q0 + sub; q < q1; q += kEsumLanes) {
         const float4 *rw = reinterpret_cast<const float4 *>(esums + (int64_t)q * SSW);
 #pragma unroll
         for (int k = 0; k < SSW / 4; ++k) {
@@ -1278,6 +1285,11 @@ __global__ void k_bwd_esum(int P, const char *__restrict__ gbuf, const float *__
             sum[4 * k] += x.x; sum[4 * k + 1] += x.y; sum[4 * k + 2] += x.z; sum[4 * k + 3] += x.w;
         }
     }
+#pragma unroll
+    for (int off = kEsumLanes / 2; off > 0; off >>= 1)
+#pragma unroll
+        for (int k = 0; k < SSW; ++k) sum[k] += __shfl_xor(sum[k], off);
+    if (i >= P || sub != 0 || q0 >= q1) return;
 #pragma unroll
     for (int d = 0; d < D; ++d) acc[(int64_t)d * P + i] += sum[d];
 #pragma unroll
@@ -1628,7 +1640,8 @@ static int run_backward(const Call &a) {
             k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag,
                                                                esums);
             if (esums)
-                k_bwd_esum<FN, D, CB><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.gb, esums, acc, D + S + cbase, flag);
+                k_bwd_esum<FN, D, CB><<<grid_for((int64_t)a.P * kEsumLanes), kBlock, 0, a.s>>>(a.P, a.gb, esums, acc,
+                                                                                             D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
         if (!binned) {
