@@ -893,10 +893,16 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
                                                            unsigned long long *__restrict__ nflag) {
     const FbBits fbits = fb_load(fbg, G.T);
     uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
-    for (int sh = 0; sh < kShards; ++sh)  // (the queue's parts)
-    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, nq = sload(&nirr[sh * kShard32]); q < nq;
-         q += gridDim.x * blockDim.x) {
-        const uint32_t i = irr[(int64_t)sh * qcap + q];
+    // (the queue's parts, as one index range over their concatenation)
+    uint32_t pre[kShards + 1];
+    pre[0] = 0;
+#pragma unroll
+    for (int sh = 0; sh < kShards; ++sh) pre[sh + 1] = pre[sh] + sload(&nirr[sh * kShard32]);
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < pre[kShards]; q += gridDim.x * blockDim.x) {
+        int sh = 0;
+#pragma unroll
+        for (int k = 1; k < kShards; ++k) sh += q >= pre[k] ? 1 : 0;
+        const uint32_t i = irr[(int64_t)sh * qcap + (q - pre[sh])];
         const float2 mm = igm[i];
         const float4 cc = igc[i];
         const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
