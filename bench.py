@@ -16,9 +16,9 @@ Workload (BASELINE.json configs): 1M anisotropic 2-D Gaussians, C = 1.
         [dmeans | dvalues | dconics] gradients per step (the north star's formulation).
     `--weak` keeps 2M query points per GPU instead.
 One step = forward + backward through the autograd Function (+ the gradient exchange for N > 1);
-binning (preprocess) is timed separately, as the metric asks.  The K timed steps carry no kernel
-events; K more steps follow with HIP events on the render kernels' stream (kernels_ms, roofline:
-an event record opens a ~5 us gap between kernels, ~1.4 % of a step).
+binning (preprocess) is timed separately, as the metric asks.  kernels_ms and the roofline come
+from HIP events on the render kernels' stream over every 4th timed step and the last (an event
+record opens a ~5 us gap between kernels: events on every step would add ~1.4 % to it).
 
 `python bench.py --gpus N` without a torch.distributed environment starts the N ranks itself
 (a torch.distributed.run child, before this process touches the GPU) and exits with its code;
@@ -311,25 +311,22 @@ def bench_sample(args, world, rank, dev, torch, dist):
 
     for _ in range(args.warmup):
         step()
-    # The timed steps run without kernel events (each event record opened a ~5 us gap between
-    # the step's kernels: 4 per step, ~1.4 % of it); the same number of steps then runs again
-    # with HIP events around the two render kernels for kernels_ms / the roofline.
+    # HIP events around the two render kernels (kernels_ms, the roofline) on every 4th timed step
+    # (and the last): an event record opens a ~5 us gap between the step's kernels, 4 per step,
+    # so events on every step would add ~1.4 % to the step they time.
+    dgs._C.timing_read(0)
+    dgs._C.timing_read(1)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for k in range(args.steps):
+        dgs._C.timing_enable(k % 4 == 3 or k == args.steps - 1)
         step(timed=True)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    dgs._C.timing_read(0)
-    dgs._C.timing_read(1)
-    dgs._C.timing_enable(True)
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
     dgs._C.timing_enable(False)
     nf, fms = dgs._C.timing_read(0)
     nb, bms = dgs._C.timing_read(1)
