@@ -134,6 +134,8 @@ def main():
     ap.add_argument("--cpu-oracle-samples", type=int, default=2048,
                     help="query points of the 1-thread C-oracle CPU baseline sample")
     ap.add_argument("--pre-reps", type=int, default=5, help="warm preprocess repetitions (median)")
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed steps for this long before the timed ones (0: none; the clock ramp)")
     ap.add_argument("--grid3", type=int, default=128,
                     help="--op volume: query points on a g^3 lattice (BASELINE config 5 names 256)")
     ap.add_argument("--op", default="sample", choices=["sample", "aggregate", "volume"],
@@ -311,23 +313,51 @@ def bench_sample(args, world, rank, dev, torch, dist):
 
     for _ in range(args.warmup):
         step()
-    # HIP events around the two render kernels (kernels_ms, the roofline) on every 4th timed step
-    # (and the last): an event record opens a ~5 us gap between the step's kernels, 4 per step,
-    # so events on every step would add ~1.4 % to the step they time.
-    dgs._C.timing_read(0)
-    dgs._C.timing_read(1)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        dgs._C.timing_enable(k % 4 == 3 or k == args.steps - 1)
-        step(timed=True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    dgs._C.timing_enable(False)
+
+    def timed_block(events):
+        # HIP events around the two render kernels (kernels_ms, the roofline) on every 4th timed
+        # step (and the last): an event record opens a ~5 us gap between the step's kernels, 4
+        # per step, so events on every step would add ~1.4 % to the step they time.
+        ar_ev.clear()
+        push_ev.clear()
+        dgs._C.timing_read(0)
+        dgs._C.timing_read(1)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for k in range(args.steps):
+            dgs._C.timing_enable(events and (k % 4 == 3 or k == args.steps - 1))
+            step(timed=True)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        dgs._C.timing_enable(False)
+        return el
+
+    # The render kernels run ~25 % slower for the first ~30 ms of sustained work (the clock ramp,
+    # profiles/r04_clock_ramp.txt): K steps right after the W warmup steps are timed
+    # and reported (ms_per_step_unsettled), then steps run until --settle-ms of them have passed,
+    # and the K timed steps of the line follow, at the clocks a training loop runs at.
+    unsettled_ms = timed_block(False) * 1e3 / args.steps if args.settle_ms > 0 else None
+    settle_steps, t_settle = 0, time.perf_counter()
+
+    def settling():  # (N > 1: rank 0's clock decides, every rank steps the same number of times)
+        go = args.settle_ms > 0 and settle_steps < 1000 and (time.perf_counter() - t_settle) * 1e3 < args.settle_ms
+        if world > 1:
+            flag = torch.tensor([1.0 if go else 0.0], device=dev)
+            dist.broadcast(flag, 0)
+            go = bool(flag.item() > 0)
+        return go
+
+    while settling():
+        for _ in range(4):
+            step()
+        settle_steps += 4
+        torch.cuda.synchronize()
+    settle_ms = (time.perf_counter() - t_settle) * 1e3
+    elapsed = timed_block(True)
     nf, fms = dgs._C.timing_read(0)
     nb, bms = dgs._C.timing_read(1)
     rank_ms = elapsed * 1e3 / args.steps
@@ -399,6 +429,9 @@ def bench_sample(args, world, rank, dev, torch, dist):
         "vs_baseline": None,
         "dtype": "f32",
         "data": "synthetic (seeded uniform means/samples, anisotropic covariances, N(0,1) values)",
+        # untimed steps between the warmup and the timed ones, and the K steps timed right after
+        # the warmup (before them): the render kernels' clock ramp
+        "settle": {"steps": settle_steps, "ms": settle_ms, "ms_per_step_unsettled": unsettled_ms},
         "config": {"workload": workload, "gaussians": P, "query_points_per_gpu": N,
                    "query_points_total": N * world, "channels": C, "function": fname,
                    "parallelism": f"query-point shards x{world}, Gaussians replicated"
