@@ -20,7 +20,7 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 9;
+constexpr uint32_t kVersion = 10;
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
@@ -112,6 +112,7 @@ struct Header {
     // slot order and k_bwd_esum adds them per Gaussian (no scattered atomics)
     uint64_t o_esum_q, o_cell_gsort, o_goff;
     int64_t Es;        // sort-path entries
+    uint64_t o_sub_lthin;  // per sub list: where its kThin entries begin (int32[4 ncells]; = lend without any)
 };
 constexpr size_t kHeaderBytes = 512;
 static_assert(sizeof(Header) <= kHeaderBytes, "header too large");
@@ -125,7 +126,7 @@ __host__ __device__ inline size_t align_up(size_t x, size_t a) { return (x + a -
 struct Layout {  // byte offsets, computed on the host
     uint64_t o_counts, o_perm, o_cell_gbeg, o_cell_gmid, o_cell_gend, o_entries, o_bwd_units, g_bytes;
     uint64_t o_gmean, o_gcon, o_mcopy, o_ccopy, o_rlist, o_rtab, o_rref, o_esum_q, o_cell_gsort, o_goff;
-    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent;
+    uint64_t o_sub_lbeg, o_sub_lmid, o_sub_lend, o_sub_ent, o_sub_lthin;
     uint64_t o_sorted, o_cell_sbeg, o_cell_send, o_fwd_units, o_cell_box, o_fsrows, o_scopy, s_bytes;
     uint64_t o_sub_sbeg, o_sub_send, o_sub_box, o_fsub_units;
 };
@@ -167,6 +168,7 @@ inline Layout make_layout(int D, int64_t P, int64_t N, int64_t T, int64_t R, int
     L.o_sub_lbeg = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lmid = o;  o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_lend = o;  o = align_up(o + 4 * (size_t)nsub, 256);
+    L.o_sub_lthin = o; o = align_up(o + 4 * (size_t)nsub, 256);
     L.o_sub_ent = o;   o = align_up(o + 4 * (size_t)esub_cap_of(D, E) + 64, 256);
     L.g_bytes = o;
     o = kHeaderBytes;
@@ -206,6 +208,7 @@ struct Bins {
     const float4 *sub_box;
     const uint2 *fsub_units;             // (sub-cell, pair-aligned first sample)
     const int32_t *sub_lbeg, *sub_lmid, *sub_lend;
+    const int32_t *sub_lthin;            // [lmid, lthin) flagged, [lthin, lend) kThin
     const uint32_t *sub_ent;             // sub lists: entries of the cell list, flagged last
     const uint32_t *esum_q;              // sorted-part list position -> Gaussian-major slot
     const int32_t *cell_gsort;           // first sorted-part position of each cell list
@@ -265,6 +268,7 @@ __device__ __forceinline__ Bins resolve(const char *gb, const char *sb) {
     B.sub_lbeg = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lbeg));
     B.sub_lmid = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lmid));
     B.sub_lend = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lend));
+    B.sub_lthin = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_sub_lthin));
     B.sub_ent = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_sub_ent));
     B.esum_q = reinterpret_cast<const uint32_t *>(gb + sload(&B.h->o_esum_q));
     B.cell_gsort = reinterpret_cast<const int32_t *>(gb + sload(&B.h->o_cell_gsort));

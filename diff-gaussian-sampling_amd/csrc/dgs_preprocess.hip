@@ -1239,7 +1239,7 @@ __device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 &mm, con
 // sub-cells whose sample box its cut meets (sub_mask).  Sub list k of the cell has the region
 // [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
 // list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
-// entries and [lmid, lend) the flagged ones.  The next group's Gaussian rows and the one
+// entries, [lmid, lend) the flagged ones and, of those, [lthin, lend) the kThin ones.  The next group's Gaussian rows and the one
 // after's entries are loaded while a group is tested (one stage: waves parked on the row
 // gathers half their cycles, PMC SQ_WAIT_ANY).  (A block-per-cell form -- masks
 // of the whole list in parallel into LDS, then one compacting wave per sub list -- was slower:
@@ -1253,12 +1253,13 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
                                                       const float4 *__restrict__ box,
                                                       const float4 *__restrict__ sbox, int CT,
                                                       int32_t *__restrict__ lbeg, int32_t *__restrict__ lmid,
-                                                      int32_t *__restrict__ lend, uint32_t *__restrict__ sub_ent) {
+                                                      int32_t *__restrict__ lend, int32_t *__restrict__ lthin,
+                                                      uint32_t *__restrict__ sub_ent) {
     const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
     const int lane = threadIdx.x & (kWave - 1);
     if (c >= ncells) return;
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0}, nth[kSubPerCell] = {0, 0, 0, 0};
     const int64_t base = (int64_t)kSubPerCell * b;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
@@ -1282,11 +1283,12 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
             sub_row(ent_c, gmean, gcon, mm_c, cc_c);
             ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
             const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
-            const bool ff = j < m_;
+            const bool ff = j < m_, thin = (ent & kThin) != 0;
 #pragma unroll
             for (int k = 0; k < kSubPerCell; ++k) {
                 const bool hit = (mask >> k) & 1u;
                 const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
+                nth[k] += (uint32_t)__popcll(__ballot(hit && thin));
                 if (hit) {
                     const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
                     // flag-free entries precede the flagged ones in the cell list, so once a group
@@ -1307,6 +1309,8 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
             lbeg[c * kSubPerCell + k] = a;
             lmid[c * kSubPerCell + k] = a + (int)nff[k];
             lend[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);
+            // (the kThin entries sort last in the cell list: the last nth of the flagged part)
+            lthin[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k] - nth[k]);
         }
 }
 
@@ -2110,10 +2114,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         int32_t *sub_lbeg = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lbeg);
         int32_t *sub_lmid = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lmid);
         int32_t *sub_lend = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lend);
+        int32_t *sub_lthin = reinterpret_cast<int32_t *>(gbuf + L.o_sub_lthin);
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
         k_sub_lists<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(
             ncells, cell_gbeg, cell_gmid, cell_gend, entries, gmean, gcon, cell_box, sub_box, G.CT, sub_lbeg, sub_lmid,
-            sub_lend, sub_ent);
+            sub_lend, sub_lthin, sub_ent);
         DGS_LAUNCH_CHECK(s, debug);
         // forward sub units per sub-cell with samples and entries: (sub-cell, kSubPairs pairs)
         const int32_t *ssb = sub_sbeg, *sse = sub_send, *slb = sub_lbeg, *sle = sub_lend;
@@ -2175,6 +2180,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_sub_sbeg = L0.o_sub_sbeg; h.o_sub_send = L0.o_sub_send; h.o_sub_box = L0.o_sub_box;
     h.o_fsub_units = L0.o_fsub_units;
     h.o_sub_lbeg = L.o_sub_lbeg; h.o_sub_lmid = L.o_sub_lmid; h.o_sub_lend = L.o_sub_lend; h.o_sub_ent = L.o_sub_ent;
+    h.o_sub_lthin = L.o_sub_lthin;
     h.fsub_cap = fsub_cap_of(D, N, ncells); h.esub_cap = esub_cap_of(D, E);
     h.stamp = ++stamp_counter;
     const TailSpec ts{G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf), reinterpret_cast<uint2 *>(srbuf),

@@ -633,9 +633,9 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
     }
 }
 
-// THIN = true: the thin pass -- per sub unit only the flagged part of the sub list, only its kThin
-// entries (the literal-order exponent, lit_prob), added onto the main pass's output.  Launched
-// only when the binning saw kThin entries.
+// THIN = true: the thin pass -- per sub unit only the kThin part of the sub list, [lthin, lend)
+// (the literal-order exponent, lit_prob), added onto the main pass's output; the main pass walks
+// [lbeg, lthin).  Launched only when the binning saw kThin entries.
 template <int FN, int D, int CB, bool THIN>
 __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
@@ -663,9 +663,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
         const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
         const int hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
         const int gb = sload(&bins.sub_lbeg[sc]), gm = sload(&bins.sub_lmid[sc]), ge = sload(&bins.sub_lend[sc]);
-        // (the thin pass: a sub list's kThin entries are its last ones -- the entry sort's order --
-        // so a list whose last entry is not kThin has none)
-        if (THIN && (gm == ge || !(sload(&bins.sub_ent[ge - 1]) & kThin))) continue;
+        // a sub list's kThin entries are its last ones (the entry sort's order): [gt, ge)
+        const int gt = sload(&bins.sub_lthin[sc]);
+        if (THIN && gt == ge) continue;
         float ctr[2];
         cell_center<D>(bins, cell, ctr);
         for (int ps = sb; ps < hi; ps += NS) {
@@ -690,9 +690,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
             if constexpr (!THIN)
                 fwd_s_groups<FN, D, CB, NPH, HBX, false, false>(bins.sub_ent, grows, bins.gcon, hr, prow, slot, gb, gm, np,
                                                                 lane, ctr, acc);
-            if (gm < ge)
-                fwd_s_groups<FN, D, CB, NPH, HBX, true, THIN>(bins.sub_ent, grows, bins.gcon, hr, prow, slot, gm, ge, np,
-                                                              lane, ctr, acc);
+            if (THIN ? gt < ge : gm < gt)
+                fwd_s_groups<FN, D, CB, NPH, HBX, true, THIN>(bins.sub_ent, grows, bins.gcon, hr, prow, slot,
+                                                              THIN ? gt : gm, THIN ? ge : gt, np, lane, ctr, acc);
             float x[64];
 #pragma unroll
             for (int i = 0; i < 64; ++i) x[i] = 0.0f;
