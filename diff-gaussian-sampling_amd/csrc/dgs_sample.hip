@@ -1426,7 +1426,8 @@ struct KernelTimer {
     int which;
     hipStream_t s;
     hipEvent_t a = nullptr, b = nullptr;
-    KernelTimer(int w, hipStream_t st) : which(w), s(st) {
+    KernelTimer(int w, hipStream_t st, uint32_t opts) : which(w), s(st) {
+        if (opts & DGS_SAMPLE_GRAPH_CAPTURE) return;  // (no events inside a captured graph)
         std::lock_guard<std::mutex> lk(g_tmu);
         if (!g_timing) return;
         if (hipEventCreate(&a) != hipSuccess || hipEventCreate(&b) != hipSuccess) { a = b = nullptr; return; }
@@ -1550,7 +1551,7 @@ static int run_forward(const Call &a) {
             if (rc) return rc;
         }
         {
-            KernelTimer t(0, a.s);  // (the main pass and the thin / tail passes behind it)
+            KernelTimer t(0, a.s, a.opts);  // (the main pass and the thin / tail passes behind it)
             if constexpr (T && D == 2 && DGS_FWD_SUB)  // sub-cell lists (units from the sub-unit hint)
                 k_forward_s<FN, D, CB, false><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
                                                                               flag);
@@ -1607,7 +1608,8 @@ static int run_backward(const Call &a) {
     // headline (2 %) the slot pass costs more than the few scattered atomics it replaces.
     UnitHint hint;
     const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
-    const int64_t Es = hinted && 4 * hint.Es >= hint.E ? hint.Es : 0;
+    // (not under graph capture: the slot buffer is a stream-ordered allocation)
+    const int64_t Es = hinted && 4 * hint.Es >= hint.E && !(a.opts & DGS_SAMPLE_GRAPH_CAPTURE) ? hint.Es : 0;
     struct SlotBuf {  // (stream-ordered; freed on every return)
         float *p = nullptr;
         hipStream_t s;
@@ -1636,7 +1638,7 @@ static int run_backward(const Call &a) {
         }
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
-            KernelTimer t(1, a.s);
+            KernelTimer t(1, a.s, a.opts);
             k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag,
                                                                esums);
             if (esums)
@@ -1782,6 +1784,8 @@ extern "C" int dgs_sample_forward_ex(int mask, int P, int D, int N, int C, const
     }
     // (debug: always the device-side input check)
     const uint32_t flags = opts && !debug ? opts->flags : 0u;
+    if ((flags & DGS_SAMPLE_GRAPH_CAPTURE) && !(flags & DGS_SAMPLE_INPUTS_BINNED))
+        return fail(DGS_ERR_ARG, "DGS_SAMPLE_GRAPH_CAPTURE requires DGS_SAMPLE_INPUTS_BINNED (the binned tensors)");
     Call a{FN, P, D, N, C, flags, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
            binning_bytes, sample_binning_bytes, o, nullptr, nullptr, nullptr,
@@ -1819,6 +1823,8 @@ extern "C" int dgs_sample_backward_ex(int mask, int P, int D, int N, int C, cons
         return DGS_OK;
     }
     const uint32_t flags = opts && !debug ? opts->flags : 0u;
+    if ((flags & DGS_SAMPLE_GRAPH_CAPTURE) && !(flags & DGS_SAMPLE_INPUTS_BINNED))
+        return fail(DGS_ERR_ARG, "DGS_SAMPLE_GRAPH_CAPTURE requires DGS_SAMPLE_INPUTS_BINNED (the binned tensors)");
     Call a{FN, P, D, N, C, flags, means, values, conics, samples, d,
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
            binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},

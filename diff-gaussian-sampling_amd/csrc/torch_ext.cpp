@@ -28,6 +28,16 @@ namespace {
 using torch::Tensor;
 
 hipStream_t cur_stream() { return at::hip::getCurrentHIPStream().stream(); }
+
+// Whether torch's current stream is being captured into a graph (torch.cuda.graph): the sample
+// calls then enqueue kernels only (DGS_SAMPLE_GRAPH_CAPTURE) and keep no packed-row records.
+bool capturing() {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(cur_stream(), &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+}
+const char *const kCaptureMsg =
+    "under graph capture, means, conics and samples must be the tensors the binning was made from "
+    "(unmodified since; a binning cannot be captured)";
 dgs_stream_t as_dgs(hipStream_t s) { return reinterpret_cast<dgs_stream_t>(s); }
 
 void check(int rc, const char *what) {
@@ -252,12 +262,16 @@ void forward_mask(int mask, const Tensor &means_in, const Tensor &values_in, con
     if (P == 0 || N == 0) return;
     const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
     dgs_sample_options o{};
+    const bool cap = capturing();
     if (inputs_binned(binning_in, means_in, conics_in, samples_in)) o.flags |= DGS_SAMPLE_INPUTS_BINNED;
-    const bool keep = means_in.requires_grad() || values_in.requires_grad() || conics_in.requires_grad();
+    else TORCH_CHECK(!cap, "sample_gaussians: ", kCaptureMsg);
+    if (cap) o.flags |= DGS_SAMPLE_GRAPH_CAPTURE;
+    const bool keep = !cap && (means_in.requires_grad() || values_in.requires_grad() || conics_in.requires_grad());
     const size_t ws = std::max(dgs_sample_workspace_size_multi(mask, P, D, N, C, 0),
                                keep ? dgs_sample_workspace_size_multi(mask, P, D, N, C, 1) : (size_t)0);
     Tensor work;
-    if (rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, false, work)) o.flags |= DGS_SAMPLE_ROWS_VALID;
+    if (!cap && rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, false, work))
+        o.flags |= DGS_SAMPLE_ROWS_VALID;
     else work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
     check(dgs_sample_forward_ex(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
                                 conics.data_ptr<float>(), samples.data_ptr<float>(), gb.data_ptr(), (size_t)gb.numel(),
@@ -298,10 +312,14 @@ Grads backward_mask(int mask, const Tensor &means_in, const Tensor &values_in, c
     if (P != 0 && N != 0) {
         const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
         dgs_sample_options o{};
+        const bool cap = capturing();
         if (inputs_binned(binning_in, means_in, conics_in, samples_in)) o.flags |= DGS_SAMPLE_INPUTS_BINNED;
+        else TORCH_CHECK(!cap, "sample_gaussians backward: ", kCaptureMsg);
+        if (cap) o.flags |= DGS_SAMPLE_GRAPH_CAPTURE;
         const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 1);
         Tensor work;
-        if (rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, true, work)) o.flags |= DGS_SAMPLE_ROWS_VALID;
+        if (!cap && rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, true, work))
+            o.flags |= DGS_SAMPLE_ROWS_VALID;
         else work = torch::empty({(int64_t)ws}, means.options().dtype(torch::kUInt8));
         check(dgs_sample_backward_ex(mask, P, D, N, C, means.data_ptr<float>(), values.data_ptr<float>(),
                                      conics.data_ptr<float>(), samples.data_ptr<float>(), dls, gb.data_ptr(),

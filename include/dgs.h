@@ -201,8 +201,16 @@ int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float 
  *     same function mask, C <= 16 and the same means / conics / values (unmodified since), whose
  *     Gaussian-row region (offset 0) the earlier call packed: the rows are reused, not repacked.
  *     A forward followed by its backward shares one workspace of the backward's size this way.
- *     A backward leaves the region overwritten (its finalize reuses it): never reuse after one. */
-enum dgs_sample_flag { DGS_SAMPLE_INPUTS_BINNED = 1, DGS_SAMPLE_ROWS_VALID = 2 };
+ *     A backward leaves the region overwritten (its finalize reuses it): never reuse after one.
+ *   DGS_SAMPLE_GRAPH_CAPTURE: the call is being captured into a HIP graph (stream capture):
+ *     it then enqueues kernels only -- no stream-ordered allocation (the backward's slot sums
+ *     fall back to atomics), no timing events -- and requires DGS_SAMPLE_INPUTS_BINNED (the
+ *     call-time path's first use builds tile lists behind a host-side record; DGS_ERR_ARG
+ *     without it).  A replay re-reads means, values, conics, samples and dL from the captured
+ *     addresses; values and dL may change between replays, means / conics / samples may not
+ *     (re-binning cannot be captured: it returns num_rendered to the host).
+ */
+enum dgs_sample_flag { DGS_SAMPLE_INPUTS_BINNED = 1, DGS_SAMPLE_ROWS_VALID = 2, DGS_SAMPLE_GRAPH_CAPTURE = 4 };
 typedef struct dgs_sample_options {
     uint32_t flags;
 } dgs_sample_options;

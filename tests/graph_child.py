@@ -1,0 +1,101 @@
+"""Child process of tests/test_gpu_graph.py (one scenario per process, so that a failure inside
+the HIP runtime's graph capture fails the test instead of ending the pytest process):
+`python tests/graph_child.py forward_backward gaussian|derivative` or `python tests/graph_child.py
+requires_binned`.  Prints "ok" on success."""
+import os
+import sys
+
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "diff-gaussian-sampling_amd"))
+
+import diff_gaussian_sampling as dgs  # noqa: E402
+from diff_gaussian_sampling import synthetic as syn  # noqa: E402
+
+RTOL, ATOL = 1e-5, 1e-6
+
+
+def _close(a, b, what):
+    scale = float(b.abs().max()) if b.numel() else 0.0
+    err = (a - b).abs()
+    bound = RTOL * b.abs() + ATOL * scale
+    assert bool((err <= bound).all()), f"{what}: max |d| {float(err.max()):.3e} (scale {scale:.3e})"
+
+
+def forward_backward(fname):
+    dev = torch.device("cuda")
+    P, N, C = 20000, 60000, 1
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, C, seed=3))
+    samples = syn.samples(N, 2, seed=9).to(dev)
+    K = 2 if fname == "derivative" else 1
+    fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative}[fname]
+    R, gb, sb, rg, srg, _ = dgs.preprocess_gaussians(means, values, covs, conics, samples, False)
+    dL = torch.randn((N,) + (2,) * (K - 1) + (C,), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    for t in (means, values, conics):
+        t.requires_grad_(True)
+
+    def step():
+        out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
+        g = torch.autograd.grad(out, (means, values, conics), dL)
+        return out, g
+
+    # eager reference, then warm-up on a side stream (torch.cuda.graph's recipe)
+    ref_out, ref_g = step()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g_out, g_g = step()
+    for _ in range(2):
+        graph.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(g_out, ref_out), "forward replay differs from the eager call"
+        for a, b, w in zip(g_g, ref_g, ("dmeans", "dvalues", "dconics")):
+            _close(a, b, f"replay {w}")
+    # values and dL change in place: the replay follows them (the rows are re-packed in the graph)
+    with torch.no_grad():
+        values.mul_(-0.5).add_(0.25)
+        dL.mul_(2.0)
+    graph.replay()
+    torch.cuda.synchronize()
+    # (the eager check after the change: values' version moved, so nothing cached is reused)
+    new_out, new_g = step()
+    assert torch.equal(g_out, new_out), "forward replay after the values change differs"
+    for a, b, w in zip(g_g, new_g, ("dmeans", "dvalues", "dconics")):
+        _close(a, b, f"replay after change {w}")
+    assert not torch.equal(new_out, ref_out)
+
+
+def requires_binned():
+    dev = torch.device("cuda")
+    P, N = 2000, 6000
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, 1, seed=4))
+    samples = syn.samples(N, 2, seed=10).to(dev)
+    R, gb, sb, rg, srg, _ = dgs.preprocess_gaussians(means, values, covs, conics, samples, False)
+    other = means.clone()  # equal values, another tensor: not provably the binned one
+    dgs.sample_gaussians(other, values, conics, samples, R, gb, sb, rg, srg, False)  # eager: fine
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    try:
+        with torch.cuda.graph(graph):
+            dgs.sample_gaussians(other, values, conics, samples, R, gb, sb, rg, srg, False)
+    except RuntimeError as e:
+        # (the library's refusal, or -- should ending the capture also fail -- its context)
+        msg = str(e) + " " + str(e.__context__)
+        assert "graph capture" in msg, msg
+    else:
+        raise AssertionError("a capture with tensors other than the binned ones did not raise")
+    torch.cuda.synchronize()
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "forward_backward":
+        forward_backward(sys.argv[2])
+    else:
+        requires_binned()
+    print("ok", flush=True)
