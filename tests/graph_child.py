@@ -35,10 +35,11 @@ def forward_backward(fname):
     for t in (means, values, conics):
         t.requires_grad_(True)
 
-    def step():
+    def step():  # (detached output: no autograd graph outlives a step -- an AccumulateGrad node
+        # kept from an eager step on another stream breaks the capture)
         out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
         g = torch.autograd.grad(out, (means, values, conics), dL)
-        return out, g
+        return out.detach(), g
 
     # eager reference, then warm-up on a side stream (torch.cuda.graph's recipe)
     ref_out, ref_g = step()
