@@ -26,8 +26,8 @@ constexpr uint32_t kVersion = 10;
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
 constexpr uint32_t kUnsafe = 0x40000000u;   // conic not positive definite, a wrap breakpoint in the
                                             // cell, or a fallback cell: the per-pair literal path
-constexpr uint32_t kThin = 0x20000000u;     // positive definite but ill-conditioned (rho^2 >= 0.82):
-                                            // packed, with the exponent in the reference's order
+constexpr uint32_t kThin = 0x20000000u;     // DGS_THIN_LITERAL only: positive definite but ill-conditioned
+                                            // (rho^2 >= 0.82): packed, the unfused reference's exponent order
 constexpr uint32_t kSlow = kGeneral | kUnsafe | kThin;
 constexpr uint32_t kIdMask = 0x1fffffffu;
 constexpr int64_t kMaxGaussians = (int64_t)kIdMask;
@@ -374,24 +374,33 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
     return touched;
 }
 
-// The fast paths evaluate the exponent in their own operation order (pre-scaled k, FMAs); that
-// is within the tolerance of the reference's order only while the fp32 rounding of the terms is
-// not amplified by cancellation.  With rho = |c1| / sqrt(c0 c2), max over X of
-// (c0 X0^2 + 2 |c1 X0 X1| + c2 X1^2) / X^T A X = (1 + rho) / (1 - rho): rho^2 < 0.82 bounds that
-// amplification by 20, so a pair's difference stays below ~5e-7 |v| (at 0.98, thin rotated
-// Gaussians -- axis ratio 25 -- differed by 1.4e-5 |v|: tests/test_gpu_parity.py thin case).
-// Positive definite with rho^2 < 0.82 (D = 2), or c0 >= 0 (D = 1); every other conic takes the
-// reference-literal power evaluation with its `power > 0 -> skip` rule (forward.cu:228).  The
-// headline's Gaussians (axis ratio <= 3: rho <= 0.8) are all on the fast paths.
-// Not positive definite (or not finite): kUnsafe, the per-pair literal path with the exact wrap.
+// The fast paths evaluate the exponent in their own operation order (pre-scaled k, FMAs).  With
+// rho = |c1| / sqrt(c0 c2), max over X of (c0 X0^2 + 2 |c1 X0 X1| + c2 X1^2) / X^T A X
+// = (1 + rho) / (1 - rho): cancellation amplifies the fp32 rounding of the exponent's terms by
+// up to that factor, in ANY operation order -- the reference's own included.  nvcc's default
+// --fmad=true (setup.py:30 passes no --fmad=false) fuses the reference's a*b + c*d exponent sum
+// (forward.cu:177 ff.), and for thin Gaussians (rho^2 >= 0.82, axis ratio >= ~10) the fused and
+// unfused reference differ by 1-2x the 1e-5 parity bound in the forward and 4-6x in the
+// gradients (tools/contraction_study.py, profiles/r05_contraction.json): no operation order is
+// "the reference's" there.  So thin conics take the fast paths like every other PD conic, under
+// the stated bound of tests/test_gpu_parity.py (within twice the reference's own compile spread);
+// DGS_THIN_LITERAL=1 restores round 4's kThin entries (the unfused reference's order, lit_prob).
+// Past rho^2 = kRho2Max (amplification > 4e4) a conic is treated as not positive definite.
+#ifndef DGS_THIN_LITERAL
+#define DGS_THIN_LITERAL 0
+#endif
+constexpr double kRho2Max = 0.9999;
+// Not positive definite, too ill-conditioned (above), or not finite: kUnsafe, the per-pair
+// literal path with the exact wrap and the reference's `power > 0 -> skip` (forward.cu:228).
 __host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float c2f) {
     const double c0 = c0f, c1 = c1f, c2 = c2f;
     if (D == 1) return !(c0 >= 0.0 && c0 < INFINITY);
-    return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY && c1 * c1 < c0 * c2);
+    return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
+             c1 * c1 < kRho2Max * (c0 * c2));
 }
-// Positive definite but ill-conditioned, rho^2 = c1^2 / (c0 c2) >= 0.82 (D = 2): kThin.  The
-// fast paths' own operation order is not within the tolerance there (above); these entries keep
-// the packed fast kernels but evaluate the exponent in the reference's order (lit_prob).
+// Positive definite but ill-conditioned, rho^2 = c1^2 / (c0 c2) >= 0.82 (D = 2).  These stay off
+// the binning's gather path (its fp32 row slices assume a well-conditioned cut) and, with
+// DGS_THIN_LITERAL, are flagged kThin for the literal-order exponent.
 __host__ __device__ inline bool conic_thin(int D, float c0f, float c1f, float c2f) {
     if (D != 2 || conic_unsafe(D, c0f, c1f, c2f)) return false;
     const double c0 = c0f, c1 = c1f, c2 = c2f;

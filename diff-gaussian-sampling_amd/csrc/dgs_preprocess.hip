@@ -385,7 +385,10 @@ __device__ __forceinline__ Cut gauss_cut(const Geom &G, const float *m, const fl
         if (k.pd) k.e[0] = sqrt(kQCut / k.c0) * (1.0 + 1e-6);
     } else {
         const double det = k.c0 * k.c2 - k.c1 * k.c1;
-        k.pd = k.c0 > 0.0 && det > 0.0 && det < INFINITY && k.c0 < INFINITY && k.c2 < INFINITY;
+        // (past kRho2Max the fp32 exponent's rounding is amplified beyond the cut's margin:
+        // such conics keep their whole tiles, like the non-PD ones)
+        k.pd = k.c0 > 0.0 && det > 0.0 && det < INFINITY && k.c0 < INFINITY && k.c2 < INFINITY &&
+               k.c1 * k.c1 < kRho2Max * (k.c0 * k.c2);
         if (k.pd) {
             k.e[0] = sqrt(kQCut * k.c2 / det) * (1.0 + 1e-6);
             k.e[1] = sqrt(kQCut * k.c0 / det) * (1.0 + 1e-6);
@@ -529,7 +532,7 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
     const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
-                           : conic_thin(D, con[0], con[1], con[2]) ? kThin : 0u;
+                           : (DGS_THIN_LITERAL && conic_thin(D, con[0], con[1], con[2])) ? kThin : 0u;
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             const uint32_t key = key_of(D, x, y, G.grid);
@@ -1596,7 +1599,8 @@ __global__ void k_xchg_sets(int P, int D, const float *__restrict__ means, const
     if (D == 2) {
         const double c0 = conics[g * S], c1 = conics[g * S + 1], c2 = conics[g * S + 2];
         const double det = c0 * c2 - c1 * c1;
-        pd = c0 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY;
+        pd = c0 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY &&
+             c1 * c1 < kRho2Max * (c0 * c2);  // (the binning's cut: gauss_cut)
         e = pd ? sqrt(kQCut * c0 / det) : INFINITY;
     } else {
         const double c0 = conics[g * S];

@@ -122,6 +122,7 @@ class ShardedGaussianSampler:
 
 # ------------------------------------------------------------------------ spatial shards (f3)
 Q_CUT = 210.0  # X^T A X above this gives expf(-q / 2) == +0 in fp32 (dgs_internal.h kQCut)
+RHO2_MAX = 0.9999  # conics with c1^2 >= RHO2_MAX c0 c2 are not culled (dgs_internal.h kRho2Max)
 
 
 def support_halfwidth(means, conics):
@@ -134,6 +135,7 @@ def support_halfwidth(means, conics):
         c0, c1, c2 = c[:, 0], c[:, 1], c[:, 2]
         det = c0 * c2 - c1 * c1
         pd = (c0 > 0) & (det > 0) & torch.isfinite(det) & torch.isfinite(c0) & torch.isfinite(c2)
+        pd &= c1 * c1 < RHO2_MAX * (c0 * c2)  # (the binning keeps whole tiles past it: gauss_cut)
         e = torch.sqrt(Q_CUT * c0 / torch.where(pd, det, torch.ones_like(det)))
     else:
         c0 = c[:, 0]

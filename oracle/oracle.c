@@ -16,8 +16,21 @@
  *
  * Arithmetic is literal: float where the reference uses FLOAT, double where the reference's
  * double literals promote (e.g. `-0.5 * (...)`, `3.0 * sqrt(...)`), expf/sqrtf/floorf for the
- * CUDA float overloads of exp/sqrt/floor.  Build with -ffp-contract=off so that no product
- * is fused into an FMA (nvcc's contraction choices are unknowable without the toolchain).
+ * CUDA float overloads of exp/sqrt/floor.
+ *
+ * FMA CONTRACTION MODELS (ORC_FMAD, one library per model; oracle/Makefile):
+ *   0  liboracle.so            gcc -ffp-contract=off: every product and sum rounded on its own
+ *                              (the model the GPU path and the parity tests are built against);
+ *   1  liboracle_fmad.so       clang -ffp-contract=fast -mfma: nvcc's default --fmad=true (the
+ *                              reference's setup.py:30 passes no --fmad=false) modelled by LLVM's
+ *                              own DAG contraction of the same expressions (NVVM is LLVM-based):
+ *                              every a*b +- c whose product feeds one add is fused; where both
+ *                              operands of an add are products (SUM2), LLVM fuses the LEFT one;
+ *   2  liboracle_fmad_alt.so   as 1, but every SUM2 site fuses the RIGHT product (the other legal
+ *                              choice of a contracting compiler at `a*b +- c*d`).
+ * The reference's atomicAdd(ptr, term) cannot fuse its addend: ACC() keeps the term rounded in
+ * every model.  Nothing here is the nvcc binary: the models bracket what it can do
+ * (tools/contraction_study.py, profiles/r05_contraction.json).
  *
  * Every function cites the reference file:line it follows.
  */
@@ -27,6 +40,10 @@
 #include <string.h>
 
 #define ORC_TILE 0.51f /* config.h:18 BLOCK_SIZE */
+
+#include "oracle_fmad.h"
+
+int orc_fmad_model(void) { return ORC_FMAD; }
 
 typedef struct {
     int P, D, N;
@@ -76,10 +93,10 @@ void orc_tile_grid(int N, int D, const float *samples, int *grid, float *off) {
 /* forward.cu:52-61 -- radius of the 3-sigma box; returns 0 when the Gaussian is skipped. */
 static float ref_radius(int D, const float *cov) {
     if (D == 1) return (float)(3.0 * (double)sqrtf(cov[0]));
-    float det = cov[0] * cov[2] - cov[1] * cov[1];
+    float det = SUM2(cov[0], cov[2], -cov[1], cov[1]); /* forward.cu:55 */
     if (det == 0.0f) return 0.0f;
     float mid = 0.5f * (cov[0] + cov[2]);
-    float disc = mid * mid - det;
+    float disc = FMA(mid, mid, -det); /* forward.cu:59 */
     double floor_disc = fmax(1e-6, (double)disc); /* CUDA max(double, float) */
     float lambda = (float)((double)mid + sqrt(floor_disc));
     return (float)(3.0 * (double)sqrtf(lambda));
@@ -100,7 +117,7 @@ static uint32_t ref_touched(int D, const float *mean, const float *cov, const in
                             const float *off, float *radius_out) {
     *radius_out = 0.0f;
     if (D == 2) {
-        float det = cov[0] * cov[2] - cov[1] * cov[1];
+        float det = SUM2(cov[0], cov[2], -cov[1], cov[1]);
         if (det == 0.0f) return 0;
     }
     float r = ref_radius(D, cov);
@@ -271,7 +288,9 @@ static int out_comps(int fn, int D) {
     return k;
 }
 
-/* forward.cu:168-275 -- one pair's contribution, accumulated into o[comp*C + ch]. */
+/* forward.cu:168-275 -- one pair's contribution, accumulated into o[comp*C + ch].  Contraction
+ * sites (ORC_FMAD): the exponent's float sum (forward.cu:177,199,223,252: SUM2), a1/a2 and the
+ * laplacian terms (FMA), and every `out += values*alpha*t` (forward.cu:182 ff.: FMA into out). */
 static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const float *v, float *o) {
     if (D == 1) {
         float x1 = c[0] * X[0];
@@ -281,10 +300,17 @@ static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const
         for (int ch = 0; ch < C; ++ch) {
             float va = v[ch] * a;
             switch (fn) {
-            case F_GAUSS: o[ch] += va; break;
-            case F_DERIV: o[ch] += va * x1; break;
-            case F_LAPL: o[ch] += va * (x1 * x1 - c[0]); break;
-            default: o[ch] = (float)((double)o[ch] + (double)va * (2.0 * c[0] * x1 - (double)(x1 * x1 * x1) + (double)(c[0] * x1)));
+            case F_GAUSS: o[ch] = FMA(v[ch], a, o[ch]); break;
+            case F_DERIV: o[ch] = FMA(va, x1, o[ch]); break;
+            case F_LAPL: o[ch] = FMA(va, FMA(x1, x1, -c[0]), o[ch]); break;
+            default: {
+                double t = 2.0 * c[0] * x1 - (double)(x1 * x1 * x1) + (double)(c[0] * x1);
+#if ORC_FMAD
+                o[ch] = (float)fma((double)va, t, (double)o[ch]);
+#else
+                o[ch] = (float)((double)o[ch] + (double)va * t);
+#endif
+            }
             }
         }
         return;
@@ -292,20 +318,18 @@ static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const
     float power;
     float x1 = c[0] * X[0], x2 = c[2] * X[1];
     if (fn == F_GAUSS)
-        power = (float)(-0.5 * (double)(c[0] * X[0] * X[0] + c[2] * X[1] * X[1]) - (double)(c[1] * X[0] * X[1]));
+        power = (float)(-0.5 * (double)SUM2(c[0] * X[0], X[0], c[2] * X[1], X[1]) - (double)(c[1] * X[0] * X[1]));
     else
-        power = (float)(-0.5 * (double)(x1 * X[0] + x2 * X[1]) - (double)(c[1] * X[0] * X[1]));
+        power = (float)(-0.5 * (double)SUM2(x1, X[0], x2, X[1]) - (double)(c[1] * X[0] * X[1]));
     if (power > 0.0) return;
     float a = expf(power);
-    float a1 = x1 + c[1] * X[1], a2 = x2 + c[1] * X[0];
+    float a1 = FMA(c[1], X[1], x1), a2 = FMA(c[1], X[0], x2);
     float t[4];
-    int nt = 0;
     switch (fn) {
     case F_GAUSS: break;
-    case F_DERIV: nt = 2; t[0] = x1 + c[1] * X[1]; t[1] = x2 + c[1] * X[0]; break;
-    case F_LAPL: nt = 3; t[0] = a1 * a1 - c[0]; t[1] = a1 * a2 - c[1]; t[2] = a2 * a2 - c[2]; break;
+    case F_DERIV: t[0] = a1; t[1] = a2; break;
+    case F_LAPL: t[0] = FMA(a1, a1, -c[0]); t[1] = FMA(a1, a2, -c[1]); t[2] = FMA(a2, a2, -c[2]); break;
     default:
-        nt = 4;
         t[0] = (float)(3.0 * c[0] * a1 - (double)(a1 * a1 * a1));
         t[1] = (float)(2.0 * c[1] * a1 - (double)(a1 * a1 * a2) + (double)(c[0] * a2));
         t[2] = (float)(2.0 * c[1] * a2 - (double)(a1 * a2 * a2) + (double)(c[2] * a1));
@@ -317,13 +341,12 @@ static void fwd_pair(int fn, int D, int C, const float *X, const float *c, const
     for (int ch = 0; ch < C; ++ch) {
         float va = v[ch] * a;
         switch (fn) {
-        case F_GAUSS: o[ch] += va; break;
-        case F_DERIV: o[ch] += va * t[0]; o[C + ch] += va * t[1]; break;
-        case F_LAPL: for (int k = 0; k < 4; ++k) o[k * C + ch] += va * t[lap_map[k]]; break;
-        default: for (int k = 0; k < 8; ++k) o[k * C + ch] += va * t[third_map[k]];
+        case F_GAUSS: o[ch] = FMA(v[ch], a, o[ch]); break;
+        case F_DERIV: o[ch] = FMA(va, t[0], o[ch]); o[C + ch] = FMA(va, t[1], o[C + ch]); break;
+        case F_LAPL: for (int k = 0; k < 4; ++k) o[k * C + ch] = FMA(va, t[lap_map[k]], o[k * C + ch]); break;
+        default: for (int k = 0; k < 8; ++k) o[k * C + ch] = FMA(va, t[third_map[k]], o[k * C + ch]);
         }
     }
-    (void)nt;
 }
 
 /* backward.cu:108-416 (oracle_bwd_body.h): bwd_pair (float sums) and bwd_pair64 (exact sums) */

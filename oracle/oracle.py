@@ -12,8 +12,14 @@ import subprocess
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(_HERE, "_build", "liboracle.so")
+# FMA contraction models (oracle.c header, oracle/Makefile): "nocontract" is the model the GPU
+# path and the parity tests are built against; "fmad" / "fmad_alt" model nvcc's default
+# --fmad=true (the reference's setup.py:30 sets no --fmad=false) with the two fusing choices at
+# a*b + c*d sites.
+MODELS = {"nocontract": "liboracle.so", "fmad": "liboracle_fmad.so", "fmad_alt": "liboracle_fmad_alt.so"}
+_LIB_PATH = os.path.join(_HERE, "_build", MODELS["nocontract"])
 _lib = None
+_libs = {}
 
 FUNCTIONS = {"gaussian": 0, "derivative": 1, "laplacian": 2, "third": 3}
 
@@ -22,13 +28,14 @@ def build():
     subprocess.run(["make", "-s", "-C", _HERE], check=True)
 
 
-def _load():
+def _load(model="nocontract"):
     global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(_LIB_PATH):
+    if model in _libs:
+        return _libs[model]
+    path = os.path.join(_HERE, "_build", MODELS[model])
+    if not os.path.exists(path):
         build()
-    lib = ctypes.CDLL(_LIB_PATH)
+    lib = ctypes.CDLL(path)
     P = ctypes.c_void_p
     i32, i64 = ctypes.c_int, ctypes.c_int64
     lib.orc_bin.restype = P
@@ -55,7 +62,10 @@ def _load():
     lib.orc_agg_backward.argtypes = [i32] * 5 + [P] * 21
     lib.orc_agg_forward64.argtypes = [i32] * 5 + [P] * 15
     lib.orc_agg_backward64.argtypes = [i32] * 5 + [P] * 21
-    _lib = lib
+    lib.orc_fmad_model.restype = i32
+    _libs[model] = lib
+    if model == "nocontract":
+        _lib = lib
     return lib
 
 
@@ -84,8 +94,9 @@ def tile_grid(samples):
 class OracleBins:
     """Reference binning (sample_points.cu:38-98, sampler_impl.cu:216-330) on the CPU."""
 
-    def __init__(self, means, covariances, samples, grid=None, offset=None):
-        lib = _load()
+    def __init__(self, means, covariances, samples, grid=None, offset=None, model="nocontract"):
+        self.model = model
+        lib = self._lib = _load(model)
         self.means = _f32(means)
         self.covariances = _f32(covariances)
         self.samples = _f32(samples)
@@ -112,31 +123,31 @@ class OracleBins:
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
-        if h and _lib is not None:
+        if h and getattr(self, "_lib", None) is not None:
             try:
-                _lib.orc_free(h)
+                self._lib.orc_free(h)
             except Exception:  # interpreter shutdown
                 pass
 
     def ranges(self):
         r = np.zeros(2 * self.T, np.uint32)
         s = np.zeros(2 * self.T, np.uint32)
-        _load().orc_ranges(self._h, _ptr(r), _ptr(s))
+        self._lib.orc_ranges(self._h, _ptr(r), _ptr(s))
         return r.reshape(self.T, 2), s.reshape(self.T, 2)
 
     def sample_keys(self):
         k = np.zeros(self.N, np.int32)
-        _load().orc_sample_keys(self._h, _ptr(k))
+        self._lib.orc_sample_keys(self._h, _ptr(k))
         return k
 
     def tile_gaussians(self, t):
-        n = _load().orc_tile_gaussians(self._h, t, None)
+        n = self._lib.orc_tile_gaussians(self._h, t, None)
         out = np.zeros(max(n, 1), np.int32)
-        _load().orc_tile_gaussians(self._h, t, _ptr(out))
+        self._lib.orc_tile_gaussians(self._h, t, _ptr(out))
         return out[:n]
 
     def forward(self, function, values, conics, subset=None, samples=None, means=None):
-        lib = _load()
+        lib = self._lib
         v = _f32(values)
         c = _f32(conics)
         m = self.means if means is None else _f32(means)
@@ -153,7 +164,7 @@ class OracleBins:
         """backward.cu:26-106.  exact=False: the float sums in serial order (one of the reference's
         atomic orders); exact=True: the same float per-pair terms summed in double (float64 arrays),
         the value every atomic order scatters around -- the GPU parity tests' reference."""
-        lib = _load()
+        lib = self._lib
         v = _f32(values)
         c = _f32(conics)
         m = self.means if means is None else _f32(means)
@@ -172,7 +183,7 @@ class OracleBins:
         return dm, dv, dc
 
     def count_pairs(self, conics, thr=-104.0, subset=None):
-        lib = _load()
+        lib = self._lib
         c = _f32(conics)
         sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
         w_ref = ctypes.c_int64()
@@ -188,10 +199,10 @@ def _i64(a):
     return np.ascontiguousarray(np.asarray(a, dtype=np.int64))
 
 
-def agg_preprocess(means, conics, radii):
+def agg_preprocess(means, conics, radii, model="nocontract"):
     """preprocess_aggregate (aggregate_neighbors.cu:323-367): (indices i64[Lnb], ranges
     i64[P] inclusive cumsum, dists [Lnb, D], densities [Lnb], inv_total [P])."""
-    lib = _load()
+    lib = _load(model)
     m, c, r = _f32(means), _f32(conics), _f32(radii)
     P, D = m.shape
     counts = np.zeros(P, np.int64)
@@ -207,11 +218,11 @@ def agg_preprocess(means, conics, radii):
     return indices, ranges, dists, dens, inv
 
 
-def agg_preprocess_rows(means, conics, radii, rows):
+def agg_preprocess_rows(means, conics, radii, rows, model="nocontract"):
     """preprocess_aggregate restricted to the rows `rows` (each an O(P) scan): compact lists
     (indices, ranges [len(rows)] inclusive cumsum, dists, densities, inv_total [len(rows)])
     equal to those rows' slices of agg_preprocess."""
-    lib = _load()
+    lib = _load(model)
     m, c, r = _f32(means), _f32(conics), _f32(radii)
     rw = np.ascontiguousarray(rows, dtype=np.int32)
     P, D = m.shape

@@ -15,6 +15,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include "oracle_fmad.h"
+
 #ifndef M_PI
 #define M_PI 3.14159265358979323846
 #endif
@@ -31,7 +33,7 @@ static int agg_collides(int D, const float *means, const float *radii, int i, in
         /* TORUS: min(dx, abs(2.0 - fmod(abs(dx), 2.0))) -- only a positive dx can shrink */
         const double w = fabs(2.0 - fmod((double)fabsf(dx), 2.0));
         dx = (float)fmin((double)dx, w);
-        dist += dx * dx;
+        dist = FMA(dx, dx, dist); /* aggregate_neighbors.cu:44: contracted under --fmad=true */
     }
     const float radius = my_radius + other_radius;
     return !(dist > radius * radius);
@@ -83,7 +85,7 @@ static void agg_fill_row(int P, int D, const float *means, const float *conics,
             if (D == 1) {
                 power = (float)(-0.5 * con[0] * X[0] * X[0]);
             } else {
-                power = (float)(-0.5 * (double)(con[0] * X[0] * X[0] + con[2] * X[1] * X[1])
+                power = (float)(-0.5 * (double)SUM2(con[0] * X[0], X[0], con[2] * X[1], X[1])
                                 - (double)(con[1] * X[0] * X[1]));
             }
             for (int d = 0; d < D; ++d) X[d] *= my_inv_radius;

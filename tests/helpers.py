@@ -10,7 +10,7 @@ FWD_NAME = {"gaussian": "sample_gaussians", "derivative": "sample_gaussians_deri
             "laplacian": "sample_gaussians_laplacian", "third": "sample_gaussians_third_derivative"}
 
 
-def _record_margin(what, margin, rtol, atol_frac, n):
+def record_margin(what, margin, rtol, atol_frac, n):
     """Appends one JSON line per check to $DGS_MARGINS (tools/margins_summary.py folds them into
     profiles/rNN_margins.json): the margin is max |got - ref| / bound, < 1 passes."""
     path = os.environ.get("DGS_MARGINS")
@@ -33,7 +33,7 @@ def close(got, ref, rtol, atol_frac, what=""):
     scale = float(np.max(np.abs(ref))) if ref.size else 0.0
     err = np.abs(got - ref)
     bound = rtol * np.abs(ref) + atol_frac * scale + 1e-30
-    _record_margin(what, float(np.max(err / bound)) if err.size else 0.0, rtol, atol_frac, int(err.size))
+    record_margin(what, float(np.max(err / bound)) if err.size else 0.0, rtol, atol_frac, int(err.size))
     bad = err > bound
     if bad.any():
         i = np.unravel_index(np.argmax(err / bound), err.shape)
@@ -58,7 +58,7 @@ def close_grad(got, exact, literal, rtol, atol_frac, what=""):
     float atomics in no fixed order; `literal` is one such order (the oracle's serial float sums),
     whose distance from the exact sum -- the reference's own run-to-run spread -- is recorded next
     to the GPU's (profiles/r04_margins.json) as the evidence for a case's stated bound."""
-    _record_margin(what + " [reference serial order vs exact]", margin_of(literal, exact, rtol, atol_frac), rtol,
+    record_margin(what + " [reference serial order vs exact]", margin_of(literal, exact, rtol, atol_frac), rtol,
                    atol_frac, int(np.size(exact)))
     close(got, exact, rtol, atol_frac, what)
 

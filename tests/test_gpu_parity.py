@@ -7,7 +7,14 @@ Floating-point outputs use the SURVEY 8c tolerance, per tensor:
 for the forward and for the gradients alike.  Gradients are compared with the oracle's exact sum
 of the reference's float per-pair terms (the reference adds them with float atomics in no fixed
 order); the one exception is the clustered case, whose stated bound is ATOL_BWD_CLUSTERED.  Per-check margins are
-recorded when $DGS_MARGINS is set (profiles/r04_margins.json).
+recorded when $DGS_MARGINS is set (profiles/r0N_margins.json).
+
+Every case also records how far the reference itself moves under nvcc's default FMA contraction
+(--fmad=true: the oracle's "fmad" model, oracle/oracle.c) as "[reference fmad vs no-contract]".
+Thin Gaussians (rho^2 >= 0.82) are where that spread exceeds the 8c bound (1-2x forward, 4-6x
+gradients: profiles/r05_contraction.json), so no operation order is the reference's there; their
+stated bound (spread=True) is: within twice the larger of the two contraction models' distances
+from the unfused model, and never tighter than the 8c bound.
 """
 import numpy as np
 import pytest
@@ -15,7 +22,7 @@ import torch
 
 from diff_gaussian_sampling import synthetic as syn
 import cases
-from helpers import FUNCS, close, close_grad, gpu_run, ref_ranges_bytes
+from helpers import FUNCS, close, close_grad, gpu_run, margin_of, record_margin, ref_ranges_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -29,9 +36,28 @@ ATOL_BWD = 1e-6  # rtol 1e-5 + atol 1e-6 max|ref|
 ATOL_BWD_CLUSTERED = 4e-6
 
 
+def _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ref_grads, models):
+    """Margins (units of the 8c bound) of the contraction models' forward and exact-sum gradients
+    from the unfused model's, recorded as "[reference <model> vs no-contract]"; returns the
+    largest over `models` per output."""
+    worst = {}
+    for model in models:
+        ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy(), model=model)
+        out = ob.forward(function, values.numpy(), conics.numpy(), subset=subset)
+        if subset is not None:
+            out = out[subset]
+        grads = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
+        for name, a, b in [("forward", out, ref_out)] + list(zip(("dmeans", "dvalues", "dconics"), grads, ref_grads)):
+            mg = margin_of(a, b, RTOL, ATOL_FWD if name == "forward" else ATOL_BWD)
+            record_margin(f"{function} {name} [reference {model} vs no-contract]", mg, RTOL, ATOL_FWD, int(np.size(b)))
+            worst[name] = max(worst.get(name, 0.0), mg)
+    return worst
+
+
 def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=None,
-                atol_fwd=ATOL_FWD, atol_bwd=ATOL_BWD):
-    """Runs every check and reports all failures together."""
+                atol_fwd=ATOL_FWD, atol_bwd=ATOL_BWD, spread=False):
+    """Runs every check and reports all failures together.  spread: thin Gaussians' stated bound
+    (module docstring) -- each output within max(1, 2 x the contraction models' spread) bounds."""
     ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
     res = gpu_run(dgs._C, function, means, values, covs, conics, samples, dL)
     errors = []
@@ -58,12 +84,19 @@ def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL,
     got = res["out"].reshape(N, -1, values.shape[1])
     if subset is not None:
         got, ref_out = got[subset], ref_out[subset]
-    attempt(close, got, ref_out, RTOL, atol_fwd, f"{function} forward")
-    # backward
     lit = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
     ex = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
+    wide = _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ex,
+                         ("fmad", "fmad_alt") if spread else ("fmad",))
+    scale = {k: max(1.0, 2.0 * v) if spread else 1.0 for k, v in wide.items()}
+    if spread:  # the GPU's own distance in units of the plain 8c bound, next to the stated one
+        for name, a, b in [("forward", got, ref_out)] + list(zip(("dmeans", "dvalues", "dconics"), res["grads"], ex)):
+            record_margin(f"{function} {name} [gpu vs no-contract, plain 8c bound; stated x{scale[name]:.2f}]",
+                          margin_of(a, b, RTOL, ATOL_FWD), RTOL, ATOL_FWD, int(np.size(b)))
+    attempt(close, got, ref_out, RTOL * scale["forward"], atol_fwd * scale["forward"], f"{function} forward")
+    # backward
     for got, e, l, name in zip(res["grads"], ex, lit, ("dmeans", "dvalues", "dconics")):
-        attempt(close_grad, got, e, l, RTOL, atol_bwd, f"{function} dL/{name}")
+        attempt(close_grad, got, e, l, RTOL * scale[name], atol_bwd * scale[name], f"{function} dL/{name}")
     assert not errors, "\n".join(errors)
     return res, ob
 
@@ -93,11 +126,12 @@ def test_parity_small_gaussians_fine_cells(dgs, oracle, function):
 def test_parity_thin_anisotropic(dgs, oracle, function, C):
     """Thin rotated Gaussians near the seams (cases.thin_case): the sub-cell lists' slices and
     the per-row cut ranges at high anisotropy, forward and backward against the oracle; C = 3 and
-    16 take the lane-per-sample / matrix-core forwards and the literal backward terms."""
+    16 take the lane-per-sample / matrix-core forwards and the literal backward terms.  Stated
+    bound: the reference's own contraction spread (module docstring, spread=True)."""
     means, values, covs, conics, samples = cases.thin_case(C=C)
     K = syn.out_components(function, 2)
     dL = syn.grad_out(samples.shape[0], K, C, seed=152)
-    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, spread=True)
 
 
 @pytest.mark.parametrize("function,C", [("gaussian", 1), ("third", 1), ("derivative", 5)])

@@ -18,8 +18,12 @@ def main(path):
         if old is None or r["margin"] > old["margin"]:
             t[key] = {"margin": round(r["margin"], 4), "rtol": r["rtol"], "atol_frac": r["atol_frac"],
                       "n": r["n"]}
-    flat = [(m["margin"], test, what, m["atol_frac"]) for test, t in by_test.items() for what, m in t.items()]
-    flat.sort(reverse=True)
+    allm = [(m["margin"], test, what, m["atol_frac"]) for test, t in by_test.items() for what, m in t.items()]
+    allm.sort(reverse=True)
+    # bracketed records are informational: the reference's own spreads ("[reference serial order
+    # vs exact]", "[reference fmad vs no-contract]") and the plain-bound view of stated-bound checks
+    flat = [f for f in allm if "[" not in f[2]]
+    info = [f for f in allm if "[" in f[2]]
     grad = [f for f in flat if "/d" in f[2] or f[2].startswith("d")]
     doc = {
         "source": path,
@@ -29,6 +33,7 @@ def main(path):
         "worst": [{"margin": m, "test": t, "what": w, "atol_frac": a} for m, t, w, a in flat[:25]],
         "worst_gradients_at_atol_1e-6": [{"margin": m, "test": t, "what": w}
                                          for m, t, w, a in grad if a == 1e-6][:25],
+        "reference_spreads_and_plain_bounds_worst": [{"margin": m, "test": t, "what": w} for m, t, w, a in info[:40]],
         "by_test": by_test,
     }
     json.dump(doc, sys.stdout, indent=1)
