@@ -567,6 +567,9 @@ bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, 
 // take that path (any call not flagged DGS_SAMPLE_INPUTS_BINNED); later calls on another stream
 // wait for that build.  Buffers without a hint (not made by this process) are rebuilt per call.
 int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, hipStream_t s, int debug);
+// Counts the library's own stream-ordered allocations (dgs_internal_allocations, dgs.h): the
+// diagnostics, dgs_tile_grid and the call-time path's first use; the hot path makes none.
+void note_internal_alloc();
 
 // ---------------------------------------------------------------------------------------
 // Host-side error state

@@ -70,11 +70,19 @@ bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, 
     return true;
 }
 
-// The binning's one host read-back target: 8 int64 of pinned host memory per host thread (the
-// calls of one thread are sequential; kept for the thread's lifetime).
+static std::atomic<int64_t> g_internal_allocs{0};
+void note_internal_alloc() { g_internal_allocs.fetch_add(1, std::memory_order_relaxed); }
+
+// The binning's one host read-back target: 16 int64 of pinned host memory per host thread (the
+// calls of one thread are sequential; kept for the thread's lifetime).  [0, 8): the totals;
+// word 8: the sample and home sorts' look-back give-up words (read at the sync); word 9: the
+// previous binning's entry-sort give-up word (copied at its end, checked at the next sync).
 static int64_t *pinned_totals() {
     static thread_local int64_t *p = nullptr;
-    if (!p && hipHostMalloc(reinterpret_cast<void **>(&p), 64, hipHostMallocDefault) != hipSuccess) p = nullptr;
+    if (!p) {
+        if (hipHostMalloc(reinterpret_cast<void **>(&p), 128, hipHostMallocDefault) != hipSuccess) p = nullptr;
+        else std::memset(p, 0, 128);
+    }
     return p;
 }
 
@@ -1631,6 +1639,7 @@ __global__ void k_xchg_sets(int P, int D, const float *__restrict__ means, const
 using namespace dgs;
 
 extern "C" const char *dgs_last_error(void) { return g_last_error.c_str(); }
+extern "C" int64_t dgs_internal_allocations(void) { return g_internal_allocs.load(std::memory_order_relaxed); }
 extern "C" int dgs_version(void) { return (int)kVersion; }
 
 namespace dgs {
@@ -1658,6 +1667,7 @@ extern "C" int dgs_tile_grid(int N, int D, const float *samples, int *grid_out, 
     float *part = nullptr;
     int *dgrid = nullptr;
     float *doff = nullptr;
+    note_internal_alloc();  // (dgs_tile_grid's scratch: dgs.h)
     DGS_TRY_HIP(hipMallocAsync(&part, sizeof(float) * 4 * nparts, s));
     DGS_TRY_HIP(hipMallocAsync(&dgrid, sizeof(int) * 2, s));
     DGS_TRY_HIP(hipMallocAsync(&doff, sizeof(float) * 2, s));
@@ -1972,7 +1982,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // the stream ~28 us past the copy before the speculative phase-B work below could start)
     int64_t *htot = pinned_totals();
     if (!htot) return fail(DGS_ERR_ALLOC, "pinned host buffer allocation failed");
+    uint32_t *herr = reinterpret_cast<uint32_t *>(htot + 8);
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipMemcpyAsync(herr + 0, rs_s + plan_s.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
+    DGS_TRY_HIP(hipMemcpyAsync(herr + 1, rs_h + plan_h.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
     // the one host sync (num_rendered is a Python int): on an event right after the copy, so the
     // speculative phase B enqueued behind it keeps the GPU busy while the host reads the totals
     hipEvent_t copied = nullptr;
@@ -1989,6 +2002,15 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         if (rc) return rc;
     }
     DGS_TRY_HIP(hipEventSynchronize(copied));
+    // a radix look-back gave up (dgs_radix.h; never observed): this binning's sample / home sort,
+    // or the previous binning's entry sort on this thread (its word lands at the end of that call)
+    if (herr[0] || herr[1] || herr[2]) {
+        const bool prev = herr[2] != 0u;
+        herr[0] = herr[1] = herr[2] = 0u;
+        return fail(DGS_ERR_HIP, prev ? "the previous binning's entry sort failed (a radix look-back gave up): its "
+                                        "results were invalid"
+                                      : "binning: a radix sort's look-back gave up (sample or home sort)");
+    }
     const int64_t R = htot[0], E = htot[1], Es = htot[4];
     *num_rendered = R;
     if (dev_grid) {
@@ -2206,6 +2228,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.ref_built = false;
     uh.ref_done = nullptr;
     hint_put(uh);
+    if (Es > 0)  // the entry sort's give-up word, checked at this thread's next binning sync
+        DGS_TRY_HIP(hipMemcpyAsync(herr + 2, B.rs_e + B.plan_e.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
     return DGS_OK;
 }
 // Sorts the call-time path's tile lists (see ensure_ref_lists in dgs_internal.h) of the binning
@@ -2225,6 +2249,7 @@ static int build_ref_lists(const Header &h, char *gbuf, hipStream_t s, int debug
     const RadixPlan plan = radix_plan(R, rbits);
     const size_t kb = align_up(4 * (size_t)R, 256);
     char *scr = nullptr;
+    note_internal_alloc();  // (the call-time path's first use: dgs.h)
     DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), 3 * kb + plan.bytes, s));
     uint32_t *keys = reinterpret_cast<uint32_t *>(scr), *vals = reinterpret_cast<uint32_t *>(scr + kb);
     uint32_t *keys_sorted = reinterpret_cast<uint32_t *>(scr + 2 * kb);
@@ -2306,6 +2331,7 @@ extern "C" int dgs_test_radix_sort(int64_t n, int bits, int key_bytes, const voi
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const RadixPlan plan = radix_plan(n, bits);
     char *scr = nullptr;
+    note_internal_alloc();
     DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&scr), plan.bytes, s));
     hipError_t e = hipMemsetAsync(scr, 0, plan.zero_bytes, s);
     if (e == hipSuccess)

@@ -212,6 +212,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
         const uint32_t kk = sk[i];
         const uint32_t o = s_delta[rs_digit(kk, shift)] + (uint32_t)i;
         const uint32_t v = sv[i];
+        if ((int64_t)o >= n) continue;  // (only after a look-back gave up: the sort has failed, err is set)
         kout[o] = (KT)kk;
         vout[o] = v;
         extra(o, v);

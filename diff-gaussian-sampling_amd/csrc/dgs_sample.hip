@@ -1468,6 +1468,20 @@ static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     return w;
 }
 
+// The backward's slot-sum region (k_bwd_esum), behind the workspace layout: wanted where the
+// binning's sort path holds >= 1/4 of the entries (thin fields: ~70 %; the headline: 2 %, where the
+// slot pass costs more than the scattered atomics it replaces), for one channel block (the sums
+// of a multi-block C accumulate over the blocks: atomics).  The caller provides it by sizing the
+// workspace with dgs_sample_workspace_size_binned; a smaller workspace takes the atomics.
+static size_t slot_region_bytes(int FN, int D, int C, const void *gb, size_t gbytes, const void *sb, size_t sbytes) {
+    UnitHint h;
+    const int CB = channel_block(C);
+    if (C > CB || !hint_get(gb, gbytes, sb, sbytes, &h) || h.Es <= 0 || 4 * h.Es < h.E) return 0;
+    const int S = D * (D + 1) / 2;
+    (void)FN;
+    return a256(sizeof(float) * (size_t)((D + S + CB + 3) / 4 * 4) * (size_t)h.Es);
+}
+
 // Grid size in blocks: exact (from the preprocess hint) or a persistent-size fallback; the
 // kernels grid-stride over the device-side unit count either way.
 static unsigned unit_blocks(const void *gb, size_t gbytes, const void *sb, size_t sbytes, bool bwd,
@@ -1500,6 +1514,7 @@ struct Call {
     Outs outs;
     float *dm, *dv, *dc;
     char *ws;
+    size_t wsbytes;
     hipStream_t s;
     int debug;
 };
@@ -1606,19 +1621,10 @@ static int run_backward(const Call &a) {
     // over the blocks, so those keep the atomics; buffers without a hint keep them too)
     // Only where the sort path holds a large share of the entries (thin fields: 70 %): at the
     // headline (2 %) the slot pass costs more than the few scattered atomics it replaces.
-    UnitHint hint;
-    const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
-    // (not under graph capture: the slot buffer is a stream-ordered allocation)
-    const int64_t Es = hinted && 4 * hint.Es >= hint.E && !(a.opts & DGS_SAMPLE_GRAPH_CAPTURE) ? hint.Es : 0;
-    struct SlotBuf {  // (stream-ordered; freed on every return)
-        float *p = nullptr;
-        hipStream_t s;
-        ~SlotBuf() { if (p) (void)hipFreeAsync(p, s); }
-    } slots{nullptr, a.s};
-    if (Es > 0 && a.C <= CB)
-        DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&slots.p),
-                                   sizeof(float) * esum_stride<FN, D, CB>() * (size_t)Es, a.s));
-    float *const esums = slots.p;
+    // (the caller's workspace: no allocation here, graph capture included)
+    const size_t slot_bytes = slot_region_bytes(FN, D, a.C, a.gb, a.gbytes, a.sb, a.sbytes);
+    float *const esums = slot_bytes > 0 && a.wsbytes >= w.total + slot_bytes
+                             ? reinterpret_cast<float *>(a.ws + w.total) : nullptr;
     if (!binned)
         if (int rc = ensure_ref_lists(a.gb, a.gbytes, a.sb, a.sbytes, a.s, a.debug)) return rc;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
@@ -1748,6 +1754,17 @@ extern "C" size_t dgs_sample_workspace_size(int function, int P, int D, int N, i
     return ws_layout(function, P, D, N, C, backward != 0).total;
 }
 
+static int mask_code(int mask);
+extern "C" size_t dgs_sample_workspace_size_binned(int mask, int P, int D, int N, int C, int backward,
+                                                  const void *binning, size_t binning_bytes,
+                                                  const void *sample_binning, size_t sample_binning_bytes) {
+    const int FN = mask_code(mask);
+    if (FN < 0) return 256;
+    const size_t base = dgs_sample_workspace_size(FN, P, D, N, C, backward);
+    if (!backward || P <= 0 || N <= 0 || C <= 0 || (D != 1 && D != 2)) return base;
+    return base + slot_region_bytes(FN, D, C, binning, binning_bytes, sample_binning, sample_binning_bytes);
+}
+
 // ------------------------------------------------------------------ entry points
 // One traversal of the pairs for every function of `mask` (bit f = dgs_function f): the
 // forward writes each function's output, the backward takes each function's dL and returns
@@ -1789,7 +1806,7 @@ extern "C" int dgs_sample_forward_ex(int mask, int P, int D, int N, int C, const
     Call a{FN, P, D, N, C, flags, means, values, conics, samples, DLs{{nullptr, nullptr, nullptr, nullptr}},
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
            binning_bytes, sample_binning_bytes, o, nullptr, nullptr, nullptr,
-           static_cast<char *>(workspace), reinterpret_cast<hipStream_t>(stream), debug};
+           static_cast<char *>(workspace), workspace_bytes, reinterpret_cast<hipStream_t>(stream), debug};
     return dispatch(a, false);
 }
 
@@ -1828,7 +1845,7 @@ extern "C" int dgs_sample_backward_ex(int mask, int P, int D, int N, int C, cons
     Call a{FN, P, D, N, C, flags, means, values, conics, samples, d,
            static_cast<const char *>(binning), static_cast<const char *>(sample_binning),
            binning_bytes, sample_binning_bytes, Outs{{nullptr, nullptr, nullptr, nullptr}},
-           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), s, debug};
+           dL_dmeans, dL_dvalues, dL_dconics, static_cast<char *>(workspace), workspace_bytes, s, debug};
     return dispatch(a, true);
 }
 
@@ -1932,6 +1949,7 @@ extern "C" int dgs_inputs_match(int P, int D, int N, const float *means, const f
     if (rc || P == 0 || N == 0) return rc;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     uint32_t *flag = nullptr;
+    note_internal_alloc();  // (a diagnostic: 4 bytes of stream-ordered scratch, dgs.h)
     DGS_TRY_HIP(hipMallocAsync(&flag, 4, s));
     DGS_TRY_HIP(hipMemsetAsync(flag, 0, 4, s));
     rc = verify_inputs(static_cast<const char *>(binning), static_cast<const char *>(sample_binning), P, D, N,

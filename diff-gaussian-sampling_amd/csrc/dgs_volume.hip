@@ -1214,6 +1214,7 @@ extern "C" int dgs_volume_count_pairs(int P, int N, const float *means, const fl
     if (N == 0 || P == 0) return DGS_OK;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     unsigned long long *d = nullptr;
+    note_internal_alloc();  // (a diagnostic)
     DGS_TRY_HIP(hipMallocAsync(reinterpret_cast<void **>(&d), 24, s));
     DGS_TRY_HIP(hipMemsetAsync(d, 0, 24, s));
     if (int rc = vol_flag_reset_verify(P, N, means, conics, samples, binning, binning_bytes, s)) return rc;

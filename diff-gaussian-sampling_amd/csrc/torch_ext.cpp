@@ -94,6 +94,13 @@ struct TKey {
     const void *ptr;
     int64_t numel, version;
 };
+// Inference tensors (torch.inference_mode) have no version counter: calls on them keep no
+// records and always take the device-side comparison (as do buffers made under inference mode).
+bool trackable(std::initializer_list<const Tensor *> ts) {
+    for (const Tensor *t : ts)
+        if (t->is_inference()) return false;
+    return true;
+}
 TKey tkey(const Tensor &t) {
     return {t.storage().getWeakStorageImpl(), t.data_ptr(), t.numel(), (int64_t)t._version()};
 }
@@ -123,6 +130,7 @@ struct RowRecord {
     TKey gb, means, values, conics;
     int mask, C;
     Tensor work;
+    hipStream_t stream;  // the stream that packed the rows: reused only on it (stream order)
 };
 std::mutex g_step_mu;
 std::vector<BinRecord> g_bins;
@@ -133,12 +141,13 @@ void bins_put(const Tensor &gb, const Tensor &means, const Tensor &conics, const
     for (auto it = g_bins.begin(); it != g_bins.end();)
         if (it->gb.storage.expired() || it->gb.ptr == gb.data_ptr()) it = g_bins.erase(it);
         else ++it;
+    if (!trackable({&gb, &means, &conics, &samples})) return;
     g_bins.push_back({tkey(gb), tkey(means), tkey(conics), tkey(samples)});
     if (g_bins.size() > 8) g_bins.erase(g_bins.begin());
 }
 
 bool inputs_binned(const Tensor &gb, const Tensor &means, const Tensor &conics, const Tensor &samples) {
-    if (always_verify()) return false;
+    if (always_verify() || !trackable({&gb, &means, &conics, &samples})) return false;
     std::lock_guard<std::mutex> lk(g_step_mu);
     for (const auto &r : g_bins)
         if (same(r.gb, gb)) return same(r.means, means) && same(r.conics, conics) && same(r.samples, samples);
@@ -148,11 +157,13 @@ bool inputs_binned(const Tensor &gb, const Tensor &means, const Tensor &conics, 
 // take = true: remove the record (a backward overwrites the rows).
 bool rows_get(const Tensor &gb, int mask, int C, const Tensor &means, const Tensor &values, const Tensor &conics,
               size_t need, bool take, Tensor &work) {
+    if (!trackable({&gb, &means, &values, &conics})) return false;
+    const hipStream_t st = cur_stream();
     std::lock_guard<std::mutex> lk(g_step_mu);
     for (auto it = g_rows.begin(); it != g_rows.end(); ++it) {
         if (it->mask != mask || it->C != C || !same(it->gb, gb)) continue;
-        const bool ok = same(it->means, means) && same(it->values, values) && same(it->conics, conics) &&
-                        (size_t)it->work.numel() >= need;
+        const bool ok = it->stream == st && same(it->means, means) && same(it->values, values) &&
+                        same(it->conics, conics) && (size_t)it->work.numel() >= need;
         if (ok) work = it->work;
         if (take || !ok) g_rows.erase(it);
         return ok;
@@ -166,7 +177,9 @@ void rows_put(const Tensor &gb, int mask, int C, const Tensor &means, const Tens
     for (auto it = g_rows.begin(); it != g_rows.end();)
         if (it->gb.storage.expired() || (it->mask == mask && it->gb.ptr == gb.data_ptr())) it = g_rows.erase(it);
         else ++it;
-    g_rows.push_back({tkey(gb), tkey(means), tkey(values), tkey(conics), mask, C, work});
+    if (!trackable({&gb, &means, &values, &conics})) return;
+    // (the workspace was allocated on the current stream and is only reused on it: rows_get)
+    g_rows.push_back({tkey(gb), tkey(means), tkey(values), tkey(conics), mask, C, work, cur_stream()});
     if (g_rows.size() > 4) g_rows.erase(g_rows.begin());  // (the per-function path of a fused call keeps one per function)
 }
 
@@ -268,7 +281,10 @@ void forward_mask(int mask, const Tensor &means_in, const Tensor &values_in, con
     if (cap) o.flags |= DGS_SAMPLE_GRAPH_CAPTURE;
     const bool keep = !cap && (means_in.requires_grad() || values_in.requires_grad() || conics_in.requires_grad());
     const size_t ws = std::max(dgs_sample_workspace_size_multi(mask, P, D, N, C, 0),
-                               keep ? dgs_sample_workspace_size_multi(mask, P, D, N, C, 1) : (size_t)0);
+                               keep ? dgs_sample_workspace_size_binned(mask, P, D, N, C, 1, gb.data_ptr(),
+                                                                       (size_t)gb.numel(), sb.data_ptr(),
+                                                                       (size_t)sb.numel())
+                                    : (size_t)0);
     Tensor work;
     if (!cap && rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, false, work))
         o.flags |= DGS_SAMPLE_ROWS_VALID;
@@ -316,7 +332,9 @@ Grads backward_mask(int mask, const Tensor &means_in, const Tensor &values_in, c
         if (inputs_binned(binning_in, means_in, conics_in, samples_in)) o.flags |= DGS_SAMPLE_INPUTS_BINNED;
         else TORCH_CHECK(!cap, "sample_gaussians backward: ", kCaptureMsg);
         if (cap) o.flags |= DGS_SAMPLE_GRAPH_CAPTURE;
-        const size_t ws = dgs_sample_workspace_size_multi(mask, P, D, N, C, 1);
+        // (the binned size: room for the slot sums where the binning wants them)
+        const size_t ws = dgs_sample_workspace_size_binned(mask, P, D, N, C, 1, gb.data_ptr(), (size_t)gb.numel(),
+                                                           sb.data_ptr(), (size_t)sb.numel());
         Tensor work;
         if (!cap && rows_get(binning_in, mask, C, means_in, values_in, conics_in, ws, true, work))
             o.flags |= DGS_SAMPLE_ROWS_VALID;
@@ -576,8 +594,12 @@ void agg_put(const Tensor &indices, const Tensor &ranges, int64_t P, const Tenso
     for (auto it = g_agg.begin(); it != g_agg.end();)
         if (it->indices == indices.data_ptr() || it->impl.expired()) it = g_agg.erase(it);
         else ++it;
+    // (inference tensors have no version counter: their entry only carries the row order, a
+    // scheduling hint, and never transposed lists: transpose_get / transpose_put skip them)
+    const bool tr = trackable({&indices, &ranges});
     g_agg.push_back({indices.data_ptr(), P, indices.numel(), order, WeakImpl(indices.getIntrusivePtr()),
-                     (int64_t)indices._version(), tstart, tslot, rstart, ranges, (int64_t)ranges._version()});
+                     tr ? (int64_t)indices._version() : -1, tr ? tstart : Tensor(), tr ? tslot : Tensor(),
+                     tr ? rstart : Tensor(), ranges, tr ? (int64_t)ranges._version() : -1});
     if (g_agg.size() > 2) g_agg.erase(g_agg.begin());
 }
 
@@ -594,6 +616,7 @@ const int32_t *order_get(const Tensor &indices, int64_t P) {
 // Entries whose indices tensor has died are dropped here too (they would pin their lists).
 bool transpose_get(const Tensor &indices, const Tensor &ranges, int64_t P, Tensor &tstart, Tensor &tslot,
                    Tensor &rstart) {
+    if (!trackable({&indices, &ranges})) return false;
     std::lock_guard<std::mutex> lk(g_agg_mu);
     for (auto it = g_agg.begin(); it != g_agg.end();)
         if (it->impl.expired()) it = g_agg.erase(it);
@@ -616,6 +639,7 @@ bool transpose_get(const Tensor &indices, const Tensor &ranges, int64_t P, Tenso
 // (built lazily: forward-only users never pay for the transposition).
 void transpose_put(const Tensor &indices, const Tensor &ranges, int64_t P, const Tensor &tstart, const Tensor &tslot,
                    const Tensor &rstart) {
+    if (!trackable({&indices, &ranges})) return;
     std::lock_guard<std::mutex> lk(g_agg_mu);
     for (auto &e : g_agg) {
         if (e.P != P || e.length != indices.numel()) continue;

@@ -456,7 +456,11 @@ class SpatialShardedGaussianSampler(ShardedGaussianSampler):
             covariances, conics, samples, grid, offset, self.xchg.held, area, self.debug)
         self.grid, self.offset = grid, offset
         self.means, self.values, self.conics, self.samples = means, values, conics, samples
-        self._versions = (means._version, conics._version, samples._version)
+        self._versions = self._now()
+
+    def _now(self):
+        ts = (self.means, self.conics, self.samples)
+        return None if any(t.is_inference() for t in ts) else tuple(t._version for t in ts)
 
     def push(self, tensors, means=None, conics=None):
         """After optimizer.step(): the owners' rows of `tensors` to every rank their updated cut
@@ -466,7 +470,7 @@ class SpatialShardedGaussianSampler(ShardedGaussianSampler):
                               self.conics if conics is None else conics)
 
     def _sample(self, function):
-        if (self.means._version, self.conics._version, self.samples._version) != self._versions:
+        if self._now() != self._versions:  # (inference tensors: unknown, not checked)
             raise RuntimeError("SpatialShardedGaussianSampler: means, conics or samples were modified in place "
                                "after preprocess; call push() (after an optimizer step) and preprocess() again")
         return _SpatialSample.apply(function, self.xchg, self.means, self.values, self.conics,

@@ -67,14 +67,22 @@ class VolumeSampler:
         self.binning = preprocess_volume(means, conics, samples, self.debug)
         self.means, self.values, self.conics, self.samples = means, values, conics, samples
         self._versions = self._now()
+        self._fresh = True
 
     def _now(self):
-        return (self.means._version, self.conics._version, self.samples._version)
+        ts = (self.means, self.conics, self.samples)
+        if any(t.is_inference() for t in ts):  # no version counter: unknown
+            return None
+        return tuple(t._version for t in ts)
 
     def _run(self, code):
-        if self._now() != self._versions:  # changed in place since the binning: re-bin
+        now = self._now()
+        # changed in place since the binning (or, for inference tensors, possibly changed: every
+        # call after the first re-bins) -> re-bin
+        if (now is None and not self._fresh) or now != self._versions:
             self.binning = preprocess_volume(self.means, self.conics, self.samples, self.debug)
             self._versions = self._now()
+        self._fresh = False
         return sample_volume(code, self.means, self.values, self.conics, self.samples, self.binning,
                              self.debug)
 

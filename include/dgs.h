@@ -4,9 +4,15 @@
  * Plain pointers, sizes and a HIP stream; no torch types.  Every device pointer is global
  * memory on the current HIP device; every array is dense row-major fp32 unless stated.
  * All entry points are asynchronous on `stream` except where a host value is returned
- * (dgs_tile_grid, dgs_preprocess), and none allocates memory on its own: buffers come from
- * the caller through `dgs_alloc_fn` (mirroring the reference's resize_functional lambdas,
- * sample_points.cu:29-35) or as explicit workspaces.
+ * (dgs_tile_grid, dgs_preprocess).  The binning, sampling and aggregation entry points allocate
+ * no device memory on their own: buffers come from the caller through `dgs_alloc_fn`
+ * (mirroring the reference's resize_functional lambdas, sample_points.cu:29-35) or as explicit
+ * workspaces.  The exceptions use small stream-ordered scratch and are counted by
+ * dgs_internal_allocations(): dgs_tile_grid (its min/max partials), dgs_inputs_match and
+ * dgs_volume_count_pairs (diagnostics), and the first call-time-path use of a binning (a
+ * forward / backward WITHOUT DGS_SAMPLE_INPUTS_BINNED sorts the reference tile lists once).
+ * The preprocess reads its one host value back into pinned host memory allocated once per host
+ * thread.
  *
  * Each function names the reference interface it replaces.  The torch extension
  * diff_gaussian_sampling._C (csrc/torch_ext.cpp) maps the 12 pybind entry points of the
@@ -140,6 +146,20 @@ int dgs_exchange_sets(int P, int D, const float *means, const float *conics, int
 /* Workspace bytes needed by dgs_sample_forward (backward == 0) or dgs_sample_backward. */
 size_t dgs_sample_workspace_size(int function, int P, int D, int N, int C, int backward);
 
+/* The workspace bytes a call on THIS binning can use to full effect (mask as in
+ * dgs_sample_forward_ex): for a backward whose binning sends >= 1/4 of its entries through the
+ * sort path (thin / anisotropic fields) that adds a per-entry slot-sum region (the entries'
+ * partial gradients are stored and summed per Gaussian in order, instead of scattered float
+ * atomics).  A workspace of dgs_sample_workspace_size bytes is still valid (the atomics then).
+ * >= dgs_sample_workspace_size_multi(mask, ...); buffers this process did not bin: the same. */
+size_t dgs_sample_workspace_size_binned(int mask, int P, int D, int N, int C, int backward,
+                                        const void *binning, size_t binning_bytes,
+                                        const void *sample_binning, size_t sample_binning_bytes);
+
+/* Stream-ordered allocations the library has made on its own since load (see the top of this
+ * file: none on the binning / sampling hot path). */
+int64_t dgs_internal_allocations(void);
+
 /* Forward: replaces SampleGaussians{,Derivative,Laplacian,Third}CUDA (sample_points.cu:100-143,
  * 198-296), CudaSampler::Sampler::forward (sampler_impl.cu:333-364) and FORWARD::render
  * (forward.cu:277-345).  out[N][K][C], K = D^function, must be zero-filled by the caller
@@ -203,8 +223,7 @@ int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float 
  *     A forward followed by its backward shares one workspace of the backward's size this way.
  *     A backward leaves the region overwritten (its finalize reuses it): never reuse after one.
  *   DGS_SAMPLE_GRAPH_CAPTURE: the call is being captured into a HIP graph (stream capture):
- *     it then enqueues kernels only -- no stream-ordered allocation (the backward's slot sums
- *     fall back to atomics), no timing events -- and requires DGS_SAMPLE_INPUTS_BINNED (the
+ *     it then enqueues kernels only -- no timing events -- and requires DGS_SAMPLE_INPUTS_BINNED (the
  *     call-time path's first use builds tile lists behind a host-side record; DGS_ERR_ARG
  *     without it).  A replay re-reads means, values, conics, samples and dL from the captured
  *     addresses; values and dL may change between replays, means / conics / samples may not
@@ -242,9 +261,10 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
 /* Diagnostics (not on the reference API): host-known facts of a binning this process made (no
  * device work): out[0] = num_rendered R, out[1] = fine (Gaussian, cell) entries E, out[2] = the
  * entries that take the reference-literal per-pair path (conics that are not positive definite,
- * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = the entries of
- * ill-conditioned positive-definite conics (rho^2 >= 0.82: the packed path with the exponent in
- * the reference's order).  DGS_ERR_BUFFER for buffers this process did not bin. */
+ * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = kThin entries (only in a
+ * DGS_THIN_LITERAL build: ill-conditioned positive-definite conics, rho^2 >= 0.82, packed with
+ * the unfused reference's exponent order; 0 otherwise).  DGS_ERR_BUFFER for buffers this process
+ * did not bin. */
 int dgs_binning_info(const void *binning, size_t binning_bytes, const void *sample_binning,
                      size_t sample_binning_bytes, int64_t *out);
 
