@@ -55,6 +55,13 @@ FLOPS_D2 = {
 }
 
 
+def traffic_key(fn, C, P, N, aniso=1.0, grid=0):
+    """profiles/traffic.json's workload key: the measured bytes of one workload are never
+    reported for another (thin fields, lattices)."""
+    return (f"{fn},C={C},P={P},N={N}" + (f",aniso={aniso:g}" if aniso > 1 else "")
+            + (f",grid={grid}" if grid else ""))
+
+
 def flops_per_live_pair(function, C):
     f = FLOPS_D2[function]
     return f["fwd"][0] + f["fwd"][1] * C, f["bwd"][0] + f["bwd"][1] * C
@@ -394,7 +401,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
         if os.path.exists(tpath):
             try:
                 tj = json.load(open(tpath))
-                wl = tj.get("workloads", {}).get(f"{fn},C={C},P={P},N={N}", {})
+                wl = tj.get("workloads", {}).get(traffic_key(fn, C, P, N, args.aniso, args.grid), {})
                 traffic = wl.get(dom)
             except Exception:
                 traffic = None
@@ -445,7 +452,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
         **pre_extra,
         "kernels_ms": {"forward_render": avg_f, "backward_render": avg_b},
         "pairs": {"W_cand": w_cand, "W_live": w_live, "num_rendered": R},
-        "entries": dict(zip(("num_rendered", "fine_entries", "literal_path_entries", "fine_cells", "thin_entries"),
+        "entries": dict(zip(("num_rendered", "fine_entries", "literal_path_entries", "fine_cells", "thin_entries",
+                             "sort_path_entries"),
                             dgs._C.binning_info(gb, sb))),
         "roofline": roofline,
         "hbm": hbm,

@@ -385,11 +385,14 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
 // "the reference's" there.  So thin conics take the fast paths like every other PD conic, under
 // the stated bound of tests/test_gpu_parity.py (within twice the reference's own compile spread);
 // DGS_THIN_LITERAL=1 restores round 4's kThin entries (the unfused reference's order, lit_prob).
-// Past rho^2 = kRho2Max (amplification > 4e4) a conic is treated as not positive definite.
+// Past rho^2 = kRho2Max (axis ratio ~63, amplification ~4000) a conic is treated as not
+// positive definite: up to there the fp32 exponent of a pair beyond the cut (X^T A X > 210) is
+// below -104.8 in any operation order (|error| <= ~3e-7 x 4000 x 210 = 0.25), so culling it
+// drops an exact +0; past it the rounding could leave a subnormal term.
 #ifndef DGS_THIN_LITERAL
 #define DGS_THIN_LITERAL 0
 #endif
-constexpr double kRho2Max = 0.9999;
+constexpr double kRho2Max = 0.999;
 // Not positive definite, too ill-conditioned (above), or not finite: kUnsafe, the per-pair
 // literal path with the exact wrap and the reference's `power > 0 -> skip` (forward.cu:228).
 __host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float c2f) {
@@ -559,6 +562,7 @@ struct UnitHint {
     int64_t Es;       // of which sort-path entries (the backward's slot sums)
     Header hdr;       // the header preprocess wrote (ensure_ref_lists reads its geometry / offsets)
     bool ref_built;   // rlist built (ensure_ref_lists), ref_done recorded after its build
+    bool capture = false;  // a graph-capturable binning: R / E / nunsafe are on the device only
     hipEvent_t ref_done;
 };
 void hint_put(const UnitHint &h);

@@ -232,7 +232,9 @@ template <typename KT>
 __global__ void k_identify(int64_t L, const KT *__restrict__ keys, uint32_t limit,
                            int32_t *__restrict__ beg, int32_t *__restrict__ end, int shift,
                            uint32_t limit2 = 0, int32_t *__restrict__ beg2 = nullptr,
-                           int32_t *__restrict__ end2 = nullptr, int shift2 = 0) {
+                           int32_t *__restrict__ end2 = nullptr, int shift2 = 0,
+                           const int64_t *__restrict__ Ldev = nullptr) {
+    if (Ldev) L = min(L, max(sload(Ldev), (int64_t)0));  // (a capacity-sized launch: the device count)
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= L) return;
     const uint32_t kr = (uint32_t)keys[i], pr = i > 0 ? (uint32_t)keys[i - 1] : 0u;
@@ -950,7 +952,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     const int32_t *__restrict__ send, const float4 *__restrict__ box, const uint64_t *__restrict__ offs,
     const uint64_t *__restrict__ cnts, const int8_t *__restrict__ greach, const uint32_t *__restrict__ fbg,
     const uint2 *__restrict__ irect, KT *__restrict__ ekeys, uint32_t *__restrict__ evals,
-    int32_t *__restrict__ counters) {
+    int32_t *__restrict__ counters, uint64_t cap) {  // cap: the arrays' capacity (capturable binning)
     __shared__ uint32_t skey[kFillCap], sval[kFillCap];
     const FbBits fbits = fb_load(fbg, G.T);
     const int64_t i0 = (int64_t)blockIdx.x * kFillBlock;
@@ -974,7 +976,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
             if (stage) {
                 skey[o - base] = key;
                 sval[o - base] = val;
-            } else {
+            } else if (o < cap) {
                 ekeys[o] = (KT)key;
                 evals[o] = val;
             }
@@ -991,6 +993,7 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
         __syncthreads();
         const int n = (int)(end - base);
         for (int k = threadIdx.x; k < n; k += kFillBlock) {
+            if (base + k >= cap) break;
             ekeys[base + k] = (KT)skey[k];
             evals[base + k] = sval[k];
         }
@@ -1025,7 +1028,8 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
                                                    const uint32_t *__restrict__ hstart,
                                                    const int32_t *__restrict__ rmax, uint32_t *__restrict__ cnt2,
                                                    unsigned long long *__restrict__ eg,
-                                                   const int32_t *__restrict__ gbeg, uint32_t *__restrict__ entries) {
+                                                   const int32_t *__restrict__ gbeg, uint32_t *__restrict__ entries,
+                                                   uint32_t ecap = 0xffffffffu) {
     const int home_w = G.grid[0] * G.n, home_h = G.grid[1] * G.n;
     const int spr = (home_w + kStripW - 1) / kStripW;
     const int wid = __builtin_amdgcn_readfirstlane(blockIdx.x * kWavesPerBlock + (int)(threadIdx.x >> 6));
@@ -1077,7 +1081,7 @@ __global__ __launch_bounds__(kBlock) void k_gather(Geom G, int P, const int8_t *
                 const uint32_t base = __builtin_amdgcn_readlane(cur, j);
                 const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32),
                                                                 __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
-                if (hit) entries[base + rank] = i;
+                if (hit && base + rank < ecap) entries[base + rank] = i;
             }
             if (lane == j) cur += (uint32_t)__popcll(bal);
         }
@@ -1102,12 +1106,14 @@ __global__ void k_copy_sorted(int64_t Es, const KT *__restrict__ keys, const uin
                               const uint32_t *__restrict__ evals, const int32_t *__restrict__ hb,
                               const int32_t *__restrict__ gbeg, const int32_t *__restrict__ gmid,
                               const uint32_t *__restrict__ gcnt, uint32_t *__restrict__ entries,
-                              uint32_t *__restrict__ esum_q) {
+                              uint32_t *__restrict__ esum_q, const int64_t *__restrict__ Esdev, int64_t Ecap) {
+    if (Esdev) Es = min(Es, max(sload(Esdev), (int64_t)0));  // (capturable binning: the device count)
     const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= Es) return;
     const uint32_t key = (uint32_t)keys[r], c = key >> 2;
     const bool fl = (key >> 1) & 1u;
     const int64_t p = fl ? (int64_t)gmid[c] + (r - hb[2 * c + 1]) : (int64_t)gbeg[c] + gcnt[c] + (r - hb[2 * c]);
+    if (p >= Ecap) return;
     const uint32_t q = sq[r];
     entries[p] = evals[q];
     esum_q[p] = q;
@@ -1421,6 +1427,21 @@ struct TailSpec {
     uint2 *granges, *sranges;
     uint32_t *rtab;
     char *gbuf, *sbuf;
+    // the graph-capturable binning (capture != 0, dgs_bin_options.capacity_E > 0): the headers'
+    // counts come from the device totals ([0] R, [1] E, [4] sort-path entries), clamped to the
+    // capacities the lists were sized for; the status word (bits: 1 E, 2 sort-path entries, 4 R
+    // over capacity, 8 the samples' own tile grid differs from the given one) and num_rendered
+    // go to the caller; a non-zero status sets the header's "inputs differ" word, so the render
+    // kernels of binned calls leave their outputs untouched (k_verify ORs it in for the others)
+    int capture, D;
+    const int64_t *totals;
+    int64_t Rcap, Ecap, Escap;
+    const int *dgrid;
+    const float *doff;
+    int grid[2];
+    float off[2];
+    int64_t *R_out;
+    uint32_t *status;
 };
 
 __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts, Header h) {
@@ -1430,6 +1451,24 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
         for (int i = threadIdx.x; i < (int)sizeof(Header); i += blockDim.x) {
             ts.gbuf[i] = src[i];
             ts.sbuf[i] = src[i];
+        }
+        if (ts.capture) {
+            __syncthreads();
+            if (threadIdx.x == 0) {
+                const int64_t R = ts.totals[0], E = ts.totals[1], Es = ts.totals[4];
+                uint32_t st = (E > ts.Ecap ? 1u : 0u) | (Es > ts.Escap ? 2u : 0u) | (R > ts.Rcap ? 4u : 0u);
+                for (int d = 0; d < ts.D; ++d)
+                    if (ts.dgrid[d] != ts.grid[d] || __float_as_uint(ts.doff[d]) != __float_as_uint(ts.off[d])) st |= 8u;
+                for (char *b : {ts.gbuf, ts.sbuf}) {
+                    Header *hh = reinterpret_cast<Header *>(b);
+                    hh->R = min(R, ts.Rcap);
+                    hh->E = min(E, ts.Ecap);
+                    hh->Es = min(Es, ts.Escap);
+                    hh->zero[0] = st ? 1u : 0u;
+                }
+                *ts.R_out = R;
+                *ts.status = st;
+            }
         }
     }
     const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
@@ -1713,14 +1752,31 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                            const float *grid_offset, float *radii, dgs_alloc_fn alloc,
                            void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream, int debug,
                            const int *dgrid, const float *doff, int *dev_grid, float *dev_off,
-                           const uint8_t *present = nullptr, double sample_area = 0.0) {
+                           const uint8_t *present = nullptr, double sample_area = 0.0,
+                           const dgs_bin_options *copt = nullptr) {
+    // the graph-capturable form (dgs.h, dgs_bin_options.capacity_E > 0): no host sync and no
+    // host read of a device value -- the lists are sized from the caller's capacities, the exact
+    // counts stay on the device (capacity-sized launches read them), overflows are reported in
+    // the status word (k_binning_tail)
+    const bool capmode = copt && copt->capacity_E > 0;
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered) return fail(DGS_ERR_ARG, "dgs_preprocess: bad arguments");
     if ((int64_t)P > kMaxGaussians) return fail(DGS_ERR_ARG, "too many Gaussians (limit 2^29 - 1)");
     *num_rendered = 0;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (capmode) {
+        if (!copt->num_rendered_device || !copt->status_device || copt->capacity_R <= 0 || copt->capacity_Es < 0)
+            return fail(DGS_ERR_ARG, "dgs_preprocess_ex: the capturable binning needs capacity_R > 0, "
+                                     "capacity_Es >= 0, num_rendered_device and status_device");
+        *num_rendered = -1;  // (on the device: *num_rendered_device)
+        if (P == 0 || N == 0) {  // sample_points.cu:69: nothing to bin
+            DGS_TRY_HIP(hipMemsetAsync(copt->num_rendered_device, 0, sizeof(int64_t), s));
+            DGS_TRY_HIP(hipMemsetAsync(copt->status_device, 0, sizeof(uint32_t), s));
+            return DGS_OK;
+        }
+    }
     if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
     if (!grid || !grid_offset) return fail(DGS_ERR_ARG, "dgs_preprocess: grid/offset required");
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
 
     Geom G;
     G.D = D;
@@ -1787,6 +1843,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     float4 *igc = ca.take<float4>(P);
     float4 *grec = ca.take<float4>(2 * (size_t)P);
     unsigned long long *fscan_a = ca.take<unsigned long long>(fused_scan_state_words(P, 2, 8));
+    // capturable binning: the samples' own tile grid (sample_points.cu:70-74), checked on the device
+    const int nparts = capmode ? (int)std::min<int64_t>(1024, grid_for(N)) : 1;
+    float *bpart = ca.take<float>(4 * (size_t)nparts);
+    int32_t *cgrid = ca.take<int32_t>(4);
+    float *coff = ca.take<float>(4);
 
     // the two phase-A sorts' scratch (each with its own zero-filled head: see dgs_radix.h)
     const int sbits = bit_length((uint64_t)ncells * kSubPerCell);  // (cell, sub-cell) keys
@@ -1815,6 +1876,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(igc, base);
         Carve::rebase(grec, base);
         Carve::rebase(fscan_a, base);
+        Carve::rebase(bpart, base);
+        Carve::rebase(cgrid, base);
+        Carve::rebase(coff, base);
         Carve::rebase(rs_s, base);
         Carve::rebase(rs_h, base);
     }
@@ -1846,6 +1910,11 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
     }
 
+    if (capmode) {
+        k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, bpart);
+        k_bounds_final<<<1, kBlock, 0, s>>>(nparts, D, bpart, cgrid, coff);
+        DGS_LAUNCH_CHECK(s, debug);
+    }
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile, radix_hist(plan_s, rs_s));
     DGS_LAUNCH_CHECK(s, debug);
@@ -1978,11 +2047,25 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
         return DGS_OK;
     };
+    PhaseB B;
+    int64_t R, E, Es;
+    int64_t *htot = nullptr;
+    uint32_t *herr = nullptr;
+    if (capmode) {  // the caller's capacities: no sync, no read-back
+        R = copt->capacity_R;
+        E = copt->capacity_E;
+        Es = std::min(copt->capacity_Es, E);
+        if (E >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "capacity_E too large (2^31)");
+        if (nsub && kSubPerCell * E >= (1LL << 31) - 64)
+            return fail(DGS_ERR_ARG, "capacity_E too large for the sub-cell lists (4 E >= 2^31)");
+        if (R >= (1LL << 31) - 64) return fail(DGS_ERR_ARG, "capacity_R exceeds 2^31");
+        if (const int rc = setup_b(E, R, B)) return rc;
+    } else {
     // (into pinned host memory: a copy to pageable memory is staged by the runtime, which held
     // the stream ~28 us past the copy before the speculative phase-B work below could start)
-    int64_t *htot = pinned_totals();
+    htot = pinned_totals();
     if (!htot) return fail(DGS_ERR_ALLOC, "pinned host buffer allocation failed");
-    uint32_t *herr = reinterpret_cast<uint32_t *>(htot + 8);
+    herr = reinterpret_cast<uint32_t *>(htot + 8);
     DGS_TRY_HIP(hipMemcpyAsync(htot, totals, 8 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipMemcpyAsync(herr + 0, rs_s + plan_s.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipMemcpyAsync(herr + 1, rs_h + plan_h.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
@@ -1995,7 +2078,6 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         ~EventGuard() { if (e) (void)hipEventDestroy(e); }
     } copied_guard{copied};
     DGS_TRY_HIP(hipEventRecord(copied, s));
-    PhaseB B;
     const SizeSpec spec = size_spec_get(P, N, D);
     if (spec.E >= 0) {
         const int rc = setup_b(spec.E + spec.E / 8 + 1024, spec.R + spec.R / 8 + 1024, B);
@@ -2011,7 +2093,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                         "results were invalid"
                                       : "binning: a radix sort's look-back gave up (sample or home sort)");
     }
-    const int64_t R = htot[0], E = htot[1], Es = htot[4];
+    R = htot[0];
+    E = htot[1];
+    Es = htot[4];
     *num_rendered = R;
     if (dev_grid) {
         const int32_t *g = reinterpret_cast<const int32_t *>(htot + 2);
@@ -2030,6 +2114,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         const int rc = setup_b(E, R, B);
         if (rc) return rc;
     }
+    }
     const Layout &L = B.L;
     const int64_t bwd_cap = B.bwd_cap;
     char *gbuf = B.gbuf;
@@ -2046,26 +2131,33 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
 
     // ---- cell lists: the sort path's entries (sorted by (cell, flag)), then per cell the
     // gathered local entries (ascending id), the sorted unflagged and the flagged ones
+    // (capturable binning: Es / E are the capacities; the sort-path count on the device, esdev)
+    const int64_t *esdev = capmode ? totals + 4 : nullptr;
+    const uint64_t escap = capmode ? (uint64_t)Es : ~0ull;
     if (Es > 0) {
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
         if (k16)
             k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
                                                             fcount, greach, fbg, irect,
-                                                            reinterpret_cast<uint16_t *>(ekeys), evals, counters);
+                                                            reinterpret_cast<uint16_t *>(ekeys), evals, counters, escap);
         else
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
-                                                            fcount, greach, fbg, irect, ekeys, evals, counters);
+                                                            fcount, greach, fbg, irect, ekeys, evals, counters, escap);
         DGS_LAUNCH_CHECK(s, debug);
         // (values: the entries' positions q, for the backward's slots; k_copy_sorted gathers evals[q])
         DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),
-                                               reinterpret_cast<uint16_t *>(ekeys_sorted), nullptr, svals, s)
-                        : radix_sort<uint32_t>(B.plan_e, Es, B.rs_e, ekeys, ekeys_sorted, nullptr, svals, s));
+                                               reinterpret_cast<uint16_t *>(ekeys_sorted), nullptr, svals, s, false,
+                                               RsNone{}, esdev)
+                        : radix_sort<uint32_t>(B.plan_e, Es, B.rs_e, ekeys, ekeys_sorted, nullptr, svals, s, false,
+                                               RsNone{}, esdev));
         DGS_LAUNCH_CHECK(s, debug);
         if (k16)
             k_identify<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(Es, reinterpret_cast<const uint16_t *>(ekeys_sorted),
-                                                                 2u * (uint32_t)ncells, hbeg, hend, 1);
+                                                                 2u * (uint32_t)ncells, hbeg, hend, 1, 0u, nullptr,
+                                                                 nullptr, 0, esdev);
         else
-            k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 1);
+            k_identify<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, 2u * (uint32_t)ncells, hbeg, hend, 1,
+                                                                 0u, nullptr, nullptr, 0, esdev);
         DGS_LAUNCH_CHECK(s, debug);
     }
     {  // per cell: [gathered (ascending id) + sorted unflagged | sorted flagged] = [gbeg, gmid, gend)
@@ -2074,6 +2166,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         uint32_t *gc = gcnt;
         int32_t *gb_ = cell_gbeg, *gm_ = cell_gmid, *ge_ = cell_gend;
         int32_t *gs_ = reinterpret_cast<int32_t *>(gbuf + L.o_cell_gsort);  // (where each sorted part begins)
+        const int64_t ecap = E;  // (exact here, or the capturable binning's capacity: lists clamped into it)
         DGS_TRY_HIP((fused_scan<1, 1>(
             (int64_t)ncells, B.fs_cells,
             [=] __device__(int64_t c, uint64_t *x) {
@@ -2083,19 +2176,19 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                 x[0] = g + (uint32_t)(he[2 * c] - hb[2 * c]) + (uint32_t)(he[2 * c + 1] - hb[2 * c + 1]);
             },
             [=] __device__(int64_t c, const uint64_t *, const uint64_t *ex) {
-                const int32_t b = (int32_t)ex[0];
-                const int32_t mid = b + (int32_t)gc[c] + (he[2 * c] - hb[2 * c]);
-                gb_[c] = b;
-                gm_[c] = mid;
-                ge_[c] = mid + (he[2 * c + 1] - hb[2 * c + 1]);
-                gs_[c] = b + (int32_t)gc[c];
+                const int64_t b = (int64_t)ex[0];
+                const int64_t mid = b + (int64_t)gc[c] + (he[2 * c] - hb[2 * c]);
+                gb_[c] = (int32_t)min(b, ecap);
+                gm_[c] = (int32_t)min(mid, ecap);
+                ge_[c] = (int32_t)min(mid + (he[2 * c + 1] - hb[2 * c + 1]), ecap);
+                gs_[c] = (int32_t)min(b + (int64_t)gc[c], ecap);
             },
             [=] __device__(const uint64_t *) {}, s)));
         DGS_LAUNCH_CHECK(s, debug);
     }
-    if (D == 2 && E > Es) {
+    if (D == 2 && (capmode || E > Es)) {
         k_gather<true><<<gather_blocks, kBlock, 0, s>>>(G, P, greach, lrows, hstart, rmax, cnt2, nullptr, cell_gbeg,
-                                                        entries);
+                                                        entries, (uint32_t)E);
         DGS_LAUNCH_CHECK(s, debug);
     }
     if (Es > 0) {
@@ -2103,10 +2196,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         if (k16)
             k_copy_sorted<uint16_t><<<grid_for(Es), kBlock, 0, s>>>(
                 Es, reinterpret_cast<const uint16_t *>(ekeys_sorted), svals, evals, hbeg, cell_gbeg, cell_gmid, gcnt,
-                entries, eq);
+                entries, eq, esdev, E);
         else
             k_copy_sorted<uint32_t><<<grid_for(Es), kBlock, 0, s>>>(Es, ekeys_sorted, svals, evals, hbeg, cell_gbeg,
-                                                                    cell_gmid, gcnt, entries, eq);
+                                                                    cell_gmid, gcnt, entries, eq, esdev, E);
         DGS_LAUNCH_CHECK(s, debug);
     }
     {  // work units: forward (cell, 64 pair-aligned samples), backward (cell, 64 list entries)
@@ -2209,8 +2302,19 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     h.o_sub_lthin = L.o_sub_lthin;
     h.fsub_cap = fsub_cap_of(D, N, ncells); h.esub_cap = esub_cap_of(D, E);
     h.stamp = ++stamp_counter;
-    const TailSpec ts{G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf), reinterpret_cast<uint2 *>(srbuf),
-                      reinterpret_cast<uint32_t *>(gbuf + L.o_rtab), gbuf, sbuf};
+    TailSpec ts{G.T, gtile, stile, reinterpret_cast<uint2 *>(rbuf), reinterpret_cast<uint2 *>(srbuf),
+                reinterpret_cast<uint32_t *>(gbuf + L.o_rtab), gbuf, sbuf};
+    if (capmode) {
+        ts.capture = 1;
+        ts.D = D;
+        ts.totals = totals;
+        ts.Rcap = R; ts.Ecap = E; ts.Escap = Es;
+        ts.dgrid = cgrid;
+        ts.doff = coff;
+        for (int d = 0; d < 2; ++d) { ts.grid[d] = G.grid[d]; ts.off[d] = G.off[d]; }
+        ts.R_out = copt->num_rendered_device;
+        ts.status = copt->status_device;
+    }
     k_binning_tail<<<1024, kBlock, 0, s>>>(c, ts, h);
     DGS_LAUNCH_CHECK(s, debug);
 
@@ -2220,7 +2324,9 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // forward's unsafe-only tail pass is not launched).
     UnitHint uh;
     uh.gbuf = gbuf; uh.sbuf = sbuf; uh.gbytes = L.g_bytes; uh.sbytes = L0.s_bytes;
-    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = htot[6]; uh.nthin = htot[7];
+    // (capturable binning: the counts are the device's; unknown here -> every pass launched)
+    uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = capmode ? -1 : htot[6]; uh.nthin = capmode ? -1 : htot[7];
+    uh.capture = capmode;
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E; uh.Es = Es;
@@ -2228,7 +2334,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.ref_built = false;
     uh.ref_done = nullptr;
     hint_put(uh);
-    if (Es > 0)  // the entry sort's give-up word, checked at this thread's next binning sync
+    if (Es > 0 && herr)  // the entry sort's give-up word, checked at this thread's next binning sync
         DGS_TRY_HIP(hipMemcpyAsync(herr + 2, B.rs_e + B.plan_e.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
     return DGS_OK;
 }
@@ -2273,7 +2379,9 @@ static std::mutex g_ref_mu;  // one build per binning, whichever stream asks fir
 int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, hipStream_t s, int debug) {
     std::lock_guard<std::mutex> lk(g_ref_mu);
     UnitHint h;
-    if (!hint_get(gbuf, gbytes, sbuf, sbytes, &h)) {  // a foreign buffer: its header, then a build
+    const bool known = hint_get(gbuf, gbytes, sbuf, sbytes, &h);
+    if (!known || (h.capture && !h.ref_built)) {  // a foreign buffer (or a capturable binning's: R is
+                                                  // on the device): its header, then a build
         Header hd;
         DGS_TRY_HIP(hipMemcpyAsync(&hd, gbuf, sizeof(hd), hipMemcpyDeviceToHost, s));
         DGS_TRY_HIP(hipStreamSynchronize(s));
@@ -2369,7 +2477,7 @@ extern "C" int dgs_preprocess_ex(int P, int D, int N, const float *means, const 
     if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_ex: sample_area must be >= 0");
     return preprocess_body(P, D, N, means, covariances, conics, samples, grid, grid_offset, radii, alloc,
                            alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present,
-                           area);
+                           area, opts);
 }
 
 // The speculation of dgs_preprocess_auto, per sample set: keyed by (samples pointer, N, D), the
@@ -2478,6 +2586,7 @@ extern "C" int dgs_binning_info(const void *binning, size_t binning_bytes, const
     out[2] = h.nunsafe;
     out[3] = h.ncells;
     out[4] = h.nthin;
+    out[5] = h.Es;
     return DGS_OK;
 }
 

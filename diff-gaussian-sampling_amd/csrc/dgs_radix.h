@@ -66,10 +66,13 @@ inline RadixPlan radix_plan(int64_t n, int bits) {
 __device__ __forceinline__ uint32_t rs_digit(uint32_t key, int shift) { return (key >> shift) & (kRsBins - 1); }
 
 // All places' digit counts in one read of the keys (LDS histograms, one global add per bin).
+// ndev (optional, device): the item count is min(n, *ndev) -- a sort sized by a capacity whose
+// exact count only the device knows (the graph-capturable binning).
 template <typename KT>
 __global__ __launch_bounds__(kRsThreads) void k_rs_hist(int64_t n, const KT *__restrict__ keys, int places,
-                                                        uint32_t *__restrict__ hist) {
+                                                        uint32_t *__restrict__ hist, const int64_t *__restrict__ ndev) {
     __shared__ uint32_t h[4 * kRsBins];
+    if (ndev) n = min(n, max(sload(ndev), (int64_t)0));
     for (int i = threadIdx.x; i < places * kRsBins; i += kRsThreads) h[i] = 0u;
     __syncthreads();
     for (int64_t i = (int64_t)blockIdx.x * kRsThreads + threadIdx.x; i < n; i += (int64_t)gridDim.x * kRsThreads) {
@@ -118,8 +121,9 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
                                                         int shift, const uint32_t *__restrict__ hist, int hstride,
                                                         unsigned long long *__restrict__ states,
                                                         uint32_t *__restrict__ ticket, uint32_t *__restrict__ err,
-                                                        Extra extra) {
+                                                        Extra extra, const int64_t *__restrict__ ndev) {
     __shared__ uint32_t sk[kRsTile], sv[kRsTile];
+    if (ndev) n = min(n, max(sload(ndev), (int64_t)0));  // (tiles past it publish empty counts)
     __shared__ uint32_t cnt[kRsWaves][kRsBins];
     __shared__ uint32_t s_tstart[kRsBins], s_delta[kRsBins];
     __shared__ uint32_t wsum[kRsWaves];
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(kRsThreads) void k_rs_pass(int64_t n, const KT *__r
 template <typename KT, class Extra = RsNone>
 static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const KT *kin, KT *kout,
                              const uint32_t *vin, uint32_t *vout, hipStream_t s, bool hist_ready = false,
-                             Extra extra = Extra{}) {
+                             Extra extra = Extra{}, const int64_t *ndev = nullptr) {
     if (n <= 0) return hipSuccess;
     if (n > p.n) return hipErrorInvalidValue;
     uint32_t *hist = reinterpret_cast<uint32_t *>(scratch);
@@ -238,7 +242,7 @@ static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const
     KT *tk = reinterpret_cast<KT *>(scratch + p.o_tkeys);
     uint32_t *tv = reinterpret_cast<uint32_t *>(scratch + p.o_tvals);
     const unsigned hb = (unsigned)(tiles < 1024 ? tiles : 1024);
-    if (!hist_ready) k_rs_hist<KT><<<hb, kRsThreads, 0, s>>>(n, kin, p.places, hist);
+    if (!hist_ready) k_rs_hist<KT><<<hb, kRsThreads, 0, s>>>(n, kin, p.places, hist, ndev);
     const KT *ki = kin;
     const uint32_t *vi = vin;
     for (int q = 0; q < p.places; ++q) {
@@ -248,11 +252,11 @@ static hipError_t radix_sort(const RadixPlan &p, int64_t n, char *scratch, const
         if (q == p.places - 1)  // (the last place: the payload too)
             k_rs_pass<KT, Extra><<<(unsigned)tiles, kRsThreads, 0, s>>>(
                 n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, p.places * kRsBins,
-                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, extra);
+                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, extra, ndev);
         else
             k_rs_pass<KT, RsNone><<<(unsigned)tiles, kRsThreads, 0, s>>>(
                 n, ki, ko, vi, vo, q * kRsBits, hist + q * kRsBins, p.places * kRsBins,
-                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, RsNone{});
+                states + (size_t)q * p.tiles * kRsBins, tickets + q, err, RsNone{}, ndev);
         ki = ko;
         vi = vo;
     }

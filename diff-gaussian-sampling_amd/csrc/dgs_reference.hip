@@ -5,10 +5,15 @@
 //                   64 of its samples in sorted order), lane = sample, the tile's Gaussian list
 //                   walked in ascending id (the reference's per-thread order) with wave-uniform
 //                   scalar loads of the CALL-TIME means / conics / values
-// k_ref_backward  : renderCUDA backward (backward.cu:26-106): unit = (tile, 64 entries of its
-//                   list), lane = Gaussian (call-time parameters), the tile's samples
-//                   wave-uniform; per lane one float atomic per gradient component per unit into
-//                   the internal-order sums that k_finalize permutes to caller order
+// k_ref_backward  : renderCUDA backward (backward.cu:26-106) over the same units, lane =
+//                   sample: per candidate Gaussian the wave's pair terms are summed across the
+//                   lanes and added with one float atomic per gradient component into the
+//                   internal-order sums that k_finalize permutes to caller order
+// Both walk a tile's Gaussian list 64 entries at a time and evaluate only the entries whose
+// call-time cut can reach the unit's sample box (ref_may_touch): every other pair adds exactly
+// +0 in the reference, so the culling changes no result (the forward's sums keep the
+// reference's per-sample order); the call-time path costs ~the live pairs, not the ~1e11 pairs
+// of the tiles.
 // Both run only when the flag is set (they exit at once otherwise); the fine-cell kernels of
 // dgs_sample.hip exit when it is set.  The arithmetic per pair is the reference's: the exact
 // period-2 wrap (ref_wrap), the literal power (ref_power), `power > 0 -> skip`, expf.
@@ -45,6 +50,9 @@ __global__ void k_verify(const char *__restrict__ gb, const char *__restrict__ s
         }
         for (int64_t i = done + t; i < n[r]; i += st) diff |= in[r][i] != cp[r][i];
     }
+    // (a graph-capturable binning whose lists overflowed their capacities marks itself invalid
+    // in the header's "inputs differ" word: the fine-cell kernels must not use it)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && sload(&h->zero[0])) diff = true;
     if (__any(diff) && (threadIdx.x & (kWave - 1)) == 0) atomicOr(flag, 1u);
 }
 
@@ -83,6 +91,108 @@ __device__ __forceinline__ void ref_displacement(const float *m, const float *s,
     X[1] = D == 2 ? ref_wrap(m[1] - s[1]) : 0.0f;
 }
 
+// Whether a Gaussian with the CALL-TIME mean m and conic c can add anything to a sample of the
+// box [lo, hi]: false only when every displacement X = m - s of the box lies in (-1, 1) on each
+// axis (so the reference applies no torus wrap, forward.cu:149-157) and some axis is farther than
+// the cut's half-width e_d = sqrt(210 Sigma_dd) -- then X^T A X > 210 and the reference's fp32
+// power is below -104.8 (rho^2 < kRho2Max, dgs_internal.h), expf(power) == +0 and the pair adds
+// exactly nothing (v * 0 * t), forward and backward.  Other conics: true.
+template <int D>
+__device__ __forceinline__ bool ref_may_touch(const float *m, const float *c, const float *lo, const float *hi) {
+    double e[2];
+    const double c0 = c[0];
+    if constexpr (D == 1) {
+        if (!(c0 > 0.0 && c0 < INFINITY)) return true;
+        e[0] = sqrt(kQCut / c0) * (1.0 + 1e-4) + 1e-7;
+    } else {
+        const double c1 = c[1], c2 = c[2], det = c0 * c2 - c1 * c1;
+        if (!(c0 > 0.0 && c2 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY &&
+              c1 * c1 < kRho2Max * (c0 * c2)))
+            return true;
+        e[0] = sqrt(kQCut * c2 / det) * (1.0 + 1e-4) + 1e-7;
+        e[1] = sqrt(kQCut * c0 / det) * (1.0 + 1e-4) + 1e-7;
+    }
+    bool far = false;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const double xa = (double)m[d] - (double)hi[d], xb = (double)m[d] - (double)lo[d];
+        if (!(xa > -1.0 && xb < 1.0)) return true;  // a wrap is possible (or NaN): keep
+        far |= fmax(fmax(xa, -xb), 0.0) > e[d];
+    }
+    return !far;
+}
+
+// Wave-wide min / max / sum (every lane gets the result).
+__device__ __forceinline__ float wave_min(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fminf(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ float wave_max(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x = fmaxf(x, __shfl_xor(x, o));
+    return x;
+}
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) x += __shfl_xor(x, o);
+    return x;
+}
+
+// A call-time unit: (tile t, kRefUnit of its samples in sorted order), lane = sample; the box of
+// the unit's samples, wave-uniform.
+struct RefUnit {
+    int t;
+    bool active;
+    int64_t sid;
+    float s[2], lo[2], hi[2];
+};
+template <int D>
+__device__ __forceinline__ RefUnit ref_unit(const Bins &bins, const uint32_t *fu, const uint32_t *sst, int T,
+                                            uint32_t unit, const float *__restrict__ samples, int lane) {
+    RefUnit u;
+    u.t = tile_of_unit(fu, T, unit);
+    const uint32_t sb = sload(&sst[u.t]), se = sload(&sst[u.t + 1]);
+    const uint32_t j = sb + (unit - sload(&fu[u.t])) * kRefUnit + lane;
+    u.active = j < se;
+    u.sid = bins.sorted_sid[u.active ? j : sb];
+    u.s[0] = samples[u.sid * D];
+    u.s[1] = D == 2 ? samples[u.sid * D + 1] : 0.0f;
+#pragma unroll
+    for (int d = 0; d < 2; ++d) {
+        u.lo[d] = wave_min(u.active ? u.s[d] : INFINITY);
+        u.hi[d] = wave_max(u.active ? u.s[d] : -INFINITY);
+    }
+    return u;
+}
+
+// The candidates of a group of kRefUnit entries [e0, e0 + 64) of tile list [.., ge): the ones
+// that may touch the unit's box (ref_may_touch, each lane one entry), as a wave-uniform bit mask
+// in list order; g = the lane's caller id.
+template <int D>
+__device__ __forceinline__ uint64_t ref_group(const Bins &bins, uint32_t e0, uint32_t ge, const float *__restrict__ means,
+                                              const float *__restrict__ conics, const RefUnit &u, int lane,
+                                              int64_t &g) {
+    constexpr int S = D * (D + 1) / 2;
+    const uint32_t e = e0 + lane;
+    const bool valid = e < ge;
+    g = valid ? (int64_t)bins.rlist[e] : 0;
+    bool keep = false;
+    if (valid) {
+        const float m[2] = {means[g * D], D == 2 ? means[g * D + 1] : 0.0f};
+        float c[3] = {0.0f, 0.0f, 0.0f};
+#pragma unroll
+        for (int k = 0; k < S; ++k) c[k] = conics[g * S + k];
+        keep = ref_may_touch<D>(m, c, u.lo, u.hi);
+    }
+    return (uint64_t)__ballot(keep);
+}
+
+// renderCUDA's forward (forward.cu:87-166) on the reference's pair set with the call-time
+// tensors: per unit the tile's Gaussian list in ascending id (the reference's per-thread order),
+// 64 entries at a time; only the candidates of ref_group are evaluated (the others add exactly
+// +0), wave-uniform, with the reference-literal pair arithmetic -- the same sums, in the same
+// order, as walking every pair.
 template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_ref_forward(const char *__restrict__ gbuf, const char *__restrict__ sbuf,
                                                         const float *__restrict__ means,
@@ -103,61 +213,59 @@ __global__ __launch_bounds__(kBlock) void k_ref_forward(const char *__restrict__
     const int nch = min(CB, C - cbase);
     const uint32_t w0 = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint32_t unit = w0; unit < nunits; unit += gridDim.x * kWavesPerBlock) {
-        const int t = tile_of_unit(fu, T, unit);
-        const uint32_t sb = sload(&sst[t]), se = sload(&sst[t + 1]);
-        const uint32_t j = sb + (unit - sload(&fu[t])) * kRefUnit + lane;
-        const bool active = j < se;
-        const int64_t sid = bins.sorted_sid[active ? j : sb];
-        const float s[2] = {samples[sid * D], D == 2 ? samples[sid * D + 1] : 0.0f};
+        const RefUnit u = ref_unit<D>(bins, fu, sst, T, unit, samples, lane);
         float acc[U][CB];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int a = 0; a < U; ++a)
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) acc[u][ch] = 0.0f;
-        const uint32_t ge = sload(&gst[t + 1]);
-        for (uint32_t e = sload(&gst[t]); e < ge; ++e) {  // ascending Gaussian id, as the reference
-            const int64_t g = sload(&bins.rlist[e]);
-            float m[2], c[3] = {0.0f, 0.0f, 0.0f}, v[CB];
-            m[0] = sload(&means[g * D]);
-            m[1] = D == 2 ? sload(&means[g * D + 1]) : 0.0f;
+            for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
+        const uint32_t ge = sload(&gst[u.t + 1]);
+        for (uint32_t e0 = sload(&gst[u.t]); e0 < ge; e0 += kWave) {
+            int64_t gl;
+            uint64_t cand = ref_group<D>(bins, e0, ge, means, conics, u, lane, gl);
+            while (cand) {  // ascending list position: ascending Gaussian id, as the reference
+                const int b = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const int64_t g = __builtin_amdgcn_readlane((int)gl, b);
+                float m[2], c[3] = {0.0f, 0.0f, 0.0f}, v[CB];
+                m[0] = sload(&means[g * D]);
+                m[1] = D == 2 ? sload(&means[g * D + 1]) : 0.0f;
 #pragma unroll
-            for (int k = 0; k < S; ++k) c[k] = sload(&conics[g * S + k]);
+                for (int k = 0; k < S; ++k) c[k] = sload(&conics[g * S + k]);
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? sload(&values[g * C + cbase + ch]) : 0.0f;
-            float X[2];
-            ref_displacement<D>(m, s, X);
-            const float p = ref_power<FN, D>(X, c);
-            if (!(p > 0.0f)) fwd_terms<FN, D, CB, float>(X, c, expf(p), v, acc);  // forward.cu:228
+                for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? sload(&values[g * C + cbase + ch]) : 0.0f;
+                float X[2];
+                ref_displacement<D>(m, u.s, X);
+                const float p = ref_power<FN, D>(X, c);
+                if (!(p > 0.0f)) fwd_terms<FN, D, CB, float>(X, c, expf(p), v, acc);  // forward.cu:228
+            }
         }
-        if (active) {
+        if (u.active) {
 #pragma unroll
             for (int ui = 0; ui < U; ++ui)
 #pragma unroll
                 for (int ch = 0; ch < CB; ++ch)
-                    if (ch < nch) store_unique<FN, D, false>(outs, sid, ui, C, cbase + ch, acc[ui][ch]);
+                    if (ch < nch) store_unique<FN, D, false>(outs, u.sid, ui, C, cbase + ch, acc[ui][ch]);
         }
     }
 }
 
-// One function f of the call's mask: this sample's dL (summed over symmetric components) and
-// the reference's per-pair gradient terms, into that function's accumulators.
+// This lane's (sample's) dL of function f, summed over symmetric components (unique terms).
 template <int f, int D, int CB>
-__device__ __forceinline__ void ref_bwd_fn(const DLs &dls, int64_t sid, int C, int cbase, int nch,
-                                           const float *X, const float *c, float G, const float *v,
-                                           float *gm, float *gv, float *gc) {
+__device__ __forceinline__ void ref_lane_dl(const DLs &dls, int64_t sid, bool active, int C, int cbase, int nch,
+                                            float (&dl)[Traits<f, D>::U][CB]) {
     constexpr int U = Traits<f, D>::U, K = Traits<f, D>::K;
-    float dl[U][CB];
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int a = 0; a < U; ++a)
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) dl[u][ch] = 0.0f;
+        for (int ch = 0; ch < CB; ++ch) dl[a][ch] = 0.0f;
+    if (!active) return;
     const float *d = dls.p[f] + sid * K * C + cbase;
 #pragma unroll
     for (int k = 0; k < K; ++k)
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch)
-            if (ch < nch) dl[unique_fk(f, D, k)][ch] += sload(&d[k * C + ch]);
-    bwd_terms<f, D, CB, float>(X, c, G, v, dl, gm, gv, gc);
+            if (ch < nch) dl[unique_fk(f, D, k)][ch] += d[k * C + ch];
 }
 
 template <int f, int D, int CB>
@@ -171,6 +279,34 @@ __device__ __forceinline__ void ref_bwd_finish_fn(const float *c, const float *v
     bwd_finish<f, D>(c, gm, gc);
 }
 
+// One Gaussian's gradient terms of function f over the unit's samples (lane = sample): the
+// reference's per-pair terms (backward.cu:108-416) summed over the wave, finished, and added to
+// the sums sm / sc / sv (every lane holds them).
+template <int f, int D, int CB>
+__device__ __forceinline__ void ref_bwd_fn_wave(const float *X, const float *c, float G, const float *v,
+                                                const float (&dl)[Traits<f, D>::U][CB], float *sm, float *sc,
+                                                float *sv) {
+    float gm[2] = {0.0f, 0.0f}, gc[3] = {0.0f, 0.0f, 0.0f}, gv[CB];
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) gv[ch] = 0.0f;
+    bwd_terms<f, D, CB, float>(X, c, G, v, dl, gm, gv, gc);
+#pragma unroll
+    for (int d = 0; d < 2; ++d) gm[d] = wave_sum(gm[d]);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) gc[k] = wave_sum(gc[k]);
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) gv[ch] = wave_sum(gv[ch]);
+    ref_bwd_finish_fn<f, D, CB>(c, v, gm, gc);
+    sm[0] += gm[0]; sm[1] += gm[1];
+    sc[0] += gc[0]; sc[1] += gc[1]; sc[2] += gc[2];
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) sv[ch] += gv[ch];
+}
+
+// renderCUDA's backward (backward.cu:26-106) on the reference's pair set with the call-time
+// tensors, over the forward's units (lane = sample): per candidate Gaussian of ref_group the
+// wave's pair terms are summed across the lanes and added with one float atomic per gradient
+// component (the reference: one per pair; its atomic order is unspecified).
 template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_ref_backward(const char *__restrict__ gbuf, const char *__restrict__ sbuf,
                                                          const float *__restrict__ means,
@@ -184,69 +320,63 @@ __global__ __launch_bounds__(kBlock) void k_ref_backward(const char *__restrict_
     const Bins bins = resolve(gbuf, sbuf);
     const int T = sload(&bins.h->T);
     const uint32_t *gst = bins.rtab + kRtGStart * (T + 1), *sst = bins.rtab + kRtSStart * (T + 1);
-    const uint32_t *bu = bins.rtab + kRtBwdUnits * (T + 1);
+    const uint32_t *fu = bins.rtab + kRtFwdUnits * (T + 1);
     const int32_t *inv = bins.perm + P;
-    const uint32_t nunits = sload(&bu[T]);
+    const uint32_t nunits = sload(&fu[T]);
     const int lane = threadIdx.x & (kWave - 1);
     const int nch = min(CB, C - cbase);
     const uint32_t w0 = blockIdx.x * kWavesPerBlock + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     for (uint32_t unit = w0; unit < nunits; unit += gridDim.x * kWavesPerBlock) {
-        const int t = tile_of_unit(bu, T, unit);
-        const uint32_t eb = sload(&gst[t]), ee = sload(&gst[t + 1]);
-        const uint32_t e = eb + (unit - sload(&bu[t])) * kRefUnit + lane;
-        const bool active = e < ee;
-        const int64_t g = bins.rlist[active ? e : eb];
-        const float m[2] = {means[g * D], D == 2 ? means[g * D + 1] : 0.0f};
-        float c[3] = {0.0f, 0.0f, 0.0f}, v[CB];
+        const RefUnit u = ref_unit<D>(bins, fu, sst, T, unit, samples, lane);
+        float dl0[Traits<0, D>::U][CB], dl1[Traits<1, D>::U][CB], dl2[Traits<2, D>::U][CB], dl3[Traits<3, D>::U][CB];
+        if constexpr ((M & 1) != 0) ref_lane_dl<0, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl0);
+        if constexpr ((M & 2) != 0) ref_lane_dl<1, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl1);
+        if constexpr ((M & 4) != 0) ref_lane_dl<2, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl2);
+        if constexpr ((M & 8) != 0) ref_lane_dl<3, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl3);
+        const uint32_t ge = sload(&gst[u.t + 1]);
+        for (uint32_t e0 = sload(&gst[u.t]); e0 < ge; e0 += kWave) {
+            int64_t gl;
+            uint64_t cand = ref_group<D>(bins, e0, ge, means, conics, u, lane, gl);
+            while (cand) {
+                const int b = __builtin_ctzll(cand);
+                cand &= cand - 1;
+                const int64_t g = __builtin_amdgcn_readlane((int)gl, b);
+                float m[2], c[3] = {0.0f, 0.0f, 0.0f}, v[CB];
+                m[0] = sload(&means[g * D]);
+                m[1] = D == 2 ? sload(&means[g * D + 1]) : 0.0f;
 #pragma unroll
-        for (int k = 0; k < S; ++k) c[k] = conics[g * S + k];
+                for (int k = 0; k < S; ++k) c[k] = sload(&conics[g * S + k]);
 #pragma unroll
-        for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? values[g * C + cbase + ch] : 0.0f;
-        float gm[4][2], gv[4][CB], gc[4][3];
+                for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? sload(&values[g * C + cbase + ch]) : 0.0f;
+                float X[2];
+                ref_displacement<D>(m, u.s, X);
+                const float p = ref_power<FN, D>(X, c);
+                // backward.cu:114/133/...: power > 0 -> skip (G = 0 adds exactly nothing)
+                const float G = u.active && !(p > 0.0f) ? expf(p) : 0.0f;
+                if (!__any(G != 0.0f)) continue;
+                float sm[2] = {0.0f, 0.0f}, sc[3] = {0.0f, 0.0f, 0.0f}, sv[CB];
 #pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            gm[f][0] = gm[f][1] = gc[f][0] = gc[f][1] = gc[f][2] = 0.0f;
+                for (int ch = 0; ch < CB; ++ch) sv[ch] = 0.0f;
+                if constexpr ((M & 1) != 0) ref_bwd_fn_wave<0, D, CB>(X, c, G, v, dl0, sm, sc, sv);
+                if constexpr ((M & 2) != 0) ref_bwd_fn_wave<1, D, CB>(X, c, G, v, dl1, sm, sc, sv);
+                if constexpr ((M & 4) != 0) ref_bwd_fn_wave<2, D, CB>(X, c, G, v, dl2, sm, sc, sv);
+                if constexpr ((M & 8) != 0) ref_bwd_fn_wave<3, D, CB>(X, c, G, v, dl3, sm, sc, sv);
+                // one component per lane: [dm(D) dc(S) dv(nch)] of the internal row
+                const int64_t i = inv[g];
+                float val = 0.0f;
+                int64_t off = -1;
 #pragma unroll
-            for (int ch = 0; ch < CB; ++ch) gv[f][ch] = 0.0f;
+                for (int d = 0; d < D; ++d)
+                    if (lane == d) { val = sm[d]; off = (int64_t)d * P + i; }
+#pragma unroll
+                for (int k = 0; k < S; ++k)
+                    if (lane == D + k) { val = sc[k]; off = (int64_t)(D + k) * P + i; }
+#pragma unroll
+                for (int ch = 0; ch < CB; ++ch)
+                    if (ch < nch && lane == D + S + ch) { val = sv[ch]; off = (int64_t)(D + S + cbase + ch) * P + i; }
+                if (off >= 0) atomicAdd(acc + off, val);
+            }
         }
-        const uint32_t se = sload(&sst[t + 1]);
-        for (uint32_t j = sload(&sst[t]); j < se; ++j) {  // the tile's samples, wave-uniform
-            const int64_t sid = sload(&bins.sorted_sid[j]);
-            const float s[2] = {sload(&samples[sid * D]), D == 2 ? sload(&samples[sid * D + 1]) : 0.0f};
-            float X[2];
-            ref_displacement<D>(m, s, X);
-            const float p = ref_power<FN, D>(X, c);
-            if (p > 0.0f) continue;  // backward.cu:114/133/...: power > 0 -> skip
-            const float G = expf(p);
-            if constexpr ((M & 1) != 0) ref_bwd_fn<0, D, CB>(dls, sid, C, cbase, nch, X, c, G, v, gm[0], gv[0], gc[0]);
-            if constexpr ((M & 2) != 0) ref_bwd_fn<1, D, CB>(dls, sid, C, cbase, nch, X, c, G, v, gm[1], gv[1], gc[1]);
-            if constexpr ((M & 4) != 0) ref_bwd_fn<2, D, CB>(dls, sid, C, cbase, nch, X, c, G, v, gm[2], gv[2], gc[2]);
-            if constexpr ((M & 8) != 0) ref_bwd_fn<3, D, CB>(dls, sid, C, cbase, nch, X, c, G, v, gm[3], gv[3], gc[3]);
-        }
-        if (!active) continue;
-        if constexpr ((M & 1) != 0) ref_bwd_finish_fn<0, D, CB>(c, v, gm[0], gc[0]);
-        if constexpr ((M & 2) != 0) ref_bwd_finish_fn<1, D, CB>(c, v, gm[1], gc[1]);
-        if constexpr ((M & 4) != 0) ref_bwd_finish_fn<2, D, CB>(c, v, gm[2], gc[2]);
-        if constexpr ((M & 8) != 0) ref_bwd_finish_fn<3, D, CB>(c, v, gm[3], gc[3]);
-        float sm[2] = {0.0f, 0.0f}, sc[3] = {0.0f, 0.0f, 0.0f}, sv[CB];
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch) sv[ch] = 0.0f;
-#pragma unroll
-        for (int f = 0; f < 4; ++f) {
-            if (!(M & (1 << f))) continue;
-            sm[0] += gm[f][0]; sm[1] += gm[f][1];
-            sc[0] += gc[f][0]; sc[1] += gc[f][1]; sc[2] += gc[f][2];
-#pragma unroll
-            for (int ch = 0; ch < CB; ++ch) sv[ch] += gv[f][ch];
-        }
-        const int64_t i = inv[g];  // internal index: k_finalize permutes to caller order
-#pragma unroll
-        for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + i, sm[d]);
-#pragma unroll
-        for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + i, sc[k]);
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch)
-            if (ch < nch) atomicAdd(acc + (int64_t)(D + S + cbase + ch) * P + i, sv[ch]);
     }
 }
 
@@ -267,7 +397,7 @@ int ref_forward(const RefCall &a) {
 
 template <int FN, int D, int CB>
 int ref_backward(const RefCall &a) {
-    const int64_t cap = a.R / kRefUnit + (a.R + 1);
+    const int64_t cap = a.N / kRefUnit + (a.N + 1);  // (the forward's units)
     k_ref_backward<FN, D, CB><<<ref_blocks(cap), kBlock, 0, a.s>>>(a.gb, a.sb, a.means, a.values, a.conics,
                                                                    a.samples, a.flag, a.dls, a.acc, a.P,
                                                                    a.C, a.cbase);

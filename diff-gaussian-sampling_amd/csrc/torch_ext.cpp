@@ -220,6 +220,30 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
                            ctx.bufs[DGS_BUF_RANGES], ctx.bufs[DGS_BUF_SAMPLE_RANGES], radii);
 }
 
+// The graph-capturable binning (dgs_bin_options.capacity_E): the caller's
+// grid / offset and capacities [E, Es, R] (binning_info of an earlier binning plus slack); no
+// host sync, so it can be captured with torch.cuda.graph together with the sample calls.
+// Returns (num_rendered int64[1] and status int32[1] on the device, binning buffers, ranges,
+// radii); status != 0: the capacities were too small or the samples' grid changed (dgs.h).
+std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>
+PreprocessCapturableCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances, const Tensor &conics,
+                         const Tensor &samples, std::vector<int> grid, std::vector<float> offset,
+                         std::vector<int64_t> capacity, const bool debug) {
+    TORCH_CHECK(capacity.size() == 3 && capacity[0] > 0 && capacity[2] > 0 && capacity[1] >= 0,
+                "capacity must be [E > 0, Es >= 0, R > 0]");
+    Tensor rdev = torch::zeros({1}, means.options().dtype(torch::kInt64));
+    Tensor status = torch::zeros({1}, means.options().dtype(torch::kInt32));
+    dgs_bin_options o{};
+    o.capacity_E = capacity[0];
+    o.capacity_Es = std::min(capacity[1], capacity[0]);
+    o.capacity_R = capacity[2];
+    o.num_rendered_device = rdev.data_ptr<int64_t>();
+    o.status_device = reinterpret_cast<uint32_t *>(status.data_ptr<int32_t>());
+    PreOut r = preprocess_impl(means, values, covariances, conics, samples, &grid, &offset, debug, &o);
+    return std::make_tuple(rdev, std::get<1>(r), std::get<2>(r), std::get<3>(r), std::get<4>(r), std::get<5>(r),
+                           status);
+}
+
 // PreprocessCUDA (sample_points.h:20-27)
 PreOut PreprocessCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances,
                       const Tensor &conics, const Tensor &samples, const bool debug) {
@@ -492,7 +516,7 @@ std::tuple<int64_t, int64_t> CountPairs(const Tensor &means_in, const Tensor &co
     return std::make_tuple(counts[0], counts[1]);
 }
 
-// (R, E, literal-path entries, fine cells, thin entries) of a binning (dgs_binning_info).
+// (R, E, literal-path entries, fine cells, thin entries, sort-path entries) of a binning (dgs_binning_info).
 extern "C" int dgs_test_radix_sort(int64_t n, int bits, int key_bytes, const void *kin, void *kout,
                                    const uint32_t *vin, uint32_t *vout, dgs_stream_t stream);
 
@@ -518,11 +542,12 @@ std::vector<int64_t> DebugFcProf() {
     return std::vector<int64_t>(o, o + 8);
 }
 
-std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in, const Tensor &sbinning_in) {
+std::tuple<int64_t, int64_t, int64_t, int64_t, int64_t, int64_t> BinningInfo(const Tensor &binning_in,
+                                                                               const Tensor &sbinning_in) {
     const Tensor gb = u8(binning_in, "binning_buffer"), sb = u8(sbinning_in, "sample_binning_buffer");
-    int64_t o[5] = {0, 0, 0, 0, 0};
+    int64_t o[6] = {0, 0, 0, 0, 0, 0};
     check(dgs_binning_info(gb.data_ptr(), (size_t)gb.numel(), sb.data_ptr(), (size_t)sb.numel(), o), "binning_info");
-    return std::make_tuple(o[0], o[1], o[2], o[3], o[4]);
+    return std::make_tuple(o[0], o[1], o[2], o[3], o[4], o[5]);
 }
 
 // Whether forward / backward with these tensors take the binned path (dgs_inputs_match).
@@ -925,6 +950,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
     m.def("exchange_sets", &ExchangeSets);
     m.def("inputs_match", &InputsMatch);
     m.def("binning_info", &BinningInfo);
+    m.def("preprocess_gaussians_capturable", &PreprocessCapturableCUDA);
     m.def("radix_sort_test", &RadixSortTest);
     m.def("debug_fc_prof", &DebugFcProf);
     m.def("volume_preprocess", &VolumePreprocess);

@@ -19,7 +19,7 @@ __all__ = [
     "sample_gaussians", "sample_gaussians_derivative", "sample_gaussians_laplacian",
     "sample_gaussians_third_derivative", "aggregate_neighbors", "preprocess_gaussians",
     "preprocess_aggregate", "call_debug", "cpu_deep_copy_tuple", "GaussianSampler",
-    "sample_gaussians_multi", "FUNCTIONS",
+    "sample_gaussians_multi", "FUNCTIONS", "preprocess_gaussians_capturable", "capacity_from",
 ]
 
 # Function names of the fused entry point (codes of dgs_function, include/dgs.h).
@@ -96,6 +96,33 @@ def preprocess_gaussians(means, values, covariances, conics, samples, debug):
     ranges, sample_ranges, radii)."""
     args = (means, values, covariances, conics, samples, debug)
     return call_debug(_C.preprocess_gaussians, debug, "preprocess", *args)
+
+
+def preprocess_gaussians_capturable(means, values, covariances, conics, samples, grid, offset, capacity,
+                                    debug=False):
+    """The graph-capturable binning (not on the reference API): no host
+    synchronisation, so a training step -- re-binning after the optimizer moved the means, then the
+    sample calls and the backward -- can be captured whole with torch.cuda.graph and replayed.
+
+    grid / offset: the tile grid of the samples (sample_points.cu:70-74; e.g. `_C.tile_grid(samples)`
+    or a first eager binning's), fixed for the captured step.  capacity = [E, Es, R]: list sizes,
+    e.g. `capacity_from(binning_buffer, sample_binning_buffer)` of an eager binning.  Returns
+    (num_rendered, binning_buffer, sample_binning_buffer, ranges, sample_ranges, radii, status)
+    with num_rendered (int64[1]) and status (int32[1]) ON THE DEVICE.  status != 0 after a replay:
+    the capacities were too small (bits 1, 2, 4) or the samples' grid changed (bit 8); the step's
+    outputs are then invalid (zeros) -- re-bin eagerly and re-capture with larger capacities.
+    The sample calls take num_rendered only for signature parity (pass any int)."""
+    args = (means, values, covariances, conics, samples, [int(g) for g in grid], [float(o) for o in offset],
+            [int(c) for c in capacity], debug)
+    return call_debug(_C.preprocess_gaussians_capturable, debug, "preprocess_capturable", *args)
+
+
+def capacity_from(binning_buffer, sample_binning_buffer, slack=0.125):
+    """[E, Es, R] of an eager binning (dgs_binning_info) widened by `slack`: capacities for
+    preprocess_gaussians_capturable."""
+    R, E, _, _, _, Es = _C.binning_info(binning_buffer, sample_binning_buffer)
+    grow = lambda x: int(x + x * slack + 1024)  # noqa: E731
+    return [grow(E), grow(Es), grow(R)]
 
 
 def preprocess_aggregate(means, conics, radii, debug):

@@ -122,7 +122,7 @@ class ShardedGaussianSampler:
 
 # ------------------------------------------------------------------------ spatial shards (f3)
 Q_CUT = 210.0  # X^T A X above this gives expf(-q / 2) == +0 in fp32 (dgs_internal.h kQCut)
-RHO2_MAX = 0.9999  # conics with c1^2 >= RHO2_MAX c0 c2 are not culled (dgs_internal.h kRho2Max)
+RHO2_MAX = 0.999  # conics with c1^2 >= RHO2_MAX c0 c2 are not culled (dgs_internal.h kRho2Max)
 
 
 def support_halfwidth(means, conics):
@@ -361,12 +361,15 @@ def grid_and_box(samples, group=None, strip=None):
         dist.all_reduce(gmn, op=dist.ReduceOp.MIN, group=group)
         dist.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
     grid = torch.ceil((gmx[:D] - gmn + 1e-6) / 0.51).to(torch.float32)
-    h = torch.stack([grid, gmn, mn, mx]).cpu()
+    rows = [grid, gmn, mn, mx]
+    if strip is not None:  # the strip flag rides along in the same transfer
+        rows.append(torch.cat([gmx[D:D + 1], torch.zeros(D - 1, dtype=gmx.dtype, device=gmx.device)]))
+    h = torch.stack(rows).cpu()
     res = ([int(g) for g in h[0]], [float(o) for o in h[1]], [float(v) for v in h[2]],
            [float(v) for v in h[3]])
     if strip is None:
         return res
-    return res + (bool(gmx[D].item() > 0),)
+    return res + (bool(h[4][0] > 0),)
 
 
 def pack_grads(grads):

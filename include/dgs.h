@@ -107,6 +107,22 @@ typedef struct dgs_bin_options {
      * shard's points fill only part of the global tile grid.  Results do not depend on it
      * beyond float summation order; 0 = the whole grid. */
     double sample_area;
+    /* > 0: the GRAPH-CAPTURABLE binning (replaces the syncs of
+     * sampler_impl.cu:257 and sample_points.cu:74).  No host synchronisation and no host read of a
+     * device value, so the call can be captured into a HIP graph and replayed (a training loop's
+     * re-binning after every optimizer step).  The lists are sized from these capacities -- e.g.
+     * the previous binning's sizes plus slack (dgs_binning_info out[1], out[5]); the grid is the
+     * one passed to dgs_preprocess_ex.  *num_rendered (host) is set to -1;
+     *   num_rendered_device (int64, device): R;
+     *   status_device (uint32, device): 0, or bits 1: entries > capacity_E, 2: sort-path entries
+     *   > capacity_Es, 4: R > capacity_R, 8: the samples' own tile grid (sample_points.cu:70-74)
+     *   differs from the one passed.
+     * A non-zero status marks the binning invalid (the lists were clamped into the capacities):
+     * sample calls on it leave binned outputs at zero, never access memory out of bounds; re-bin
+     * eagerly or with larger capacities.  capacity_Es <= capacity_E, capacity_R > 0. */
+    int64_t capacity_E, capacity_Es, capacity_R;
+    int64_t *num_rendered_device;
+    uint32_t *status_device;
 } dgs_bin_options;
 
 /* dgs_preprocess with options (NULL = dgs_preprocess). */
@@ -263,8 +279,10 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
  * entries that take the reference-literal per-pair path (conics that are not positive definite,
  * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = kThin entries (only in a
  * DGS_THIN_LITERAL build: ill-conditioned positive-definite conics, rho^2 >= 0.82, packed with
- * the unfused reference's exponent order; 0 otherwise).  DGS_ERR_BUFFER for buffers this process
- * did not bin. */
+ * the unfused reference's exponent order; 0 otherwise), out[5] = sort-path entries (the
+ * capturable binning's capacity_Es).  A capturable binning reports its capacities for R / E and
+ * -1 for the device-only counts.  DGS_ERR_BUFFER for buffers this process did not bin.
+ * out must hold 6 values. */
 int dgs_binning_info(const void *binning, size_t binning_bytes, const void *sample_binning,
                      size_t sample_binning_bytes, int64_t *out);
 

@@ -72,6 +72,75 @@ def forward_backward(fname):
     assert not torch.equal(new_out, ref_out)
 
 
+def rebin_step(fname):
+    """the whole PIGS step -- re-binning (preprocess_gaussians_capturable),
+    forward, loss and loss.backward() into .grad -- captured as ONE graph with torch's
+    whole-network recipe (warm-up on a side stream, grads set to None before the capture), then
+    replayed after in-place steps of the means (the optimizer's move): every replay must match an
+    eager preprocess + forward + backward of the moved means at the parity bound, with status 0."""
+    dev = torch.device("cuda")
+    P, N, C = 20000, 60000, 1
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, C, seed=3))
+    samples = syn.samples(N, 2, seed=9).to(dev)
+    K = 2 if fname == "derivative" else 1
+    fwd = {"gaussian": dgs.sample_gaussians, "derivative": dgs.sample_gaussians_derivative}[fname]
+    target = torch.randn((N,) + (2,) * (K - 1) + (C,), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    R0, gb0, sb0, _, _, _ = dgs.preprocess_gaussians(means, values, covs, conics, samples, False)
+    grid, off = dgs._C.tile_grid(samples)
+    cap = dgs.capacity_from(gb0, sb0, slack=0.25)
+    for t in (means, values, conics):
+        t.requires_grad_(True)
+
+    def step():
+        R, gb, sb, rg, srg, _, st = dgs.preprocess_gaussians_capturable(means.detach(), values.detach(), covs,
+                                                                         conics.detach(), samples, grid, off, cap)
+        out = fwd(means, values, conics, samples, cap[2], gb, sb, rg, srg, False)
+        (out - target).square().sum().backward()
+        return out, st, R
+
+    def eager():
+        R, gb, sb, rg, srg, _ = dgs.preprocess_gaussians(means.detach(), values.detach(), covs, conics.detach(),
+                                                         samples, False)
+        out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
+        g = torch.autograd.grad((out - target).square().sum(), (means, values, conics))
+        return out.detach(), g, R
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            for t in (means, values, conics):
+                t.grad = None
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    for t in (means, values, conics):
+        t.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g_out, g_st, g_R = step()
+    gen = torch.Generator(device=dev).manual_seed(11)
+    for it in range(3):
+        with torch.no_grad():  # the optimizer's in-place move of the means (no re-capture)
+            means.add_(torch.randn(means.shape, device=dev, generator=gen) * 2e-3)
+        graph.replay()
+        torch.cuda.synchronize()
+        assert int(g_st.item()) == 0, f"replay {it}: status {int(g_st.item())}"
+        ref_out, ref_g, ref_R = eager()
+        assert int(g_R.item()) == ref_R, f"replay {it}: num_rendered {int(g_R.item())} != {ref_R}"
+        _close(g_out.detach(), ref_out, f"replay {it} forward")
+        for p, r, w in zip((means, values, conics), ref_g, ("dmeans", "dvalues", "dconics")):
+            _close(p.grad, r, f"replay {it} {w}")
+    # a capacity overflow is reported, never out of bounds: a tiny capacity, eager
+    R, gb, sb, rg, srg, _, st = dgs.preprocess_gaussians_capturable(means.detach(), values.detach(), covs,
+                                                                     conics.detach(), samples, grid, off,
+                                                                     [4096, 1024, 4096])
+    out = dgs._C.sample_gaussians(means.detach(), values.detach(), conics.detach(), samples, 0, gb, sb, rg, srg,
+                                  False)
+    torch.cuda.synchronize()
+    assert int(st.item()) & 1, f"overflow not reported: status {int(st.item())}"
+    assert torch.isfinite(out).all()
+
+
 def requires_binned():
     dev = torch.device("cuda")
     P, N = 2000, 6000
@@ -97,6 +166,8 @@ def requires_binned():
 if __name__ == "__main__":
     if sys.argv[1] == "forward_backward":
         forward_backward(sys.argv[2])
+    elif sys.argv[1] == "rebin_step":
+        rebin_step(sys.argv[2])
     else:
         requires_binned()
     print("ok", flush=True)

@@ -75,7 +75,7 @@ def test_no_internal_allocation_thin_field(oracle):
                                 radii.data_ptr(), cb, None, ctypes.byref(R), stream, 0))
     assert requests, "the binning's buffers come from the callback"
     gb, sb = held[0][-1], held[1][-1]
-    info = (ctypes.c_int64 * 5)()
+    info = (ctypes.c_int64 * 6)()
     _ok(lib, lib.dgs_binning_info(gb.data_ptr(), gb.numel(), sb.data_ptr(), sb.numel(), info))
     plain = lib.dgs_sample_workspace_size(0, P, D, N, C, 1)
     binned = lib.dgs_sample_workspace_size_binned(1, P, D, N, C, 1, gb.data_ptr(), gb.numel(), sb.data_ptr(),

@@ -33,5 +33,12 @@ def test_graph_capture_forward_backward(fname):
     _child("forward_backward", fname)
 
 
+@pytest.mark.parametrize("fname", ["gaussian", "derivative"])
+def test_graph_capture_rebin_step(fname):
+    """The whole PIGS step in one graph: capturable re-binning + forward + loss.backward() into
+    .grad, replayed after in-place moves of the means (graph_child.rebin_step)."""
+    _child("rebin_step", fname)
+
+
 def test_graph_capture_requires_binned_tensors():
     _child("requires_binned")
