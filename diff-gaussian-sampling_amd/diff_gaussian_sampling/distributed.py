@@ -48,27 +48,45 @@ def global_tile_grid(samples, group=None):
     return [int(g) for g in grid.cpu()], [float(o) for o in mn.cpu()]
 
 
-def allreduce_grads(grads, group=None):
-    """Sums (dmeans, dvalues, dconics) over ranks with one collective on a packed buffer."""
+def allreduce_grads(grads, group=None, chunks=1):
+    """Sums (dmeans, dvalues, dconics) over ranks: the packed rows [dmeans | dvalues | dconics]
+    (P x (D + C + S) floats), one collective, or `chunks` row blocks whose collectives are issued
+    back to back (async_op): block k's all-reduce runs on the communication stream while block
+    k + 1 is packed on the compute stream, and RCCL pipelines the blocks over xGMI.  The sum of an
+    element does not depend on the blocking at world 2 (a + b); at more ranks the ring's order
+    may differ in the last bit (tests/test_distributed.py checks world 2 bit for bit)."""
     if _world(group) == 1:
         return grads
-    flat = torch.cat([g.reshape(-1) for g in grads])
-    dist.all_reduce(flat, group=group)
+    P = grads[0].shape[0]
+    cols = [g.reshape(P, -1) for g in grads]
+    widths = [c.shape[1] for c in cols]
+    chunks = max(1, min(int(chunks), P)) if P else 1
+    bounds = [P * k // chunks for k in range(chunks + 1)]
+    blocks, works = [], []
+    for k in range(chunks):  # pack block k, then start its collective (async)
+        r0, r1 = bounds[k], bounds[k + 1]
+        blk = torch.cat([c[r0:r1] for c in cols], dim=1).contiguous()
+        blocks.append(blk)
+        works.append(dist.all_reduce(blk, group=group, async_op=True))
+    for w in works:
+        w.wait()
+    packed = blocks[0] if chunks == 1 else torch.cat(blocks, dim=0)
     out, o = [], 0
-    for g in grads:
-        out.append(flat[o:o + g.numel()].view_as(g))
-        o += g.numel()
+    for g, w in zip(grads, widths):
+        out.append(packed[:, o:o + w].reshape(g.shape))
+        o += w
     return tuple(out)
 
 
 class _ShardedSample(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, function, group, means, values, conics, samples, num_rendered, binning,
+    def forward(ctx, function, comm, means, values, conics, samples, num_rendered, binning,
                 sample_binning, ranges, sample_ranges, debug):
         fwd = getattr(_C, _FWD[function])
         out = call_debug(fwd, debug, "shard_fw", means, values, conics, samples, num_rendered,
                          binning, sample_binning, ranges, sample_ranges, debug)
-        ctx.function, ctx.group, ctx.debug, ctx.num_rendered = function, group, debug, num_rendered
+        ctx.function, ctx.debug, ctx.num_rendered = function, debug, num_rendered
+        ctx.group, ctx.chunks = comm  # (process group, row blocks of the gradient all-reduce)
         ctx.save_for_backward(means, values, conics, samples, binning, sample_binning, ranges,
                               sample_ranges)
         return out
@@ -80,17 +98,19 @@ class _ShardedSample(torch.autograd.Function):
         grads = call_debug(bwd, ctx.debug, "shard_bw", means, values, conics, samples,
                            ctx.num_rendered, grad_out.contiguous(), binning, sample_binning,
                            ranges, sample_ranges, ctx.debug)
-        gm, gv, gc = allreduce_grads(grads, ctx.group)
+        gm, gv, gc = allreduce_grads(grads, ctx.group, ctx.chunks)
         return (None, None, gm, gv, gc) + (None,) * 7
 
 
 class ShardedGaussianSampler:
     """GaussianSampler over a process group: this rank's `samples` are its shard; gradients
-    flowing back to (means, values, conics) are the sums over all shards."""
+    flowing back to (means, values, conics) are the sums over all shards (allreduce_grads, in
+    `chunks` pipelined row blocks)."""
 
-    def __init__(self, debug=False, group=None):
+    def __init__(self, debug=False, group=None, chunks=4):
         self.debug = debug
         self.group = group
+        self.chunks = max(1, int(chunks))
 
     def preprocess(self, means, values, covariances, conics, samples):
         grid, offset = global_tile_grid(samples, self.group)
@@ -102,7 +122,7 @@ class ShardedGaussianSampler:
         self.means, self.values, self.conics, self.samples = means, values, conics, samples
 
     def _sample(self, function):
-        return _ShardedSample.apply(function, self.group, self.means, self.values, self.conics,
+        return _ShardedSample.apply(function, (self.group, self.chunks), self.means, self.values, self.conics,
                                     self.samples, self.num_rendered, self.binning_buffer,
                                     self.sample_binning_buffer, self.ranges, self.sample_ranges,
                                     self.debug)

@@ -375,6 +375,24 @@ int dgs_agg_backward_tr(int P, int D, int L, int K, int E, const float *features
                         float *dL_dkeys, float *dL_dfrequencies, float *dL_ddistance_transform,
                         void *workspace, size_t workspace_bytes, dgs_stream_t stream, int debug);
 
+/* ---- the dense sharded path's collective (the reference is single-GPU) ---- */
+
+/* RCCL communicators for callers without torch.distributed.  RCCL (librccl.so.1) is loaded on
+ * first use.  dgs_comm_unique_id writes dgs_comm_id_bytes() bytes (ncclUniqueId) on one rank,
+ * which the caller distributes; every rank then calls dgs_comm_init (ncclCommInitRank). */
+size_t dgs_comm_id_bytes(void);
+int dgs_comm_unique_id(void *id_out);
+int dgs_comm_init(void **comm_out, int nranks, const void *id, int rank);
+int dgs_comm_destroy(void *comm);
+
+/* Sums the packed per-Gaussian gradients [dmeans | dvalues | dconics] (device float[count], in
+ * place) over the communicator's ranks: the one all-reduce of query-point sharding (each rank's
+ * backward is a partial sum over its points).  chunk_elems > 0 issues it as back-to-back chunks
+ * (RCCL pipelines them; a caller can start optimizer work on the first chunks early).  comm: a
+ * communicator of dgs_comm_init (an ncclComm_t of the same RCCL library).  Asynchronous on
+ * `stream`. */
+int dgs_allreduce_grads(float *grads, size_t count, void *comm, size_t chunk_elems, dgs_stream_t stream);
+
 /* Benchmark support: bracket every forward (which = 0) / backward (which = 1) render-kernel
  * launch with HIP events on its stream.  dgs_timing_read waits for the recorded events, adds
  * their durations into *total_ms, clears the record and returns the launch count. */

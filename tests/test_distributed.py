@@ -94,6 +94,37 @@ def test_allreduce_grads_single_process_passthrough():
     assert allreduce_grads(g) is g
 
 
+def _chunk_worker(rank, world, port, outdir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from diff_gaussian_sampling.distributed import allreduce_grads
+        g = torch.Generator().manual_seed(400 + rank)
+        P = 1001  # (not a multiple of the block counts)
+        grads = (torch.randn(P, 2, generator=g), torch.randn(P, 3, generator=g), torch.randn(P, 3, generator=g))
+        res = {}
+        for chunks in (1, 2, 4, 7):
+            out = allreduce_grads(tuple(t.clone() for t in grads), chunks=chunks)
+            res[f"c{chunks}"] = np.concatenate([o.reshape(P, -1).numpy() for o in out], 1)
+        np.savez(os.path.join(outdir, f"chunk{rank}.npz"), **res,
+                 mine=np.concatenate([t.numpy() for t in grads], 1))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chunked_allreduce_equals_unchunked(tmp_path):
+    """allreduce_grads in 2, 4, 7 pipelined row blocks equals the one-collective sum bit for bit
+    at world 2 (and is the sum of both ranks' partial gradients)."""
+    port = _free_port()
+    mp.start_processes(_chunk_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="fork")
+    r = [np.load(tmp_path / f"chunk{k}.npz") for k in range(2)]
+    want = r[0]["mine"] + r[1]["mine"]
+    for k in range(2):
+        for c in ("c2", "c4", "c7"):
+            assert np.array_equal(r[k][c], r[k]["c1"]), (k, c)
+        assert np.array_equal(r[k]["c1"], want)
+
+
 def _spatial_problem():
     """Gaussians small against the strips (h = 2 / sqrt(P) = 0.01, cut half-widths ~0.2), so
     most of them reach one rank only; the uniform points wrap across y = +-1 (rank 0 <-> W-1)."""

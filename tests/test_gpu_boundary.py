@@ -157,3 +157,31 @@ def test_data_write_missed_without_verify_caught_with_debug(dgs, oracle):
     ref_new = ob.forward("gaussian", values.numpy(), conics.numpy(), means=(means + 0.002).numpy()).reshape(stale.shape)
     close(stale.cpu().numpy(), ref_old, 1e-5, 1e-6, "the .data write is missed (binned copies)")
     close(fresh.cpu().numpy(), ref_new, 1e-5, 1e-6, "debug=True catches it (call-time path)")
+
+
+def test_allreduce_grads_one_rank_communicator():
+    """dgs_allreduce_grads through ctypes on a 1-rank RCCL communicator made by
+    dgs_comm_init: the sum over one rank is the input, whole and in chunks; the call is
+    asynchronous on the stream.  (More ranks need more GPUs: the driver's multi-GPU bench runs
+    the torch.distributed path.)"""
+    lib = _lib()
+    lib.dgs_comm_id_bytes.restype = _SZ
+    lib.dgs_comm_unique_id.argtypes = [_P]
+    lib.dgs_comm_init.argtypes = [ctypes.POINTER(_P), _I, _P, _I]
+    lib.dgs_comm_destroy.argtypes = [_P]
+    lib.dgs_allreduce_grads.argtypes = [_P, _SZ, _P, _SZ, _P]
+    uid = ctypes.create_string_buffer(int(lib.dgs_comm_id_bytes()))
+    _ok(lib, lib.dgs_comm_unique_id(uid))
+    comm = _P()
+    torch.cuda.set_device(0)
+    _ok(lib, lib.dgs_comm_init(ctypes.byref(comm), 1, uid, 0))
+    try:
+        g = torch.randn(1_000_003, device="cuda", generator=torch.Generator(device="cuda").manual_seed(3))
+        ref = g.clone()
+        stream = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+        for chunk in (0, 65536):
+            _ok(lib, lib.dgs_allreduce_grads(g.data_ptr(), g.numel(), comm, chunk, stream))
+            torch.cuda.synchronize()
+            assert torch.equal(g, ref)
+    finally:
+        _ok(lib, lib.dgs_comm_destroy(comm))
