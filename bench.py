@@ -125,6 +125,10 @@ def main():
     ap.add_argument("--N", type=int, default=None,
                     help="query points per GPU (default: 2M on one GPU, 1M per GPU for N > 1)")
     ap.add_argument("--weak", action="store_true", help="N > 1: 2M query points per GPU")
+    ap.add_argument("--ar-chunks", type=int, default=4,
+                    help="--shard dense: row blocks of the pipelined gradient all-reduce")
+    ap.add_argument("--push-sync", action="store_true",
+                    help="--shard spatial: the exact push (one host sync per step) instead of the sync-free one")
     ap.add_argument("--shard", default="spatial", choices=["spatial", "dense"],
                     help="N > 1: spatial = rank r owns the strip r of the points along y and the "
                          "gradient sum moves only the Gaussians that reach another strip "
@@ -189,7 +193,7 @@ def main():
 def bench_sample(args, world, rank, dev, torch, dist):
     import diff_gaussian_sampling as dgs
     from diff_gaussian_sampling import synthetic as syn
-    from diff_gaussian_sampling.distributed import (SupportExchange, grid_and_box, pack_grads,
+    from diff_gaussian_sampling.distributed import (SupportExchange, allreduce_grads, grid_and_box, pack_grads,
                                                     shard_extents)
 
     P, C, D = args.P, args.C, 2
@@ -303,9 +307,9 @@ def bench_sample(args, world, rank, dev, torch, dist):
                 e0.record()
             if spatial:  # partial rows to their owners (owner-side optimizer, SupportExchange)
                 xchg.reduce(pack_grads((means.grad, values.grad, conics.grad)))
-            else:
-                torch.cat([means.grad.reshape(-1), values.grad.reshape(-1), conics.grad.reshape(-1)], out=flat)
-                dist.all_reduce(flat)
+            else:  # the packed gradients in pipelined row blocks (distributed.allreduce_grads)
+                g = allreduce_grads((means.grad, values.grad, conics.grad), chunks=args.ar_chunks)
+                means.grad, values.grad, conics.grad = g
             if timed:
                 e1.record()
                 ar_ev.append((e0, e1))
@@ -313,7 +317,7 @@ def bench_sample(args, world, rank, dev, torch, dist):
                 if timed:
                     p0, p1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                     p0.record()
-                xchg.push([means, values, conics], means, conics)
+                xchg.push([means, values, conics], means, conics, sync=args.push_sync)
                 if timed:
                     p1.record()
                     push_ev.append((p0, p1))

@@ -230,6 +230,7 @@ class SupportExchange:
         mask, owner = exchange_sets(means, conics, self.extents)
         self.owner = owner
         self.owned = owner == rank
+        self.owned_idx = torch.nonzero(self.owned).flatten()  # (owners never change)
         touch_me = _bits(mask, rank)
         self.held = touch_me | self.owned
         # rows sent in the reduce, grouped by owner (ascending id within a group)
@@ -237,9 +238,22 @@ class SupportExchange:
         so = owner[snd]
         snd = snd[torch.argsort(so, stable=True)]
         send_n = torch.bincount(so, minlength=W)
-        recv, recv_n = self._by_rank(mask, torch.nonzero(self.owned).flatten())
+        recv, recv_n = self._by_rank(mask, self.owned_idx)
         n = torch.stack([send_n, recv_n]).cpu()
         self._set_lists(list(torch.split(snd, [int(v) for v in n[0]])), list(torch.split(recv, [int(v) for v in n[1]])))
+        # the sync-free push (push(..., sync=False)): per (owner -> rank) pair a row capacity,
+        # the same on both sides (both know the pair's count of the last exact exchange)
+        self._set_caps([int(v) for v in n[1]], [int(v) for v in n[0]])
+        self.overflow = None  # device flag of the last sync-free push (checked at the next preprocess)
+        self._last_push = None
+        # the padded push writes its padding slots to an owned row of the receiver: usable only
+        # when every rank owns one (decided once, the same on every rank)
+        self._padded_ok = self.owned_idx.numel() > 0
+        if W > 1:
+            ok = torch.tensor([int(self._padded_ok)],
+                              device=torch.device("cpu") if dist.get_backend(group) == "gloo" else dev)
+            dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)
+            self._padded_ok = bool(int(ok.item()))
 
     def _by_rank(self, mask, rows):
         """`rows` grouped by every other rank whose bit is set in mask[rows] (a row appears once per
@@ -256,6 +270,18 @@ class SupportExchange:
         self.send_idx, self.recv_idx = send, recv
         self.send_cat = torch.cat(send)
         self.recv_cat = torch.cat(recv)
+        self.padded = None  # exact lists (set by the sync-free push: padded ones)
+
+    @staticmethod
+    def cap_of(n):
+        """Row capacity of an (owner -> rank) pair whose last exact exchange moved n rows."""
+        return n + n // 4 + 16 if n else 0
+
+    def _set_caps(self, push_send, push_recv):
+        """push_send[r]: rows this rank (owner) sent to r in the last exact push; push_recv[q]: rows
+        it received from owner q.  Pairs with no rows stay at capacity 0 until an exact push."""
+        self.cap_send = [self.cap_of(v) if r != self.rank else 0 for r, v in enumerate(push_send)]
+        self.cap_recv = [self.cap_of(v) if q != self.rank else 0 for q, v in enumerate(push_recv)]
 
     def _counts_a2a(self, counts):
         """all-to-all of one int per rank pair (host lists in, host list out)."""
@@ -266,8 +292,9 @@ class SupportExchange:
         return [int(v) for v in got.cpu()]
 
     def rows_moved(self):
-        """Gaussian rows this rank sends in one reduce."""
-        return sum(self.send_splits)
+        """Gaussian rows this rank sends in one reduce (the padded blocks' capacities after a
+        sync-free push)."""
+        return sum(self.cap_recv) if self.padded is not None else sum(self.send_splits)
 
     def _a2a(self, out, inp, out_splits, in_splits):
         if inp.is_cuda and dist.get_backend(self.group) == "gloo":  # gloo: host staging
@@ -293,6 +320,8 @@ class SupportExchange:
         rank owns hold the sum over all ranks and every other row is 0."""
         if self.world == 1:
             return G
+        if self.padded is not None:
+            return self._reduce_padded(G)
         if self.debug:
             self._check_splits()
         F = G.shape[1]
@@ -308,18 +337,108 @@ class SupportExchange:
             o += n
         return G
 
+    def _reduce_padded(self, G):
+        """reduce() on the sync-free push's padded lists: every pair's block has its capacity of
+        rows (host-known splits); a block's valid rows are counted on the device, the others are
+        sent for the padding id (an owned row of the receiver) and added as exact zeros."""
+        pd = self.padded
+        F = G.shape[1]
+        send = G.index_select(0, pd["red_send_ids"]).contiguous()
+        recv = torch.empty((sum(self.cap_send), F), dtype=G.dtype, device=G.device)
+        self._a2a(recv, send, self.cap_send, self.cap_recv)
+        G.masked_fill_(~self.owned[:, None], 0.0)
+        o = 0
+        for r in range(self.world):  # added in rank order: deterministic
+            n = self.cap_send[r]
+            if n:
+                valid = (torch.arange(n, device=G.device) < pd["send_cnt"][r]).to(G.dtype)
+                G.index_add_(0, pd["push_send_ids"][o:o + n], recv[o:o + n] * valid[:, None])
+            o += n
+        return G
+
     @torch.no_grad()
-    def push(self, tensors, means, conics):
+    def push(self, tensors, means, conics, sync=True):
         """After the optimizer step on the owned rows: send every owner's rows of `tensors` (each
         [P, ...], float32; updated in place on the receivers) to the ranks its updated cut
         reaches, computed from `means` / `conics` (the updated ones; only the owned rows are
-        read).  Updates `held` and the next reduce's row lists.  Returns the rows sent."""
-        W, me = self.world, self.rank
-        dev = self.owner.device
+        read).  Updates `held` and the next reduce's row lists.  Returns the rows sent (a device
+        count with sync=False).
+
+        sync=False: no host synchronisation.  Every (owner -> rank) pair moves a block of its
+        capacity (the last exact push's count + 25 % + 16, the same on both sides) with the valid
+        rows counted on the device; a pair with more rows than its capacity sets the device flag
+        `overflow`, which the next SpatialShardedGaussianSampler.preprocess reads in its one host
+        transfer and answers with an exact push (all ranks together) before binning."""
+        W = self.world
         if W == 1:
             return 0
-        mask, _ = exchange_sets(means, conics, self.extents)
-        ids, send_n = self._by_rank(mask, torch.nonzero(self.owned).flatten())
+        self._last_push = (tensors, means, conics)
+        if not sync and self._padded_ok:
+            return self._push_padded(tensors, means, conics)
+        return self._push_exact(tensors, means, conics)
+
+    @torch.no_grad()
+    def _push_padded(self, tensors, means, conics):
+        W, me = self.world, self.rank
+        dev = self.owner.device
+        oi = self.owned_idx
+        dummy = oi[:1]  # an owned row: no rank ever sends it to its owner
+        mask, _ = exchange_sets(means.index_select(0, oi), conics.index_select(0, oi), self.extents)
+        bits = ((mask[None, :] >> torch.arange(W, device=dev)[:, None]) & 1).bool()  # [W, n_owned]
+        bits[me] = False
+        cnt = bits.sum(1)  # rows per destination (device)
+        pos = torch.cumsum(bits.to(torch.int64), 1) - 1
+        caps = torch.tensor(self.cap_send, dtype=torch.int64, device=dev)
+        base = torch.cumsum(caps, 0) - caps
+        tot = int(sum(self.cap_send))
+        keep = bits & (pos < caps[:, None])
+        slot = torch.where(keep, base[:, None] + pos, torch.full_like(pos, tot))
+        buf = dummy.expand(tot + 1).clone()
+        buf.scatter_(0, slot.reshape(-1), oi.expand(W, -1).reshape(-1))
+        send_ids = buf[:tot]
+        overflow = (cnt > caps).any()
+        recv_cnt = torch.empty_like(cnt)
+        self._a2a(recv_cnt, cnt, [1] * W, [1] * W)
+        cols = [t.reshape(t.shape[0], -1) for t in tensors]
+        F = sum(c.shape[1] for c in cols)
+        rows = torch.cat([c.index_select(0, send_ids) for c in cols], 1).float().contiguous()
+        rtot = int(sum(self.cap_recv))
+        got_ids = torch.empty(rtot, dtype=torch.long, device=dev)
+        got_rows = torch.empty((rtot, F), dtype=torch.float32, device=dev)
+        self._a2a(got_ids, send_ids, self.cap_recv, self.cap_send)
+        self._a2a(got_rows, rows, self.cap_recv, self.cap_send)
+        slot_in = torch.cat([torch.arange(n, device=dev) for n in self.cap_recv]) if rtot else \
+            torch.zeros(0, dtype=torch.long, device=dev)
+        owner_of = torch.repeat_interleave(torch.arange(W, device=dev),
+                                           torch.tensor(self.cap_recv, device=dev)) if rtot else slot_in
+        valid = slot_in < recv_cnt[owner_of]
+        ids = torch.where(valid, got_ids, dummy.expand(rtot))
+        o = 0
+        for t, c in zip(tensors, cols):
+            k = c.shape[1]
+            new = torch.where(valid[:, None], got_rows[:, o:o + k].to(c.dtype), c.index_select(0, ids))
+            c.index_copy_(0, ids, new)  # (the padding slots write the dummy row's own value back)
+            if c.data_ptr() != t.data_ptr():
+                t.copy_(c.reshape(t.shape))
+            o += k
+        held = self.owned.clone()
+        held.index_fill_(0, ids, True)
+        self.held = held
+        # the next reduce: send back what was received (per owner block), receive into the blocks
+        # this rank pushed, valid counts as pushed
+        self.padded = {"red_send_ids": ids, "push_send_ids": send_ids, "send_cnt": cnt}
+        self.overflow = overflow
+        return cnt.sum()
+
+    @torch.no_grad()
+    def _push_exact(self, tensors, means, conics):
+        W, me = self.world, self.rank
+        dev = self.owner.device
+        oi = self.owned_idx
+        m_o, _ = exchange_sets(means.index_select(0, oi), conics.index_select(0, oi), self.extents)
+        mask = torch.zeros(self.owner.numel(), dtype=m_o.dtype, device=dev)
+        mask[oi] = m_o
+        ids, send_n = self._by_rank(mask, oi)
         if dist.get_backend(self.group) == "gloo":
             out_splits = [int(v) for v in send_n.cpu()]
             in_splits = self._counts_a2a(out_splits)
@@ -348,6 +467,8 @@ class SupportExchange:
         self.held = held
         send = list(torch.split(got_ids, in_splits))  # ascending per owner (the owner sent them so)
         self._set_lists(send, out_ids)
+        self._set_caps(out_splits, in_splits)
+        self.overflow = None
         return int(ids.numel())
 
 
@@ -365,31 +486,37 @@ def shard_extents(samples, group=None):
     return torch.stack(out)
 
 
-def grid_and_box(samples, group=None, strip=None):
+def grid_and_box(samples, group=None, strip=None, flag=None):
     """(grid, offset) of the union of every rank's samples (global_tile_grid) and this rank's
     own bounding box (lo[D], hi[D]), read back in ONE host transfer.  strip = (lo, hi) of this
     rank along the sharding axis: also returns whether ANY rank's samples leave its strip (folded
-    into the MAX all-reduce, so every rank learns it together), else None."""
+    into the MAX all-reduce, so every rank learns it together), else None.  flag (a device
+    bool, e.g. the sync-free push's overflow): also returns whether it is set on ANY rank."""
     D = samples.shape[1]
     mn = samples.min(0).values
     mx = samples.max(0).values
     gmn, gmx = mn.clone(), mx.clone()
+    extra = []
     if strip is not None:
-        out = ((mn[D - 1] < strip[0]) | (mx[D - 1] > strip[1])).float().reshape(1)
-        gmx = torch.cat([gmx, out])
+        extra.append(((mn[D - 1] < strip[0]) | (mx[D - 1] > strip[1])).float().reshape(1))
+    if flag is not None:
+        extra.append(torch.as_tensor(flag, device=mx.device).float().reshape(1))
+    gmx = torch.cat([gmx] + extra)
     if _world(group) > 1:
         dist.all_reduce(gmn, op=dist.ReduceOp.MIN, group=group)
         dist.all_reduce(gmx, op=dist.ReduceOp.MAX, group=group)
     grid = torch.ceil((gmx[:D] - gmn + 1e-6) / 0.51).to(torch.float32)
     rows = [grid, gmn, mn, mx]
-    if strip is not None:  # the strip flag rides along in the same transfer
-        rows.append(torch.cat([gmx[D:D + 1], torch.zeros(D - 1, dtype=gmx.dtype, device=gmx.device)]))
+    for k in range(len(extra)):  # the flags ride along in the same transfer
+        rows.append(torch.cat([gmx[D + k:D + k + 1], torch.zeros(D - 1, dtype=gmx.dtype, device=gmx.device)]))
     h = torch.stack(rows).cpu()
     res = ([int(g) for g in h[0]], [float(o) for o in h[1]], [float(v) for v in h[2]],
            [float(v) for v in h[3]])
-    if strip is None:
-        return res
-    return res + (bool(h[4][0] > 0),)
+    if strip is not None:
+        res = res + (bool(h[4][0] > 0),)
+    if flag is not None:
+        res = res + (bool(h[-1][0] > 0),)
+    return res
 
 
 def pack_grads(grads):
@@ -461,8 +588,11 @@ class SpatialShardedGaussianSampler(ShardedGaussianSampler):
             e = torch.as_tensor(known).detach().double().cpu()[rank]
             strip = (float(e[0]), float(e[1])) if samples.shape[0] else (-math.inf, math.inf)
         # (an empty rank never leaves its strip)
-        grid, offset, lo, hi, *left = grid_and_box(samples, self.group, strip) if strip is not None else \
-            grid_and_box(samples, self.group)
+        ovf = self.xchg.overflow if self.xchg is not None else None
+        grid, offset, lo, hi, *flags = grid_and_box(samples, self.group, strip, ovf)
+        left = flags[:1] if strip is not None else []
+        if ovf is not None and flags[-1]:  # some pair outgrew its capacity: every rank re-pushes exactly
+            self.xchg._push_exact(*self.xchg._last_push)
         if left and left[0]:  # raised on every rank together (no rank left waiting in a collective)
             raise ValueError(f"rank {rank}: the samples of some rank leave its strip along the sharding axis "
                              f"(this rank: [{lo[D - 1]}, {hi[D - 1]}] in [{strip[0]}, {strip[1]}]); pass "

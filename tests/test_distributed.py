@@ -205,13 +205,15 @@ def _cov_of(conics):
 ADAM_STEPS, ADAM_LR = 3, 1e-3
 
 
-def _adam_worker(rank, world, port, outdir):
+def _adam_worker(rank, world, port, outdir, mode="sync"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         import diff_gaussian_sampling.distributed as dd
         from oracle_stub import OracleC
         dd._C = OracleC()
+        if mode == "overflow":  # capacities far below the counts: every padded push overflows
+            dd.SupportExchange.cap_of = staticmethod(lambda n: max(n // 8, 1) if n else 0)
         means, values, covs, conics, samples, w = _spatial_problem()
         order = torch.argsort(samples[:, 1])
         shard = torch.tensor_split(order, world)[rank].sort().values
@@ -224,7 +226,9 @@ def _adam_worker(rank, world, port, outdir):
             opt.zero_grad()
             (sampler.sample_gaussians_derivative() * w[shard]).sum().backward()
             opt.step()
-            moved.append(sampler.push([m, v, c]))
+            moved.append(int(sampler.xchg.push([m, v, c], m, c, sync=mode == "sync")))
+        # (the next step's preprocess -- where a padded push's overflow is answered by an exact one)
+        sampler.preprocess(m, v, _cov_of(c), c, samples[shard])
         np.savez(os.path.join(outdir, f"adam{rank}.npz"), m=m.detach().numpy(), v=v.detach().numpy(),
                  c=c.detach().numpy(), owned=sampler.xchg.owned.numpy(), held=sampler.xchg.held.numpy(),
                  moved=np.asarray(moved))
@@ -232,15 +236,19 @@ def _adam_worker(rank, world, port, outdir):
         dist.destroy_process_group()
 
 
-def test_spatial_shards_adam_matches_single_process(tmp_path, oracle):
+@pytest.mark.parametrize("mode", ["sync", "padded", "overflow"])
+def test_spatial_shards_adam_matches_single_process(tmp_path, oracle, mode):
     """Three Adam steps of a 2-rank spatially sharded run (owner-side reduce, optimizer over the
     full tensors, push of the owners' rows) against the same loop in one process over all the
     points: every rank's held rows -- the owned and the pushed ones, i.e. every row its strip
-    reads -- equal the single-process parameters."""
+    reads -- equal the single-process parameters.  mode: the exact push (host-known counts), the
+    sync-free padded push (capacities from the last exact exchange, device-side counts), and the
+    padded push with capacities too small (its overflow is answered by an exact push at the next
+    preprocess)."""
     import diff_gaussian_sampling.distributed as dd
     from oracle_stub import OracleC
     world = 2
-    mp.spawn(_adam_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_adam_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True)
     means, values, covs, conics, samples, w = _spatial_problem()
     saved = dd._C
     dd._C = OracleC()
