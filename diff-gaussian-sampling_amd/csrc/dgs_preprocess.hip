@@ -490,11 +490,22 @@ __device__ __forceinline__ bool visit_local(const Geom &G, const Cut &k, const i
 // grid and its cut within kGatherReach fine cells of the mean's (home) cell.  Their local
 // entries are produced per cell by k_gather (no sort); everything else goes through the
 // per-Gaussian enumeration and the entry sort.  Returns the reach in cells, 0 if not regular.
-constexpr int kGatherReach = 6, kGatherRows = 2 * kGatherReach + 1;
+// Thin conics (rho^2 >= 0.82) are regular too unless DGS_THIN_LITERAL (their kThin flag needs the
+// sort): local_rows' fp32 slice margins hold for them -- the slice centre's rounding is relative
+// to |x|, and the sqrt argument's cancellation costs at most sqrt(eps) e0 sqrt(1 - rho^2) <= tol
+// (rho^2 < kRho2Max keeps det well away from 0).
+#ifndef DGS_THIN_GATHER
+#define DGS_THIN_GATHER 1
+#endif
+#ifndef DGS_GATHER_REACH
+#define DGS_GATHER_REACH 6
+#endif
+constexpr int kGatherReach = DGS_GATHER_REACH, kGatherRows = 2 * kGatherReach + 1;
+static_assert(kGatherRows <= 32, "local_rows keeps one bit per row");
 __device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k,
                                             const KeyRect &kr) {
     if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2]) ||
-        conic_thin(2, con[0], con[1], con[2]))
+        ((DGS_THIN_LITERAL || !DGS_THIN_GATHER) && conic_thin(2, con[0], con[1], con[2])))
         return 0;
     if (!(k.e[0] + 3.0 * G.fs < 0.9 && k.e[1] + 3.0 * G.fs < 0.9)) return 0;
     // every tile visited at most once (a rect wider than the grid visits a tile repeatedly,
@@ -509,6 +520,10 @@ __device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float
     }
     return reach <= kGatherReach ? reach : 0;
 }
+
+// Unculled Gaussians take k_wide (one wave per Gaussian) instead of enumerate_fine.
+__device__ __forceinline__ bool wide_gauss(const Cut &k) { return !k.cull; }
+constexpr unsigned kWideBlocks = 128;  // (grid-strided over the device-side queue length)
 
 // Enumerate the fine entries (cell, id|flag) of one Gaussian, in the reference's tile-key
 // order (sampler_impl.cu:94-124), restricted to non-empty cells that pass the exact cull.
@@ -569,9 +584,9 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
                     }
                     for (int fx = fxl; fx <= fxh; ++fx) {
                         const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
-                        // (empty cells get no units, so an entry there is never read: only
-                        // the box-classified cells need the two loads of this test)
-                        if (!local && send[cell] <= sbeg[cell]) continue;
+                        // Empty cells get no units: an entry there would never be read, and its
+                        // backward slot (k_bwd_esum sums every slot of a Gaussian) never written.
+                        if (send[cell] <= sbeg[cell]) continue;
                         if (k.cull && D == 1) {
                             const double slack = kCellSlack * G.fs;
                             const double o = tc[0] * (double)kTile;
@@ -903,7 +918,8 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
                                                            const uint32_t *__restrict__ fbg, const int8_t *__restrict__ greach,
                                                            const uint32_t *__restrict__ irr, const uint32_t *__restrict__ nirr,
                                                            int qcap, uint64_t *__restrict__ counts,
-                                                           unsigned long long *__restrict__ nflag) {
+                                                           unsigned long long *__restrict__ nflag,
+                                                           uint32_t *__restrict__ wq, uint32_t *__restrict__ nwq) {
     const FbBits fbits = fb_load(fbg, G.T);
     uint32_t nu = 0, nt = 0;  // kUnsafe / kThin entries (k_fine_fill emits the same ones): read back at the sync
     // (the queue's parts, as one index range over their concatenation)
@@ -920,6 +936,10 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
         const float4 cc = igc[i];
         const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
         const Cut k = gauss_cut(G, m, c);
+        if (wide_gauss(k)) {  // (k_wide counts it)
+            wq[atomicAdd(nwq, 1u)] = i;
+            continue;
+        }
         uint64_t n = 0;
         const auto count = [&](uint32_t, uint32_t v) {
             ++n;
@@ -939,9 +959,119 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
     }
 }
 
+// (cell, class) sort key of an entry: flag-free, flagged, then the thin (kThin) ones last in a
+// cell -- the forward's main and thin passes then meet few mixed groups; key >> 1 = (cell, flagged)
+__device__ __forceinline__ uint32_t entry_key(uint32_t cell, uint32_t val) {
+    return (cell << 2) | ((val & kSlow) ? 2u : 0u) | ((val & kThin) ? 1u : 0u);
+}
+
+// Unculled Gaussians (not positive definite, past kRho2Max, or a cut half-width >= 0.5) enter
+// every non-empty fine cell of every tile of their rect: ~1500 entries each.  One thread per
+// Gaussian (enumerate_fine) made them a serial tail -- 107 such Gaussians of the axis-ratio-25
+// field held k_fine_count_irr and k_fine_fill at 1.7 and 2.4 ms.  Here one wave per Gaussian,
+// lanes over a tile's cells in index order, emits the same entries in the same order
+// (enumerate_fine with cull = false: every tile of the rect, cells 0 .. n^D - 1 that hold
+// samples, classified by their sample box, then the tile's fallback cell when it holds samples).
+// k_fine_count_irr queues them (wq); !FILL counts (counts[i], the kUnsafe / kThin totals), FILL
+// writes them from offs[i] on.
+
+template <bool FILL, typename KT>
+__global__ __launch_bounds__(kBlock) void k_wide(Geom G, const float2 *__restrict__ igm, const float4 *__restrict__ igc,
+                                                 const int32_t *__restrict__ sbeg, const int32_t *__restrict__ send,
+                                                 const float4 *__restrict__ box, const uint32_t *__restrict__ fbg,
+                                                 const uint32_t *__restrict__ wq, const uint32_t *__restrict__ nwq,
+                                                 uint64_t *__restrict__ counts, const uint64_t *__restrict__ offs,
+                                                 KT *__restrict__ ekeys, uint32_t *__restrict__ evals, uint64_t cap,
+                                                 unsigned long long *__restrict__ nflag, int32_t *__restrict__ counters) {
+    const FbBits fbits = fb_load(fbg, G.T);
+    const int D = G.D, lane = threadIdx.x & (kWave - 1);
+    const uint64_t below = (1ull << lane) - 1ull;
+    const int nc = D == 2 ? G.n * G.n : G.n;
+    const uint32_t nq = sload(nwq);
+    uint32_t nu = 0, nt = 0;
+    for (uint32_t q = blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6); q < nq; q += gridDim.x * kWavesPerBlock) {
+        const uint32_t i = __builtin_amdgcn_readfirstlane(wq[q]);
+        const float2 mm = igm[i];
+        const float4 cc = igc[i];
+        const float m[2] = {mm.x, mm.y}, con[3] = {cc.x, cc.y, cc.z};
+        const KeyRect kr = ref_key_rect(D, m, cc.w, G.grid, G.off);
+        const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
+                               : (DGS_THIN_LITERAL && conic_thin(D, con[0], con[1], con[2])) ? kThin : 0u;
+        uint64_t o = FILL ? offs[i] : 0;
+        for (int y = kr.y0; y < kr.y1; ++y)
+            for (int x = kr.x0; x < kr.x1; ++x) {
+                const uint32_t key = key_of(D, x, y, G.grid);
+                if (key >= (uint32_t)G.T) continue;
+                const uint32_t base = key * (uint32_t)G.CT;
+                for (int j0 = 0; j0 < nc; j0 += kWave) {
+                    const int j = j0 + lane;
+                    bool hit = false;
+                    uint32_t val = 0;
+                    if (j < nc) {
+                        const uint32_t cell = base + (uint32_t)j;
+                        if (send[cell] > sbeg[cell]) {  // (enumerate_fine's classification, !local)
+                            const float4 bx = box[cell];
+                            const double blo[2] = {bx.x, bx.y}, bhi[2] = {bx.z, bx.w};
+                            bool inside = true, constant = true;
+#pragma unroll
+                            for (int d = 0; d < 2; ++d) {
+                                if (d >= D) break;
+                                const double eps =
+                                    1e-6 * (1.0 + fabs((double)m[d]) + fmax(fabs(blo[d]), fabs(bhi[d])));
+                                const double wa = (double)m[d] - bhi[d] - eps, wb = (double)m[d] - blo[d] + eps;
+                                inside = inside && wa >= -1.0 && wb <= 1.0;
+                                constant = constant && wrap_shift(wa) == wrap_shift(wb);
+                            }
+                            hit = true;
+                            val = i | uflag | (inside ? 0u : (constant ? kGeneral : kGeneral | kUnsafe));
+                        }
+                    }
+                    const uint64_t hm = __ballot(hit);
+                    if (hit) {
+                        nu += (val & kUnsafe) ? 1u : 0u;
+                        nt += (val & kThin) ? 1u : 0u;
+                        if (FILL) {
+                            const uint64_t at = o + (uint64_t)__popcll(hm & below);
+                            if (at < cap) {
+                                ekeys[at] = (KT)entry_key(base + (uint32_t)j, val);
+                                evals[at] = val;
+                            }
+                        }
+                    }
+                    o += (uint64_t)__popcll(hm);
+                }
+                if (fbits.full(key)) {  // whole tile: general path
+                    const uint32_t cell = base + (uint32_t)(G.CT - 1), val = i | kUnsafe | kGeneral;
+                    if (lane == 0) {
+                        ++nu;
+                        if (FILL && o < cap) {
+                            ekeys[o] = (KT)entry_key(cell, val);
+                            evals[o] = val;
+                        }
+                    }
+                    ++o;
+                }
+            }
+        if (!FILL && lane == 0) counts[i] = o;
+    }
+    for (int off = kWave / 2; off > 0; off >>= 1) {
+        nu += __shfl_xor(nu, off);
+        nt += __shfl_xor(nt, off);
+    }
+    if (lane == 0) {
+        if (FILL) {
+            if (nu) atomicAdd(reinterpret_cast<uint32_t *>(&counters[kNumUnsafe]), nu);
+        } else {  // (k_fine_count_irr's totals, read back at the sync)
+            if (nu) atomicAdd(&nflag[shard_of_block() * kShard64], (unsigned long long)nu);
+            if (nt) atomicAdd(&nflag[shard_of_block() * kShard64 + 1], (unsigned long long)nt);
+        }
+    }
+}
+
 // The block's Gaussians own one contiguous output range (offs is an exclusive scan in i
 // order); it is staged in LDS and written out coalesced when it fits (per-lane runs of ~15
-// entries at 64 different addresses per store were most of this kernel's time).
+// entries at 64 different addresses per store were most of this kernel's time).  A block with
+// an unculled (k_wide) Gaussian writes directly: k_wide fills that Gaussian's part of the range.
 constexpr int kFillBlock = 128, kFillCap = 3072;
 
 // KT: the entry key type -- uint16_t when every (cell, flag) key fits 16 bits (the radix sort
@@ -959,20 +1089,24 @@ __global__ __launch_bounds__(kFillBlock) void k_fine_fill(
     const int64_t i = i0 + threadIdx.x;
     const int64_t ilast = min((int64_t)P, i0 + kFillBlock) - 1;
     const uint64_t base = offs[i0], end = offs[ilast] + cnts[ilast];
-    const bool stage = end - base <= (uint64_t)kFillCap;
-    uint32_t nunsafe = 0;
-    if (i < P && cnts[i] > 0) {
+    bool mine = i < P && cnts[i] > 0;
+    float m[2] = {0.0f, 0.0f}, c[3] = {0.0f, 0.0f, 0.0f}, r = 0.0f;
+    Cut k;
+    if (mine) {
         const float2 mm = igm[i];
         const float4 cc = igc[i];
-        const float r = cc.w;
-        const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
-        const Cut k = gauss_cut(G, m, c);
+        m[0] = mm.x, m[1] = mm.y, c[0] = cc.x, c[1] = cc.y, c[2] = cc.z, r = cc.w;
+        k = gauss_cut(G, m, c);
+    }
+    const bool wide = mine && wide_gauss(k);
+    const bool stage = __syncthreads_or(wide) == 0 && end - base <= (uint64_t)kFillCap;
+    mine = mine && !wide;
+    uint32_t nunsafe = 0;
+    if (mine) {
         const bool skip = greach[i] > 0;  // (k_fine_count's decision)
         uint64_t o = offs[i];
         const auto put = [&](uint32_t cell, uint32_t val) {
-            // (cell, class): flag-free, flagged, then the thin (kThin) ones last in a cell -- the
-            // forward's main and thin passes then meet few mixed groups; key >> 1 = (cell, flagged)
-            const uint32_t key = (cell << 2) | ((val & kSlow) ? 2u : 0u) | ((val & kThin) ? 1u : 0u);
+            const uint32_t key = entry_key(cell, val);
             if (stage) {
                 skey[o - base] = key;
                 sval[o - base] = val;
@@ -1836,6 +1970,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // k_fine_count's queue: kShards parts of qcap ids (a part takes the blocks b = s mod kShards)
     const int qcap = (int)((grid_for(P) + kShards - 1) / kShards) * kBlock;
     uint32_t *irr = ca.take<uint32_t>((size_t)kShards * qcap), *nirr = ca.take<uint32_t>(kShards * kShard32);
+    uint32_t *wq = ca.take<uint32_t>(P), *nwq = ca.take<uint32_t>(kShard32);  // k_wide's queue
     uint2 *irect = ca.take<uint2>(P);  // reference rects in internal order
     unsigned long long *eg = ca.take<unsigned long long>(kShards * kShard64);  // per copy [gathered, kUnsafe, kThin entries]
     int32_t *rmax = ca.take<int32_t>(kShards * kShard32);
@@ -1867,6 +2002,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         Carve::rebase(fbg, base);
         Carve::rebase(irr, base);
         Carve::rebase(nirr, base);
+        Carve::rebase(wq, base);
+        Carve::rebase(nwq, base);
         Carve::rebase(irect, base);
         Carve::rebase(hstart, base);
         Carve::rebase(gcnt, base);
@@ -1904,6 +2041,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         zl.add(rmax, 4 * kShards * kShard32);
         zl.add(fbg, sizeof(uint32_t) * ((size_t)(G.T + 31) / 32 + 2));
         zl.add(nirr, 4 * kShards * kShard32);
+        zl.add(nwq, 4 * kShard32);
         zl.add(rs_s, plan_s.zero_bytes);
         zl.add(rs_h, plan_h.zero_bytes);
         DGS_TRY_HIP(zl.launch(s));
@@ -1944,7 +2082,10 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                                                 qcap, eg + 1);
     DGS_LAUNCH_CHECK(s, debug);
     k_fine_count_irr<<<std::min(grid_for(P), 2048u), kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg,
-                                                                     greach, irr, nirr, qcap, fcount, eg + 1);
+                                                                     greach, irr, nirr, qcap, fcount, eg + 1, wq, nwq);
+    DGS_LAUNCH_CHECK(s, debug);
+    k_wide<false, uint32_t><<<kWideBlocks, kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg, wq, nwq,
+                                                           fcount, nullptr, nullptr, nullptr, 0, eg + 1, nullptr);
     DGS_LAUNCH_CHECK(s, debug);
     const unsigned gather_blocks = (unsigned)(((int64_t)home_h * ((home_w + kStripW - 1) / kStripW) * kGatherRows +
                                                kWavesPerBlock - 1) / kWavesPerBlock);
@@ -2136,13 +2277,21 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     const uint64_t escap = capmode ? (uint64_t)Es : ~0ull;
     if (Es > 0) {
         const unsigned fb = (unsigned)((P + kFillBlock - 1) / kFillBlock);
-        if (k16)
+        if (k16) {
             k_fine_fill<uint16_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
                                                             fcount, greach, fbg, irect,
                                                             reinterpret_cast<uint16_t *>(ekeys), evals, counters, escap);
-        else
+            k_wide<true, uint16_t><<<kWideBlocks, kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg, wq,
+                                                                  nwq, nullptr, foffs,
+                                                                  reinterpret_cast<uint16_t *>(ekeys), evals, escap,
+                                                                  nullptr, counters);
+        } else {
             k_fine_fill<uint32_t><<<fb, kFillBlock, 0, s>>>(P, G, igm, igc, cell_sbeg, cell_send, cell_box, foffs,
                                                             fcount, greach, fbg, irect, ekeys, evals, counters, escap);
+            k_wide<true, uint32_t><<<kWideBlocks, kBlock, 0, s>>>(G, igm, igc, cell_sbeg, cell_send, cell_box, fbg, wq,
+                                                                  nwq, nullptr, foffs, ekeys, evals, escap, nullptr,
+                                                                  counters);
+        }
         DGS_LAUNCH_CHECK(s, debug);
         // (values: the entries' positions q, for the backward's slots; k_copy_sorted gathers evals[q])
         DGS_TRY_HIP(k16 ? radix_sort<uint16_t>(B.plan_e, Es, B.rs_e, reinterpret_cast<const uint16_t *>(ekeys),

@@ -249,7 +249,7 @@ class SupportExchange:
         # the padded push writes its padding slots to an owned row of the receiver: usable only
         # when every rank owns one (decided once, the same on every rank)
         self._padded_ok = self.owned_idx.numel() > 0
-        if W > 1:
+        if W > 1 and dist.is_available() and dist.is_initialized():  # (no group: a set-only exchange)
             ok = torch.tensor([int(self._padded_ok)],
                               device=torch.device("cpu") if dist.get_backend(group) == "gloo" else dev)
             dist.all_reduce(ok, op=dist.ReduceOp.MIN, group=group)

@@ -84,3 +84,41 @@ def ref_ranges_bytes(orc_bins):
     pad = np.zeros(2, np.uint32)
     return (np.concatenate([r.reshape(-1), pad]).view(np.uint8),
             np.concatenate([s.reshape(-1), pad]).view(np.uint8))
+
+
+# Thin Gaussians' stated bound (tests/test_gpu_parity.py module docstring): the GPU within
+# THIN_SPREAD_FACTOR times the larger distance of the two FMA-contraction models of the reference
+# (oracle "fmad" / "fmad_alt", i.e. nvcc's default --fmad=true) from the unfused model, per
+# tensor, never tighter than the 8c bound.  The fast path's exponent (pre-scaled k, its own FMA
+# order) is one more operation order of the same cancellation-amplified sum: profiles/
+# r05_margins.json records it at 1-2.6x the models' spread on cases.thin_case.
+THIN_SPREAD_FACTOR = 3.0
+
+
+def model_spread(oracle, functions, means, values, covs, conics, samples, dLs, subset=None, rtol=1e-5, atol=1e-6):
+    """Margins (units of the 8c bound) of the contraction models' forward outputs (per function)
+    and exact-sum gradients (summed over `functions`) from the unfused model's, each recorded as
+    "[reference <model> vs no-contract]"; returns {output name: the larger of the two models}."""
+    refs = {}
+    for model in ("nocontract", "fmad", "fmad_alt"):
+        ob = oracle.OracleBins(np.asarray(means), np.asarray(covs), np.asarray(samples), model=model)
+        outs, grads = {}, None
+        for f, dL in zip(functions, dLs):
+            o = ob.forward(f, np.asarray(values), np.asarray(conics), subset=subset)
+            outs[f] = o if subset is None else o[subset]
+            g = ob.backward(f, np.asarray(values), np.asarray(conics), np.asarray(dL), subset=subset, exact=True)
+            grads = list(g) if grads is None else [a + b for a, b in zip(grads, g)]
+        refs[model] = (outs, grads)
+    worst = {}
+    for model in ("fmad", "fmad_alt"):
+        pairs = [(f"{f} forward", refs[model][0][f], refs["nocontract"][0][f]) for f in functions]
+        pairs += list(zip(("dmeans", "dvalues", "dconics"), refs[model][1], refs["nocontract"][1]))
+        for name, a, b in pairs:
+            mg = margin_of(a, b, rtol, atol)
+            record_margin(f"{name} [reference {model} vs no-contract]", mg, rtol, atol, int(np.size(b)))
+            worst[name] = max(worst.get(name, 0.0), mg)
+    return worst
+
+
+def spread_scale(worst, factor=THIN_SPREAD_FACTOR):
+    return {k: max(1.0, factor * v) for k, v in worst.items()}

@@ -13,7 +13,7 @@ import torch
 
 from diff_gaussian_sampling import synthetic as syn
 import cases
-from helpers import close
+from helpers import close, model_spread, spread_scale
 
 pytestmark = pytest.mark.gpu
 
@@ -34,19 +34,23 @@ def _run(dgs, functions, means, values, covs, conics, samples, dLs):
     return [o.cpu().numpy() for o in outs], [g.cpu().numpy() for g in grads]
 
 
-def _check(dgs, oracle, functions, means, values, covs, conics, samples, seed=7):
+def _check(dgs, oracle, functions, means, values, covs, conics, samples, seed=7, spread=False):
+    """spread: the thin Gaussians' stated bound (helpers.THIN_SPREAD_FACTOR, test_gpu_parity.py)."""
     N, D, C = samples.shape[0], samples.shape[1], values.shape[1]
     dLs = [syn.grad_out(N, syn.out_components(f, D), C, seed=seed + i) for i, f in enumerate(functions)]
     outs, grads = _run(dgs, functions, means, values, covs, conics, samples, dLs)
     ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
+    sc = spread_scale(model_spread(oracle, functions, means, values, covs, conics, samples, dLs)) if spread else {}
     ref_g = None
     for f, o, dL in zip(functions, outs, dLs):
         ref = ob.forward(f, values.numpy(), conics.numpy())
-        close(o.reshape(N, -1, C), ref, RTOL, ATOL_FWD, f"multi {functions} {f} forward")
+        k = sc.get(f"{f} forward", 1.0)
+        close(o.reshape(N, -1, C), ref, RTOL * k, ATOL_FWD * k, f"multi {functions} {f} forward")
         g = ob.backward(f, values.numpy(), conics.numpy(), dL.numpy(), exact=True)
         ref_g = list(g) if ref_g is None else [a + b for a, b in zip(ref_g, g)]
     for name, got, ref in zip(("means", "values", "conics"), grads, ref_g):
-        close(got, ref, RTOL, ATOL_BWD, f"multi {functions} dL/d{name}")
+        k = sc.get(f"d{name}", 1.0)
+        close(got, ref, RTOL * k, ATOL_BWD * k, f"multi {functions} dL/d{name}")
 
 
 @pytest.mark.parametrize("functions", MULTI, ids=lambda f: "+".join(x[:3] for x in f))
@@ -68,7 +72,7 @@ def test_multi_edge_and_seam(dgs, oracle, functions):
 def test_multi_thin_anisotropic(dgs, oracle, functions):
     """Thin rotated Gaussians (cases.thin_case): the fused moment-form backward and the fused
     forward next to the reference-literal path of the ill-conditioned conics."""
-    _check(dgs, oracle, functions, *cases.thin_case(P=3000, n=20000), seed=51)
+    _check(dgs, oracle, functions, *cases.thin_case(P=3000, n=20000), seed=51, spread=True)
 
 
 def test_multi_order_and_fallback(dgs, oracle):
