@@ -385,14 +385,16 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
 // "the reference's" there.  So thin conics take the fast paths like every other PD conic, under
 // the stated bound of tests/test_gpu_parity.py (within twice the reference's own compile spread);
 // DGS_THIN_LITERAL=1 restores round 4's kThin entries (the unfused reference's order, lit_prob).
-// Past rho^2 = kRho2Max (axis ratio ~63, amplification ~4000) a conic is treated as not
-// positive definite: up to there the fp32 exponent of a pair beyond the cut (X^T A X > 210) is
-// below -104.8 in any operation order (|error| <= ~3e-7 x 4000 x 210 = 0.25), so culling it
-// drops an exact +0; past it the rounding could leave a subnormal term.
+// Past rho^2 = kRho2Max (axis ratio ~89, amplification A = (1 + rho) / (1 - rho) ~8000) a conic
+// is treated as not positive definite: up to there the fp32 exponent of a pair beyond the cut
+// (X^T A X > 210, power < -105) is below -104.5 in any operation order (|error| <= ~3e-7 x A x 210
+// = 0.5; expf is +0 below -103.97), so culling it drops an exact +0; past it the rounding could
+// leave a subnormal term.  (0.999 -- A ~4000 -- left the axis-ratio-25 field's 107 thinnest
+// Gaussians, rho^2 up to 0.99925, unculled: ~1500 literal-path entries each, +0.19 ms per forward.)
 #ifndef DGS_THIN_LITERAL
 #define DGS_THIN_LITERAL 0
 #endif
-constexpr double kRho2Max = 0.999;
+constexpr double kRho2Max = 0.9995;
 // Not positive definite, too ill-conditioned (above), or not finite: kUnsafe, the per-pair
 // literal path with the exact wrap and the reference's `power > 0 -> skip` (forward.cu:228).
 __host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float c2f) {

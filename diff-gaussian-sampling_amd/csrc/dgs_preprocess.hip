@@ -440,44 +440,49 @@ __device__ __forceinline__ bool axis_setup(const Geom &G, const Cut &k, int d, i
 
 // The row's cells that meet the ellipse X^T A X <= q (D = 2, culled): project the ellipse's
 // slice over the row's X1 band onto X0 (a slice of a convex set is convex, so "box meets
-// ellipse" <=> the cell's X0 range meets that interval).  Same margins as box_hits_ellipse,
-// widened slightly: an extra candidate only evaluates exact zeros.  row_slice gives the
-// interval [xl, xu] for fine row fy of tile row tc1 (false: the band misses the cut), row_cols
-// narrows [fxl, fxh] of tile column tc0 to it.
-__device__ __forceinline__ bool row_slice(const Geom &G, const Cut &k, int tc1, int fy, int ks1, double &xl, double &xu,
-                                 double &tol) {
-    DGS_CUT_CONTRACT
-    const double BS = (double)kTile, slack = kCellSlack * G.fs;
-    const double o1 = tc1 * BS;
-    const double qc = kQCut * (1.0 + 1e-6) + 1e-12;
-    double ya = k.md[1] - (o1 + (fy + 1) * G.fs + slack) - k.epsx[1] - 2.0 * ks1;
-    double yb = k.md[1] - (o1 + fy * G.fs - slack) + k.epsx[1] - 2.0 * ks1;
-    ya = fmax(ya, -k.e[1]);
-    yb = fmin(yb, k.e[1]);
-    if (ya > yb) return false;
-    const double c0 = k.c0, c1 = k.c1, c2 = k.c2;
-    const double det = c0 * c2 - c1 * c1;
-    const double e0 = sqrt(qc * c2 / det);
-    const double yu = fmin(fmax(-c1 * e0 / c2, ya), yb);  // argmax of the upper root
-    const double yl = fmin(fmax(c1 * e0 / c2, ya), yb);   // argmin of the lower root
-    xu = (-c1 * yu + sqrt(fmax(qc * c0 - det * yu * yu, 0.0))) / c0;
-    xl = (-c1 * yl - sqrt(fmax(qc * c0 - det * yl * yl, 0.0))) / c0;
-    tol = 1e-7 * (1.0 + fabs(xu) + fabs(xl)) + 1e-9;
-    return true;
-}
-
-__device__ __forceinline__ void row_cols(const Geom &G, const Cut &k, int tc0, int ks0, double xl, double xu, double tol,
-                                int &fxl, int &fxh) {
-    DGS_CUT_CONTRACT
-    const double slack = kCellSlack * G.fs;
-    const double o0 = tc0 * (double)kTile;
-    const double A = k.md[0] - o0 - slack - k.epsx[0] - 2.0 * ks0;
-    const double B = k.md[0] - o0 + slack + k.epsx[0] - 2.0 * ks0;
-    const double fa = ceil((A - (xu + tol)) * G.ifs - 1.0 - 1e-9);
-    const double fb2 = floor((B - (xl - tol)) * G.ifs + 1e-9);
-    if (fa > (double)fxl) fxl = fa > (double)G.n ? G.n : (int)fa;
-    if (fb2 < (double)fxh) fxh = fb2 < -1.0 ? -1 : (int)fb2;
-}
+// ellipse" <=> the cell's X0 range meets that interval), in fp32 with local_rows' construction
+// and margins: the slice ends' fp32 error is at most ~sqrt(8 eps) e0 sqrt(1 - rho^2) where the
+// sqrt argument cancels (the ellipse's top and bottom), so tol = 2e-3 e0 + 1e-5 (|xl| + |xu|) in
+// displacement units, and 1e-4 of a cell on the cell index.  An extra candidate only evaluates
+// exact zeros.  (The fp64 form -- a division and two square roots per row, det and e0 per row --
+// was most of k_fine_count_irr's and k_fine_fill's issue slots in thin fields, whose sort path
+// holds three quarters of the entries.)  Per Gaussian init(); per row cols() narrows [fxl, fxh]
+// for the visit whose tile-relative mean (torus shift included) is (md0, md1).
+struct Slice32 {
+    float qcc0, c1, det, ic0, yu0, yl0, e1, eps0, eps1, tol0, fs, ifs, slack;
+    __device__ __forceinline__ void init(const Geom &G, const Cut &k) {
+        const float qc = (float)(kQCut * (1.0 + 1e-6));
+        const float c0f = (float)k.c0, c2f = (float)k.c2, e0 = (float)k.e[0];
+        c1 = (float)k.c1;
+        det = (float)(k.c0 * k.c2 - k.c1 * k.c1);
+        ic0 = 1.0f / c0f;
+        yu0 = -c1 * e0 / c2f;
+        yl0 = c1 * e0 / c2f;
+        qcc0 = qc * c0f;
+        e1 = (float)k.e[1];
+        eps0 = (float)k.epsx[0] + 1e-6f;
+        eps1 = (float)k.epsx[1] + 1e-6f;
+        tol0 = 2e-3f * e0 + 1e-5f;
+        fs = (float)G.fs;
+        ifs = (float)G.ifs;
+        slack = (float)(kCellSlack * G.fs);
+    }
+    __device__ __forceinline__ bool cols(int fy, float md0, float md1, int n, int &fxl, int &fxh) const {
+        const float ya = fmaxf(md1 - ((float)(fy + 1) * fs + slack) - eps1, -e1);
+        const float yb = fminf(md1 - ((float)fy * fs - slack) + eps1, e1);
+        if (!(ya <= yb)) return false;
+        const float yu = fminf(fmaxf(yu0, ya), yb), yl = fminf(fmaxf(yl0, ya), yb);
+        // (v_sqrt_f32, ~1 ulp: far inside tol)
+        const float xu = (-c1 * yu + __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yu * yu, 0.0f))) * ic0;
+        const float xl = (-c1 * yl - __builtin_amdgcn_sqrtf(fmaxf(qcc0 - det * yl * yl, 0.0f))) * ic0;
+        const float tol = tol0 + 1e-5f * (fabsf(xu) + fabsf(xl));
+        const float fa = ceilf((md0 - slack - eps0 - (xu + tol)) * ifs - 1.0f - 1e-4f);
+        const float fb = floorf((md0 + slack + eps0 - (xl - tol)) * ifs + 1e-4f);
+        fxl = max(fxl, (int)fminf(fmaxf(fa, -1.0f), (float)n));
+        fxh = min(fxh, (int)fmaxf(fminf(fb, (float)n), -1.0f));
+        return true;
+    }
+};
 
 // A tile visit is `local` when the cut reaches it unshifted (ks = 0) and stays well inside one
 // period, so every cell it meets holds |X| < 1 (no wrap, no sample-box test).
@@ -558,6 +563,8 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
     const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
                            : (DGS_THIN_LITERAL && conic_thin(D, con[0], con[1], con[2])) ? kThin : 0u;
+    Slice32 sl;
+    if (k.cull && D == 2) sl.init(G, k);
     for (int y = kr.y0; y < kr.y1; ++y)
         for (int x = kr.x0; x < kr.x1; ++x) {
             const uint32_t key = key_of(D, x, y, G.grid);
@@ -575,13 +582,13 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
             const bool direct = x >= 0 && x < G.grid[0] && (D == 1 || (y >= 0 && y < G.grid[1]));
             if (any && !(skip_local && local && direct)) {
                 const int ylo = D == 2 ? flo[1] : 0, yhi = D == 2 ? fhi[1] : 0;
+                // (the visit's tile-relative mean, torus shift included: |md| < 2, so the fp32
+                // rounding is far inside eps0 / eps1)
+                const float md0 = (float)(k.md[0] - tc[0] * (double)kTile - 2.0 * ks[0]);
+                const float md1 = (float)(k.md[1] - tc[1] * (double)kTile - 2.0 * ks[1]);
                 for (int fy = ylo; fy <= yhi; ++fy) {
                     int fxl = flo[0], fxh = fhi[0];
-                    if (k.cull && D == 2) {
-                        double xl, xu, tol;
-                        if (!row_slice(G, k, tc[1], fy, ks[1], xl, xu, tol)) continue;
-                        row_cols(G, k, tc[0], ks[0], xl, xu, tol, fxl, fxh);
-                    }
+                    if (k.cull && D == 2 && !sl.cols(fy, md0, md1, G.n, fxl, fxh)) continue;
                     for (int fx = fxl; fx <= fxh; ++fx) {
                         const uint32_t cell = base + (uint32_t)(fy * G.n + fx);
                         // Empty cells get no units: an entry there would never be read, and its
@@ -1072,7 +1079,10 @@ __global__ __launch_bounds__(kBlock) void k_wide(Geom G, const float2 *__restric
 // order); it is staged in LDS and written out coalesced when it fits (per-lane runs of ~15
 // entries at 64 different addresses per store were most of this kernel's time).  A block with
 // an unculled (k_wide) Gaussian writes directly: k_wide fills that Gaussian's part of the range.
-constexpr int kFillBlock = 128, kFillCap = 3072;
+#ifndef DGS_FILL_CAP
+#define DGS_FILL_CAP 3072
+#endif
+constexpr int kFillBlock = 128, kFillCap = DGS_FILL_CAP;
 
 // KT: the entry key type -- uint16_t when every (cell, flag) key fits 16 bits (the radix sort
 // then moves 6 instead of 8 bytes per entry and pass).

@@ -95,7 +95,7 @@ __device__ __forceinline__ void ref_displacement(const float *m, const float *s,
 // box [lo, hi]: false only when every displacement X = m - s of the box lies in (-1, 1) on each
 // axis (so the reference applies no torus wrap, forward.cu:149-157) and some axis is farther than
 // the cut's half-width e_d = sqrt(210 Sigma_dd) -- then X^T A X > 210 and the reference's fp32
-// power is below -104.8 (rho^2 < kRho2Max, dgs_internal.h), expf(power) == +0 and the pair adds
+// power is below -104.5 (rho^2 < kRho2Max, dgs_internal.h), expf(power) == +0 and the pair adds
 // exactly nothing (v * 0 * t), forward and backward.  Other conics: true.
 template <int D>
 __device__ __forceinline__ bool ref_may_touch(const float *m, const float *c, const float *lo, const float *hi) {

@@ -142,7 +142,7 @@ class ShardedGaussianSampler:
 
 # ------------------------------------------------------------------------ spatial shards (f3)
 Q_CUT = 210.0  # X^T A X above this gives expf(-q / 2) == +0 in fp32 (dgs_internal.h kQCut)
-RHO2_MAX = 0.999  # conics with c1^2 >= RHO2_MAX c0 c2 are not culled (dgs_internal.h kRho2Max)
+RHO2_MAX = 0.9995  # conics with c1^2 >= RHO2_MAX c0 c2 are not culled (dgs_internal.h kRho2Max)
 
 
 def support_halfwidth(means, conics):
