@@ -242,8 +242,9 @@ int dgs_sample_backward_multi(int mask, int P, int D, int N, int C, const float 
  *     it then enqueues kernels only -- no timing events -- and requires DGS_SAMPLE_INPUTS_BINNED (the
  *     call-time path's first use builds tile lists behind a host-side record; DGS_ERR_ARG
  *     without it).  A replay re-reads means, values, conics, samples and dL from the captured
- *     addresses; values and dL may change between replays, means / conics / samples may not
- *     (re-binning cannot be captured: it returns num_rendered to the host).
+ *     addresses; values and dL may change between replays.  means / conics / samples may change
+ *     only when the graph also holds their re-binning: a capturable dgs_preprocess_ex (capacity
+ *     options above) captured before the sample calls (tests/graph_child.py: rebin_step).
  */
 enum dgs_sample_flag { DGS_SAMPLE_INPUTS_BINNED = 1, DGS_SAMPLE_ROWS_VALID = 2, DGS_SAMPLE_GRAPH_CAPTURE = 4 };
 typedef struct dgs_sample_options {
