@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-gp}
 mkdir -p $O
-for sc in torch_recipe dgs_recipe torch_eager_then_capture dgs_eager_then_capture; do
+for sc in torch_recipe dgs_recipe torch_eager_then_capture dgs_eager_then_capture dgs_after_history; do
   timeout -k 10 120 python -u tools/graph_probe2.py $sc > $O/$sc.log 2>&1
   rc=$?
   echo "$sc rc=$rc: $(tail -1 $O/$sc.log)"

@@ -4,7 +4,7 @@ set -u
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/${1:-gp3}
 mkdir -p $O
-for sc in plain memset malloc_only malloc_free; do
+for sc in plain memset malloc_only malloc_free raise_inside sync_inside; do
   timeout -k 10 120 python -u tools/graph_probe3.py $sc > $O/$sc.log 2>&1
   rc=$?
   echo "$sc rc=$rc: $(grep "$sc:" $O/$sc.log | tail -1)"

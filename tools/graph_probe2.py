@@ -11,6 +11,10 @@ inside torch.cuda.graph.  One scenario per process:
                           loss.backward() into the existing .grad -- the round-4 failing pattern,
                           with torch ops only
   dgs_eager_then_capture  the same with the sampler
+  dgs_after_history       round 4's crash came after 15 other tests in the same process
+                          (gpurun_out/r04g/tests.log): eager binnings, forwards and backwards of
+                          other sizes, functions and C first (their host-side records and freed
+                          buffers), then dgs_recipe's capture
 
 Prints "<scenario>: ok" (plus the max gradient difference replay vs eager) on success.
 tools/gpu_graph_probe.sh runs them from the safest to the riskiest and stops at a crash.
@@ -55,7 +59,34 @@ def make_dgs():
     return params, loss
 
 
+def history():
+    import diff_gaussian_sampling as dgs
+    from diff_gaussian_sampling import synthetic as syn
+    dev = torch.device("cuda")
+    for k, (P, N, C, fn) in enumerate([(500, 2000, 1, "gaussian"), (3000, 9000, 3, "derivative"),
+                                       (800, 4000, 16, "laplacian"), (5000, 20000, 1, "third"),
+                                       (20000, 60000, 1, "gaussian")]):
+        means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, C, seed=20 + k))
+        samples = syn.samples(N, 2, seed=40 + k).to(dev)
+        for t in (means, values, conics):
+            t.requires_grad_(True)
+        sampler = dgs.GaussianSampler(False)
+        sampler.preprocess(means, values, covs, conics, samples)
+        f = {"gaussian": sampler.sample_gaussians, "derivative": sampler.sample_gaussians_derivative,
+             "laplacian": sampler.sample_gaussians_laplacian, "third": sampler.sample_gaussians_third_derivative}[fn]
+        for _ in range(3):
+            f().square().sum().backward()
+        with torch.no_grad():
+            means.add_(1e-3)  # an in-place step: the next call verifies and takes the call-time path
+        f().sum().backward()
+        del sampler, means, values, covs, conics, samples
+    torch.cuda.synchronize()
+
+
 def run(scenario):
+    if scenario == "dgs_after_history":
+        history()
+        scenario = "dgs_recipe"
     params, loss = (make_dgs if scenario.startswith("dgs") else make_torch)()
     eager_first = scenario.endswith("eager_then_capture")
     if eager_first:  # default stream: AccumulateGrad / .grad made here

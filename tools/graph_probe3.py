@@ -13,6 +13,10 @@ op plus raw HIP calls on the capturing stream through ctypes (the HIP library to
   malloc_free    + hipMallocAsync, hipMemsetAsync into it, hipFreeAsync, all inside the capture
                    (round 4's slot-sum pattern)
   malloc_only    + hipMallocAsync inside the capture, hipFreeAsync after it
+  raise_inside   a Python exception inside the capture (torch.cuda.graph's __exit__ still ends it)
+  sync_inside    + hipStreamSynchronize on the capturing stream (illegal under capture: the
+                   round-4 library synced there when its call-time tile lists were first built,
+                   and then returned an error, raised inside the capture), then the capture ends
 
 Prints "<scenario>: ok (rc of each HIP call)" when the capture ends and the graph replays.
 """
@@ -48,6 +52,20 @@ def run(scenario):
         y = x * 2.0  # warm-up of the op outside the capture
     torch.cuda.current_stream().wait_stream(s)
     torch.cuda.synchronize()
+    if scenario in ("raise_inside", "sync_inside"):
+        try:
+            with torch.cuda.graph(g):
+                st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+                y = x * 3.0
+                if scenario == "sync_inside":
+                    hip.hipStreamSynchronize.argtypes = [ctypes.c_void_p]
+                    rcs.append(hip.hipStreamSynchronize(st))
+                    print(f"{scenario}: hipStreamSynchronize rc {rcs[-1]}; raising inside the capture", flush=True)
+                raise RuntimeError("an error raised inside the capture")
+        except Exception as e:  # (what torch.cuda.graph's __exit__ made of it)
+            rcs.append(f"{type(e).__name__}: {e}"[:200])
+        print(f"{scenario}: ok, the capture ended without a crash (rc {rcs})", flush=True)
+        return
     with torch.cuda.graph(g):
         st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
         y = x * 2.0
