@@ -26,7 +26,15 @@ struct RefCall {
     int64_t R;       // num_rendered (sizes the backward's grid)
     hipStream_t s;
     int debug;
+    float4 *cbox;    // P float4 of the caller's workspace (its Gaussian-row region, idle on this
+                     // path) for the call-time cuts (ref_boxes); null: tested from means / conics
 };
+
+// The call-time cut of every Gaussian (caller order) into a.cbox: {m0, m1, e0, e1}, e = the cut's
+// half-widths (ref_may_touch's, rounded up to fp32; +inf: never culled).  Exits at once unless
+// *a.flag is set.  Run after the fine-cell kernels, which read that region when the flag is clear.
+template <int D>
+int ref_boxes(const RefCall &a);
 
 // Compares the call's means / conics / samples with the binning's copies; ORs 1 into *flag on
 // any difference (bitwise).  The flag must be zeroed earlier on the stream.

@@ -92,11 +92,15 @@ __device__ __forceinline__ void ref_displacement(const float *m, const float *s,
 }
 
 // Whether a Gaussian with the CALL-TIME mean m and conic c can add anything to a sample of the
-// box [lo, hi]: false only when every displacement X = m - s of the box lies in (-1, 1) on each
-// axis (so the reference applies no torus wrap, forward.cu:149-157) and some axis is farther than
-// the cut's half-width e_d = sqrt(210 Sigma_dd) -- then X^T A X > 210 and the reference's fp32
-// power is below -104.5 (rho^2 < kRho2Max, dgs_internal.h), expf(power) == +0 and the pair adds
-// exactly nothing (v * 0 * t), forward and backward.  Other conics: true.
+// box [lo, hi]: false only when, on some axis, the reference's wrap (forward.cu:149-157) is one
+// constant shift k over the box's displacements [m - hi, m - lo] (wrap_shift equal at both ends:
+// it is piecewise constant and monotone in |x| on each side of 0) and the wrapped interval
+// [m - hi - k, m - lo - k] lies beyond the cut's half-width e_d = sqrt(210 Sigma_dd) -- then
+// X^T A X > 210 and the reference's fp32 power is below -104.5 (rho^2 < kRho2Max,
+// dgs_internal.h), expf(power) == +0 and the pair adds exactly nothing (v * 0 * t), forward and
+// backward.  Other conics: true.  (Without the shifted test every Gaussian of a tile list that
+// reached it through the torus -- its rect's keys wrapped, sampler_impl.cu:94-124 -- was kept:
+// 90 % of the candidates of an edge tile.)
 template <int D>
 __device__ __forceinline__ bool ref_may_touch(const float *m, const float *c, const float *lo, const float *hi) {
     double e[2];
@@ -116,8 +120,63 @@ __device__ __forceinline__ bool ref_may_touch(const float *m, const float *c, co
 #pragma unroll
     for (int d = 0; d < D; ++d) {
         const double xa = (double)m[d] - (double)hi[d], xb = (double)m[d] - (double)lo[d];
-        if (!(xa > -1.0 && xb < 1.0)) return true;  // a wrap is possible (or NaN): keep
-        far |= fmax(fmax(xa, -xb), 0.0) > e[d];
+        if (!(xa == xa && xb == xb)) return true;  // NaN: keep
+        const double k = wrap_shift(xa);
+        if (k != wrap_shift(xb)) return true;  // a wrap breakpoint inside the box: keep
+        far |= fmax(fmax(xa - k, k - xb), 0.0) > e[d];
+    }
+    return !far;
+}
+
+// ref_may_touch's cut, once per Gaussian and call (dgs_reference.h: ref_boxes): the group test
+// then reads one float4 per entry instead of the mean and conic, and compares in fp32.
+template <int D>
+__global__ void k_ref_boxes(int P, const float *__restrict__ means, const float *__restrict__ conics,
+                            const uint32_t *__restrict__ flag, float4 *__restrict__ cbox) {
+    if (sload(flag) == 0u) return;
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= P) return;
+    constexpr int S = D * (D + 1) / 2;
+    double e[2] = {INFINITY, INFINITY};
+    const double c0 = conics[g * S];
+    if constexpr (D == 1) {
+        if (c0 > 0.0 && c0 < INFINITY) e[0] = sqrt(kQCut / c0) * (1.0 + 1e-4) + 1e-7;
+    } else {
+        const double c1 = conics[g * S + 1], c2 = conics[g * S + 2], det = c0 * c2 - c1 * c1;
+        if (c0 > 0.0 && c2 > 0.0 && det > 0.0 && det < INFINITY && c0 < INFINITY && c2 < INFINITY &&
+            c1 * c1 < kRho2Max * (c0 * c2)) {
+            e[0] = sqrt(kQCut * c2 / det) * (1.0 + 1e-4) + 1e-7;
+            e[1] = sqrt(kQCut * c0 / det) * (1.0 + 1e-4) + 1e-7;
+        }
+    }
+    // (rounded up: the fp32 test below is never tighter than ref_may_touch's fp64 one)
+    const float e0 = __double2float_ru(e[0]), e1 = __double2float_ru(e[1]);
+    cbox[g] = make_float4(means[g * D], D == 2 ? means[g * D + 1] : 0.0f, e0, e1);
+}
+
+template <int D>
+int ref_boxes(const RefCall &a) {
+    if (!a.cbox || a.P == 0) return DGS_OK;
+    k_ref_boxes<D><<<grid_for(a.P), kBlock, 0, a.s>>>(a.P, a.means, a.conics, a.flag, a.cbox);
+    DGS_LAUNCH_CHECK(a.s, a.debug);
+    return DGS_OK;
+}
+template int ref_boxes<1>(const RefCall &);
+template int ref_boxes<2>(const RefCall &);
+
+// ref_may_touch on a k_ref_boxes record, in fp32: m - s rounds by at most 2^-22 for |m - s| < 4,
+// so the interval widened by 4e-7 holds the exact one; equal shifts at its ends mean one shift
+// over it, and the far test on it keeps every pair the fp64 test keeps.
+template <int D>
+__device__ __forceinline__ bool ref_may_touch_box(const float4 &b, const float *lo, const float *hi) {
+    const float m[2] = {b.x, b.y}, e[2] = {b.z, b.w};
+    bool far = false;
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+        const float xa = m[d] - hi[d] - 4e-7f, xb = m[d] - lo[d] + 4e-7f;
+        const float k = wrap_shift_f(xa);
+        if (!(k == wrap_shift_f(xb))) return true;  // a wrap breakpoint inside (or NaN): keep
+        far = far || xa - k > e[d] || xb - k < -e[d];
     }
     return !far;
 }
@@ -171,21 +230,75 @@ __device__ __forceinline__ RefUnit ref_unit(const Bins &bins, const uint32_t *fu
 // in list order; g = the lane's caller id.
 template <int D>
 __device__ __forceinline__ uint64_t ref_group(const Bins &bins, uint32_t e0, uint32_t ge, const float *__restrict__ means,
-                                              const float *__restrict__ conics, const RefUnit &u, int lane,
-                                              int64_t &g) {
+                                              const float *__restrict__ conics, const float4 *__restrict__ cbox,
+                                              const RefUnit &u, int lane, int64_t &g) {
     constexpr int S = D * (D + 1) / 2;
     const uint32_t e = e0 + lane;
     const bool valid = e < ge;
     g = valid ? (int64_t)bins.rlist[e] : 0;
     bool keep = false;
     if (valid) {
-        const float m[2] = {means[g * D], D == 2 ? means[g * D + 1] : 0.0f};
-        float c[3] = {0.0f, 0.0f, 0.0f};
+        if (cbox) {
+            keep = ref_may_touch_box<D>(cbox[g], u.lo, u.hi);
+        } else {
+            const float m[2] = {means[g * D], D == 2 ? means[g * D + 1] : 0.0f};
+            float c[3] = {0.0f, 0.0f, 0.0f};
 #pragma unroll
-        for (int k = 0; k < S; ++k) c[k] = conics[g * S + k];
-        keep = ref_may_touch<D>(m, c, u.lo, u.hi);
+            for (int k = 0; k < S; ++k) c[k] = conics[g * S + k];
+            keep = ref_may_touch<D>(m, c, u.lo, u.hi);
+        }
     }
     return (uint64_t)__ballot(keep);
+}
+
+// The call-time cuts' group walk (ref_boxes given): the tile list's entries 64 at a time, each
+// lane one entry -- its caller id and k_ref_boxes record, the next group's loaded while this one
+// is tested and evaluated -- and, for the candidates (ref_may_touch_box), the lane's conic and
+// values gathered once for the group; the candidates are then evaluated wave-uniform with their
+// parameters read from the owning lane (readlane: no per-candidate memory round trip).
+template <int D, int CB>
+struct RefLanes {
+    int64_t g;
+    float4 b;  // {m0, m1, e0, e1}
+    float c[3], v[CB];
+};
+template <int D, int CB>
+__device__ __forceinline__ uint64_t ref_group_lanes(const float *__restrict__ conics, const float *__restrict__ values,
+                                                    int C, int cbase, int nch, const RefUnit &u, bool valid,
+                                                    RefLanes<D, CB> &L) {
+    constexpr int S = D * (D + 1) / 2;
+    const bool keep = valid && ref_may_touch_box<D>(L.b, u.lo, u.hi);
+    const uint64_t cand = (uint64_t)__ballot(keep);
+    if (cand) {
+        L.c[0] = L.c[1] = L.c[2] = 0.0f;
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) L.v[ch] = 0.0f;
+        if (keep) {
+#pragma unroll
+            for (int k = 0; k < S; ++k) L.c[k] = conics[L.g * S + k];
+#pragma unroll
+            for (int ch = 0; ch < CB; ++ch)
+                if (ch < nch) L.v[ch] = values[L.g * C + cbase + ch];
+        }
+    }
+    return cand;
+}
+template <int D, int CB>
+__device__ __forceinline__ void ref_lane_load(const Bins &bins, const float4 *__restrict__ cbox, uint32_t e, uint32_t ge,
+                                              RefLanes<D, CB> &L) {
+    L.g = e < ge ? (int64_t)bins.rlist[e] : 0;
+    L.b = e < ge ? cbox[L.g] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+}
+// The candidate in lane b: mean, conic, values (wave-uniform) and its caller id.
+template <int D, int CB>
+__device__ __forceinline__ int64_t ref_take(const RefLanes<D, CB> &L, int b, float *m, float *c, float *v) {
+    m[0] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(L.b.x), b));
+    m[1] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(L.b.y), b));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) c[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(L.c[k]), b));
+#pragma unroll
+    for (int ch = 0; ch < CB; ++ch) v[ch] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(L.v[ch]), b));
+    return (int64_t)__builtin_amdgcn_readlane((int)L.g, b);
 }
 
 // renderCUDA's forward (forward.cu:87-166) on the reference's pair set with the call-time
@@ -200,7 +313,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_forward(const char *__restrict__
                                                         const float *__restrict__ conics,
                                                         const float *__restrict__ samples,
                                                         const uint32_t *__restrict__ flag, const Outs outs,
-                                                        int C, int cbase) {
+                                                        int C, int cbase, const float4 *__restrict__ cbox) {
     if (sload(flag) == 0u) return;  // the binned tensors were passed: the fine-cell kernels did it
     using Tr = Traits<FN, D>;
     constexpr int U = Tr::U, S = Tr::S;
@@ -220,9 +333,30 @@ __global__ __launch_bounds__(kBlock) void k_ref_forward(const char *__restrict__
 #pragma unroll
             for (int ch = 0; ch < CB; ++ch) acc[a][ch] = 0.0f;
         const uint32_t ge = sload(&gst[u.t + 1]);
+        if (cbox) {
+            RefLanes<D, CB> cur, nxt;
+            uint32_t e0 = sload(&gst[u.t]);
+            ref_lane_load<D, CB>(bins, cbox, e0 + lane, ge, nxt);
+            for (; e0 < ge; e0 += kWave) {
+                cur.g = nxt.g;
+                cur.b = nxt.b;
+                if (e0 + kWave < ge) ref_lane_load<D, CB>(bins, cbox, e0 + kWave + lane, ge, nxt);
+                uint64_t cand = ref_group_lanes<D, CB>(conics, values, C, cbase, nch, u, e0 + lane < ge, cur);
+                while (cand) {  // ascending list position: ascending Gaussian id, as the reference
+                    const int b = __builtin_ctzll(cand);
+                    cand &= cand - 1;
+                    float m[2], c[3], v[CB];
+                    ref_take<D, CB>(cur, b, m, c, v);
+                    float X[2];
+                    ref_displacement<D>(m, u.s, X);
+                    const float p = ref_power<FN, D>(X, c);
+                    if (!(p > 0.0f)) fwd_terms<FN, D, CB, float>(X, c, expf(p), v, acc);  // forward.cu:228
+                }
+            }
+        } else {
         for (uint32_t e0 = sload(&gst[u.t]); e0 < ge; e0 += kWave) {
             int64_t gl;
-            uint64_t cand = ref_group<D>(bins, e0, ge, means, conics, u, lane, gl);
+            uint64_t cand = ref_group<D>(bins, e0, ge, means, conics, cbox, u, lane, gl);
             while (cand) {  // ascending list position: ascending Gaussian id, as the reference
                 const int b = __builtin_ctzll(cand);
                 cand &= cand - 1;
@@ -239,6 +373,7 @@ __global__ __launch_bounds__(kBlock) void k_ref_forward(const char *__restrict__
                 const float p = ref_power<FN, D>(X, c);
                 if (!(p > 0.0f)) fwd_terms<FN, D, CB, float>(X, c, expf(p), v, acc);  // forward.cu:228
             }
+        }
         }
         if (u.active) {
 #pragma unroll
@@ -314,7 +449,8 @@ __global__ __launch_bounds__(kBlock) void k_ref_backward(const char *__restrict_
                                                          const float *__restrict__ conics,
                                                          const float *__restrict__ samples,
                                                          const uint32_t *__restrict__ flag, const DLs dls,
-                                                         float *__restrict__ acc, int P, int C, int cbase) {
+                                                         float *__restrict__ acc, int P, int C, int cbase,
+                                                         const float4 *__restrict__ cbox) {
     if (sload(flag) == 0u) return;
     constexpr int M = fn_mask(FN), S = D * (D + 1) / 2;
     const Bins bins = resolve(gbuf, sbuf);
@@ -334,20 +470,35 @@ __global__ __launch_bounds__(kBlock) void k_ref_backward(const char *__restrict_
         if constexpr ((M & 4) != 0) ref_lane_dl<2, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl2);
         if constexpr ((M & 8) != 0) ref_lane_dl<3, D, CB>(dls, u.sid, u.active, C, cbase, nch, dl3);
         const uint32_t ge = sload(&gst[u.t + 1]);
+        RefLanes<D, CB> cur, nxt;
+        if (cbox) ref_lane_load<D, CB>(bins, cbox, sload(&gst[u.t]) + lane, ge, nxt);
         for (uint32_t e0 = sload(&gst[u.t]); e0 < ge; e0 += kWave) {
             int64_t gl;
-            uint64_t cand = ref_group<D>(bins, e0, ge, means, conics, u, lane, gl);
+            uint64_t cand;
+            if (cbox) {
+                cur.g = nxt.g;
+                cur.b = nxt.b;
+                if (e0 + kWave < ge) ref_lane_load<D, CB>(bins, cbox, e0 + kWave + lane, ge, nxt);
+                cand = ref_group_lanes<D, CB>(conics, values, C, cbase, nch, u, e0 + lane < ge, cur);
+            } else {
+                cand = ref_group<D>(bins, e0, ge, means, conics, cbox, u, lane, gl);
+            }
             while (cand) {
                 const int b = __builtin_ctzll(cand);
                 cand &= cand - 1;
-                const int64_t g = __builtin_amdgcn_readlane((int)gl, b);
                 float m[2], c[3] = {0.0f, 0.0f, 0.0f}, v[CB];
-                m[0] = sload(&means[g * D]);
-                m[1] = D == 2 ? sload(&means[g * D + 1]) : 0.0f;
+                int64_t g;
+                if (cbox) {
+                    g = ref_take<D, CB>(cur, b, m, c, v);
+                } else {
+                    g = __builtin_amdgcn_readlane((int)gl, b);
+                    m[0] = sload(&means[g * D]);
+                    m[1] = D == 2 ? sload(&means[g * D + 1]) : 0.0f;
 #pragma unroll
-                for (int k = 0; k < S; ++k) c[k] = sload(&conics[g * S + k]);
+                    for (int k = 0; k < S; ++k) c[k] = sload(&conics[g * S + k]);
 #pragma unroll
-                for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? sload(&values[g * C + cbase + ch]) : 0.0f;
+                    for (int ch = 0; ch < CB; ++ch) v[ch] = ch < nch ? sload(&values[g * C + cbase + ch]) : 0.0f;
+                }
                 float X[2];
                 ref_displacement<D>(m, u.s, X);
                 const float p = ref_power<FN, D>(X, c);
@@ -382,15 +533,15 @@ __global__ __launch_bounds__(kBlock) void k_ref_backward(const char *__restrict_
 
 // Persistent grids: the work is known only on the device; when the flag is clear every block
 // exits after one scalar load.
-static unsigned ref_blocks(int64_t units) {
-    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + kWavesPerBlock - 1) / kWavesPerBlock, 1024));
+static unsigned ref_blocks(int64_t units) {  // (up to 8 waves per SIMD: the walk is latency-bound)
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>((units + kWavesPerBlock - 1) / kWavesPerBlock, 8192));
 }
 
 template <int FN, int D, int CB>
 int ref_forward(const RefCall &a) {
     const int64_t cap = a.N / kRefUnit + (a.N + 1);  // >= the device-side unit count
     k_ref_forward<FN, D, CB><<<ref_blocks(cap), kBlock, 0, a.s>>>(a.gb, a.sb, a.means, a.values, a.conics,
-                                                                  a.samples, a.flag, a.outs, a.C, a.cbase);
+                                                                  a.samples, a.flag, a.outs, a.C, a.cbase, a.cbox);
     DGS_LAUNCH_CHECK(a.s, a.debug);
     return DGS_OK;
 }
@@ -400,7 +551,7 @@ int ref_backward(const RefCall &a) {
     const int64_t cap = a.N / kRefUnit + (a.N + 1);  // (the forward's units)
     k_ref_backward<FN, D, CB><<<ref_blocks(cap), kBlock, 0, a.s>>>(a.gb, a.sb, a.means, a.values, a.conics,
                                                                    a.samples, a.flag, a.dls, a.acc, a.P,
-                                                                   a.C, a.cbase);
+                                                                   a.C, a.cbase, a.cbox);
     DGS_LAUNCH_CHECK(a.s, a.debug);
     return DGS_OK;
 }

@@ -1520,11 +1520,12 @@ struct Call {
 };
 
 // The call-time path's arguments (dgs_reference.h).
-static RefCall ref_call(const Call &a, float *acc, const uint32_t *flag, int cbase) {
+// cbox: the workspace's Gaussian-row region (>= 16 P bytes), idle on the call-time path.
+static RefCall ref_call(const Call &a, float *acc, const uint32_t *flag, int cbase, float *cbox) {
     UnitHint h;
     const int64_t R = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &h) ? h.R : (int64_t)1 << 40;
     return RefCall{a.gb, a.sb, a.means, a.values, a.conics, a.samples, a.dls, a.outs, acc, flag,
-                   a.P, a.N, a.C, cbase, R, a.s, a.debug};
+                   a.P, a.N, a.C, cbase, R, a.s, a.debug, reinterpret_cast<float4 *>(cbox)};
 }
 
 // The word the render kernels test for "the call's inputs differ from the binned ones": the
@@ -1597,8 +1598,10 @@ static int run_forward(const Call &a) {
             }
         }
         // the call-time path (exits at once unless the inputs differ from the binned ones)
-        if (!binned) {
-            const int rc = ref_forward<FN, D, CB>(ref_call(a, nullptr, flag, cbase));
+        if (!binned) {  // (the Gaussian rows are not read on this path: the cuts go there)
+            const RefCall rc_ = ref_call(a, nullptr, flag, cbase, grows);
+            int rc = ref_boxes<D>(rc_);
+            if (!rc) rc = ref_forward<FN, D, CB>(rc_);
             if (rc) return rc;
         }
     }
@@ -1652,8 +1655,10 @@ static int run_backward(const Call &a) {
                                                                                              D + S + cbase, flag);
         }
         DGS_LAUNCH_CHECK(a.s, a.debug);
-        if (!binned) {
-            const int rc = ref_backward<FN, D, CB>(ref_call(a, acc, flag, cbase));
+        if (!binned) {  // (after k_backward, the last reader of the Gaussian rows)
+            const RefCall rc_ = ref_call(a, acc, flag, cbase, grows);
+            int rc = ref_boxes<D>(rc_);
+            if (!rc) rc = ref_backward<FN, D, CB>(rc_);
             if (rc) return rc;
         }
     }

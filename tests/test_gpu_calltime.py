@@ -203,3 +203,20 @@ def test_step_cache_rows_and_identity(dgs, oracle):
         close(g[0].cpu().numpy(), dm, RTOL, ATOL_BWD, f"backward {k} dL/dmeans")
         close(g[1].cpu().numpy(), dv, RTOL, ATOL_BWD, f"backward {k} dL/dvalues")
         close(g[2].cpu().numpy(), dc, RTOL, ATOL_BWD, f"backward {k} dL/dconics")
+
+
+@pytest.mark.parametrize("function", ["gaussian", "derivative"])
+@pytest.mark.parametrize("D", [1, 2])
+def test_seam_means_moved(dgs, oracle, function, D):
+    """Means near the torus seams moved in place (some across x = +-1): the stale tile lists hold
+    Gaussians that reach a tile through the torus (wrapped rect keys), and the call-time cull
+    tests them after the reference's constant wrap shift over the unit's box (ref_may_touch)."""
+    import cases
+    pre = cases.seam_case(D=D)
+    g = torch.Generator().manual_seed(432)
+    P = pre[0].shape[0]
+    step = (torch.randn(P, D, generator=g) * 0.02).float()
+    call = (pre[0] + step, pre[1], pre[2], pre[3], pre[4])
+    N = pre[4].shape[0]
+    dL = syn.grad_out(N, syn.out_components(function, D), pre[1].shape[1], seed=433)
+    assert not _run(dgs, oracle, function, pre, call, dL)
