@@ -1175,10 +1175,11 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     }
 }
 
-// The slot row width of a Gaussian's sums (k_bwd_esum): [dm(D) dc(S) dv(CB)] padded to 4 floats.
+// The slot row width of a Gaussian's sums (k_bwd_esum): [dm(D) dc(S) dv(CB)] padded to 2 floats
+// (8-byte pieces: 24-byte rows at D = 2, C = 1, where 4-float padding wrote and read 32).
 template <int FN, int D, int CB>
 __host__ __device__ constexpr int esum_stride() {
-    return (D + Traits<FN, D>::S + CB + 3) / 4 * 4;
+    return (D + Traits<FN, D>::S + CB + 1) / 2 * 2;
 }
 
 // One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
@@ -1210,9 +1211,9 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
         for (int k = 0; k < S; ++k) row[D + k] = sc[k];
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) row[D + S + ch] = sv[ch];
-        float4 *o = reinterpret_cast<float4 *>(esums + (int64_t)bins.esum_q[eb + lane] * SSW);
+        float2 *o = reinterpret_cast<float2 *>(esums + (int64_t)bins.esum_q[eb + lane] * SSW);
 #pragma unroll
-        for (int k = 0; k < SSW / 4; ++k) o[k] = make_float4(row[4 * k], row[4 * k + 1], row[4 * k + 2], row[4 * k + 3]);
+        for (int k = 0; k < SSW / 2; ++k) o[k] = make_float2(row[2 * k], row[2 * k + 1]);
     } else if (active) {
 #pragma unroll
         for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
@@ -1256,7 +1257,7 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
 
 // The sort-path entries' sums (k_backward's slots), per Gaussian in slot order -- its entries'
 // order of k_fine_fill -- added to the atomics' sums (plain adds: k_backward has finished).
-// (kEsumLanes lanes per Gaussian stride over its slots, 32-byte rows side by side, then a
+// (kEsumLanes lanes per Gaussian stride over its slots, slot rows side by side, then a
 // shuffle reduction: one thread per Gaussian walked ~24 rows serially in thin fields)
 constexpr int kEsumLanes = 8;
 template <int FN, int D, int CB>
@@ -1278,11 +1279,11 @@ __global__ void k_bwd_esum(int P, const char *__restrict__ gbuf, const float *__
 #pragma unroll
     for (int k = 0; k < SSW; ++k) sum[k] = 0.0f;
     for (uint32_t q = q0 + sub; q < q1; q += kEsumLanes) {
-        const float4 *rw = reinterpret_cast<const float4 *>(esums + (int64_t)q * SSW);
+        const float2 *rw = reinterpret_cast<const float2 *>(esums + (int64_t)q * SSW);
 #pragma unroll
-        for (int k = 0; k < SSW / 4; ++k) {
-            const float4 x = rw[k];
-            sum[4 * k] += x.x; sum[4 * k + 1] += x.y; sum[4 * k + 2] += x.z; sum[4 * k + 3] += x.w;
+        for (int k = 0; k < SSW / 2; ++k) {
+            const float2 x = rw[k];
+            sum[2 * k] += x.x; sum[2 * k + 1] += x.y;
         }
     }
 #pragma unroll
@@ -1479,7 +1480,7 @@ static size_t slot_region_bytes(int FN, int D, int C, const void *gb, size_t gby
     if (C > CB || !hint_get(gb, gbytes, sb, sbytes, &h) || h.Es <= 0 || 4 * h.Es < h.E) return 0;
     const int S = D * (D + 1) / 2;
     (void)FN;
-    return a256(sizeof(float) * (size_t)((D + S + CB + 3) / 4 * 4) * (size_t)h.Es);
+    return a256(sizeof(float) * (size_t)((D + S + CB + 1) / 2 * 2) * (size_t)h.Es);  // (esum_stride)
 }
 
 // Grid size in blocks: exact (from the preprocess hint) or a persistent-size fallback; the
