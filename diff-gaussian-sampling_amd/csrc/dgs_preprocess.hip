@@ -943,10 +943,18 @@ __global__ __launch_bounds__(kBlock) void k_fine_count_irr(Geom G, const float2 
         const float4 cc = igc[i];
         const float m[2] = {mm.x, mm.y}, c[3] = {cc.x, cc.y, cc.z};
         const Cut k = gauss_cut(G, m, c);
-        if (wide_gauss(k)) {  // (k_wide counts it)
-            wq[atomicAdd(nwq, 1u)] = i;
-            continue;
+        // (k_wide counts the unculled ones: one queue append per wave, consecutive slots -- a field
+        // of non-positive-definite conics must not serialise on one counter)
+        const bool wide = wide_gauss(k);
+        const uint64_t wm = __ballot(wide);
+        if (wm) {
+            const int lane = threadIdx.x & (kWave - 1), lead = __ffsll((unsigned long long)wm) - 1;
+            uint32_t wbase = 0;
+            if (lane == lead) wbase = atomicAdd(nwq, (uint32_t)__popcll(wm));
+            wbase = __shfl(wbase, lead);
+            if (wide) wq[wbase + (uint32_t)__popcll(wm & ((1ull << lane) - 1ull))] = i;
         }
+        if (wide) continue;
         uint64_t n = 0;
         const auto count = [&](uint32_t, uint32_t v) {
             ++n;

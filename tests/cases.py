@@ -210,3 +210,32 @@ def wide_domain_case(n=20000, P=3000, half=40.0, seed=141):
     values = torch.randn(P, 1, generator=g).float()
     samples = ((torch.rand(n, 2, generator=g) * 2.0 - 1.0) * half).float()
     return means, values, covs, conics, samples
+
+
+def unculled_case(P=1500, n=12000, seed=191):
+    """Gaussians the binning cannot cull (k_wide: one wave each, every non-empty cell of their
+    tiles): a third with non-positive-definite conics (c1^2 > c0 c2: the reference's `power > 0`
+    skip), a third positive definite but past kRho2Max (rho^2 in (0.9995, 0.9999): axis ratio
+    ~90-200), a third with cuts wider than half the domain's period (sigma ~ 0.05)."""
+    g = torch.Generator().manual_seed(seed)
+    means = (torch.rand(P, 2, generator=g) * 2 - 1).float()
+    k = torch.arange(P) % 3
+    c0 = 40.0 + 80.0 * torch.rand(P, generator=g)
+    c2 = 40.0 + 80.0 * torch.rand(P, generator=g)
+    sgn = torch.where(torch.rand(P, generator=g) < 0.5, -1.0, 1.0)
+    rho = torch.where(k == 0, 1.05 + 0.5 * torch.rand(P, generator=g),
+                      torch.sqrt(0.9995 + 0.0004 * torch.rand(P, generator=g)))
+    c1 = sgn * rho * torch.sqrt(c0 * c2)
+    big = k == 2
+    c0 = torch.where(big, 1.0 / (0.04 + 0.02 * torch.rand(P, generator=g)) ** 2, c0)
+    c2 = torch.where(big, 1.0 / (0.04 + 0.02 * torch.rand(P, generator=g)) ** 2, c2)
+    c1 = torch.where(big, 0.3 * torch.sqrt(c0 * c2) * sgn, c1)
+    conics = torch.stack([c0, c1, c2], 1).float()
+    # covariances: the inverse where it exists (positive definite), a round one of the conic's
+    # scale otherwise (the reference reads covariances for the radius only)
+    det = c0 * c2 - c1 * c1
+    pd = det > 0
+    covs = torch.where(pd[:, None], torch.stack([c2 / det, -c1 / det, c0 / det], 1),
+                       torch.stack([1.0 / c0, torch.zeros(P), 1.0 / c2], 1)).float()
+    values = torch.randn(P, 1, generator=g).float()
+    return means, values, covs, conics, syn.samples(n, 2, seed=seed + 1)
