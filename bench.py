@@ -157,6 +157,9 @@ def main():
                     help="also time fwd + bwd after an in-place step on the means WITHOUT re-binning: the "
                          "call-time path (the reference's whole tile pair set, dgs_reference.hip), next to "
                          "re-binning + the binned step")
+    ap.add_argument("--pigs-graph", action="store_true",
+                    help="also time the PIGS step -- re-binning + forward + backward -- eagerly and as ONE "
+                         "captured HIP graph (preprocess_gaussians_capturable, SURVEY 8f row f1)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -505,6 +508,58 @@ def bench_sample(args, world, rank, dev, torch, dist):
                               "ms_rebin_plus_step": rebin_ms,
                               "note": "fwd + bwd after an in-place means update without re-preprocess (the "
                                       "reference's tile pair set, evaluated on the GPU) vs preprocess + fwd + bwd"}
+    if args.pigs_graph and world == 1 and not multi:
+        # The PIGS loop re-bins after every optimizer step.  Eager: preprocess (one host sync) +
+        # forward + backward.  Graph: the same three captured once with torch.cuda.graph
+        # (the capturable binning keeps R / E / status on the device) and replayed; the binning
+        # runs in full at every replay.  Both from the same tensors, K steps each, medians.
+        grid, off = dgs._C.tile_grid(samples)
+        cap = dgs.capacity_from(gb, sb, slack=0.125)
+        md, vd, cd = means.detach(), values.detach(), conics.detach()
+
+        def pigs_eager():
+            for t in (means, values, conics):
+                t.grad = None
+            R2, gb2, sb2, rg2, srg2, _ = dgs._C.preprocess_gaussians(md, vd, covs, cd, samples, False)
+            fwd(means, values, conics, samples, R2, gb2, sb2, rg2, srg2, False).backward(dLv)
+
+        def pigs_body():
+            R2, gb2, sb2, rg2, srg2, _, st2 = dgs.preprocess_gaussians_capturable(md, vd, covs, cd, samples, grid,
+                                                                                    off, cap)
+            fwd(means, values, conics, samples, cap[2], gb2, sb2, rg2, srg2, False).backward(dLv)
+            return st2
+
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                for t in (means, values, conics):
+                    t.grad = None
+                pigs_body()
+        torch.cuda.current_stream().wait_stream(side)
+        for t in (means, values, conics):
+            t.grad = None
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            g_st = pigs_body()
+        times = {}
+        for name, fn in (("eager", pigs_eager), ("graph", graph.replay)):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ms = []
+            for _ in range(max(args.steps, 5)):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                ms.append((time.perf_counter() - t0) * 1e3)
+            times[name] = sorted(ms)[len(ms) // 2]
+        result["pigs_graph"] = {"ms_per_step_eager": times["eager"], "ms_per_step_graph": times["graph"],
+                                "graph_status": int(g_st.item()), "capacity": cap,
+                                "note": "re-binning + fwd + bwd per step, host-timed medians; graph = one "
+                                        "torch.cuda.graph replay of preprocess_gaussians_capturable + the sample "
+                                        "call + backward"}
+        del graph
     if rank == 0 and world == 1 and not args.no_cpu and not multi:
         cpu_baselines(result, means.detach().cpu(), values.detach().cpu(), covs.cpu(),
                       conics.detach().cpu(), samples.cpu(), dL.cpu(), fn, w_live, N, args, torch)
