@@ -543,14 +543,14 @@ def bench_sample(args, world, rank, dev, torch, dist):
         with torch.cuda.graph(graph):
             g_st = pigs_body()
         times = {}
-        for name, fn in (("eager", pigs_eager), ("graph", graph.replay)):
+        for name, run_step in (("eager", pigs_eager), ("graph", graph.replay)):
             for _ in range(3):
-                fn()
+                run_step()
             torch.cuda.synchronize()
             ms = []
             for _ in range(max(args.steps, 5)):
                 t0 = time.perf_counter()
-                fn()
+                run_step()
                 torch.cuda.synchronize()
                 ms.append((time.perf_counter() - t0) * 1e3)
             times[name] = sorted(ms)[len(ms) // 2]
