@@ -1309,6 +1309,9 @@ __global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, int CT, const in
     }
 }
 
+#ifndef DGS_SUBL_DEPTH
+#define DGS_SUBL_DEPTH 2  // k_sub_lists: Gaussian-row groups in flight ahead of the tested one (1: 24 us slower at the headline)
+#endif
 #ifndef DGS_SUB_SLICE
 #define DGS_SUB_SLICE 1  // k_sub_lists: per-sub-row slices instead of per-sub-box minimisations
 #endif
@@ -1443,14 +1446,30 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
         float2 mm_c;
         float4 cc_c;
         sub_row(ent_c, gmean, gcon, mm_c, cc_c);
+#if DGS_SUBL_DEPTH > 1
+        // (three stages: group g + 1's and g + 2's Gaussians, g + 3's entries)
+        float2 mm_n;
+        float4 cc_n;
+        sub_row(ent_n, gmean, gcon, mm_n, cc_n);
+        uint32_t ent_nn = b + 2 * kWave + lane < e ? entries[b + 2 * kWave + lane] : kUnsafe;
+#endif
         for (int j0 = b; j0 < e; j0 += kWave) {
             const int j = j0 + lane;
             const uint32_t ent = ent_c;
             const float2 mm = mm_c;
             const float4 cc = cc_c;
+#if DGS_SUBL_DEPTH > 1
+            ent_c = ent_n;
+            mm_c = mm_n;
+            cc_c = cc_n;
+            ent_n = ent_nn;
+            sub_row(ent_n, gmean, gcon, mm_n, cc_n);
+            ent_nn = j + 3 * kWave < e ? entries[j + 3 * kWave] : kUnsafe;
+#else
             ent_c = ent_n;
             sub_row(ent_c, gmean, gcon, mm_c, cc_c);
             ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
+#endif
             const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
             const bool ff = j < m_, thin = (ent & kThin) != 0;
 #pragma unroll
