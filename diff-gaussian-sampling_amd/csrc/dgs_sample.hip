@@ -245,9 +245,6 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // value l in lane l.  Row delivery per pair is negligible here (the lane-per-sample form is
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
-#ifndef DGS_FWD_EXACT_TAIL
-#define DGS_FWD_EXACT_TAIL 1  // sub-cell forward: the last partial block of 4 pairs evaluates its pairs only
-#endif
 #ifndef DGS_BWD_PIPE
 #define DGS_BWD_PIPE 1  // backward pair loop: the next batch of pair rows in flight during this one
 #endif
@@ -491,19 +488,10 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
         F32s<16> t;
         if (b < HB) t = hr[b < HB ? b : 0];
         else t = sload_f<16>(prow + (int64_t)b * PPL * PRF);
-        if (DGS_FWD_EXACT_TAIL && (b + 1) * PPL > np) {
-            // the pass's last, partial block: only its pairs (a sub-cell holds ~18.5 pairs, so
-            // evaluating the whole 4-pair block wasted ~1.5 pair evaluations per group)
 #pragma unroll
-            for (int j = 0; j < PPL; ++j)
-                if (b * PPL + j < NPH && b * PPL + j < np)
-                    fwd_t_pair<FN, D, CB, WRAP, LIT>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
-        } else {
-#pragma unroll
-            for (int j = 0; j < PPL; ++j)
-                if (b * PPL + j < NPH)
-                    fwd_t_pair<FN, D, CB, WRAP, LIT>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
-        }
+        for (int j = 0; j < PPL; ++j)
+            if (b * PPL + j < NPH)
+                fwd_t_pair<FN, D, CB, WRAP, LIT>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
     }
 }
 

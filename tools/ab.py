@@ -19,6 +19,10 @@ ap.add_argument("--kbench-args", default="")
 ap.add_argument("variants", nargs="+")
 a = ap.parse_args()
 res = {v: [] for v in a.variants}
+for v in a.variants:  # a mistyped variant would silently time the in-tree build
+    pv = v.partition(":")[0]
+    if pv != "base" and not os.path.isdir(os.path.join(REPO, pv, "diff_gaussian_sampling")):
+        sys.exit(f"no variant package at {os.path.join(REPO, pv)} (tools/variant.sh builds variants/NAME)")
 for r in range(a.rounds):
     for v in a.variants:
         env = dict(os.environ)
