@@ -20,13 +20,13 @@ namespace dgs {
 // ---------------------------------------------------------------------------------------
 constexpr float kTile = 0.51f;         // BLOCK_SIZE
 constexpr uint32_t kMagic = 0x44475342u;  // "DGSB"
-constexpr uint32_t kVersion = 10;
+constexpr uint32_t kVersion = DGS_ABI_VERSION;  // (the binning header's version too)
 // Fine-list entry = internal Gaussian id | flags.  Entries of a cell are sorted so that the
 // flagged ones come last (the render kernels then see whole flag-free batches).
 constexpr uint32_t kGeneral = 0x80000000u;  // per-pair exact torus wrap needed in this cell
 constexpr uint32_t kUnsafe = 0x40000000u;   // conic not positive definite, a wrap breakpoint in the
                                             // cell, or a fallback cell: the per-pair literal path
-constexpr uint32_t kThin = 0x20000000u;     // DGS_THIN_LITERAL only: positive definite but ill-conditioned
+constexpr uint32_t kThin = 0x20000000u;     // reserved (round 4's literal-order thin pass; no entry carries it)
                                             // (rho^2 >= 0.82): packed, the unfused reference's exponent order
 constexpr uint32_t kSlow = kGeneral | kUnsafe | kThin;
 constexpr uint32_t kIdMask = 0x1fffffffu;
@@ -383,17 +383,14 @@ __device__ inline uint32_t ref_touched(int D, const float *mean, const float *co
 // unfused reference differ by 1-2x the 1e-5 parity bound in the forward and 4-6x in the
 // gradients (tools/contraction_study.py, profiles/r05_contraction.json): no operation order is
 // "the reference's" there.  So thin conics take the fast paths like every other PD conic, under
-// the stated bound of tests/test_gpu_parity.py (within twice the reference's own compile spread);
-// DGS_THIN_LITERAL=1 restores round 4's kThin entries (the unfused reference's order, lit_prob).
+// the stated bound of tests/test_gpu_parity.py (an a-priori bound on the exponent's
+// rounding in any operation order).  (Round 4's kThin literal-order pass was removed in round 6.)
 // Past rho^2 = kRho2Max (axis ratio ~89, amplification A = (1 + rho) / (1 - rho) ~8000) a conic
 // is treated as not positive definite: up to there the fp32 exponent of a pair beyond the cut
 // (X^T A X > 210, power < -105) is below -104.5 in any operation order (|error| <= ~3e-7 x A x 210
 // = 0.5; expf is +0 below -103.97), so culling it drops an exact +0; past it the rounding could
 // leave a subnormal term.  (0.999 -- A ~4000 -- left the axis-ratio-25 field's 107 thinnest
 // Gaussians, rho^2 up to 0.99925, unculled: ~1500 literal-path entries each, +0.19 ms per forward.)
-#ifndef DGS_THIN_LITERAL
-#define DGS_THIN_LITERAL 0
-#endif
 constexpr double kRho2Max = 0.9995;
 // Not positive definite, too ill-conditioned (above), or not finite: kUnsafe, the per-pair
 // literal path with the exact wrap and the reference's `power > 0 -> skip` (forward.cu:228).
@@ -403,9 +400,8 @@ __host__ __device__ inline bool conic_unsafe(int D, float c0f, float c1f, float 
     return !(c0 > 0.0 && c2 > 0.0 && c0 < INFINITY && c2 < INFINITY && fabs(c1) < INFINITY &&
              c1 * c1 < kRho2Max * (c0 * c2));
 }
-// Positive definite but ill-conditioned, rho^2 = c1^2 / (c0 c2) >= 0.82 (D = 2).  These stay off
-// the binning's gather path (its fp32 row slices assume a well-conditioned cut) and, with
-// DGS_THIN_LITERAL, are flagged kThin for the literal-order exponent.
+// Positive definite but ill-conditioned, rho^2 = c1^2 / (c0 c2) >= 0.82 (D = 2): kept off the
+// binning's gather path in -DDGS_THIN_GATHER=0 builds only (a tuning knob).
 __host__ __device__ inline bool conic_thin(int D, float c0f, float c1f, float c2f) {
     if (D != 2 || conic_unsafe(D, c0f, c1f, c2f)) return false;
     const double c0 = c0f, c1 = c1f, c2 = c2f;

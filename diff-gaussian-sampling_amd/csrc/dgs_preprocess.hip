@@ -86,6 +86,14 @@ static int64_t *pinned_totals() {
     return p;
 }
 
+// The event after the copy of the previous binning's entry-sort give-up word into pinned word 9
+// (per host thread, like the buffer): that binning may have run on another stream, so the next
+// binning waits for the copy itself before reading and clearing the word.
+static hipEvent_t &giveup_copied() {
+    static thread_local hipEvent_t e = nullptr;
+    return e;
+}
+
 static int bit_length(uint64_t v) {
     int b = 0;
     while (v) { ++b; v >>= 1; }
@@ -495,8 +503,7 @@ __device__ __forceinline__ bool visit_local(const Geom &G, const Cut &k, const i
 // grid and its cut within kGatherReach fine cells of the mean's (home) cell.  Their local
 // entries are produced per cell by k_gather (no sort); everything else goes through the
 // per-Gaussian enumeration and the entry sort.  Returns the reach in cells, 0 if not regular.
-// Thin conics (rho^2 >= 0.82) are regular too unless DGS_THIN_LITERAL (their kThin flag needs the
-// sort): local_rows' fp32 slice margins hold for them -- the slice centre's rounding is relative
+// Thin conics (rho^2 >= 0.82) are regular too: local_rows' fp32 slice margins hold for them -- the slice centre's rounding is relative
 // to |x|, and the sqrt argument's cancellation costs at most sqrt(eps) e0 sqrt(1 - rho^2) <= tol
 // (rho^2 < kRho2Max keeps det well away from 0).
 #ifndef DGS_THIN_GATHER
@@ -510,7 +517,7 @@ static_assert(kGatherRows <= 32, "local_rows keeps one bit per row");
 __device__ __forceinline__ int gather_reach(const Geom &G, const float *m, float r, const float *con, const Cut &k,
                                             const KeyRect &kr) {
     if (G.D != 2 || !(r > 0.0f) || !k.cull || conic_unsafe(2, con[0], con[1], con[2]) ||
-        ((DGS_THIN_LITERAL || !DGS_THIN_GATHER) && conic_thin(2, con[0], con[1], con[2])))
+        (!DGS_THIN_GATHER && conic_thin(2, con[0], con[1], con[2])))
         return 0;
     if (!(k.e[0] + 3.0 * G.fs < 0.9 && k.e[1] + 3.0 * G.fs < 0.9)) return 0;
     // every tile visited at most once (a rect wider than the grid visits a tile repeatedly,
@@ -561,8 +568,7 @@ __device__ __forceinline__ void enumerate_fine(const Geom &G, const float *m, fl
                                       Emit emit) {
     const int D = G.D;
     const KeyRect kr = ref_key_rect(D, m, r, G.grid, G.off);
-    const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
-                           : (DGS_THIN_LITERAL && conic_thin(D, con[0], con[1], con[2])) ? kThin : 0u;
+    const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
     Slice32 sl;
     if (k.cull && D == 2) sl.init(G, k);
     for (int y = kr.y0; y < kr.y1; ++y)
@@ -1010,8 +1016,7 @@ __global__ __launch_bounds__(kBlock) void k_wide(Geom G, const float2 *__restric
         const float4 cc = igc[i];
         const float m[2] = {mm.x, mm.y}, con[3] = {cc.x, cc.y, cc.z};
         const KeyRect kr = ref_key_rect(D, m, cc.w, G.grid, G.off);
-        const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe
-                               : (DGS_THIN_LITERAL && conic_thin(D, con[0], con[1], con[2])) ? kThin : 0u;
+        const uint32_t uflag = conic_unsafe(D, con[0], con[1], con[2]) ? kUnsafe : 0u;
         uint64_t o = FILL ? offs[i] : 0;
         for (int y = kr.y0; y < kr.y1; ++y)
             for (int x = kr.x0; x < kr.x1; ++x) {
@@ -1511,7 +1516,9 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(int ncells, const int32_t 
 // call-time path (dgs_reference.hip).
 // Run lazily (ensure_ref_lists) over the internal ids: the binned means (gmean), radius and
 // tile-list offset (rref) of caller id g = perm[i].
-__global__ void k_ref_keys(int P, Geom G, const float2 *__restrict__ gmean, const int32_t *__restrict__ perm,
+// (Writes stay below R, the list size the scratch was sized for: a capturable binning clamps its
+// header's R to capacity_R while the offsets keep the true counts.)
+__global__ void k_ref_keys(int P, int64_t R, Geom G, const float2 *__restrict__ gmean, const int32_t *__restrict__ perm,
                            const uint32_t *__restrict__ rref, uint32_t *__restrict__ keys, uint32_t *__restrict__ vals) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= P) return;
@@ -1523,7 +1530,7 @@ __global__ void k_ref_keys(int P, Geom G, const float2 *__restrict__ gmean, cons
     const KeyRect kr = ref_key_rect(G.D, m, r, G.grid, G.off);
     uint64_t o = rref[g];  // (tile-list offset, caller order)
     for (int y = kr.y0; y < kr.y1; ++y)
-        for (int x = kr.x0; x < kr.x1; ++x) {
+        for (int x = kr.x0; x < kr.x1 && (int64_t)o < R; ++x) {
             keys[o] = key_of(G.D, x, y, G.grid);
             vals[o] = (uint32_t)g;
             ++o;
@@ -1613,6 +1620,7 @@ struct TailSpec {
     float off[2];
     int64_t *R_out;
     uint32_t *status;
+    int sticky;  // DGS_BIN_STATUS_STICKY: OR into *status (it records every replay's overflows)
 };
 
 __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts, Header h) {
@@ -1638,7 +1646,7 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
                     hh->zero[0] = st ? 1u : 0u;
                 }
                 *ts.R_out = R;
-                *ts.status = st;
+                *ts.status = ts.sticky ? (*ts.status | st) : st;
             }
         }
     }
@@ -1942,7 +1950,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         *num_rendered = -1;  // (on the device: *num_rendered_device)
         if (P == 0 || N == 0) {  // sample_points.cu:69: nothing to bin
             DGS_TRY_HIP(hipMemsetAsync(copt->num_rendered_device, 0, sizeof(int64_t), s));
-            DGS_TRY_HIP(hipMemsetAsync(copt->status_device, 0, sizeof(uint32_t), s));
+            if (!(copt->flags & DGS_BIN_STATUS_STICKY))
+                DGS_TRY_HIP(hipMemsetAsync(copt->status_device, 0, sizeof(uint32_t), s));
             return DGS_OK;
         }
     }
@@ -2262,6 +2271,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         if (rc) return rc;
     }
     DGS_TRY_HIP(hipEventSynchronize(copied));
+    if (hipEvent_t g = giveup_copied()) DGS_TRY_HIP(hipEventSynchronize(g));  // (word 9 has landed)
     // a radix look-back gave up (dgs_radix.h; never observed): this binning's sample / home sort,
     // or the previous binning's entry sort on this thread (its word lands at the end of that call)
     if (herr[0] || herr[1] || herr[2]) {
@@ -2500,6 +2510,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         for (int d = 0; d < 2; ++d) { ts.grid[d] = G.grid[d]; ts.off[d] = G.off[d]; }
         ts.R_out = copt->num_rendered_device;
         ts.status = copt->status_device;
+        ts.sticky = (copt->flags & DGS_BIN_STATUS_STICKY) ? 1 : 0;
     }
     k_binning_tail<<<1024, kBlock, 0, s>>>(c, ts, h);
     DGS_LAUNCH_CHECK(s, debug);
@@ -2520,8 +2531,12 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     uh.ref_built = false;
     uh.ref_done = nullptr;
     hint_put(uh);
-    if (Es > 0 && herr)  // the entry sort's give-up word, checked at this thread's next binning sync
+    if (Es > 0 && herr) {  // the entry sort's give-up word, checked at this thread's next binning sync
         DGS_TRY_HIP(hipMemcpyAsync(herr + 2, B.rs_e + B.plan_e.o_tickets + 63 * 4, 4, hipMemcpyDeviceToHost, s));
+        hipEvent_t &g = giveup_copied();
+        if (!g) DGS_TRY_HIP(hipEventCreateWithFlags(&g, hipEventDisableTiming));
+        DGS_TRY_HIP(hipEventRecord(g, s));
+    }
     return DGS_OK;
 }
 // Sorts the call-time path's tile lists (see ensure_ref_lists in dgs_internal.h) of the binning
@@ -2547,7 +2562,7 @@ static int build_ref_lists(const Header &h, char *gbuf, hipStream_t s, int debug
     uint32_t *keys_sorted = reinterpret_cast<uint32_t *>(scr + 2 * kb);
     hipError_t e = hipMemsetAsync(scr + 3 * kb, 0, plan.zero_bytes, s);
     if (e == hipSuccess) {
-        k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
+        k_ref_keys<<<grid_for(P), kBlock, 0, s>>>((int)P, R, G, reinterpret_cast<const float2 *>(gbuf + h.o_gmean),
                                                   reinterpret_cast<const int32_t *>(gbuf + h.o_perm),
                                                   reinterpret_cast<const uint32_t *>(gbuf + h.o_rref), keys, vals);
         e = hipGetLastError();
@@ -2574,6 +2589,12 @@ int ensure_ref_lists(const void *gbuf, size_t gbytes, const void *sbuf, size_t s
         if (hd.magic != kMagic || hd.version != kVersion || hd.g_bytes > gbytes || hd.R < 0 ||
             hd.R >= (1LL << 31))
             return DGS_OK;  // (not a binning: the render kernels' own header check makes it loud)
+        // A capturable binning that overflowed a capacity (or binned with a stale grid) clamped
+        // its header's R and left its lists short: there is no pair set to evaluate other tensors
+        // on.  The status word said so; re-bin eagerly (no out-of-bounds lists).
+        if (hd.zero[0])
+            return fail(DGS_ERR_BUFFER, "the binning's status is non-zero (a capacity overflowed or the grid changed): "
+                                        "re-bin before calling with tensors other than the binned ones");
         return build_ref_lists(hd, static_cast<char *>(const_cast<void *>(gbuf)), s, debug);
     }
     if (h.ref_built) {
@@ -2658,6 +2679,11 @@ extern "C" int dgs_preprocess_ex(int P, int D, int N, const float *means, const 
                                  const float *grid_offset, const dgs_bin_options *opts, float *radii,
                                  dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
                                  dgs_stream_t stream, int debug) {
+    if (opts && opts->struct_size != sizeof(dgs_bin_options))
+        return fail(DGS_ERR_ARG, "dgs_preprocess_ex: dgs_bin_options.struct_size must be sizeof(dgs_bin_options) "
+                                 "(a caller built against another dgs.h; see DGS_ABI_VERSION)");
+    if (opts && (opts->flags & ~(uint32_t)DGS_BIN_STATUS_STICKY))
+        return fail(DGS_ERR_ARG, "dgs_preprocess_ex: unknown dgs_bin_options.flags");
     const uint8_t *present = opts ? opts->present : nullptr;
     const double area = opts ? opts->sample_area : 0.0;
     if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_ex: sample_area must be >= 0");

@@ -175,29 +175,6 @@ __device__ __forceinline__ f2 general_prob(f2 *X, const float *c, const float *k
     return f2{Ga, Gb};
 }
 
-// kThin entries (D = 2): the reference's exponent in its own operation order -- float products
-// (c0 X0) X0, (c2 X1) X1, (c1 X0) X1 without contraction, their sum, then -0.5 a - b rounded once
-// (forward.cu:227 et seq.; the FMA below is that single rounding since -0.5 a is exact) -- and its
-// `power > 0 -> skip` rule; exp2 of power * log2(e).  Packed like the fast path: the flagged
-// groups that hold such an entry take this form for all their lanes.
-template <typename V>
-__device__ __forceinline__ V lit_prob(const V *X, const float *c) {
-    DGS_NO_CONTRACT
-    const V t0 = (bc<V>(c[0]) * X[0]) * X[0];
-    const V t1 = (bc<V>(c[2]) * X[1]) * X[1];
-    const V b = (bc<V>(c[1]) * X[0]) * X[1];
-    const V a = t0 + t1;
-    const V p = vfma(bc<V>(-0.5f), a, -b);
-    V G = vexp2(p * kLog2e);
-    if constexpr (sizeof(V) == 4) {
-        G = p > 0.0f ? 0.0f : G;
-    } else {
-        G.x = p.x > 0.0f ? 0.0f : G.x;
-        G.y = p.y > 0.0f ? 0.0f : G.y;
-    }
-    return G;
-}
-
 // Raw conic of a Gaussian row (FN != gaussian keeps it in the row).
 template <int FN, int D, int RS>
 __device__ __forceinline__ void row_conic(const float (&r)[RS], float *c) {
@@ -266,31 +243,25 @@ __host__ __device__ constexpr bool fwd_transposed() {
 // WRAP: some lane's entry crosses the torus seam.  Its wrap (forward.cu:149-157) is a
 // constant even shift over the cell (preprocess sends the other seam entries to the general
 // path), subtracted exactly: sh = 0 for every other lane.
-// LIT: kThin entries in the group -- the exponent from the raw conic `cl` in the reference's
-// order (lit_prob) for every lane.
-template <int FN, int D, int CB, bool WRAP, bool LIT = false>
+template <int FN, int D, int CB, bool WRAP>
 __device__ __forceinline__ void fwd_t_pair(const float *pr, const float *m, const float *sh, const float *c,
-                                           const float *kk, const float *v, f2 (&acc)[Traits<FN, D>::U][CB],
-                                           const float *cl = nullptr) {
+                                           const float *kk, const float *v, f2 (&acc)[Traits<FN, D>::U][CB]) {
     f2 X[2] = {m[0] - f2{pr[0], pr[1]}, D == 2 ? m[1] - f2{pr[2], pr[3]} : bc<f2>(0.0f)};
     if constexpr (WRAP) {
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
     }
-    f2 G;
-    if constexpr (LIT && D == 2) G = lit_prob<f2>(X, cl);
-    else G = fast_prob<D, f2>(X, kk);
-    fwd_terms<FN, D, CB, f2>(X, c, G, v, acc);
+    fwd_terms<FN, D, CB, f2>(X, c, fast_prob<D, f2>(X, kk), v, acc);
 }
 
 // s_waitcnt lgkmcnt(0) (gfx9 encoding: vmcnt 63, expcnt 7, lgkmcnt 0)
 #define DGS_WAIT_LGKM0() __builtin_amdgcn_s_waitcnt(0xC07F)
 
-template <int FN, int D, int CB, int NP, bool WRAP, bool FULL, bool LIT = false>
+template <int FN, int D, int CB, int NP, bool WRAP, bool FULL>
 __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, int p0, int np,
                                             const float *m, const float *sh, const float *c,
                                             const float *kk, const float *v,
-                                            f2 (&acc)[NP][Traits<FN, D>::U][CB], const float *cl = nullptr) {
+                                            f2 (&acc)[NP][Traits<FN, D>::U][CB]) {
     constexpr int LW = 16;  // (x8 loads measured 6x slower: the unrolled pass stopped interleaving)
     constexpr int PRF = 2 * D, PPL = LW / PRF;  // floats per pair row, pairs per s_load_dwordx16
     if constexpr (FULL) {
@@ -311,7 +282,7 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
             __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
             for (int j = 0; j < PPL; ++j)
-                fwd_t_pair<FN, D, CB, WRAP, LIT>(&cur.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
+                fwd_t_pair<FN, D, CB, WRAP>(&cur.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
             __builtin_amdgcn_sched_barrier(0);
             if (b + 1 < NB) cur = nxt;
         }
@@ -322,7 +293,7 @@ __device__ __forceinline__ void fwd_t_pairs(const float *__restrict__ fsrows, in
             const F32s<LW> sr = sload_f<LW>(fsrows + (int64_t)(p0 + q) * PRF);
 #pragma unroll
             for (int j = 0; j < PPL; ++j) {
-                if (q + j < NP) fwd_t_pair<FN, D, CB, WRAP, LIT>(&sr.v[j * PRF], m, sh, c, kk, v, acc[q + j], cl);
+                if (q + j < NP) fwd_t_pair<FN, D, CB, WRAP>(&sr.v[j * PRF], m, sh, c, kk, v, acc[q + j]);
             }
         }
     }
@@ -348,8 +319,8 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
     // a padding lane, or a kUnsafe entry (done by the tail pass), adds exactly 0.  Flagged
     // groups zero the whole row (an unsafe conic may overflow); a padding lane of a flag-free
     // group holds a copy of a well-conditioned row (finite terms), so zero values suffice.
-    if constexpr (FLAGGED) {  // (kUnsafe: the tail pass; kThin: the thin pass, k_forward_s<..., true>)
-        if (!active || (ent & (kUnsafe | kThin))) {
+    if constexpr (FLAGGED) {  // (kUnsafe: the tail pass)
+        if (!active || (ent & kUnsafe)) {
 #pragma unroll
             for (int k = 0; k < RS; ++k) r[k] = 0.0f;
         }
@@ -364,7 +335,7 @@ __device__ __forceinline__ void fwd_t_group(const float *__restrict__ fsrows, fl
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     float sh[2] = {0.0f, 0.0f};  // the lane's constant wrap shift (kGeneral entries)
     if constexpr (FLAGGED) {
-        if (active && (ent & (kGeneral | kUnsafe | kThin)) == kGeneral) {
+        if (active && (ent & (kGeneral | kUnsafe)) == kGeneral) {
 #pragma unroll
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
@@ -476,11 +447,10 @@ __global__ __launch_bounds__(kBlock) void k_forward_t(const char *__restrict__ g
 // The first HB (DGS_FWD_HB = 2) blocks of 4 pair rows are hoisted (at 4 blocks, 64 SGPRs, the kernel spilled SGPRs into VGPR lanes: a
 // v_readlane per dword inside the loop); the pass's later blocks, needed by the larger sub-cells
 // only, are loaded where they are used.
-template <int FN, int D, int CB, int NPH, int HB, bool WRAP, bool LIT = false>
+template <int FN, int D, int CB, int NPH, int HB, bool WRAP>
 __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const float *__restrict__ prow, int np,
                                             const float *m, const float *sh, const float *c, const float *kk,
-                                            const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB],
-                                            const float *cl = nullptr) {
+                                            const float *v, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
     constexpr int PRF = 2 * D, PPL = 16 / PRF, NB = (NPH + PPL - 1) / PPL;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
@@ -491,7 +461,7 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
 #pragma unroll
         for (int j = 0; j < PPL; ++j)
             if (b * PPL + j < NPH)
-                fwd_t_pair<FN, D, CB, WRAP, LIT>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j], cl);
+                fwd_t_pair<FN, D, CB, WRAP>(&t.v[j * PRF], m, sh, c, kk, v, acc[b * PPL + j]);
     }
 }
 
@@ -549,17 +519,16 @@ __device__ __forceinline__ void fwd_l_pairs(uint32_t slot, int np, const float *
     }
 }
 
-// THIN (the thin pass): only the kThin lanes, with the literal-order exponent; otherwise every
-// lane but the kUnsafe (tail pass) and kThin (thin pass) ones, with the fast exponent.
-template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED, bool THIN>
+// FLAGGED: every lane but the kUnsafe ones (the tail pass), with the lane's constant wrap shift.
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
 __device__ __forceinline__ void fwd_s_group(const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
                                             float (&r)[grow_stride<FN, D, CB>()],
                                             uint32_t ent, bool active, int np, const float *ctr,
-                                            const float4 *__restrict__ gcon, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
+                                            f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
     constexpr int RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
     bool on = active;
     if constexpr (FLAGGED) {
-        on = THIN ? active && (ent & kThin) : active && !(ent & (kUnsafe | kThin));
+        on = active && !(ent & kUnsafe);
         if (!on) {
 #pragma unroll
             for (int k = 0; k < RS; ++k) r[k] = 0.0f;
@@ -580,23 +549,15 @@ __device__ __forceinline__ void fwd_s_group(const F32s<16> (&hr)[HB], const floa
             for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
         }
     }
-    if constexpr (THIN) {
-        float cl[3] = {0.0f, 0.0f, 0.0f};
-        if (on) {
-            const float4 q = gcon[ent & kIdMask];
-            cl[0] = q.x; cl[1] = q.y; cl[2] = q.z;
-        }
-        fwd_s_pairs<FN, D, CB, NPH, HB, FLAGGED, true>(hr, prow, np, m, sh, c, &r[D], &r[B], acc, cl);
-    } else if constexpr (DGS_FWD_LDS) {
+    if constexpr (DGS_FWD_LDS) {
         fwd_l_pairs<FN, D, CB, NPH, FLAGGED>(slot, np, m, sh, c, &r[D], &r[B], acc);
     } else {
         fwd_s_pairs<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, np, m, sh, c, &r[D], &r[B], acc);
     }
 }
 
-template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED, bool THIN>
+template <int FN, int D, int CB, int NPH, int HB, bool FLAGGED>
 __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, const float *__restrict__ grows,
-                                             const float4 *__restrict__ gcon,
                                              const F32s<16> (&hr)[HB], const float *__restrict__ prow, uint32_t slot,
                                              int eb, int ee, int np, int lane,
                                              const float *ctr, f2 (&acc)[NPH][Traits<FN, D>::U][CB]) {
@@ -614,18 +575,14 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
         float r_nxt[RS];
         load_grow<RS>(grows, e_nxt, r_nxt);
         const uint32_t e_nn = ents[min(g0 + 2 * kWave + lane, last)];
-        // flagged groups with no lane for this pass are skipped (the entry sort puts a cell's kThin
-        // entries after its other flagged ones, so the main and the thin pass share few groups)
+        // flagged groups with no lane for this pass (all kUnsafe: the tail pass) are skipped
         bool work = true;
         if constexpr (FLAGGED) {
             const bool act = g0 + lane < ee;
-            work = __builtin_amdgcn_readfirstlane(
-                       (uint32_t)(__ballot(act && (THIN ? (e_cur & kThin) != 0 : (e_cur & (kUnsafe | kThin)) == 0)) !=
-                                  0ull)) != 0u;
+            work = __builtin_amdgcn_readfirstlane((uint32_t)(__ballot(act && (e_cur & kUnsafe) == 0) != 0ull)) != 0u;
         }
         if (work)
-            fwd_s_group<FN, D, CB, NPH, HB, FLAGGED, THIN>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr,
-                                                           gcon, acc);
+            fwd_s_group<FN, D, CB, NPH, HB, FLAGGED>(hr, prow, slot, r_cur, e_cur, g0 + lane < ee, np, ctr, acc);
 #pragma unroll
         for (int k = 0; k < RS; ++k) r_cur[k] = r_nxt[k];
         e_cur = e_nxt;
@@ -633,10 +590,9 @@ __device__ __forceinline__ void fwd_s_groups(const uint32_t *__restrict__ ents, 
     }
 }
 
-// THIN = true: the thin pass -- per sub unit only the kThin part of the sub list, [lthin, lend)
-// (the literal-order exponent, lit_prob), added onto the main pass's output; the main pass walks
-// [lbeg, lthin).  Launched only when the binning saw kThin entries.
-template <int FN, int D, int CB, bool THIN>
+// Per sub unit the sub list [lbeg, lthin): its flag-free part, then its flagged part [lmid, lthin)
+// (lthin = lend: no entry carries the round-4 kThin flag since round 6).
+template <int FN, int D, int CB>
 __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ gbuf,
                                                       const char *__restrict__ sbuf,
                                                       const float *__restrict__ grows,
@@ -663,9 +619,8 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
         const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
         const int hi = min(sb + 2 * kSubPairs, sload(&bins.sub_send[sc]));
         const int gb = sload(&bins.sub_lbeg[sc]), gm = sload(&bins.sub_lmid[sc]), ge = sload(&bins.sub_lend[sc]);
-        // a sub list's kThin entries are its last ones (the entry sort's order): [gt, ge)
         const int gt = sload(&bins.sub_lthin[sc]);
-        if (THIN && gt == ge) continue;
+        (void)ge;
         float ctr[2];
         cell_center<D>(bins, cell, ctr);
         for (int ps = sb; ps < hi; ps += NS) {
@@ -687,12 +642,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
 #pragma unroll
                     for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
             constexpr int HBX = DGS_FWD_LDS ? 1 : HB;
-            if constexpr (!THIN)
-                fwd_s_groups<FN, D, CB, NPH, HBX, false, false>(bins.sub_ent, grows, bins.gcon, hr, prow, slot, gb, gm, np,
-                                                                lane, ctr, acc);
-            if (THIN ? gt < ge : gm < gt)
-                fwd_s_groups<FN, D, CB, NPH, HBX, true, THIN>(bins.sub_ent, grows, bins.gcon, hr, prow, slot,
-                                                              THIN ? gt : gm, THIN ? ge : gt, np, lane, ctr, acc);
+            fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
+            if (gm < gt)
+                fwd_s_groups<FN, D, CB, NPH, HBX, true>(bins.sub_ent, grows, hr, prow, slot, gm, gt, np, lane, ctr, acc);
             float x[64];
 #pragma unroll
             for (int i = 0; i < 64; ++i) x[i] = 0.0f;
@@ -709,7 +661,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
             const int slot = lane / UC, comp = lane - slot * UC;
             const int j = ps + slot, ui = comp / CB, ch = comp - ui * CB;
             if (lane < NS * UC && j >= lo && j < hi && ch < nch) {
-                store_unique<FN, D, THIN>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
+                store_unique<FN, D, false>(outs, bins.sorted_sid[j], ui, C, cbase + ch, sum);
             }
         }
     }
@@ -759,7 +711,7 @@ __device__ __forceinline__ void fwd_accumulate(const Bins &bins, const float *__
         if (!(e & kSlow)) {
             G = fast_prob<D, float>(X, &r[D]);
         } else {
-            const bool lit = (e & (kUnsafe | kThin)) != 0;  // the reference-literal power
+            const bool lit = (e & kUnsafe) != 0;  // the reference-literal power
             if (lit) {
                 const float4 cr = sload(&crows[id]);
                 c[0] = cr.x; c[1] = cr.y; c[2] = cr.z;
@@ -875,18 +827,11 @@ __device__ __forceinline__ void fwd_mx_groups(const Bins &bins, const float *__r
         for (int t = 0; t < 4; ++t) {
             bool act = e0 + 4 * t + kq < ee;
             float sh[2] = {0.0f, 0.0f};
-            bool thin = false;
-            float cl[3] = {0.0f, 0.0f, 0.0f};
             if constexpr (FLAGGED) {
                 act = act && !(ent[t] & kUnsafe);  // unsafe conics: the tail pass
                 if (act && (ent[t] & kGeneral)) {
 #pragma unroll
                     for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(hd[t][d] - ctr[d]);
-                }
-                thin = D == 2 && act && (ent[t] & kThin);  // the literal-order exponent (lit_prob)
-                if (thin) {
-                    const float4 q = bins.gcon[ent[t] & kIdMask];
-                    cl[0] = q.x; cl[1] = q.y; cl[2] = q.z;
                 }
             }
             float c[3];
@@ -899,9 +844,7 @@ __device__ __forceinline__ void fwd_mx_groups(const Bins &bins, const float *__r
                     X[0] = X[0] - sh[0];
                     if constexpr (D == 2) X[1] = X[1] - sh[1];
                 }
-                float G;
-                if constexpr (FLAGGED && D == 2) G = thin ? lit_prob<float>(X, cl) : fast_prob<D, float>(X, &hd[t][D]);
-                else G = fast_prob<D, float>(X, &hd[t][D]);
+                const float G = fast_prob<D, float>(X, &hd[t][D]);
                 float tu[U][1];
 #pragma unroll
                 for (int u = 0; u < U; ++u) tu[u][0] = 0.0f;
@@ -975,8 +918,7 @@ __global__ __launch_bounds__(kBlock) void k_forward_mx(const char *__restrict__ 
 
 // ------------------------------------------------------------------ backward kernel
 // MODE 0: fast path; 1: plus the lane's constant torus-wrap shift sh (kGeneral entries);
-// 2: the fully general per-pair path (some lane has a kUnsafe entry); 3: mode 1 with the
-// exponent in the reference's order from the raw conic (some lane has a kThin entry, lit_prob).
+// 2: the fully general per-pair path (some lane has a kUnsafe entry).
 template <int FN, int D, int CB, int MODE, typename V>
 __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const float *sh,
                                            const float *c, const float *kk, const float *v,
@@ -988,18 +930,15 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) dl[a][ch] = srow[D + a * CB + ch];
     V X[2] = {m[0] - srow[0], D == 2 ? m[1] - srow[1] : bc<V>(0.0f)};
-    if constexpr (MODE == 1 || MODE == 3) {
+    if constexpr (MODE == 1) {
         X[0] = X[0] - sh[0];
         if constexpr (D == 2) X[1] = X[1] - sh[1];
     }
     if constexpr (FN == 0 && D == 2 && CB == 1 && MODE != 2 && DGS_QFORM && DGS_VFACTOR) {
         // gaussian, C = 1: the exponent from the quadratic monomials q = (X0^2, X0 X1, X1^2)
-        // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16 (mode 3:
-        // the exponent in the reference's order instead, the same moments)
+        // that the conic moments need anyway -- 15 packed ops per two pairs instead of 16
         const V q0 = X[0] * X[0], q1 = X[0] * X[1], q2 = X[1] * X[1];
-        V e;
-        if constexpr (MODE == 3) e = lit_prob<V>(X, c);
-        else e = vexp2(vfma(bc<V>(kk[2]), q2, vfma(bc<V>(kk[1]), q1, kk[0] * q0)));
+        const V e = vexp2(vfma(bc<V>(kk[2]), q2, vfma(bc<V>(kk[1]), q1, kk[0] * q0)));
         const V t = e * dl[0][0];
         V *gm = acc, *gv = acc + 2, *gc = acc + 3;
         gv[0] += t;
@@ -1012,7 +951,6 @@ __device__ __forceinline__ void bwd_sample(const V *srow, const float *m, const 
     }
     V G;
     if constexpr (MODE == 2) G = general_prob<FN, D>(X, c, kk, wrap, unsafe);
-    else if constexpr (MODE == 3 && D == 2) G = lit_prob<V>(X, c);
     else G = fast_prob<D, V>(X, kk);
     if constexpr (bwd_mom<FN, D, CB>()) bwd_mom_terms<FN, V>(X, c, G, &srow[D], acc);
     else bwd_terms<FN, D, CB, V>(X, c, G, v, dl, acc, acc + 2, acc + 2 + CB);
@@ -1123,7 +1061,7 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     using V = typename std::conditional<pair_rows<FN, D, CB>(), f2, float>::type;
     constexpr int B = Tr::GBASE;
     const bool wrap = (ent & kGeneral) != 0;
-    const bool unsafe = (ent & (kUnsafe | kThin)) != 0;  // (mode 2: the literal power for both)
+    const bool unsafe = (ent & kUnsafe) != 0;  // (mode 2: the literal power)
     const float c[3] = {cr.x, cr.y, cr.z};
     const float m[2] = {r[0], D == 2 ? r[1] : 0.0f};
     // register accumulators: [gm(2) gv(CB) gc(3)], or the kMomAcc sums of the moment form
@@ -1134,14 +1072,6 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
     float sh[2] = {0.0f, 0.0f};
     if (__any(active && (ent & kUnsafe))) {
         bwd_loop<FN, D, CB, 2, V>(sb, se, srows, m, sh, c, &r[D], &r[B], wrap, unsafe, ra);
-    } else if (D == 2 && __any(active && (ent & kThin))) {
-        if (active && wrap) {
-            float ctr[2];
-            cell_center<D>(bins, cell, ctr);
-#pragma unroll
-            for (int d = 0; d < D; ++d) sh[d] = wrap_shift_f(m[d] - ctr[d]);
-        }
-        bwd_loop<FN, D, CB, 3, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     } else if (__any(active && wrap)) {
         if (active && wrap) {
             float ctr[2];
@@ -1550,9 +1480,9 @@ static int run_forward(const Call &a) {
     const unsigned sub_blocks = unit_blocks(a.gb, a.gbytes, a.sb, a.sbytes, false, kWavesPerBlock, true);
     constexpr bool T = fwd_transposed<FN, D, CB>(), MX = !T && fwd_mfma<FN, D, CB>();
     UnitHint hint;  // without a hint (foreign buffers) the tail pass runs unconditionally
-    hint.nunsafe = hint.nthin = -1;
+    hint.nunsafe = -1;
     const bool hinted = hint_get(a.gb, a.gbytes, a.sb, a.sbytes, &hint);
-    const bool has_unsafe = !hinted || hint.nunsafe != 0, has_thin = !hinted || hint.nthin != 0;
+    const bool has_unsafe = !hinted || hint.nunsafe != 0;
     if (!binned)  // (the call-time path's tile lists, at the binning's first such call)
         if (int rc = ensure_ref_lists(a.gb, a.gbytes, a.sb, a.sbytes, a.s, a.debug)) return rc;
     for (int cbase = 0; cbase < a.C; cbase += CB) {
@@ -1570,8 +1500,7 @@ static int run_forward(const Call &a) {
         {
             KernelTimer t(0, a.s, a.opts);  // (the main pass and the thin / tail passes behind it)
             if constexpr (T && D == 2 && DGS_FWD_SUB)  // sub-cell lists (units from the sub-unit hint)
-                k_forward_s<FN, D, CB, false><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase,
-                                                                              flag);
+                k_forward_s<FN, D, CB><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else if constexpr (T)
                 k_forward_t<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C, cbase, flag);
             else if constexpr (MX)
@@ -1580,13 +1509,6 @@ static int run_forward(const Call &a) {
                 k_forward<FN, D, CB, false><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows,
                                                                           a.samples, a.outs, a.C, cbase, flag);
             DGS_LAUNCH_CHECK(a.s, a.debug);
-            if constexpr (T && D == 2) {
-                if (has_thin) {  // the kThin entries, packed with the literal-order exponent (the thin pass)
-                    k_forward_s<FN, D, CB, true><<<sub_blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, a.outs, a.C,
-                                                                                 cbase, flag);
-                    DGS_LAUNCH_CHECK(a.s, a.debug);
-                }
-            }
             if constexpr (T || MX) {
                 if (has_unsafe) {  // unsafe-conic entries, same stream: after the main pass
                     // (grid-strided over a capped grid: it exits at once when the device-side
@@ -1957,6 +1879,11 @@ extern "C" int dgs_inputs_match(int P, int D, int N, const float *means, const f
     uint32_t *flag = nullptr;
     note_internal_alloc();  // (a diagnostic: 4 bytes of stream-ordered scratch, dgs.h)
     DGS_TRY_HIP(hipMallocAsync(&flag, 4, s));
+    struct FreeGuard {  // (freed on every path, the error paths included)
+        uint32_t *p;
+        hipStream_t s;
+        ~FreeGuard() { (void)hipFreeAsync(p, s); }
+    } guard{flag, s};
     DGS_TRY_HIP(hipMemsetAsync(flag, 0, 4, s));
     rc = verify_inputs(static_cast<const char *>(binning), static_cast<const char *>(sample_binning), P, D, N,
                        means, conics, samples, flag, s, 0);
@@ -1964,7 +1891,6 @@ extern "C" int dgs_inputs_match(int P, int D, int N, const float *means, const f
     uint32_t h = 0;
     DGS_TRY_HIP(hipMemcpyAsync(&h, flag, 4, hipMemcpyDeviceToHost, s));
     DGS_TRY_HIP(hipStreamSynchronize(s));
-    DGS_TRY_HIP(hipFreeAsync(flag, s));
     *match = h ? 0 : 1;
     return DGS_OK;
 }

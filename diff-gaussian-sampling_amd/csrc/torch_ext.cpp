@@ -228,12 +228,23 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
 std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>
 PreprocessCapturableCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances, const Tensor &conics,
                          const Tensor &samples, std::vector<int> grid, std::vector<float> offset,
-                         std::vector<int64_t> capacity, const bool debug) {
+                         std::vector<int64_t> capacity, const bool debug,
+                         const c10::optional<Tensor> &status_in) {
     TORCH_CHECK(capacity.size() == 3 && capacity[0] > 0 && capacity[2] > 0 && capacity[1] >= 0,
                 "capacity must be [E > 0, Es >= 0, R > 0]");
     Tensor rdev = torch::zeros({1}, means.options().dtype(torch::kInt64));
-    Tensor status = torch::zeros({1}, means.options().dtype(torch::kInt32));
     dgs_bin_options o{};
+    o.struct_size = sizeof(dgs_bin_options);
+    Tensor status;
+    if (status_in.has_value() && status_in->defined()) {  // sticky: the caller's word, ORed into
+        status = *status_in;
+        TORCH_CHECK(status.is_cuda() && status.scalar_type() == torch::kInt32 && status.numel() == 1 &&
+                        status.is_contiguous() && status.device() == means.device(),
+                    "status must be a contiguous int32[1] tensor on the means' device");
+        o.flags = DGS_BIN_STATUS_STICKY;
+    } else {
+        status = torch::zeros({1}, means.options().dtype(torch::kInt32));
+    }
     o.capacity_E = capacity[0];
     o.capacity_Es = std::min(capacity[1], capacity[0]);
     o.capacity_R = capacity[2];
@@ -265,6 +276,7 @@ PreOut PreprocessShardedCUDA(const Tensor &means, const Tensor &values, const Te
                              std::vector<float> offset, const c10::optional<Tensor> &present_in,
                              const double sample_area, const bool debug) {
     dgs_bin_options o{};
+    o.struct_size = sizeof(dgs_bin_options);
     Tensor present;
     if (present_in.has_value() && present_in->defined()) {
         TORCH_CHECK(present_in->scalar_type() == torch::kUInt8 || present_in->scalar_type() == torch::kBool,

@@ -20,6 +20,7 @@ __all__ = [
     "sample_gaussians_third_derivative", "aggregate_neighbors", "preprocess_gaussians",
     "preprocess_aggregate", "call_debug", "cpu_deep_copy_tuple", "GaussianSampler",
     "sample_gaussians_multi", "FUNCTIONS", "preprocess_gaussians_capturable", "capacity_from",
+    "BinningStatusMonitor", "BinningOverflow",
 ]
 
 # Function names of the fused entry point (codes of dgs_function, include/dgs.h).
@@ -99,7 +100,7 @@ def preprocess_gaussians(means, values, covariances, conics, samples, debug):
 
 
 def preprocess_gaussians_capturable(means, values, covariances, conics, samples, grid, offset, capacity,
-                                    debug=False):
+                                    debug=False, status=None):
     """The graph-capturable binning (not on the reference API): no host
     synchronisation, so a training step -- re-binning after the optimizer moved the means, then the
     sample calls and the backward -- can be captured whole with torch.cuda.graph and replayed.
@@ -108,13 +109,62 @@ def preprocess_gaussians_capturable(means, values, covariances, conics, samples,
     or a first eager binning's), fixed for the captured step.  capacity = [E, Es, R]: list sizes,
     e.g. `capacity_from(binning_buffer, sample_binning_buffer)` of an eager binning.  Returns
     (num_rendered, binning_buffer, sample_binning_buffer, ranges, sample_ranges, radii, status)
-    with num_rendered (int64[1]) and status (int32[1]) ON THE DEVICE.  status != 0 after a replay:
-    the capacities were too small (bits 1, 2, 4) or the samples' grid changed (bit 8); the step's
+    with num_rendered (int64[1]) and status (int32[1]) ON THE DEVICE.  status != 0: the
+    capacities were too small (bits 1, 2, 4) or the samples' grid changed (bit 8); the step's
     outputs are then invalid (zeros) -- re-bin eagerly and re-capture with larger capacities.
+    status: None (a fresh word, overwritten per call) or a caller's int32[1] device tensor the
+    binning ORs its bits into (sticky across replays: BinningStatusMonitor.status).
     The sample calls take num_rendered only for signature parity (pass any int)."""
     args = (means, values, covariances, conics, samples, [int(g) for g in grid], [float(o) for o in offset],
-            [int(c) for c in capacity], debug)
+            [int(c) for c in capacity], debug, status)
     return call_debug(_C.preprocess_gaussians_capturable, debug, "preprocess_capturable", *args)
+
+
+class BinningOverflow(RuntimeError):
+    """A captured step's capturable binning reported a non-zero status (BinningStatusMonitor)."""
+
+
+class BinningStatusMonitor:
+    """Watches the sticky status of a captured PIGS step without a host sync inside the step.
+
+    `status` (int32[1], allocated here, outside any capture) is passed to
+    preprocess_gaussians_capturable(..., status=monitor.status), which ORs every replay's overflow
+    bits into it.  `record()` goes INSIDE the captured step, after the binning: an async copy of
+    the word into pinned host memory (a graph node).  `check()` goes after each `graph.replay()`:
+    it waits for the PREVIOUS replay only (the GPU keeps running the one just launched) and raises
+    BinningOverflow when that replay -- or any before it -- overflowed.  A step whose binning
+    overflowed has zero outputs and gradients (dgs.h), so the loop learns of it one step later at
+    most; `reset()` clears the word after an eager re-binning and re-capture."""
+
+    def __init__(self, device=None):
+        device = torch.device("cuda") if device is None else torch.device(device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=device)
+        self._host = torch.zeros(1, dtype=torch.int32).pin_memory()
+        self._prev = None
+        self.replays = 0
+
+    def record(self):
+        """Inside the captured step (after the binning): the status word -> pinned memory."""
+        self._host.copy_(self.status, non_blocking=True)
+
+    def check(self):
+        """After each replay: raises BinningOverflow if an earlier replay's binning overflowed."""
+        prev, self._prev = self._prev, torch.cuda.Event()
+        self._prev.record()
+        self.replays += 1
+        if prev is not None:
+            prev.synchronize()  # (the previous replay; the current one keeps the GPU busy)
+            st = int(self._host[0])
+            if st != 0:
+                raise BinningOverflow(f"capturable binning status {st} by replay {self.replays - 1}: "
+                                      "re-bin eagerly, widen the capacities and re-capture")
+
+    def reset(self):
+        """Clears the sticky word (after an eager re-binning and re-capture)."""
+        torch.cuda.synchronize(self.status.device)
+        self.status.zero_()
+        self._host.zero_()
+        self._prev = None
 
 
 def capacity_from(binning_buffer, sample_binning_buffer, slack=0.125):

@@ -58,6 +58,8 @@ def allreduce_grads(grads, group=None, chunks=1):
     if _world(group) == 1:
         return grads
     P = grads[0].shape[0]
+    if P == 0:  # (nothing to sum; reshape(0, -1) would raise -- ADVICE r05)
+        return grads
     cols = [g.reshape(P, -1) for g in grads]
     widths = [c.shape[1] for c in cols]
     chunks = max(1, min(int(chunks), P)) if P else 1
@@ -282,6 +284,22 @@ class SupportExchange:
         it received from owner q.  Pairs with no rows stay at capacity 0 until an exact push."""
         self.cap_send = [self.cap_of(v) if r != self.rank else 0 for r, v in enumerate(push_send)]
         self.cap_recv = [self.cap_of(v) if q != self.rank else 0 for q, v in enumerate(push_recv)]
+        # their device forms, built here (at an exact exchange, which synchronises anyway) so the
+        # sync-free push and reduce build nothing from host lists (a pageable H2D copy blocks)
+        dev = self.owner.device
+        self._caps_dev = torch.tensor(self.cap_send, dtype=torch.int64, device=dev)
+        rtot = int(sum(self.cap_recv))
+        self._slot_in = (torch.cat([torch.arange(n, device=dev) for n in self.cap_recv]) if rtot
+                         else torch.zeros(0, dtype=torch.long, device=dev))
+        self._owner_of = (torch.repeat_interleave(torch.arange(self.world, device=dev),
+                                                  torch.tensor(self.cap_recv, device=dev), output_size=rtot)
+                          if rtot else self._slot_in)
+        stot = int(sum(self.cap_send))
+        self._slot_out = (torch.cat([torch.arange(n, device=dev) for n in self.cap_send]) if stot
+                          else torch.zeros(0, dtype=torch.long, device=dev))
+        self._dest_of = (torch.repeat_interleave(torch.arange(self.world, device=dev),
+                                                 torch.tensor(self.cap_send, device=dev), output_size=stot)
+                         if stot else self._slot_out)
 
     def _counts_a2a(self, counts):
         """all-to-all of one int per rank pair (host lists in, host list out)."""
@@ -347,12 +365,15 @@ class SupportExchange:
         recv = torch.empty((sum(self.cap_send), F), dtype=G.dtype, device=G.device)
         self._a2a(recv, send, self.cap_send, self.cap_recv)
         G.masked_fill_(~self.owned[:, None], 0.0)
+        # padding slots (beyond a block's device-side count) add exact zeros: masked with where,
+        # not multiplied (0 * inf would be NaN)
+        valid = self._slot_out < pd["send_cnt"][self._dest_of]
+        recv = torch.where(valid[:, None], recv, torch.zeros((), dtype=recv.dtype, device=recv.device))
         o = 0
         for r in range(self.world):  # added in rank order: deterministic
             n = self.cap_send[r]
             if n:
-                valid = (torch.arange(n, device=G.device) < pd["send_cnt"][r]).to(G.dtype)
-                G.index_add_(0, pd["push_send_ids"][o:o + n], recv[o:o + n] * valid[:, None])
+                G.index_add_(0, pd["push_send_ids"][o:o + n], recv[o:o + n])
             o += n
         return G
 
@@ -388,7 +409,7 @@ class SupportExchange:
         bits[me] = False
         cnt = bits.sum(1)  # rows per destination (device)
         pos = torch.cumsum(bits.to(torch.int64), 1) - 1
-        caps = torch.tensor(self.cap_send, dtype=torch.int64, device=dev)
+        caps = self._caps_dev
         base = torch.cumsum(caps, 0) - caps
         tot = int(sum(self.cap_send))
         keep = bits & (pos < caps[:, None])
@@ -407,11 +428,7 @@ class SupportExchange:
         got_rows = torch.empty((rtot, F), dtype=torch.float32, device=dev)
         self._a2a(got_ids, send_ids, self.cap_recv, self.cap_send)
         self._a2a(got_rows, rows, self.cap_recv, self.cap_send)
-        slot_in = torch.cat([torch.arange(n, device=dev) for n in self.cap_recv]) if rtot else \
-            torch.zeros(0, dtype=torch.long, device=dev)
-        owner_of = torch.repeat_interleave(torch.arange(W, device=dev),
-                                           torch.tensor(self.cap_recv, device=dev)) if rtot else slot_in
-        valid = slot_in < recv_cnt[owner_of]
+        valid = self._slot_in < recv_cnt[self._owner_of]
         ids = torch.where(valid, got_ids, dummy.expand(rtot))
         o = 0
         for t, c in zip(tensors, cols):

@@ -95,8 +95,24 @@ int dgs_preprocess(int P, int D, int N, const float *means, const float *covaria
                    const float *grid_offset, float *radii, dgs_alloc_fn alloc, void *alloc_ctx,
                    int64_t *num_rendered, dgs_stream_t stream, int debug);
 
-/* Options of dgs_preprocess_ex (zero-initialise, then set what is wanted). */
+/* The ABI this header describes (dgs_version() returns it).  11: dgs_bin_options starts with
+ * struct_size and flags; dgs_binning_info writes 6 values. */
+#define DGS_ABI_VERSION 11
+
+/* dgs_bin_options.flags */
+enum {
+    /* the capturable binning ORs its status into *status_device instead of storing it: a
+     * status word allocated once, outside the captured step, then records every overflow of
+     * every replay until the caller clears it (diff_gaussian_sampling.BinningStatusMonitor) */
+    DGS_BIN_STATUS_STICKY = 1
+};
+
+/* Options of dgs_preprocess_ex (zero-initialise, set struct_size = sizeof(dgs_bin_options), then
+ * set what is wanted; a struct of another size -- a caller built against another ABI -- is
+ * refused with DGS_ERR_ARG). */
 typedef struct dgs_bin_options {
+    uint32_t struct_size;
+    uint32_t flags; /* DGS_BIN_STATUS_STICKY */
     /* device uint8[P] or NULL.  Gaussians with present[g] == 0 are left out of the binning the
      * way a det == 0 Gaussian is (radius 0, no tiles, no pairs; radii[g] = 0 and they do not
      * count in num_rendered).  A rank of a spatially sharded run bins only the rows it holds
@@ -278,9 +294,8 @@ int dgs_count_pairs(int P, int D, int N, const float *means, const float *conics
 /* Diagnostics (not on the reference API): host-known facts of a binning this process made (no
  * device work): out[0] = num_rendered R, out[1] = fine (Gaussian, cell) entries E, out[2] = the
  * entries that take the reference-literal per-pair path (conics that are not positive definite,
- * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = kThin entries (only in a
- * DGS_THIN_LITERAL build: ill-conditioned positive-definite conics, rho^2 >= 0.82, packed with
- * the unfused reference's exponent order; 0 otherwise), out[5] = sort-path entries (the
+ * wrap breakpoints, fallback cells), out[3] = fine cells, out[4] = 0 (round 4's kThin entries;
+ * the literal-order thin pass was removed in round 6), out[5] = sort-path entries (the
  * capturable binning's capacity_Es).  A capturable binning reports its capacities for R / E and
  * -1 for the device-only counts.  DGS_ERR_BUFFER for buffers this process did not bin.
  * out must hold 6 values. */

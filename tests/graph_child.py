@@ -35,8 +35,8 @@ def forward_backward(fname):
     for t in (means, values, conics):
         t.requires_grad_(True)
 
-    def step():  # (detached output: no autograd graph outlives a step -- an AccumulateGrad node
-        # kept from an eager step on another stream breaks the capture)
+    def step():  # (detached output: no autograd graph outlives a step; INTEGRATION.md §4 has the
+        # capture recipe and what is known about round 4's capture-time crash)
         out = fwd(means, values, conics, samples, R, gb, sb, rg, srg, False)
         g = torch.autograd.grad(out, (means, values, conics), dL)
         return out.detach(), g
@@ -139,6 +139,78 @@ def rebin_step(fname):
     torch.cuda.synchronize()
     assert int(st.item()) & 1, f"overflow not reported: status {int(st.item())}"
     assert torch.isfinite(out).all()
+    # other means on that binning would take the call-time path over its clamped lists: refused
+    # loudly instead (no out-of-bounds tile lists)
+    try:
+        dgs._C.sample_gaussians(means.detach() + 1e-3, values.detach(), conics.detach(), samples, 0, gb, sb, rg,
+                                srg, False)
+        torch.cuda.synchronize()
+    except RuntimeError as e:
+        assert "status" in str(e), str(e)
+    else:
+        raise AssertionError("a call-time evaluation on an overflowed binning did not raise")
+
+
+def overflow_monitor():
+    """a captured PIGS step whose binning overflows at replay k is reported by
+    BinningStatusMonitor.check() after replay k + 1 at the latest, with no host sync inside the
+    step (the sticky status word is copied to pinned memory by a node of the graph)."""
+    dev = torch.device("cuda")
+    P, N = 20000, 60000
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, 1, seed=3))
+    samples = syn.samples(N, 2, seed=9).to(dev)
+    target = torch.randn((N, 1), device=dev, generator=torch.Generator(device=dev).manual_seed(5))
+    _, gb0, sb0, _, _, _ = dgs.preprocess_gaussians(means, values, covs, conics, samples, False)
+    grid, off = dgs._C.tile_grid(samples)
+    cap = dgs.capacity_from(gb0, sb0, slack=0.25)
+    mon = dgs.BinningStatusMonitor(dev)
+    for t in (means, values, conics):
+        t.requires_grad_(True)
+
+    def step():
+        R, gb, sb, rg, srg, _, st = dgs.preprocess_gaussians_capturable(
+            means.detach(), values.detach(), covs, conics.detach(), samples, grid, off, cap, status=mon.status)
+        mon.record()
+        out = dgs.sample_gaussians(means, values, conics, samples, 0, gb, sb, rg, srg, False)
+        (out - target).square().sum().backward()
+        return st
+
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(3):
+            for t in (means, values, conics):
+                t.grad = None
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    assert int(mon.status.item()) == 0
+    for t in (means, values, conics):
+        t.grad = None
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        g_st = step()
+    assert g_st.data_ptr() == mon.status.data_ptr()
+    k = 3
+    raised_at = None
+    for it in range(k + 3):
+        if it == k:  # the Gaussians grow 4x in area in place: the captured capacity overflows
+            with torch.no_grad():
+                covs.mul_(4.0)
+                conics.mul_(0.25)
+        graph.replay()
+        try:
+            mon.check()
+        except dgs.BinningOverflow as e:
+            raised_at = it
+            print("raised:", e, flush=True)
+            break
+    assert raised_at is not None, "the overflow was never reported"
+    assert k <= raised_at <= k + 1, f"overflow at replay {k} reported at replay {raised_at}"
+    torch.cuda.synchronize()
+    assert int(mon.status.item()) & 1
+    mon.reset()
+    assert int(mon.status.item()) == 0
 
 
 def requires_binned():
@@ -168,6 +240,8 @@ if __name__ == "__main__":
         forward_backward(sys.argv[2])
     elif sys.argv[1] == "rebin_step":
         rebin_step(sys.argv[2])
+    elif sys.argv[1] == "overflow_monitor":
+        overflow_monitor()
     else:
         requires_binned()
     print("ok", flush=True)

@@ -185,3 +185,38 @@ def test_spatial_sampler_two_ranks_real_C(dgs, oracle, tmp_path):
             nz = noise[h]
             np.testing.assert_allclose(a[~nz], b[~nz], rtol=2e-5, atol=1e-6 * np.abs(refp[k]).max())
             assert np.all(np.abs(a[nz] - b[nz]) <= 2 * ADAM_LR * ADAM_STEPS), k
+
+
+def test_padded_push_and_reduce_without_host_sync(dgs):
+    """the sync-free push and the padded reduce issue no host synchronisation.
+    One process plays rank 0 of 2 strips with a device-copy stand-in for the all-to-all (no
+    process group), and the push + reduce run under torch.cuda.set_sync_debug_mode("error"): any
+    blocking H2D copy, .item() or output-size readback inside them raises."""
+    import diff_gaussian_sampling.distributed as dd
+    dev = torch.device("cuda:0")
+    P, D, C = 4000, 2, 1
+    means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, D, C, seed=7))
+    ext = torch.tensor([[-1.0, 0.0], [0.0, 1.0]], dtype=torch.float64)
+    xchg = dd.SupportExchange(means, conics, ext, rank=0)
+    assert xchg.world == 2 and xchg._padded_ok
+
+    def a2a(out, inp, out_splits, in_splits):  # (what rank 1 would send: shape-correct, device only)
+        n = min(out.numel(), inp.numel())
+        out.view(-1)[n:].zero_()
+        if n:
+            out.view(-1)[:n].copy_(inp.reshape(-1)[:n])
+
+    xchg._a2a = a2a
+    moved = means.clone()
+    torch.cuda.synchronize()
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        sent = xchg.push([moved, values], moved, conics, sync=False)
+        G = torch.randn(P, 6, device=dev)
+        xchg.reduce(G)
+    finally:
+        torch.cuda.set_sync_debug_mode("default")
+    torch.cuda.synchronize()
+    assert xchg.padded is not None and sent.is_cuda
+    assert torch.isfinite(G).all()
+    assert bool((G[~xchg.owned] == 0).all())
