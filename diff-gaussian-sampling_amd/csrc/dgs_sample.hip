@@ -643,6 +643,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
                     for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
             constexpr int HBX = DGS_FWD_LDS ? 1 : HB;
             fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
+#ifdef DGS_TIMING_TWICE
+            fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
+#endif
             if (gm < gt)
                 fwd_s_groups<FN, D, CB, NPH, HBX, true>(bins.sub_ent, grows, hr, prow, slot, gm, gt, np, lane, ctr, acc);
             float x[64];
@@ -1082,6 +1085,9 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
         bwd_loop<FN, D, CB, 1, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
     } else {
         bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
+#ifdef DGS_TIMING_TWICE  // (timing build only: the pair loop twice -- its cost by difference)
+        bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
+#endif
     }
     if constexpr (bwd_mom<FN, D, CB>()) {
         float sum[kMomAcc];
@@ -1112,6 +1118,23 @@ __host__ __device__ constexpr int esum_stride() {
     return (D + Traits<FN, D>::S + CB + 1) / 2 * 2;
 }
 
+// DGS_BWD_STAMPS builds (tuning only): per-unit wave-time sums of k_backward's phases (s_memtime,
+// lane 0 of each wave): [0] setup (unit, entry, rows landed), [1] the pair loop and the finish,
+// [2] the stores / atomics, [3] units; read back with dgs_debug_bwd_stamps.
+#ifndef DGS_BWD_STAMPS
+#define DGS_BWD_STAMPS 0
+#endif
+#if DGS_BWD_STAMPS
+constexpr int kStampCopies = 1024;  // (one word per slot took every wave's atomics: ~88 per us)
+__device__ unsigned long long g_bwd_stamps[kStampCopies][8];
+#define BWD_STAMP(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define BWD_ADD(slot, a, b) \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_bwd_stamps[blockIdx.x % kStampCopies][slot], (unsigned long long)((b) - (a)))
+#else
+#define BWD_STAMP(v)
+#define BWD_ADD(slot, a, b)
+#endif
+
 // One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
 // conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane
 // (a slot store for the sorted part, below).
@@ -1127,7 +1150,10 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
     const int64_t id = ent & kIdMask;
     const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
     float sm[2], sc[3], sv[CB];
+    BWD_STAMP(ts1);
     bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, cr, sm, sc, sv);
+    BWD_STAMP(ts2);
+    BWD_ADD(1, ts1, ts2);
     // Sort-path entries (the sorted part of the list: scattered ids, one cache line per lane and
     // atomic) store their sums in their Gaussian-major slot instead; k_bwd_esum adds them up.
     const bool slot = esums != nullptr && eb + lane >= sload(&bins.cell_gsort[cell]);
@@ -1152,6 +1178,14 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
 #pragma unroll
         for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
     }
+#if DGS_BWD_STAMPS
+#if DGS_BWD_STAMPS > 1  // (2: wait for the atomics too -- they are fire-and-forget otherwise)
+    __builtin_amdgcn_s_waitcnt(0);
+#endif
+    BWD_STAMP(ts3);
+    BWD_ADD(2, ts2, ts3);
+    if ((threadIdx.x & 63) == 0) atomicAdd(&g_bwd_stamps[blockIdx.x % kStampCopies][3], 1ull);
+#endif
 }
 
 // The lane's entry of unit u (clamped to the unit's last entry for padding lanes).
@@ -1164,7 +1198,10 @@ __device__ __forceinline__ uint32_t bwd_entry(const Bins &bins, uint2 u, int lan
 // persistent, software-pipelined form (rows of unit k + 1 in flight during unit k) measured
 // 5-15 % slower: the hardware's dynamic wave dispatch balances the uneven units better.
 template <int FN, int D, int CB>
-__global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__ gbuf,  // (5 waves per SIMD: <= 96 VGPRs)
+#ifndef DGS_BWD_WAVES
+#define DGS_BWD_WAVES 5  // (launch bound: >= 5 waves per SIMD, <= 96 VGPRs; the kernel holds 68: 7 waves)
+#endif
+__global__ __launch_bounds__(kBlock, DGS_BWD_WAVES) void k_backward(const char *__restrict__ gbuf,
                                                      const char *__restrict__ sbuf,
                                                      const float *__restrict__ grows,
                                                      const float *__restrict__ srows,
@@ -1177,10 +1214,16 @@ __global__ __launch_bounds__(kBlock, 5) void k_backward(const char *__restrict__
     const int stride = gridDim.x * kWavesPerBlock;
     const int lane = threadIdx.x & (kWave - 1);
     for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+        BWD_STAMP(ts0);
         const uint2 u = sload(&bins.bwd_units[unit]);
         const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
         load_grow<RS>(grows, ent, r);
+#if DGS_BWD_STAMPS
+        __builtin_amdgcn_s_waitcnt(0);
+        BWD_STAMP(tsl);
+        BWD_ADD(0, ts0, tsl);
+#endif
         bwd_unit<FN, D, CB>(bins, srows, acc, P, vrow0, u, ent, r, bins.gcon[ent & kIdMask], lane, esums);
     }
 }
@@ -1893,6 +1936,24 @@ extern "C" int dgs_inputs_match(int P, int D, int N, const float *means, const f
     DGS_TRY_HIP(hipStreamSynchronize(s));
     *match = h ? 0 : 1;
     return DGS_OK;
+}
+
+// Tuning hook: k_backward's phase sums of a DGS_BWD_STAMPS build (reset after reading).
+extern "C" int dgs_debug_bwd_stamps(unsigned long long *out8) {
+#if DGS_BWD_STAMPS
+    std::vector<unsigned long long> all((size_t)dgs::kStampCopies * 8, 0ull);
+    DGS_TRY_HIP(hipMemcpyFromSymbol(all.data(), HIP_SYMBOL(dgs::g_bwd_stamps), all.size() * 8));
+    for (int k = 0; k < 8; ++k) {
+        out8[k] = 0;
+        for (int c = 0; c < dgs::kStampCopies; ++c) out8[k] += all[(size_t)c * 8 + k];
+    }
+    std::fill(all.begin(), all.end(), 0ull);
+    DGS_TRY_HIP(hipMemcpyToSymbol(HIP_SYMBOL(dgs::g_bwd_stamps), all.data(), all.size() * 8));
+    return DGS_OK;
+#else
+    (void)out8;
+    return fail(DGS_ERR_ARG, "not a DGS_BWD_STAMPS build");
+#endif
 }
 
 extern "C" void dgs_timing_enable(int on) {

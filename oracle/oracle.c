@@ -457,3 +457,87 @@ void orc_count_pairs(const orc_bins *b, const float *means, const float *conics,
     *w_ref = ref;
     *w_live = live;
 }
+
+/* A-PRIORI BOUND of the exponent's evaluation order.  The reference
+ * evaluates power = -0.5 (c0 X0 X0 + c2 X1 X1) - c1 X0 X1 (forward.cu:177, 199, 223, 252;
+ * backward.cu:110 ff.) in SOME fp32 operation order: unfused (gcc), contracted by nvcc's default
+ * --fmad=true in either of its legal ways, or -- on the GPU path -- pre-scaled by log2(e) and
+ * summed with FMAs.  Every such order rounds each of the three terms through at most
+ * ORC_ORDER_OPS operations (the coefficient's scaling, two products, two sums, the final
+ * rounding), so |power_any - power_exact| <= gamma_k * M, M = 0.5|c0 X0^2| + |c1 X0 X1| +
+ * 0.5|c2 X1^2| (standard floating-point summation analysis; gamma_k = k u / (1 - k u), u = 2^-24).
+ * Every output and gradient term of the pair is exp(power) times factors that do not depend on
+ * power, so the term moves by at most |term| (exp(gamma_k M) - 1) ~ |term| gamma_k M.  The bound
+ * of an element is the sum of that over its pairs -- it depends only on the reference's
+ * expression and the inputs, not on any GPU result.  The thin-Gaussian parity tests state
+ *   |gpu - ref| <= 1e-5 |ref| + 1e-6 max|ref| + B.
+ * (At well-conditioned conics M ~ |power| and B is far below the 8c bound; cancellation at
+ * rho^2 -> 1 makes M >> |power|: there no order is "the reference's".) */
+#define ORC_ORDER_OPS 6
+
+static double pair_mag(int D, const float *X, const float *c) {
+    if (D == 1) return 0.5 * fabs((double)c[0] * X[0] * X[0]);
+    return 0.5 * fabs((double)c[0] * X[0] * X[0]) + fabs((double)c[1] * X[0] * X[1]) + 0.5 * fabs((double)c[2] * X[1] * X[1]);
+}
+
+static double order_gamma(void) {
+    const double u = ldexp(1.0, -24), k = ORC_ORDER_OPS;
+    return k * u / (1.0 - k * u);
+}
+
+/* bound[N][K][C] (double, caller zero-initialises): the forward's per-element B. */
+void orc_forward_bound(const orc_bins *b, int fn, int C, const float *means, const float *values,
+                       const float *conics, const float *samples, double *bound, int nsub, const int32_t *sub) {
+    const int D = b->D, S = D * (D + 1) / 2, K = out_comps(fn, D);
+    const double gam = order_gamma();
+    float *tmp = (float *)malloc(sizeof(float) * (size_t)K * C);
+    int count = sub ? nsub : b->N;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        double *o = bound + (int64_t)sid * K * C;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            const float *c = conics + (int64_t)g * S;
+            memset(tmp, 0, sizeof(float) * (size_t)K * C);
+            fwd_pair(fn, D, C, X, c, values + (int64_t)g * C, tmp); /* this pair's terms */
+            const double e = expm1(gam * pair_mag(D, X, c));
+            for (int k = 0; k < K * C; ++k) o[k] += fabs((double)tmp[k]) * e;
+        }
+    }
+    free(tmp);
+}
+
+/* The gradients' per-element B (dmeans[P][D], dvalues[P][C], dconics[P][S], double, caller
+ * zero-initialises): the same per-pair rule over the pair's float gradient terms. */
+void orc_backward_bound(const orc_bins *b, int fn, int C, const float *means, const float *values,
+                        const float *conics, const float *samples, const float *dL_dout, double *dmeans,
+                        double *dvalues, double *dconics, int nsub, const int32_t *sub) {
+    const int D = b->D, S = D * (D + 1) / 2, K = out_comps(fn, D);
+    const double gam = order_gamma();
+    double *tv = (double *)malloc(sizeof(double) * (size_t)C);
+    int count = sub ? nsub : b->N;
+    for (int q = 0; q < count; ++q) {
+        int sid = sub ? sub[q] : q;
+        uint32_t t = (uint32_t)b->skey[sid];
+        if (t >= (uint32_t)b->T) continue;
+        const float *dL = dL_dout + (int64_t)sid * K * C;
+        for (int64_t j = b->gstart[t]; j < b->gstart[t + 1]; ++j) {
+            int g = b->glist[j];
+            float X[2];
+            displacement(D, means + (int64_t)g * D, samples + (int64_t)sid * D, X);
+            const float *c = conics + (int64_t)g * S;
+            double tm[2] = {0.0, 0.0}, tc[3] = {0.0, 0.0, 0.0};
+            memset(tv, 0, sizeof(double) * (size_t)C);
+            bwd_pair64(fn, D, C, X, c, values + (int64_t)g * C, dL, tm, tv, tc); /* this pair's terms */
+            const double e = expm1(gam * pair_mag(D, X, c));
+            for (int k = 0; k < D; ++k) dmeans[(int64_t)g * D + k] += fabs(tm[k]) * e;
+            for (int k = 0; k < C; ++k) dvalues[(int64_t)g * C + k] += fabs(tv[k]) * e;
+            for (int k = 0; k < S; ++k) dconics[(int64_t)g * S + k] += fabs(tc[k]) * e;
+        }
+    }
+    free(tv);
+}

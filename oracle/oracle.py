@@ -52,6 +52,8 @@ def _load(model="nocontract"):
     lib.orc_forward.argtypes = [P, i32, i32, P, P, P, P, P, i32, P]
     lib.orc_backward.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
     lib.orc_backward64.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
+    lib.orc_forward_bound.argtypes = [P, i32, i32, P, P, P, P, P, i32, P]
+    lib.orc_backward_bound.argtypes = [P, i32, i32, P, P, P, P, P, P, P, P, i32, P]
     lib.orc_count_pairs.argtypes = [P, P, P, P, ctypes.c_double, i32, P, P, P]
     lib.orc_tile_grid.argtypes = [i32, i32, P, P, P]
     lib.orc_agg_counts.argtypes = [i32, i32, P, P, P]
@@ -180,6 +182,32 @@ class OracleBins:
         (lib.orc_backward64 if exact else lib.orc_backward)(self._h, FUNCTIONS[function], C, _ptr(m), _ptr(v), _ptr(c), _ptr(s),
                          _ptr(dL), _ptr(dm), _ptr(dv), _ptr(dc),
                          0 if sub is None else len(sub), _ptr(sub))
+        return dm, dv, dc
+
+    def order_bound(self, function, values, conics, dL_dout=None, subset=None):
+        """The a-priori bound of the exponent's evaluation order (oracle.c orc_forward_bound /
+        orc_backward_bound): per output element, sum over its pairs of |term| x
+        (exp(gamma_6 M) - 1), M = 0.5|c0 X0^2| + |c1 X0 X1| + 0.5|c2 X1^2|.  Returns the forward's
+        [N, K, C] bound, or with dL_dout the gradients' (dmeans, dvalues, dconics) bounds; float64."""
+        lib = self._lib
+        v = _f32(values)
+        c = _f32(conics)
+        C = v.shape[1]
+        sub = None if subset is None else np.ascontiguousarray(subset, dtype=np.int32)
+        ns = 0 if sub is None else len(sub)
+        if dL_dout is None:
+            K = out_components(function, self.D)
+            out = np.zeros((self.N, K, C), np.float64)
+            lib.orc_forward_bound(self._h, FUNCTIONS[function], C, _ptr(self.means), _ptr(v), _ptr(c),
+                                  _ptr(self.samples), _ptr(out), ns, _ptr(sub))
+            return out
+        S = self.D * (self.D + 1) // 2
+        dL = _f32(dL_dout).reshape(self.N, -1)
+        dm = np.zeros((self.P, self.D), np.float64)
+        dv = np.zeros((self.P, C), np.float64)
+        dc = np.zeros((self.P, S), np.float64)
+        lib.orc_backward_bound(self._h, FUNCTIONS[function], C, _ptr(self.means), _ptr(v), _ptr(c),
+                               _ptr(self.samples), _ptr(dL), _ptr(dm), _ptr(dv), _ptr(dc), ns, _ptr(sub))
         return dm, dv, dc
 
     def count_pairs(self, conics, thr=-104.0, subset=None):

@@ -11,7 +11,8 @@ profiles/r05_contraction.json):
     are identical in every model -- only radii move, by ulps;
   * outside thin Gaussians the models' float outputs stay well inside the 8c bound;
   * for thin Gaussians (rho^2 >= 0.82) they do not: the spread exceeds the bound, which is why
-    tests/test_gpu_parity.py states a spread-based bound there.
+    tests/test_gpu_parity.py states the 8c bound plus the a-priori exponent-order bound there
+    (oracle.c orc_forward_bound / orc_backward_bound) -- and the models fall inside THAT bound.
 """
 import os
 
@@ -94,6 +95,34 @@ def test_thin_spread_exceeds_bound(oracle):
         b = oracle.OracleBins(means, covs, samples, model=m)
         worst = max(worst, margin_of(b.forward("gaussian", values, conics, subset=sub)[sub], f0, 1e-5, 1e-6))
     assert worst > 1.0, worst
+
+
+@pytest.mark.parametrize("function", ["gaussian", "third"])
+def test_thin_models_within_apriori_bound(oracle, function):
+    """The a-priori exponent-order bound (the thin stated bound of test_gpu_parity.py, computed
+    from the reference's expression alone) holds the reference's own contraction models: every
+    fmad / fmad_alt output and exact-sum gradient is within 1e-5 |ref| + 1e-6 max|ref| + B of the
+    unfused model on cases.thin_case, where they are 1-7x the plain 8c bound apart."""
+    means, values, covs, conics, samples = (t.numpy() for t in cases.thin_case())
+    N = samples.shape[0]
+    K = 1 if function == "gaussian" else 8
+    dL = syn.grad_out(N, K, 1, seed=5).numpy()
+    b0 = oracle.OracleBins(means, covs, samples)
+    sub = np.nonzero(b0.sample_keys() < b0.T)[0][:6000].astype(np.int32)
+    f0 = b0.forward(function, values, conics, subset=sub)[sub]
+    g0 = b0.backward(function, values, conics, dL, subset=sub, exact=True)
+    fb = b0.order_bound(function, values, conics, subset=sub)[sub]
+    gb = b0.order_bound(function, values, conics, dL, subset=sub)
+    plain = 0.0
+    for m in MODELS:
+        b = oracle.OracleBins(means, covs, samples, model=m)
+        f = b.forward(function, values, conics, subset=sub)[sub]
+        plain = max(plain, margin_of(f, f0, 1e-5, 1e-6))
+        assert margin_of(f, f0, 1e-5, 1e-6, fb) < 0.5, m
+        for a, r, bb in zip(b.backward(function, values, conics, dL, subset=sub, exact=True), g0, gb):
+            plain = max(plain, margin_of(a, r, 1e-5, 1e-6))
+            assert margin_of(a, r, 1e-5, 1e-6, bb) < 0.5, m
+    assert plain > 1.0, plain  # (the bound is needed: the plain 8c bound does not hold them)
 
 
 def test_det_zero_decisions(oracle):

@@ -13,7 +13,7 @@ import torch
 
 from diff_gaussian_sampling import synthetic as syn
 import cases
-from helpers import close, model_spread, spread_scale
+from helpers import close, margin_of, model_distances, order_bounds, record_margin
 
 pytestmark = pytest.mark.gpu
 
@@ -34,23 +34,31 @@ def _run(dgs, functions, means, values, covs, conics, samples, dLs):
     return [o.cpu().numpy() for o in outs], [g.cpu().numpy() for g in grads]
 
 
-def _check(dgs, oracle, functions, means, values, covs, conics, samples, seed=7, spread=False):
-    """spread: the thin Gaussians' stated bound (helpers.THIN_SPREAD_FACTOR, test_gpu_parity.py)."""
+def _check(dgs, oracle, functions, means, values, covs, conics, samples, seed=7, apriori=False):
+    """apriori: the thin Gaussians' stated bound -- the 8c bound plus the a-priori exponent-order
+    bound (helpers.order_bounds, test_gpu_parity.py)."""
     N, D, C = samples.shape[0], samples.shape[1], values.shape[1]
     dLs = [syn.grad_out(N, syn.out_components(f, D), C, seed=seed + i) for i, f in enumerate(functions)]
     outs, grads = _run(dgs, functions, means, values, covs, conics, samples, dLs)
     ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
-    sc = spread_scale(model_spread(oracle, functions, means, values, covs, conics, samples, dLs)) if spread else {}
+    bounds = order_bounds(ob, functions, values, conics, dLs) if apriori else {}
+    models = model_distances(oracle, functions, means, values, covs, conics, samples, dLs, bounds) if apriori else None
     ref_g = None
     for f, o, dL in zip(functions, outs, dLs):
         ref = ob.forward(f, values.numpy(), conics.numpy())
-        k = sc.get(f"{f} forward", 1.0)
-        close(o.reshape(N, -1, C), ref, RTOL * k, ATOL_FWD * k, f"multi {functions} {f} forward")
+        if apriori:
+            record_margin(f"multi {f} forward [gpu vs fmad, 8c + a-priori bound]",
+                          margin_of(o.reshape(N, -1, C), models["fmad"][0][f], RTOL, ATOL_FWD, bounds[f"{f} forward"]),
+                          RTOL, ATOL_FWD, int(ref.size))
+        close(o.reshape(N, -1, C), ref, RTOL, ATOL_FWD, f"multi {functions} {f} forward", bounds.get(f"{f} forward"))
         g = ob.backward(f, values.numpy(), conics.numpy(), dL.numpy(), exact=True)
         ref_g = list(g) if ref_g is None else [a + b for a, b in zip(ref_g, g)]
-    for name, got, ref in zip(("means", "values", "conics"), grads, ref_g):
-        k = sc.get(f"d{name}", 1.0)
-        close(got, ref, RTOL * k, ATOL_BWD * k, f"multi {functions} dL/d{name}")
+    for i, (name, got, ref) in enumerate(zip(("means", "values", "conics"), grads, ref_g)):
+        if apriori:
+            record_margin(f"multi d{name} [gpu vs fmad, 8c + a-priori bound]",
+                          margin_of(got, models["fmad"][1][i], RTOL, ATOL_BWD, bounds[f"d{name}"]), RTOL, ATOL_BWD,
+                          int(ref.size))
+        close(got, ref, RTOL, ATOL_BWD, f"multi {functions} dL/d{name}", bounds.get(f"d{name}"))
 
 
 @pytest.mark.parametrize("functions", MULTI, ids=lambda f: "+".join(x[:3] for x in f))
@@ -72,7 +80,7 @@ def test_multi_edge_and_seam(dgs, oracle, functions):
 def test_multi_thin_anisotropic(dgs, oracle, functions):
     """Thin rotated Gaussians (cases.thin_case): the fused moment-form backward and the fused
     forward next to the reference-literal path of the ill-conditioned conics."""
-    _check(dgs, oracle, functions, *cases.thin_case(P=3000, n=20000), seed=51, spread=True)
+    _check(dgs, oracle, functions, *cases.thin_case(P=3000, n=20000), seed=51, apriori=True)
 
 
 def test_multi_order_and_fallback(dgs, oracle):

@@ -11,11 +11,14 @@ recorded when $DGS_MARGINS is set (profiles/r0N_margins.json).
 
 Every case also records how far the reference itself moves under nvcc's default FMA contraction
 (--fmad=true: the oracle's "fmad" model, oracle/oracle.c) as "[reference fmad vs no-contract]".
-Thin Gaussians (rho^2 >= 0.82) are where that spread exceeds the 8c bound (1-4x forward, 4-17x
-gradients: profiles/r05_contraction.json), so no operation order is the reference's there; their
-stated bound (spread=True) is: within THIN_SPREAD_FACTOR (3) times the larger of the two
-contraction models' distances from the unfused model, never tighter than the 8c bound.  The
-GPU's fast-path order measured 1-2.6x that spread (profiles/r05_margins.json).
+Thin Gaussians (rho^2 >= 0.82) are where that spread exceeds the 8c bound (1-7x: cancellation in
+the exponent's sum), so no operation order is the reference's there.  Their stated bound
+(apriori=True) is the 8c bound PLUS the a-priori bound of the exponent's evaluation order
+(helpers.py, oracle.c orc_forward_bound / orc_backward_bound):
+    |gpu - ref| <= 1e-5 |ref| + 1e-6 max|ref| + sum over the element's pairs of |term| gamma_6 M,
+M = 0.5|c0 X0^2| + |c1 X0 X1| + 0.5|c2 X1^2|, computed from the reference's expression and the
+inputs alone (no tunable factor, no GPU data).  The GPU's distance from the contracted model is
+recorded too, since nvcc's default build contracts (setup.py:30).
 """
 import numpy as np
 import pytest
@@ -23,8 +26,7 @@ import torch
 
 from diff_gaussian_sampling import synthetic as syn
 import cases
-from helpers import (FUNCS, THIN_SPREAD_FACTOR, close, close_grad, gpu_run, margin_of, record_margin,
-                     ref_ranges_bytes)
+from helpers import FUNCS, close, close_grad, gpu_run, margin_of, record_margin, ref_ranges_bytes
 
 pytestmark = pytest.mark.gpu
 
@@ -38,29 +40,33 @@ ATOL_BWD = 1e-6  # rtol 1e-5 + atol 1e-6 max|ref|
 ATOL_BWD_CLUSTERED = 4e-6
 
 
-def _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ref_grads, models):
-    """Margins (units of the 8c bound) of the contraction models' forward and exact-sum gradients
-    from the unfused model's, recorded as "[reference <model> vs no-contract]"; returns the
-    largest over `models` per output."""
-    worst = {}
+def _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ref_grads, models,
+                  bounds):
+    """Margins of the contraction models' forward and exact-sum gradients from the unfused model's,
+    recorded in units of the 8c bound ("[reference <model> vs no-contract]") and, with `bounds`,
+    of the stated thin bound; returns {model: {output name: array}}."""
+    outs = {}
     for model in models:
         ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy(), model=model)
         out = ob.forward(function, values.numpy(), conics.numpy(), subset=subset)
         if subset is not None:
             out = out[subset]
         grads = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
+        outs[model] = dict(zip(("forward", "dmeans", "dvalues", "dconics"), [out] + list(grads)))
         for name, a, b in [("forward", out, ref_out)] + list(zip(("dmeans", "dvalues", "dconics"), grads, ref_grads)):
-            mg = margin_of(a, b, RTOL, ATOL_FWD if name == "forward" else ATOL_BWD)
-            record_margin(f"{function} {name} [reference {model} vs no-contract]", mg, RTOL, ATOL_FWD, int(np.size(b)))
-            worst[name] = max(worst.get(name, 0.0), mg)
-    return worst
+            atol = ATOL_FWD if name == "forward" else ATOL_BWD
+            record_margin(f"{function} {name} [reference {model} vs no-contract]", margin_of(a, b, RTOL, atol), RTOL,
+                          atol, int(np.size(b)))
+            if bounds:
+                record_margin(f"{function} {name} [reference {model} vs no-contract, 8c + a-priori bound]",
+                              margin_of(a, b, RTOL, atol, bounds[name]), RTOL, atol, int(np.size(b)))
+    return outs
 
 
 def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, subset=None,
-                atol_fwd=ATOL_FWD, atol_bwd=ATOL_BWD, spread=False, stated=None):
-    """Runs every check and reports all failures together.  spread: thin Gaussians' stated bound
-    (module docstring) -- each output within max(1, THIN_SPREAD_FACTOR x the contraction models'
-    spread) bounds."""
+                atol_fwd=ATOL_FWD, atol_bwd=ATOL_BWD, apriori=False, stated=None):
+    """Runs every check and reports all failures together.  apriori: thin Gaussians' stated bound
+    (module docstring) -- the 8c bound plus the a-priori exponent-order bound per element."""
     ob = oracle.OracleBins(means.numpy(), covs.numpy(), samples.numpy())
     res = gpu_run(dgs._C, function, means, values, covs, conics, samples, dL)
     errors = []
@@ -89,19 +95,34 @@ def _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL,
         got, ref_out = got[subset], ref_out[subset]
     lit = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)
     ex = ob.backward(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset, exact=True)
-    wide = _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ex,
-                         ("fmad", "fmad_alt") if spread else ("fmad",))
-    scale = {k: max(1.0, THIN_SPREAD_FACTOR * v) if spread else 1.0 for k, v in wide.items()}
-    if stated:  # a fixed stated bound per output (units of the 8c bound), tighter than the spread
-        scale = {k: float(stated.get(k, 1.0)) for k in scale}
-    if spread or stated:  # the GPU's own distance in units of the plain 8c bound, next to the stated one
-        for name, a, b in [("forward", got, ref_out)] + list(zip(("dmeans", "dvalues", "dconics"), res["grads"], ex)):
+    bounds = {}
+    if apriori:
+        fb = ob.order_bound(function, values.numpy(), conics.numpy(), subset=subset)
+        bounds["forward"] = fb if subset is None else fb[subset]
+        bounds.update(zip(("dmeans", "dvalues", "dconics"),
+                          ob.order_bound(function, values.numpy(), conics.numpy(), dL.numpy(), subset=subset)))
+    models = _model_spread(oracle, function, means, values, covs, conics, samples, dL, subset, ref_out, ex,
+                           ("fmad", "fmad_alt") if apriori else ("fmad",), bounds)
+    scale = {k: float(stated.get(k, 1.0)) if stated else 1.0 for k in ("forward", "dmeans", "dvalues", "dconics")}
+    gpu = dict(zip(("forward", "dmeans", "dvalues", "dconics"), [got] + list(res["grads"])))
+    refs = dict(zip(("forward", "dmeans", "dvalues", "dconics"), [ref_out] + list(ex)))
+    if apriori or stated:  # the GPU's own distances: plain 8c bound, stated bound, from the contracted model
+        for name in gpu:
+            a, b = gpu[name], refs[name]
             record_margin(f"{function} {name} [gpu vs no-contract, plain 8c bound; stated x{scale[name]:.2f}]",
                           margin_of(a, b, RTOL, ATOL_FWD), RTOL, ATOL_FWD, int(np.size(b)))
-    attempt(close, got, ref_out, RTOL * scale["forward"], atol_fwd * scale["forward"], f"{function} forward")
+            if apriori:
+                record_margin(f"{function} {name} [gpu vs no-contract, 8c + a-priori bound]",
+                              margin_of(a, b, RTOL, ATOL_FWD, bounds[name]), RTOL, ATOL_FWD, int(np.size(b)))
+                record_margin(f"{function} {name} [gpu vs fmad, 8c + a-priori bound]",
+                              margin_of(a, models["fmad"][name], RTOL, ATOL_FWD, bounds[name]), RTOL, ATOL_FWD,
+                              int(np.size(b)))
+    attempt(close, got, ref_out, RTOL * scale["forward"], atol_fwd * scale["forward"], f"{function} forward",
+            bounds.get("forward"))
     # backward
     for got, e, l, name in zip(res["grads"], ex, lit, ("dmeans", "dvalues", "dconics")):
-        attempt(close_grad, got, e, l, RTOL * scale[name], atol_bwd * scale[name], f"{function} dL/{name}")
+        attempt(close_grad, got, e, l, RTOL * scale[name], atol_bwd * scale[name], f"{function} dL/{name}",
+                bounds.get(name))
     assert not errors, "\n".join(errors)
     return res, ob
 
@@ -132,11 +153,11 @@ def test_parity_thin_anisotropic(dgs, oracle, function, C):
     """Thin rotated Gaussians near the seams (cases.thin_case): the sub-cell lists' slices and
     the per-row cut ranges at high anisotropy, forward and backward against the oracle; C = 3 and
     16 take the lane-per-sample / matrix-core forwards and the literal backward terms.  Stated
-    bound: the reference's own contraction spread (module docstring, spread=True)."""
+    bound: the 8c bound plus the a-priori exponent-order bound (module docstring, apriori=True)."""
     means, values, covs, conics, samples = cases.thin_case(C=C)
     K = syn.out_components(function, 2)
     dL = syn.grad_out(samples.shape[0], K, C, seed=152)
-    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, spread=True)
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, apriori=True)
 
 
 @pytest.mark.parametrize("function,C", [("gaussian", 1), ("third", 1), ("derivative", 5)])
@@ -176,12 +197,12 @@ def test_parity_unculled_many(dgs, oracle, function):
     bound except dmeans, stated at 8x it: the third past kRho2Max (amplification up to ~2e4)
     cancels in its mean gradient, 3.7x the bound measured on MI355X.  (The contraction models
     differ by up to ~1e4x the bound on this case -- non-PD conics flip `power > 0` skips -- so
-    the spread-based thin bound would not constrain anything here; the literal path follows the
-    unfused reference, whose skip decisions the GPU reproduces.)"""
+    no exponent-order bound would constrain anything here; the literal path follows the unfused
+    reference, whose skip decisions the GPU reproduces.)"""
     means, values, covs, conics, samples = cases.unculled_case()
     K = syn.out_components(function, 2)
     dL = syn.grad_out(samples.shape[0], K, 1, seed=192)
-    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL, spread=True,
+    _check_case(dgs, oracle, function, means, values, covs, conics, samples, dL,
                 stated={"forward": 1.0, "dmeans": 8.0, "dvalues": 1.0, "dconics": 1.0})
 
 
