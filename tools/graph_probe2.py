@@ -17,7 +17,7 @@ inside torch.cuda.graph.  One scenario per process:
                           buffers), then dgs_recipe's capture
 
 Prints "<scenario>: ok" (plus the max gradient difference replay vs eager) on success.
-tools/gpu_graph_probe.sh runs them from the safest to the riskiest and stops at a crash.
+tools/gpu.sh graph runs them from the safest to the riskiest and stops at a crash.
 """
 import os
 import sys

@@ -1,4 +1,4 @@
-"""One warm preprocess call's kernel timeline from a rocprofv3 kernel trace (tools/gpu_r04.sh's
+"""One warm preprocess call's kernel timeline from a rocprofv3 kernel trace (tools/gpu.sh (round 4: tools/gpu_r04.sh, in git history)'s
 profprep): start, gap before, duration per kernel, and the busy sum."""
 import csv
 import sys
