@@ -223,7 +223,16 @@ __device__ __forceinline__ void cell_center(const Bins &bins, int cell, float *c
 // bound by the scalar cache's random-row throughput, tools/ubench.hip).
 
 #ifndef DGS_BWD_PIPE
-#define DGS_BWD_PIPE 1  // backward pair loop: the next batch of pair rows in flight during this one
+// backward pair loop: the next batch of pair rows in flight during this one; 2 (round 6): two
+// batch buffers in turn, no register copy of the look-ahead batch per iteration (-3 %)
+#define DGS_BWD_PIPE 2
+#endif
+#ifndef DGS_BWD_PRIO
+// backward wave priority (round 6, -1 % on top of DGS_BWD_PIPE 2): s_setprio 3 while a wave is not in
+// its pair loop -- kernel entry and header loads (3), each unit's dependent unit -> entry -> row
+// loads (1), the finish and the atomics (2) -- and 0 inside it, so a wave waiting on its setup
+// chain issues its loads ahead of the VALU-bound waves instead of behind them
+#define DGS_BWD_PRIO 3
 #endif
 #ifndef DGS_FWD_SUB
 #define DGS_FWD_SUB 1  // D = 2 transposed forward over the sub-cell lists (k_forward_s)
@@ -471,6 +480,9 @@ __device__ __forceinline__ void fwd_s_pairs(const F32s<16> (&hr)[HB], const floa
 #ifndef DGS_FWD_HB
 #define DGS_FWD_HB 2  // sub-cell forward: blocks of 4 pair rows hoisted into SGPRs for the list walk (4: SGPR spills, 2.7 % slower)
 #endif
+#ifndef DGS_FWD_PRIO
+#define DGS_FWD_PRIO 0  // tuning: s_setprio 3 for a sub unit's setup, 0 for its list walk
+#endif
 #ifndef DGS_FWD_LDS
 #define DGS_FWD_LDS 0  // sub-cell forward: the pass's pair rows staged in LDS (else hoisted into SGPRs)
 #endif
@@ -614,6 +626,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
     const int wv = threadIdx.x >> 6;
     const uint32_t slot = (uint32_t)(size_t)(lds_cf4 *)(&srows[wv][0]);  // (addrspacecast: the LDS offset)
     for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+#if DGS_FWD_PRIO
+        __builtin_amdgcn_s_setprio(3);  // (the unit's loads issue first; 0 again for the list walk)
+#endif
         const uint2 u = sload(&bins.fsub_units[unit]);
         const int sc = (int)u.x, cell = sc / kSubPerCell, sb = (int)u.y;
         const int lo = max(sb, sload(&bins.sub_sbeg[sc]));
@@ -642,6 +657,9 @@ __global__ __launch_bounds__(kBlock) void k_forward_s(const char *__restrict__ g
 #pragma unroll
                     for (int ch = 0; ch < CB; ++ch) acc[q][a][ch] = bc<f2>(0.0f);
             constexpr int HBX = DGS_FWD_LDS ? 1 : HB;
+#if DGS_FWD_PRIO
+            __builtin_amdgcn_s_setprio(0);
+#endif
             fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
 #ifdef DGS_TIMING_TWICE
             fwd_s_groups<FN, D, CB, NPH, HBX, false>(bins.sub_ent, grows, hr, prow, slot, gb, gm, np, lane, ctr, acc);
@@ -1007,7 +1025,40 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
             bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
             ++p;
         }
-        if constexpr (DGS_BWD_PIPE) {
+        if constexpr (DGS_BWD_PIPE == 2) {
+            // two batch buffers in turn (no register copy of the look-ahead batch per iteration)
+            if (p + NB <= pf) {
+                const int plast = pf - NB;
+                F32s<NB * PR> b0 = sload_f<NB * PR>(srows + (int64_t)p * PR), b1;
+                for (;;) {
+                    DGS_WAIT_LGKM0();
+                    __builtin_amdgcn_sched_barrier(0);
+                    b1 = sload_f<NB * PR>(srows + (int64_t)min(p + NB, plast) * PR);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        pair_fields<RSS, D>(&b0.v[q * PR], f, 0);
+                        bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    p += NB;
+                    if (p + NB > pf) break;
+                    DGS_WAIT_LGKM0();
+                    __builtin_amdgcn_sched_barrier(0);
+                    b0 = sload_f<NB * PR>(srows + (int64_t)min(p + NB, plast) * PR);
+                    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+                    for (int q = 0; q < NB; ++q) {
+                        pair_fields<RSS, D>(&b1.v[q * PR], f, 0);
+                        bwd_sample<FN, D, CB, MODE, V>(f, m, sh, c, kk, v, wrap, unsafe, acc);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                    p += NB;
+                    if (p + NB > pf) break;
+                }
+                DGS_WAIT_LGKM0();  // (the last look-ahead, unused)
+            }
+        } else if constexpr (DGS_BWD_PIPE) {
             // The next batch of pair rows is in flight while this one is evaluated.  Scalar loads
             // complete out of order, so each batch is waited for with lgkmcnt(0) BEFORE the next
             // one is issued; scheduling barriers keep the compiler from moving the load across.
@@ -1150,8 +1201,14 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
     const int64_t id = ent & kIdMask;
     const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
     float sm[2], sc[3], sv[CB];
+#if DGS_BWD_PRIO
+    __builtin_amdgcn_s_setprio(0);
+#endif
     BWD_STAMP(ts1);
     bwd_sums<FN, D, CB>(bins, srows, cell, sb, se, ent, active, r, cr, sm, sc, sv);
+#if DGS_BWD_PRIO > 1
+    __builtin_amdgcn_s_setprio(3);  // (2: the finish and the atomics too -- the wave's slot frees sooner)
+#endif
     BWD_STAMP(ts2);
     BWD_ADD(1, ts1, ts2);
     // Sort-path entries (the sorted part of the list: scattered ids, one cache line per lane and
@@ -1189,9 +1246,17 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
 }
 
 // The lane's entry of unit u (clamped to the unit's last entry for padding lanes).
+#ifndef DGS_BWD_ENTRY_FREE
+#define DGS_BWD_ENTRY_FREE 0  // 1: clamp to the list end E instead (no wait for cell_gend first)
+#endif
 __device__ __forceinline__ uint32_t bwd_entry(const Bins &bins, uint2 u, int lane) {
+#if DGS_BWD_ENTRY_FREE
+    // (padding lanes read the next cells' entries: valid rows, never stored -- bwd_unit's `active`)
+    return bins.entries[min((int64_t)u.y + lane, sload(&bins.h->E) - 1)];
+#else
     const int ee = min((int)u.y + kWave, sload(&bins.cell_gend[u.x]));
     return bins.entries[min((int)u.y + lane, ee - 1)];
+#endif
 }
 
 // One wave per unit (exact grid from the preprocess hint; grid-strided otherwise).  A
@@ -1207,6 +1272,9 @@ __global__ __launch_bounds__(kBlock, DGS_BWD_WAVES) void k_backward(const char *
                                                      const float *__restrict__ srows,
                                                      float *__restrict__ acc, int P, int vrow0,
                                                      const uint32_t *__restrict__ dirty, float *__restrict__ esums) {
+#if DGS_BWD_PRIO > 2
+    __builtin_amdgcn_s_setprio(3);  // (3: from the kernel's entry, its header loads included)
+#endif
     if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
     constexpr int RS = grow_stride<FN, D, CB>();
     const Bins bins = resolve(gbuf, sbuf);
@@ -1215,6 +1283,9 @@ __global__ __launch_bounds__(kBlock, DGS_BWD_WAVES) void k_backward(const char *
     const int lane = threadIdx.x & (kWave - 1);
     for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
         BWD_STAMP(ts0);
+#if DGS_BWD_PRIO
+        __builtin_amdgcn_s_setprio(3);  // (the unit's loads issue first; bwd_unit drops it again)
+#endif
         const uint2 u = sload(&bins.bwd_units[unit]);
         const uint32_t ent = bwd_entry(bins, u, lane);
         float r[RS];
