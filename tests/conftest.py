@@ -4,7 +4,8 @@ import sys
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PKG_ROOT = os.path.join(REPO, "diff-gaussian-sampling_amd")
+# (DGS_TEST_PKG_ROOT: run the suite against a tools/variant.sh build, e.g. variants/NAME)
+PKG_ROOT = os.environ.get("DGS_TEST_PKG_ROOT") or os.path.join(REPO, "diff-gaussian-sampling_amd")
 for p in (REPO, PKG_ROOT):
     if p not in sys.path:
         sys.path.insert(0, p)
