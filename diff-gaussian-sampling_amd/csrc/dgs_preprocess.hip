@@ -1317,9 +1317,6 @@ __global__ __launch_bounds__(kBlock) void k_sub_box(int ncells, int CT, const in
 #ifndef DGS_SUBL_DEPTH
 #define DGS_SUBL_DEPTH 2  // k_sub_lists: Gaussian-row groups in flight ahead of the tested one (1: 24 us slower at the headline)
 #endif
-#ifndef DGS_SUBL_WG
-#define DGS_SUBL_WG 0  // sub lists: one 4-wave block per cell (k_sub_lists_wg) instead of one wave
-#endif
 #ifndef DGS_SUB_SLICE
 #define DGS_SUB_SLICE 1  // k_sub_lists: per-sub-row slices instead of per-sub-box minimisations
 #endif
@@ -1519,118 +1516,6 @@ __global__ __launch_bounds__(kBlock) void k_sub_lists(SubListArgs A) {
     const int c = block_unit_index() * (kBlock / kWave) + (threadIdx.x >> 6);  // (XCD remap: neighbouring cells share Gaussians)
     if (c >= A.ncells) return;
     sub_lists_wave(A, c, threadIdx.x & (kWave - 1));
-}
-
-// The same lists with one 256-thread block per cell (round 6): the single wave per cell walked
-// ~19 dependent groups (latency-bound, ~13 waves per SIMD over the launch).  Here each of the
-// four waves takes a quarter of the cell list: phase 1 tests its groups (sub_mask, the rows two
-// groups ahead) into an LDS byte per entry and counts its hits per sub list; after one barrier
-// every wave knows where its quarter lands in each sub list's [flag-free | flagged] regions, and
-// phase 2 writes its entries there in cell-list order -- the single-wave kernel's output, bit
-// for bit.  Lists longer than kSubWgMax entries take the single-wave walk (wave 0).
-constexpr int kSubWgMax = 8192;
-__global__ __launch_bounds__(kBlock) void k_sub_lists_wg(SubListArgs A) {
-    const int c = block_unit_index();
-    if (c >= A.ncells) return;
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & (kWave - 1);
-    const int b = A.gbeg[c], m_ = A.gmid[c], e = A.gend[c], n = e - b;
-    if (n > kSubWgMax) {
-        if (w == 0) sub_lists_wave(A, c, lane);
-        return;
-    }
-    __shared__ uint8_t smask[kSubWgMax];
-    __shared__ uint32_t scnt[kWavesPerBlock][2 * kSubPerCell];
-    const int64_t base = (int64_t)kSubPerCell * b;
-    const bool work = b < e && (c % A.CT) != A.CT - 1;  // (the fallback cell: every entry is kUnsafe)
-    const int G = (n + kWave - 1) / kWave, per = (G + kWavesPerBlock - 1) / kWavesPerBlock;
-    const int jb = b + kWave * min(G, w * per), je = min(e, b + kWave * min(G, (w + 1) * per));
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
-    if (work && jb < je) {
-        const float4 bx = A.box[c];
-        const float ctr[2] = {0.5f * (bx.x + bx.z), 0.5f * (bx.y + bx.w)};  // = cell_center
-        float4 sb[kSubPerCell];
-#pragma unroll
-        for (int k = 0; k < kSubPerCell; ++k) sb[k] = A.sbox[c * kSubPerCell + k];
-        uint32_t ent_c = jb + lane < je ? A.entries[jb + lane] : kUnsafe;
-        uint32_t ent_n = jb + kWave + lane < je ? A.entries[jb + kWave + lane] : kUnsafe;
-        float2 mm_c, mm_n;
-        float4 cc_c, cc_n;
-        sub_row(ent_c, A.gmean, A.gcon, mm_c, cc_c);
-        sub_row(ent_n, A.gmean, A.gcon, mm_n, cc_n);
-        uint32_t ent_nn = jb + 2 * kWave + lane < je ? A.entries[jb + 2 * kWave + lane] : kUnsafe;
-        for (int j0 = jb; j0 < je; j0 += kWave) {
-            const int j = j0 + lane;
-            const uint32_t ent = ent_c;
-            const float2 mm = mm_c;
-            const float4 cc = cc_c;
-            ent_c = ent_n;
-            mm_c = mm_n;
-            cc_c = cc_n;
-            ent_n = ent_nn;
-            sub_row(ent_n, A.gmean, A.gcon, mm_n, cc_n);
-            ent_nn = j + 3 * kWave < je ? A.entries[j + 3 * kWave] : kUnsafe;
-            const uint32_t mask = j < je ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
-            if (j < je) smask[j - b] = (uint8_t)mask;
-            const bool ff = j < m_;
-#pragma unroll
-            for (int k = 0; k < kSubPerCell; ++k) {
-                const bool hit = (mask >> k) & 1u;
-                nff[k] += (uint32_t)__popcll(__ballot(hit && ff));
-                nfl[k] += (uint32_t)__popcll(__ballot(hit && !ff));
-            }
-        }
-    }
-    if (lane == 0)
-#pragma unroll
-        for (int k = 0; k < kSubPerCell; ++k) {
-            scnt[w][k] = nff[k];
-            scnt[w][kSubPerCell + k] = nfl[k];
-        }
-    __syncthreads();
-    uint32_t off_ff[kSubPerCell], off_fl[kSubPerCell], tff[kSubPerCell], tfl[kSubPerCell];
-#pragma unroll
-    for (int k = 0; k < kSubPerCell; ++k) {
-        uint32_t pf = 0, pl = 0, af = 0, al = 0;
-#pragma unroll
-        for (int q = 0; q < kWavesPerBlock; ++q) {
-            const uint32_t f = scnt[q][k], l = scnt[q][kSubPerCell + k];
-            if (q < w) { pf += f; pl += l; }
-            af += f;
-            al += l;
-        }
-        tff[k] = af;
-        tfl[k] = al;
-        off_ff[k] = pf;
-        off_fl[k] = af + pl;
-    }
-    if (work && jb < je) {
-        for (int j0 = jb; j0 < je; j0 += kWave) {
-            const int j = j0 + lane;
-            const uint32_t ent = j < je ? A.entries[j] : 0u;
-            const uint32_t mask = j < je ? (uint32_t)smask[j - b] : 0u;
-            const bool ff = j < m_;
-#pragma unroll
-            for (int k = 0; k < kSubPerCell; ++k) {
-                const bool hit = (mask >> k) & 1u;
-                const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
-                if (hit) {
-                    const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
-                    A.sub_ent[base + (int64_t)k * n + (ff ? off_ff[k] : off_fl[k]) + below] = ent;
-                }
-                off_ff[k] += (uint32_t)__popcll(bf);
-                off_fl[k] += (uint32_t)__popcll(bl);
-            }
-        }
-    }
-    if (threadIdx.x == 0)
-#pragma unroll
-        for (int k = 0; k < kSubPerCell; ++k) {
-            const int a = (int)(base + (int64_t)k * n);
-            A.lbeg[c * kSubPerCell + k] = a;
-            A.lmid[c * kSubPerCell + k] = a + (int)tff[k];
-            A.lend[c * kSubPerCell + k] = a + (int)(tff[k] + tfl[k]);
-            A.lthin[c * kSubPerCell + k] = a + (int)(tff[k] + tfl[k]);  // (no kThin entries)
-        }
 }
 
 // (The per-cell list sizes and layout, the forward / backward work units and the forward sub
@@ -2559,10 +2444,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         uint32_t *sub_ent = reinterpret_cast<uint32_t *>(gbuf + L.o_sub_ent);
         const SubListArgs sa{ncells,   G.CT,     cell_gbeg, cell_gmid, cell_gend, entries,  gmean,  gcon,
                              cell_box, sub_box,  sub_lbeg,  sub_lmid,  sub_lend,  sub_lthin, sub_ent};
-        if (DGS_SUBL_WG)
-            k_sub_lists_wg<<<(unsigned)ncells, kBlock, 0, s>>>(sa);
-        else
-            k_sub_lists<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(sa);
+        k_sub_lists<<<(unsigned)((ncells + kWavesPerBlock - 1) / kWavesPerBlock), kBlock, 0, s>>>(sa);
         DGS_LAUNCH_CHECK(s, debug);
         // forward sub units per sub-cell with samples and entries: (sub-cell, kSubPairs pairs)
         const int32_t *ssb = sub_sbeg, *sse = sub_send, *slb = sub_lbeg, *sle = sub_lend;
