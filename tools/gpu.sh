@@ -11,8 +11,10 @@
 #   bash tools/gpu.sh sq      TAG [ARGS...]    the SQ issue / wait counters, two passes
 #   bash tools/gpu.sh ab      TAG VARIANT...   tools/ab.py: headline and --aniso 25 medians
 #   bash tools/gpu.sh graph   TAG              the graph-capture probes (tools/graph_probe2.py)
-#   bash tools/gpu.sh final   TAG              the round's refresh: tests, smoke, every bench line
-#                                              with its trace, PMC traffic and SQ counters
+#   bash tools/gpu.sh final   TAG              the round's refresh, part 1: tests (margins) and smoke
+#   bash tools/gpu.sh lines   TAG              part 2: every bench line (headline with the PIGS graph,
+#                                              thin, config 2, call-time) with traces, PMC traffic, SQ
+#                                              counters and the 2-rank rehearsal
 # Every GPU step runs under its own timeout; the first failure ends the call.
 set -u
 cd "$GRAFT_REPO_ROOT"
@@ -92,9 +94,10 @@ case $CMD in
     sq) step_sq main "$@" ;;
     ab) step_ab "$@" ;;
     graph) step_graph ;;
-    final)
-        { step_tests; [ $? -le 1 ]; } && step_smoke \
-        && step_bench head --pigs-graph \
+    final)  # (two gpurun calls: each stays within gpurun's 20-minute limit)
+        { step_tests; [ $? -le 1 ]; } && step_smoke && echo ALLDONE ;;
+    lines)
+        step_bench head --pigs-graph \
         && step_prof head \
         && step_bench thin --aniso 25 \
         && step_prof thin --aniso 25 \
