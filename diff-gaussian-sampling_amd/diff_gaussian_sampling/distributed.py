@@ -300,6 +300,21 @@ class SupportExchange:
         self._dest_of = (torch.repeat_interleave(torch.arange(self.world, device=dev),
                                                  torch.tensor(self.cap_send, device=dev), output_size=stot)
                          if stot else self._slot_out)
+        # the padded push's one all-to-all: per (owner -> rank) pair a block of capacity + 1 rows,
+        # [count | ids and rows], so the counts, ids and rows travel in ONE collective
+        def layout(caps):
+            blk = [n + 1 if n else 0 for n in caps]
+            pos, hdr_rows, hdr_ranks, o = [], [], [], 0
+            for r, n in enumerate(caps):
+                if n:
+                    hdr_rows.append(o)
+                    hdr_ranks.append(r)
+                    pos.extend(range(o + 1, o + 1 + n))
+                o += blk[r]
+            t = lambda v: torch.tensor(v, dtype=torch.long, device=dev)  # noqa: E731
+            return blk, t(pos), t(hdr_rows), t(hdr_ranks)
+        self._pk_send_splits, self._pk_pos_send, self._pk_hdr_send, self._pk_hdr_send_ranks = layout(self.cap_send)
+        self._pk_recv_splits, self._pk_pos_recv, self._pk_hdr_recv, self._pk_hdr_recv_ranks = layout(self.cap_recv)
 
     def _counts_a2a(self, counts):
         """all-to-all of one int per rank pair (host lists in, host list out)."""
@@ -418,16 +433,21 @@ class SupportExchange:
         buf.scatter_(0, slot.reshape(-1), oi.expand(W, -1).reshape(-1))
         send_ids = buf[:tot]
         overflow = (cnt > caps).any()
-        recv_cnt = torch.empty_like(cnt)
-        self._a2a(recv_cnt, cnt, [1] * W, [1] * W)
         cols = [t.reshape(t.shape[0], -1) for t in tensors]
         F = sum(c.shape[1] for c in cols)
-        rows = torch.cat([c.index_select(0, send_ids) for c in cols], 1).float().contiguous()
         rtot = int(sum(self.cap_recv))
-        got_ids = torch.empty(rtot, dtype=torch.long, device=dev)
-        got_rows = torch.empty((rtot, F), dtype=torch.float32, device=dev)
-        self._a2a(got_ids, send_ids, self.cap_recv, self.cap_send)
-        self._a2a(got_rows, rows, self.cap_recv, self.cap_send)
+        # one collective: per destination block [count | (id, row) x capacity], ids and counts as
+        # int32 bits in the float32 column 0 (an all-to-all moves bytes)
+        pk = torch.zeros((sum(self._pk_send_splits), 1 + F), dtype=torch.float32, device=dev)
+        pk[self._pk_hdr_send, 0] = cnt.index_select(0, self._pk_hdr_send_ranks).to(torch.int32).view(torch.float32)
+        pk[self._pk_pos_send, 0] = send_ids.to(torch.int32).view(torch.float32)
+        pk[self._pk_pos_send, 1:] = torch.cat([c.index_select(0, send_ids) for c in cols], 1).float()
+        got = torch.empty((sum(self._pk_recv_splits), 1 + F), dtype=torch.float32, device=dev)
+        self._a2a(got, pk, self._pk_recv_splits, self._pk_send_splits)
+        recv_cnt = torch.zeros(W, dtype=torch.int32, device=dev)
+        recv_cnt[self._pk_hdr_recv_ranks] = got[self._pk_hdr_recv, 0].contiguous().view(torch.int32)
+        got_ids = got[self._pk_pos_recv, 0].contiguous().view(torch.int32).long()
+        got_rows = got[self._pk_pos_recv, 1:]
         valid = self._slot_in < recv_cnt[self._owner_of]
         ids = torch.where(valid, got_ids, dummy.expand(rtot))
         o = 0
