@@ -1104,6 +1104,32 @@ __device__ __forceinline__ void bwd_loop(int sb, int se, const float *__restrict
     }
 }
 
+// A lane's register sums -> its finished gradient sums (moment form or v-factored terms).
+template <int FN, int D, int CB, typename V>
+__device__ __forceinline__ void bwd_finish_sums(const V *ra, const float *c, float vB, float (&sm)[2], float (&sc)[3],
+                                                float (&sv)[CB]) {
+    if constexpr (bwd_mom<FN, D, CB>()) {
+        float sum[kMomAcc];
+#pragma unroll
+        for (int k = 0; k < kMomAcc; ++k) sum[k] = hsum(ra[k]);
+        bwd_mom_finish(c, vB, sum, sm, sc, sv[0]);
+    } else {
+        const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
+        sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
+#pragma unroll
+        for (int k = 0; k < 3; ++k) sc[k] = hsum(gc[k]);
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) sv[ch] = hsum(gv[ch]);
+        if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
+#pragma unroll
+            for (int d = 0; d < 2; ++d) sm[d] *= vB;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) sc[k] *= vB;
+        }
+        bwd_finish<FN, D>(c, sm, sc);
+    }
+}
+
 // The gradient sums of one lane's Gaussian (entry ent, row r, conic cr) over the samples
 // [sb, se) of `cell` (sorted order), finished into sm[D], sc[S], sv[CB].  The mode (fast /
 // constant wrap shift / general) is chosen for the whole wave from its active lanes' flags.
@@ -1140,26 +1166,7 @@ __device__ __forceinline__ void bwd_sums(const Bins &bins, const float *__restri
         bwd_loop<FN, D, CB, 0, V>(sb, se, srows, m, sh, c, &r[D], &r[B], false, false, ra);
 #endif
     }
-    if constexpr (bwd_mom<FN, D, CB>()) {
-        float sum[kMomAcc];
-#pragma unroll
-        for (int k = 0; k < kMomAcc; ++k) sum[k] = hsum(ra[k]);
-        bwd_mom_finish(c, r[B], sum, sm, sc, sv[0]);
-    } else {
-        const V *gm = ra, *gv = ra + 2, *gc = ra + 2 + CB;
-        sm[0] = hsum(gm[0]); sm[1] = hsum(gm[1]);
-#pragma unroll
-        for (int k = 0; k < 3; ++k) sc[k] = hsum(gc[k]);
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch) sv[ch] = hsum(gv[ch]);
-        if constexpr (FN == 0 && CB == 1 && DGS_VFACTOR) {  // v-factored moments (bwd_terms)
-#pragma unroll
-            for (int d = 0; d < 2; ++d) sm[d] *= r[B];
-#pragma unroll
-            for (int k = 0; k < 3; ++k) sc[k] *= r[B];
-        }
-        bwd_finish<FN, D>(c, sm, sc);
-    }
+    bwd_finish_sums<FN, D, CB, V>(ra, c, r[B], sm, sc, sv);
 }
 
 // The slot row width of a Gaussian's sums (k_bwd_esum): [dm(D) dc(S) dv(CB)] padded to 2 floats
@@ -1186,6 +1193,38 @@ __device__ unsigned long long g_bwd_stamps[kStampCopies][8];
 #define BWD_ADD(slot, a, b)
 #endif
 
+// A lane's finished sums for list position pos (Gaussian id): sort-path entries (the sorted part
+// of the list: scattered ids, one cache line per lane and atomic) store them in their
+// Gaussian-major slot (k_bwd_esum adds them up); the others add them with one atomic each.
+template <int FN, int D, int CB>
+__device__ __forceinline__ void bwd_store(const Bins &bins, float *__restrict__ acc, int P, int vrow0, int cell, int pos,
+                                          int64_t id, bool active, const float (&sm)[2], const float (&sc)[3],
+                                          const float (&sv)[CB], float *__restrict__ esums) {
+    constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
+    const bool slot = esums != nullptr && pos >= sload(&bins.cell_gsort[cell]);
+    if (active && slot) {
+        float row[SSW];
+#pragma unroll
+        for (int k = 0; k < SSW; ++k) row[k] = 0.0f;
+#pragma unroll
+        for (int d = 0; d < D; ++d) row[d] = sm[d];
+#pragma unroll
+        for (int k = 0; k < S; ++k) row[D + k] = sc[k];
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) row[D + S + ch] = sv[ch];
+        float2 *o = reinterpret_cast<float2 *>(esums + (int64_t)bins.esum_q[pos] * SSW);
+#pragma unroll
+        for (int k = 0; k < SSW / 2; ++k) o[k] = make_float2(row[2 * k], row[2 * k + 1]);
+    } else if (active) {
+#pragma unroll
+        for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
+#pragma unroll
+        for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
+#pragma unroll
+        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
+    }
+}
+
 // One backward unit: (cell, <= 64 entries of its list), lane = Gaussian (entry ent, row r,
 // conic cr), the cell's samples wave-uniform; one atomicAdd per gradient component per lane
 // (a slot store for the sorted part, below).
@@ -1194,7 +1233,6 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
                                          float *__restrict__ acc, int P, int vrow0, uint2 u,
                                          uint32_t ent, const float (&r)[grow_stride<FN, D, CB>()],
                                          float4 cr, int lane, float *__restrict__ esums) {
-    constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
     const int cell = (int)u.x, eb = (int)u.y;
     const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
     const bool active = eb + lane < ee;
@@ -1211,30 +1249,7 @@ __device__ __forceinline__ void bwd_unit(const Bins &bins, const float *__restri
 #endif
     BWD_STAMP(ts2);
     BWD_ADD(1, ts1, ts2);
-    // Sort-path entries (the sorted part of the list: scattered ids, one cache line per lane and
-    // atomic) store their sums in their Gaussian-major slot instead; k_bwd_esum adds them up.
-    const bool slot = esums != nullptr && eb + lane >= sload(&bins.cell_gsort[cell]);
-    if (active && slot) {
-        float row[SSW];
-#pragma unroll
-        for (int k = 0; k < SSW; ++k) row[k] = 0.0f;
-#pragma unroll
-        for (int d = 0; d < D; ++d) row[d] = sm[d];
-#pragma unroll
-        for (int k = 0; k < S; ++k) row[D + k] = sc[k];
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch) row[D + S + ch] = sv[ch];
-        float2 *o = reinterpret_cast<float2 *>(esums + (int64_t)bins.esum_q[eb + lane] * SSW);
-#pragma unroll
-        for (int k = 0; k < SSW / 2; ++k) o[k] = make_float2(row[2 * k], row[2 * k + 1]);
-    } else if (active) {
-#pragma unroll
-        for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
-#pragma unroll
-        for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
-#pragma unroll
-        for (int ch = 0; ch < CB; ++ch) atomicAdd(acc + (int64_t)(vrow0 + ch) * P + id, sv[ch]);
-    }
+    bwd_store<FN, D, CB>(bins, acc, P, vrow0, cell, eb + lane, id, active, sm, sc, sv, esums);
 #if DGS_BWD_STAMPS
 #if DGS_BWD_STAMPS > 1  // (2: wait for the atomics too -- they are fire-and-forget otherwise)
     __builtin_amdgcn_s_waitcnt(0);
