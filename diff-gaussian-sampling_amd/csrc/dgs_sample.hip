@@ -80,6 +80,7 @@ __global__ void k_pack_gauss(int P, const char *__restrict__ gbuf, const float *
 template <int FN, int D, int CB>
 __host__ __device__ constexpr bool pair_rows() { return srow_stride<FN, D, CB>() <= 16; }
 
+constexpr int kSrowPad = 16;
 template <int FN, int D, int CB>
 __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char *__restrict__ sbuf,
                                const DLs dls, int C, int cbase, float *__restrict__ rows,
@@ -91,7 +92,8 @@ __global__ void k_pack_samples(int N, const char *__restrict__ gbuf, const char 
     if (acc_zero)
         for (int64_t k = j; k < acc_n4; k += (int64_t)gridDim.x * blockDim.x) acc_zero[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     constexpr bool PK = pair_rows<FN, D, CB>();
-    if (j >= (PK ? (int64_t)(N + 1) / 2 * 2 : (int64_t)N)) return;
+    // (scalar layout: kSrowPad zero rows after the last sample, read by k_backward_mx's last steps)
+    if (j >= (PK ? (int64_t)(N + 1) / 2 * 2 : (int64_t)N + kSrowPad)) return;
     constexpr int M = fn_mask(FN), RSS = srow_stride<FN, D, CB>();
     float out[RSS];
 #pragma unroll
@@ -1314,6 +1316,243 @@ __global__ __launch_bounds__(kBlock, DGS_BWD_WAVES) void k_backward(const char *
     }
 }
 
+// (b) Matrix-core backward (gaussian, D = 2, CB = 16: BASELINE config 2's C = 16).  Per pair
+// (s, g) the gaussian backward is
+//   dL/dG = sum_c dl[s][c] v[g][c]                      (16 MACs: a [samples x channels] x
+//                                                          [channels x Gaussians] product)
+//   dv[g][c] += G dl[s][c]                              (16 MACs: [channels x samples] x
+//                                                          [samples x Gaussians])
+//   moments of t = G dL/dG over X, X X^T                (the VALU: exponent, exp, 5 FMAs)
+// In k_backward both contractions run on the VALU: ~32 of the ~47 operations per pair.  Here
+// they run on v_mfma_f32_16x16x4_f32 (exact f32: an fmaf chain), beside the VALU work of other
+// waves and of the wave's own next step (separate pipes, MI355X_MICROARCH.md).
+// A wave takes a unit's entries 16 at a time: lane (q = lane >> 4, col = lane & 15) holds
+// Gaussian col, and a 16-sample step gives it samples 4q + i (i = 0..3) -- the C/D layout of
+// the first product, whose K index runs over the channels c = 4q + j of the operands' 4
+// steps j.  The second product's K index (samples) is then taken as s = 4q + j, so its B
+// operand of step j is exactly register j of the VALU's G: no cross-lane movement per pair.
+// Its result leaves dv[c = 4q + i][col] in register i.  MODE as in k_backward: 0 fast, 1 the
+// lanes' constant wrap shifts, 2 some entry of the unit is unsafe (the literal power, per pair).
+#ifndef DGS_BWD_MX
+#define DGS_BWD_MX 1
+#endif
+template <int FN, int D, int CB>
+__host__ __device__ constexpr bool bwd_mfma() {
+    return DGS_BWD_MX && FN == 0 && D == 2 && CB == 16;
+}
+
+#ifndef DGS_BWD_MX_NG
+#define DGS_BWD_MX_NG 4  // 16-entry groups per pass over the samples (4: the whole unit at once)
+#endif
+
+// One 16-sample step's operands of lane (q, col): samples s0 + 4q + i (position; dl[.][col], the
+// second product's A) and sample s0 + col (dl[.][4q + j], the first product's A).  Rows past the
+// cell are the next cell's, or k_pack_samples' zero rows past N: finite, and their G is 0.
+struct MxStep {
+    float2 xy[4];
+    float a2[4];
+    float2 a1[2];
+};
+template <int D>
+__device__ __forceinline__ void mx_load(const float *__restrict__ ps, const float *__restrict__ pc, int col, int rss,
+                                        MxStep &st) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        st.xy[i] = *reinterpret_cast<const float2 *>(ps + i * rss);
+        st.a2[i] = ps[i * rss + D + col];
+    }
+    st.a1[0] = reinterpret_cast<const float2 *>(pc)[0];
+    st.a1[1] = reinterpret_cast<const float2 *>(pc)[1];
+}
+
+// Entries [eg, eg + 16 NG) of the unit (clamped to ee - 1; lanes past ee are not stored).
+template <int FN, int D, int CB, int NG, int MODE>
+__device__ __forceinline__ void bwd_mx_pass(const Bins &bins, const float *__restrict__ grows,
+                                            const float *__restrict__ srows, float *__restrict__ acc, int P,
+                                            int vrow0, int cell, int sb, int se, int eg, int ee, int q, int col,
+                                            const float *ctr, float *__restrict__ esums) {
+    constexpr int RSS = srow_stride<FN, D, CB>(), RS = grow_stride<FN, D, CB>(), B = Traits<FN, D>::GBASE;
+    constexpr int S = Traits<FN, D>::S, SSW = esum_stride<FN, D, CB>();
+    static_assert(D == 2 && CB == 16 && RS % 4 == 0 && RSS % 2 == 0, "matrix-core backward layout");
+    int pos[NG];
+    uint32_t ent[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        pos[g] = min(eg + 16 * g + col, ee - 1);
+        ent[g] = bins.entries[pos[g]];
+    }
+    float4 hd[NG];  // m0 m1 k0 k1
+    float k2[NG], bv[NG][4], sh0[NG], sh1[NG];  // bv: the first product's B, step j: v[col][4q + j]
+    float4 cr[NG];  // raw conics (the finish; MODE 2: the literal power)
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        const float *grow = grows + (int64_t)(ent[g] & kIdMask) * RS;
+        hd[g] = *reinterpret_cast<const float4 *>(grow);
+        k2[g] = grow[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bv[g][j] = grow[B + 4 * q + j];
+        if constexpr (MODE == 2) cr[g] = bins.gcon[ent[g] & kIdMask];
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        sh0[g] = sh1[g] = 0.0f;
+        if constexpr (MODE == 1) {
+            if (ent[g] & kGeneral) {
+                sh0[g] = wrap_shift_f(hd[g].x - ctr[0]);
+                sh1[g] = wrap_shift_f(hd[g].y - ctr[1]);
+            }
+        }
+    }
+    float mom[NG][5];  // sum t X0, t X1, t X0^2, t X0 X1, t X1^2
+    f32x4_t gv[NG];
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) mom[g][k] = 0.0f;
+        gv[g] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+    }
+    const float *ps = srows + (int64_t)(sb + 4 * q) * RSS;
+    const float *pc = srows + (int64_t)(sb + col) * RSS + D + 4 * q;
+    MxStep cur, nxt;
+    mx_load<D>(ps, pc, col, RSS, cur);
+#ifdef DGS_TIMING_TWICE  // (timing build only: the step loop twice -- its cost by difference)
+    for (int rep = 0; rep < 2; ++rep) {
+    ps = srows + (int64_t)(sb + 4 * q) * RSS;
+    pc = srows + (int64_t)(sb + col) * RSS + D + 4 * q;
+    mx_load<D>(ps, pc, col, RSS, cur);
+#endif
+    for (int base = sb; base < se; base += 16) {
+        ps += 16 * RSS;
+        pc += 16 * RSS;
+        if (base + 16 < se) mx_load<D>(ps, pc, col, RSS, nxt);  // (the next step's rows in flight)
+        const float a1[4] = {cur.a1[0].x, cur.a1[0].y, cur.a1[1].x, cur.a1[1].y};
+        f32x4_t dg[NG];  // dL/dG of (sample base + 4q + i, Gaussian col of group g)
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            dg[g] = f32x4_t{0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+            for (int j = 0; j < 4; ++j) dg[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(a1[j], bv[g][j], dg[g], 0, 0, 0);
+        }
+        bool ok[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) ok[i] = base + 4 * q + i < se;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) {
+            float G[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                float X0 = hd[g].x - cur.xy[i].x, X1 = hd[g].y - cur.xy[i].y;
+                if constexpr (MODE == 1) {  // fl(m - s) - shift: exact (see fwd_t_pairs)
+                    X0 = X0 - sh0[g];
+                    X1 = X1 - sh1[g];
+                }
+                float e;
+                if constexpr (MODE == 2) {  // (the reference's wrap of X and, for unsafe conics, its power)
+                    float X[2] = {X0, X1};
+                    const float c[3] = {cr[g].x, cr[g].y, cr[g].z}, kk[3] = {hd[g].z, hd[g].w, k2[g]};
+                    e = general_prob<FN, D>(X, c, kk, (ent[g] & kGeneral) != 0, (ent[g] & kUnsafe) != 0);
+                    X0 = X[0];
+                    X1 = X[1];
+                }
+                const float q0 = X0 * X0, q1 = X0 * X1, q2 = X1 * X1;
+                if constexpr (MODE != 2) e = fast_exp2(fmaf(k2[g], q2, fmaf(hd[g].w, q1, hd[g].z * q0)));
+                G[i] = ok[i] ? e : 0.0f;
+                const float t = G[i] * dg[g][i];
+                mom[g][0] = fmaf(t, X0, mom[g][0]);
+                mom[g][1] = fmaf(t, X1, mom[g][1]);
+                mom[g][2] = fmaf(t, q0, mom[g][2]);
+                mom[g][3] = fmaf(t, q1, mom[g][3]);
+                mom[g][4] = fmaf(t, q2, mom[g][4]);
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gv[g] = __builtin_amdgcn_mfma_f32_16x16x4f32(cur.a2[j], G[j], gv[g], 0, 0, 0);
+        }
+        cur = nxt;
+    }
+#ifdef DGS_TIMING_TWICE
+    }
+#endif
+    const int gsort = esums != nullptr ? sload(&bins.cell_gsort[cell]) : 0;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+        // the moments over the four sample quarters (lanes col + 16 q), then the gradient sums
+#pragma unroll
+        for (int k = 0; k < 5; ++k) {
+            mom[g][k] += __shfl_xor(mom[g][k], 16);
+            mom[g][k] += __shfl_xor(mom[g][k], 32);
+        }
+        const int64_t id = ent[g] & kIdMask;
+        if constexpr (MODE != 2) cr[g] = bins.gcon[id];
+        const float c[3] = {cr[g].x, cr[g].y, cr[g].z};
+        float sm[2] = {mom[g][0], mom[g][1]}, sc[3] = {mom[g][2], mom[g][3], mom[g][4]};
+        bwd_finish<FN, D>(c, sm, sc);
+        if (eg + 16 * g + col >= ee) continue;
+#ifdef DGS_TIMING_NO_STORE  // (timing build only: no stores -- their cost by difference)
+        if (sm[0] != 1.2345e-30f) continue;
+#endif
+        if (esums != nullptr && pos[g] >= gsort) {  // (the row of bwd_store: [dm dc dv pad])
+            float *o = esums + (int64_t)bins.esum_q[pos[g]] * SSW;
+            if (q == 0) {
+                o[0] = sm[0]; o[1] = sm[1];
+#pragma unroll
+                for (int k = 0; k < S; ++k) o[D + k] = sc[k];
+                if constexpr (SSW > D + S + CB) o[SSW - 1] = 0.0f;
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[D + S + 4 * q + i] = gv[g][i];
+        } else {
+            if (q == 0) {
+#pragma unroll
+                for (int d = 0; d < D; ++d) atomicAdd(acc + (int64_t)d * P + id, sm[d]);
+#pragma unroll
+                for (int k = 0; k < S; ++k) atomicAdd(acc + (int64_t)(D + k) * P + id, sc[k]);
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) atomicAdd(acc + (int64_t)(vrow0 + 4 * q + i) * P + id, gv[g][i]);
+        }
+    }
+}
+
+#ifndef DGS_BWD_MX_WAVES
+#define DGS_BWD_MX_WAVES 3  // (launch bound: >= 3 waves per SIMD, <= 168 VGPRs; 2 waves at the free allocation: +9 %)
+#endif
+template <int FN, int D, int CB>
+__global__ __launch_bounds__(kBlock, DGS_BWD_MX_WAVES) void k_backward_mx(const char *__restrict__ gbuf, const char *__restrict__ sbuf,
+                                                        const float *__restrict__ grows,
+                                                        const float *__restrict__ srows, float *__restrict__ acc,
+                                                        int P, int vrow0, const uint32_t *__restrict__ dirty,
+                                                        float *__restrict__ esums) {
+    if (sload(dirty)) return;  // call-time tensors differ from the binned ones: dgs_reference.hip
+    constexpr int NG = DGS_BWD_MX_NG;
+    const Bins bins = resolve(gbuf, sbuf);
+    const int nunits = sload(&bins.counts[kNumBwdUnits]);
+    const int stride = gridDim.x * kWavesPerBlock;
+    const int lane = threadIdx.x & (kWave - 1), q = lane >> 4, col = lane & 15;
+    for (int unit = wave_unit_index(nunits); unit < nunits; unit += stride) {
+        const uint2 u = sload(&bins.bwd_units[unit]);
+        const int cell = (int)u.x, eb = (int)u.y;
+        const int ee = min(eb + kWave, sload(&bins.cell_gend[cell]));
+        const uint32_t ent = bwd_entry(bins, u, lane);
+        const bool active = eb + lane < ee;
+        const int sb = sload(&bins.cell_sbeg[cell]), se = sload(&bins.cell_send[cell]);
+        if (__any(active && (ent & kUnsafe))) {
+            for (int eg = eb; eg < ee; eg += 16)  // (one group at a time: the general path's registers)
+                bwd_mx_pass<FN, D, CB, 1, 2>(bins, grows, srows, acc, P, vrow0, cell, sb, se, eg, ee, q, col, nullptr,
+                                             esums);
+        } else if (__any(active && (ent & kGeneral))) {
+            float ctr[2];
+            cell_center<D>(bins, cell, ctr);
+            for (int eg = eb; eg < ee; eg += 16 * NG)
+                bwd_mx_pass<FN, D, CB, NG, 1>(bins, grows, srows, acc, P, vrow0, cell, sb, se, eg, ee, q, col, ctr,
+                                              esums);
+        } else {
+            for (int eg = eb; eg < ee; eg += 16 * NG)
+                bwd_mx_pass<FN, D, CB, NG, 0>(bins, grows, srows, acc, P, vrow0, cell, sb, se, eg, ee, q, col, nullptr,
+                                              esums);
+        }
+    }
+}
+
 // The sort-path entries' sums (k_backward's slots), per Gaussian in slot order -- its entries'
 // order of k_fine_fill -- added to the atomics' sums (plain adds: k_backward has finished).
 // (kEsumLanes lanes per Gaussian stride over its slots, slot rows side by side, then a
@@ -1521,7 +1760,8 @@ static WsLayout ws_layout(int FN, int P, int D, int N, int C, bool backward) {
     const int CB = channel_block(C), nblk = (C + CB - 1) / CB;
     WsLayout w;
     w.grows = a256((size_t)P * grow_stride_rt(FN, D, CB) * 4 + 64);
-    w.srows = backward ? a256(((size_t)N + 1) * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;  // pair rows: N rounded up to even
+    // pair rows: N rounded up to even; scalar rows: kSrowPad zero rows after the last
+    w.srows = backward ? a256(((size_t)N + kSrowPad) * srow_stride_rt(FN, D, CB) * 4 + 64) : 0;
     w.acc = backward ? a256((size_t)(D + D * (D + 1) / 2 + nblk * CB) * P * 4) : 0;
     w.flag = w.grows + w.srows + w.acc;
     w.total = w.flag + 256;
@@ -1689,7 +1929,7 @@ static int run_backward(const Call &a) {
             DGS_LAUNCH_CHECK(a.s, a.debug);
         }
         // sample rows (+ the zero-fill of the sums and of the check word, first block only)
-        k_pack_samples<FN, D, CB><<<grid_for(a.N + 1), kBlock, 0, a.s>>>(
+        k_pack_samples<FN, D, CB><<<grid_for(a.N + kSrowPad), kBlock, 0, a.s>>>(
             a.N, a.gb, a.sb, a.dls, a.C, cbase, srows, cbase == 0 ? reinterpret_cast<float4 *>(acc) : nullptr,
             (int64_t)(w.acc / 16), cbase == 0 && !binned ? flag : nullptr);
         DGS_LAUNCH_CHECK(a.s, a.debug);
@@ -1700,8 +1940,12 @@ static int run_backward(const Call &a) {
         // dm/dc accumulate over all channel blocks (dL_dG is a sum over channels)
         {
             KernelTimer t(1, a.s, a.opts);
-            k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase, flag,
-                                                               esums);
+            if constexpr (bwd_mfma<FN, D, CB>())
+                k_backward_mx<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase,
+                                                                      flag, esums);
+            else
+                k_backward<FN, D, CB><<<blocks, kBlock, 0, a.s>>>(a.gb, a.sb, grows, srows, acc, a.P, D + S + cbase,
+                                                                   flag, esums);
             if (esums)
                 k_bwd_esum<FN, D, CB><<<grid_for((int64_t)a.P * kEsumLanes), kBlock, 0, a.s>>>(a.P, a.gb, esums, acc,
                                                                                              D + S + cbase, flag);

@@ -54,9 +54,13 @@ def test_ctypes_aggregate_matches_extension(dgs):
     ga = dgs._C.aggregate_neighbors_backward(*t, *a[:4], *fa[:3], a[4], g, False)
     gb = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False)
     gc = dgs_ctypes.aggregate_neighbors_backward(*t, *b[:4], *fb[:3], b[4], g, False, transposed=False)
+    # the two shared-array gradients (d/dfrequencies, d/ddistance_transform: a handful of
+    # elements, each a float sum over EVERY slot) at test_gpu_aggregate's LIT_SHARED = 1e-4: the
+    # atomic form's order moved one of them by 2.8e-5 relative on MI355X
     for x, y, z in zip(ga, gb, gc):
-        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))
-        np.testing.assert_allclose(x.cpu().numpy(), z.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(x.abs().max()))
+        rtol = 1e-4 if x.numel() <= 64 else 1e-5
+        np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=rtol, atol=1e-6 * float(x.abs().max()))
+        np.testing.assert_allclose(x.cpu().numpy(), z.cpu().numpy(), rtol=rtol, atol=1e-6 * float(x.abs().max()))
 
 
 def test_ctypes_multi_matches_extension(dgs):

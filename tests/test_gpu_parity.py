@@ -233,6 +233,36 @@ def test_parity_torus_seam(dgs, oracle, function, D, C):
     _check_case(dgs, oracle, function, means, values, covs, conics, s, dL)
 
 
+@pytest.mark.parametrize("case,C", [("seam", 16), ("thin", 16), ("unculled", 16), ("edge", 16),
+                                    ("mixed", 12), ("synthetic", 20)])
+def test_parity_gaussian_matrix_core_backward(dgs, oracle, case, C):
+    """The gaussian at C >= 9 (channel block 16) takes the matrix-core backward (k_backward_mx):
+    its constant-shift wrap path (seam), the slot sums of sort-path entries (thin: ~70 % of the
+    entries), units with unsafe conics (unculled, edge: k_backward's per-lane path inside the
+    same launch), padding channels (C = 12) and two channel blocks (C = 20: the atomics
+    accumulate dmeans / dconics over the blocks)."""
+    apriori = False
+    if case == "seam":
+        means, values, covs, conics, s = cases.seam_case(D=2, C=C)
+    elif case == "thin":
+        means, values, covs, conics, s = cases.thin_case(C=C)
+        apriori = True
+    elif case == "unculled":
+        means, _, covs, conics, s = cases.unculled_case()
+        values = torch.randn(means.shape[0], C, generator=torch.Generator().manual_seed(193))
+    elif case == "edge":
+        means, _, covs, conics, s = cases.edge_case()
+        values = torch.randn(means.shape[0], C, generator=torch.Generator().manual_seed(33))
+    elif case == "mixed":
+        means, values, covs, conics, s = cases.mixed_scales_case(C=C)
+    else:
+        means, values, covs, conics = syn.gaussians(900, 2, C, seed=14)
+        s = syn.samples(7000, 2, seed=15)
+    dL = syn.grad_out(s.shape[0], 1, C, seed=134)
+    stated = {"forward": 1.0, "dmeans": 8.0, "dvalues": 1.0, "dconics": 1.0} if case == "unculled" else None
+    _check_case(dgs, oracle, "gaussian", means, values, covs, conics, s, dL, apriori=apriori, stated=stated)
+
+
 def test_parity_d1_zero_variance(dgs, oracle):
     means, values, covs, conics, samples = cases.d1_zero_variance_case()
     dL = syn.grad_out(samples.shape[0], 1, 1, seed=52)
