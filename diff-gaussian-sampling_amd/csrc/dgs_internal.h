@@ -561,10 +561,13 @@ struct UnitHint {
     Header hdr;       // the header preprocess wrote (ensure_ref_lists reads its geometry / offsets)
     bool ref_built;   // rlist built (ensure_ref_lists), ref_done recorded after its build
     bool capture = false;  // a graph-capturable binning: R / E / nunsafe are on the device only
+    bool own_grid = false;  // the grid was the samples' own (dgs_preprocess_auto[_ex])
     hipEvent_t ref_done;
 };
 void hint_put(const UnitHint &h);
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out);
+// The newest binning whose sample buffer is (sbuf, sbytes) (dgs_bin_options.samples_binned).
+bool hint_by_sbuf(const void *sbuf, size_t sbytes, UnitHint *out);
 // The call-time path's tile lists (rlist) of a binning: built on `s` at the first call that may
 // take that path (any call not flagged DGS_SAMPLE_INPUTS_BINNED); later calls on another stream
 // wait for that build.  Buffers without a hint (not made by this process) are rebuilt per call.

@@ -46,6 +46,10 @@ int check_hip(hipError_t e, const char *what) {
 // ------------------------------------------------------------------------ launch hints
 static std::mutex g_hint_mu;
 static std::unordered_map<const void *, UnitHint> g_hints;
+// the same records keyed by the sample buffer (hint_by_sbuf): a binning buffer's address is reused
+// once the caller frees it, which replaces its g_hints entry while its sample buffer -- kept by the
+// caller for dgs_bin_options.samples_binned -- is still alive
+static std::unordered_map<const void *, UnitHint> g_shints;
 static void hint_drop(UnitHint &h) {  // (under g_hint_mu)
     if (h.ref_done) (void)hipEventDestroy(h.ref_done);
     h.ref_done = nullptr;
@@ -59,6 +63,10 @@ void hint_put(const UnitHint &h) {
     auto it = g_hints.find(h.gbuf);
     if (it != g_hints.end()) hint_drop(it->second);
     g_hints[h.gbuf] = h;
+    if (g_shints.size() > 4096) g_shints.clear();
+    UnitHint sh = h;
+    sh.ref_done = nullptr;  // (owned by the g_hints entry)
+    g_shints[h.sbuf] = sh;
 }
 bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, UnitHint *out) {
     std::lock_guard<std::mutex> lk(g_hint_mu);
@@ -70,7 +78,16 @@ bool hint_get(const void *gbuf, size_t gbytes, const void *sbuf, size_t sbytes, 
     return true;
 }
 
+bool hint_by_sbuf(const void *sbuf, size_t sbytes, UnitHint *out) {
+    std::lock_guard<std::mutex> lk(g_hint_mu);
+    auto it = g_shints.find(sbuf);  // (the latest binning whose sample buffer has this address)
+    if (it == g_shints.end() || it->second.sbytes != sbytes) return false;
+    *out = it->second;
+    return true;
+}
+
 static std::atomic<int64_t> g_internal_allocs{0};
+static std::atomic<int64_t> g_sample_reuse{0};
 void note_internal_alloc() { g_internal_allocs.fetch_add(1, std::memory_order_relaxed); }
 
 // The binning's one host read-back target: 16 int64 of pinned host memory per host thread (the
@@ -1675,6 +1692,40 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
     }
 }
 
+// The sample side of an earlier binning of the same samples on the same grid and fine cells
+// (dgs_bin_options.samples_binned): its regions copied (up to 8 word arrays), and per cell what
+// the skipped launches (k_sample_cells, the sample sort, k_identify, k_sub_box) also leave in
+// scratch: the tiles' sample counts (stile, for ref_tables_block's sample ranges and call-time
+// tables) and the fallback-cell bits (fbg).
+struct ReuseSpec {
+    const uint32_t *src[8];
+    uint32_t *dst[8];
+    int64_t n[8];  // words
+    int count;
+    const int32_t *sbeg, *send;  // the source's cell ranges
+    int ncells, CT, T;
+    uint32_t *stile, *fbg;
+};
+__global__ __launch_bounds__(kBlock) void k_sample_reuse(ReuseSpec r) {
+    const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x, st = (int64_t)gridDim.x * blockDim.x;
+    for (int k = 0; k < r.count; ++k) {
+        int64_t done = 0;
+        if (((reinterpret_cast<uintptr_t>(r.src[k]) | reinterpret_cast<uintptr_t>(r.dst[k])) & 15) == 0) {
+            const int64_t n4 = r.n[k] >> 2;
+            const uint4 *s4 = reinterpret_cast<const uint4 *>(r.src[k]);
+            uint4 *d4 = reinterpret_cast<uint4 *>(r.dst[k]);
+            for (int64_t i = t; i < n4; i += st) d4[i] = s4[i];
+            done = n4 << 2;
+        }
+        for (int64_t i = done + t; i < r.n[k]; i += st) r.dst[k][i] = r.src[k][i];
+    }
+    for (int64_t c = t; c < r.ncells; c += st) {
+        const int cnt = r.send[c] - r.sbeg[c];
+        if (cnt > 0) atomicAdd(&r.stile[(size_t)(c % kShards) * (r.T + 1) + c / r.CT], (uint32_t)cnt);
+        set_fb_bit((int)c, r.CT, cnt > 0, r.fbg);
+    }
+}
+
 // Means and conics in internal order (the forward/backward read them coalesced from here).
 // Also stores perm (internal -> caller id) and its inverse back to back in gperm (one pass
 // over the permutation instead of two launches).
@@ -1943,7 +1994,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
                            void *alloc_ctx, int64_t *num_rendered, dgs_stream_t stream, int debug,
                            const int *dgrid, const float *doff, int *dev_grid, float *dev_off,
                            const uint8_t *present = nullptr, double sample_area = 0.0,
-                           const dgs_bin_options *copt = nullptr) {
+                           const dgs_bin_options *copt = nullptr, bool own_grid = false) {
     // the graph-capturable form (dgs.h, dgs_bin_options.capacity_E > 0): no host sync and no
     // host read of a device value -- the lists are sized from the caller's capacities, the exact
     // counts stay on the device (capacity-sized launches read them), overflows are reported in
@@ -1988,6 +2039,13 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     G.ifs = 1.0 / G.fs;
     const int ncells = G.ncells;
     const int home_w = G.grid[0] * G.n, home_h = D == 2 ? G.grid[1] * G.n : 1;
+    // an earlier binning of the same samples on this grid and these fine cells: its sample side
+    UnitHint prev;
+    const bool reuse = !capmode && copt && copt->samples_binned &&
+                       hint_by_sbuf(copt->samples_binned, copt->samples_binned_bytes, &prev) &&
+                       prev.hdr.N == N && prev.hdr.D == D && prev.hdr.T == G.T && prev.hdr.n == G.n &&
+                       prev.hdr.CT == G.CT && prev.hdr.ncells == G.ncells && prev.hdr.grid[0] == G.grid[0] &&
+                       prev.hdr.grid[1] == G.grid[1] && std::memcmp(prev.hdr.off, G.off, sizeof(G.off)) == 0;
 
     // ---- sample-side buffer (size known now) and the reference range buffers
     const int64_t fwd_cap = (N + kFwdUnit - 1) / kFwdUnit + 2 * std::min<int64_t>(N, ncells) + 1;
@@ -2110,6 +2168,37 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         k_bounds_final<<<1, kBlock, 0, s>>>(nparts, D, bpart, cgrid, coff);
         DGS_LAUNCH_CHECK(s, debug);
     }
+    if (reuse) {  // ---- samples: copied from the earlier binning of the same samples
+        const Header &ph = prev.hdr;
+        const char *ps = static_cast<const char *>(prev.sbuf);
+        ReuseSpec r{};
+        const auto add = [&](int64_t so, int64_t dofs, size_t bytes) {
+            r.src[r.count] = reinterpret_cast<const uint32_t *>(ps + so);
+            r.dst[r.count] = reinterpret_cast<uint32_t *>(sbuf + dofs);
+            r.n[r.count] = (int64_t)(bytes / 4);
+            ++r.count;
+        };
+        add(ph.o_sorted, L0.o_sorted, sizeof(int32_t) * (size_t)N);
+        add(ph.o_cell_box, L0.o_cell_box, sizeof(float4) * (size_t)ncells);
+        add(ph.o_cell_sbeg, L0.o_cell_sbeg, sizeof(int32_t) * (size_t)ncells);
+        add(ph.o_cell_send, L0.o_cell_send, sizeof(int32_t) * (size_t)ncells);
+        add(ph.o_fsrows, L0.o_fsrows, fsrows_bytes(N, D));
+        if (nsub) {
+            add(ph.o_sub_sbeg, L0.o_sub_sbeg, sizeof(int32_t) * (size_t)nsub);
+            add(ph.o_sub_send, L0.o_sub_send, sizeof(int32_t) * (size_t)nsub);
+            add(ph.o_sub_box, L0.o_sub_box, sizeof(float4) * (size_t)nsub);
+        }
+        r.sbeg = reinterpret_cast<const int32_t *>(ps + ph.o_cell_sbeg);
+        r.send = reinterpret_cast<const int32_t *>(ps + ph.o_cell_send);
+        r.ncells = ncells;
+        r.CT = G.CT;
+        r.T = G.T;
+        r.stile = stile;
+        r.fbg = fbg;
+        k_sample_reuse<<<1024, kBlock, 0, s>>>(r);
+        DGS_LAUNCH_CHECK(s, debug);
+        g_sample_reuse.fetch_add(1, std::memory_order_relaxed);
+    } else {
     // ---- samples: fine cell keys, stable radix sort, per-cell ranges
     k_sample_cells<<<hist_grid(N), kBlock, 0, s>>>(N, G, samples, skeys, sids, stile, radix_hist(plan_s, rs_s));
     DGS_LAUNCH_CHECK(s, debug);
@@ -2126,6 +2215,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         k_cell_box<<<(unsigned)((ncells + kBlock / kWave - 1) / (kBlock / kWave)), kBlock, 0, s>>>(
             ncells, D, G.CT, cell_sbeg, cell_send, fsrows, cell_box, fbg);
     DGS_LAUNCH_CHECK(s, debug);
+    }
 
     // ---- Gaussians: reference radius/touched, spatial renumbering, fine entry counts
     k_gauss_prep<<<hist_grid(P), kBlock, 0, s>>>(P, G, means, covariances, conics, radii, touched, gtile,
@@ -2535,6 +2625,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     // (capturable binning: the counts are the device's; unknown here -> every pass launched)
     uh.nfwd = fwd_cap; uh.nbwd = bwd_cap; uh.nunsafe = capmode ? -1 : htot[6]; uh.nthin = capmode ? -1 : htot[7];
     uh.capture = capmode;
+    uh.own_grid = own_grid;
     uh.nfsub = fsub_cap_of(D, N, ncells);
     uh.ncells = ncells;
     uh.P = P; uh.D = D; uh.N = N; uh.R = R; uh.E = E; uh.Es = Es;
@@ -2698,6 +2789,8 @@ extern "C" int dgs_preprocess_ex(int P, int D, int N, const float *means, const 
     const uint8_t *present = opts ? opts->present : nullptr;
     const double area = opts ? opts->sample_area : 0.0;
     if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_ex: sample_area must be >= 0");
+    if (opts && opts->samples_binned && opts->capacity_E > 0)
+        return fail(DGS_ERR_ARG, "dgs_preprocess_ex: samples_binned is not for the capturable binning (capacity_E > 0)");
     return preprocess_body(P, D, N, means, covariances, conics, samples, grid, grid_offset, radii, alloc,
                            alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present,
                            area, opts);
@@ -2738,15 +2831,45 @@ static bool same_grid(int D, const int *ga, const float *oa, const int *gb, cons
     return true;
 }
 
+extern "C" int64_t dgs_sample_reuse_count(void) { return g_sample_reuse.load(std::memory_order_relaxed); }
+
 extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, const float *covariances,
                                    const float *conics, const float *samples, float *radii,
                                    dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
                                    int *grid_out, float *offset_out, dgs_stream_t stream, int debug) {
+    return dgs_preprocess_auto_ex(P, D, N, means, covariances, conics, samples, nullptr, radii, alloc, alloc_ctx,
+                                  num_rendered, grid_out, offset_out, stream, debug);
+}
+
+extern "C" int dgs_preprocess_auto_ex(int P, int D, int N, const float *means, const float *covariances,
+                                      const float *conics, const float *samples, const dgs_bin_options *opts,
+                                      float *radii, dgs_alloc_fn alloc, void *alloc_ctx, int64_t *num_rendered,
+                                      int *grid_out, float *offset_out, dgs_stream_t stream, int debug) {
     if (D != 1 && D != 2) return fail(DGS_ERR_ARG, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
     if (P < 0 || N < 0 || !alloc || !num_rendered || !grid_out || !offset_out)
         return fail(DGS_ERR_ARG, "dgs_preprocess_auto: bad arguments");
+    if (opts && opts->struct_size != sizeof(dgs_bin_options))
+        return fail(DGS_ERR_ARG, "dgs_preprocess_auto_ex: dgs_bin_options.struct_size must be sizeof(dgs_bin_options) "
+                                 "(a caller built against another dgs.h; see DGS_ABI_VERSION)");
+    if (opts && (opts->flags || opts->capacity_E > 0))
+        return fail(DGS_ERR_ARG, "dgs_preprocess_auto_ex: flags and capacities are for dgs_preprocess_ex");
+    const uint8_t *present = opts ? opts->present : nullptr;
+    const double area = opts ? opts->sample_area : 0.0;
+    if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_auto_ex: sample_area must be >= 0");
     *num_rendered = 0;
     if (P == 0 || N == 0) return DGS_OK;  // sample_points.cu:69: nothing to bin
+    {  // the same samples, binned earlier on their own grid: that grid (no grid pass, no speculation)
+        UnitHint ph;
+        if (opts && opts->samples_binned && hint_by_sbuf(opts->samples_binned, opts->samples_binned_bytes, &ph) &&
+            ph.own_grid && ph.hdr.N == N && ph.hdr.D == D) {
+            const int g[2] = {ph.hdr.grid[0], ph.hdr.grid[1]};
+            const float o[2] = {ph.hdr.off[0], ph.hdr.off[1]};
+            for (int d = 0; d < D; ++d) { grid_out[d] = g[d]; offset_out[d] = o[d]; }
+            return preprocess_body(P, D, N, means, covariances, conics, samples, g, o, radii, alloc, alloc_ctx,
+                                   num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present, area, opts,
+                                   true);
+        }
+    }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     // sample_points.cu:70-74 on the device (torch's CUDA arithmetic, k_bounds_final)
     const int nparts = (int)std::min<int64_t>(1024, grid_for(N));
@@ -2780,7 +2903,7 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     int dg[2] = {0, 0};
     float dof[2] = {0.0f, 0.0f};
     int rc = preprocess_body(P, D, N, means, covariances, conics, samples, guess, goff, radii, alloc, alloc_ctx,
-                             num_rendered, stream, debug, dgrid, doff, dg, dof);
+                             num_rendered, stream, debug, dgrid, doff, dg, dof, present, area, opts, true);
     if (rc) return rc;
     const bool hit = same_grid(D, dg, dof, guess, goff);
     {
@@ -2792,7 +2915,7 @@ extern "C" int dgs_preprocess_auto(int P, int D, int N, const float *means, cons
     }
     if (!hit)
         rc = preprocess_body(P, D, N, means, covariances, conics, samples, dg, dof, radii, alloc, alloc_ctx,
-                             num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr);
+                             num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present, area, opts, true);
     for (int d = 0; d < D; ++d) { grid_out[d] = dg[d]; offset_out[d] = dof[d]; }
     return rc;
 }

@@ -183,9 +183,38 @@ void rows_put(const Tensor &gb, int mask, int C, const Tensor &means, const Tens
     if (g_rows.size() > 4) g_rows.erase(g_rows.begin());  // (the per-function path of a fused call keeps one per function)
 }
 
+// The sample buffer of the last eager binnings per samples tensor (dgs_bin_options.samples_binned):
+// a later binning of the same, unchanged samples copies its sample side instead of sorting the
+// samples again (the training loop re-bins after every optimizer step; its points stay put).
+struct SampleRecord {
+    TKey samples;
+    Tensor sb;
+    hipStream_t stream;  // the binning's stream: copied from only on it (stream order)
+};
+std::vector<SampleRecord> g_samples;
+
+Tensor samples_get(const Tensor &samples) {
+    if (always_verify() || !trackable({&samples})) return Tensor();
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    const hipStream_t st = cur_stream();
+    for (const auto &r : g_samples)
+        if (r.stream == st && same(r.samples, samples)) return r.sb;
+    return Tensor();
+}
+
+void samples_put(const Tensor &samples, const Tensor &sb) {
+    std::lock_guard<std::mutex> lk(g_step_mu);
+    for (auto it = g_samples.begin(); it != g_samples.end();)
+        if (it->samples.storage.expired() || same(it->samples, samples)) it = g_samples.erase(it);
+        else ++it;
+    if (!trackable({&samples}) || sb.numel() == 0) return;
+    g_samples.push_back({tkey(samples), sb, cur_stream()});
+    if (g_samples.size() > 2) g_samples.erase(g_samples.begin());  // (a train and a test set, say)
+}
+
 PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Tensor &cov_in,
                        const Tensor &conics_in, const Tensor &samples_in, const std::vector<int> *grid_in,
-                       const std::vector<float> *off_in, bool debug, const dgs_bin_options *opts = nullptr) {
+                       const std::vector<float> *off_in, bool debug, const dgs_bin_options *opts_in = nullptr) {
     const Tensor means = f32(means_in, "means"), covs = f32(cov_in, "covariances");
     const Tensor conics = f32(conics_in, "conics"), samples = f32(samples_in, "samples");
     (void)values_in;
@@ -195,6 +224,19 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
     AllocCtx ctx{means.device()};
     for (int i = 0; i < 4; ++i) ctx.bufs[i] = empty_u8(means.device());
     int64_t rendered = 0;
+    // the eager binnings (not the capturable one): the sample buffer of an earlier binning of
+    // these samples, if they are unchanged since
+    dgs_bin_options o{};
+    if (opts_in) o = *opts_in;
+    o.struct_size = sizeof(dgs_bin_options);
+    const bool eager = o.capacity_E <= 0;
+    Tensor prev_sb;
+    if (eager && samples.data_ptr() == samples_in.data_ptr()) prev_sb = samples_get(samples_in);
+    if (prev_sb.defined()) {
+        o.samples_binned = prev_sb.data_ptr();
+        o.samples_binned_bytes = (size_t)prev_sb.numel();
+    }
+    const dgs_bin_options *opts = &o;
     if (P != 0 && N != 0) {
         TORCH_CHECK(D == 1 || D == 2, "only D = 1 or D = 2 is supported (the reference leaves D = 3 undefined)");
         TORCH_CHECK(samples.size(-1) == D, "samples must have the same dimension as means");
@@ -208,14 +250,16 @@ PreOut preprocess_impl(const Tensor &means_in, const Tensor &values_in, const Te
         } else {  // the grid of sample_points.cu:70-74 on the device: one host sync per call
             int grid[2];
             float off[2];
-            check(dgs_preprocess_auto(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
-                                      conics.data_ptr<float>(), samples.data_ptr<float>(),
-                                      radii.data_ptr<float>(), alloc_cb, &ctx, &rendered, grid, off,
-                                      as_dgs(cur_stream()), debug ? 1 : 0),
+            check(dgs_preprocess_auto_ex(P, D, N, means.data_ptr<float>(), covs.data_ptr<float>(),
+                                         conics.data_ptr<float>(), samples.data_ptr<float>(), opts,
+                                         radii.data_ptr<float>(), alloc_cb, &ctx, &rendered, grid, off,
+                                         as_dgs(cur_stream()), debug ? 1 : 0),
                   "preprocess_gaussians");
         }
     }
     if (ctx.bufs[DGS_BUF_BINNING].numel() > 0) bins_put(ctx.bufs[DGS_BUF_BINNING], means_in, conics_in, samples_in);
+    // (the samples tensor as passed: a float32 contiguous one is its own binning input)
+    if (eager && samples.data_ptr() == samples_in.data_ptr()) samples_put(samples_in, ctx.bufs[DGS_BUF_SAMPLE_BINNING]);
     return std::make_tuple(rendered, ctx.bufs[DGS_BUF_BINNING], ctx.bufs[DGS_BUF_SAMPLE_BINNING],
                            ctx.bufs[DGS_BUF_RANGES], ctx.bufs[DGS_BUF_SAMPLE_RANGES], radii);
 }

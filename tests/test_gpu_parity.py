@@ -407,6 +407,53 @@ def test_preprocess_speculation_per_sample_set(dgs, oracle):
         both(inplace)
 
 
+def test_sample_side_reuse(dgs):
+    """Re-binning the same, unchanged samples tensor copies the previous binning's sample side
+    (dgs_bin_options.samples_binned; dgs_sample_reuse_count counts it): num_rendered, both range
+    arrays, the radii and the forward equal a fresh binning's (of a clone of the samples: another
+    tensor, so the full path) bit for bit, the gradients at the atomics' order tolerance, with the
+    means moved between binnings as a training loop does.  A version bump or an in-place change
+    of the samples takes the full path."""
+    import ctypes
+    import os
+    lib = ctypes.CDLL(os.path.join(os.path.dirname(dgs.__file__), "libdgs.so"))
+    lib.dgs_sample_reuse_count.restype = ctypes.c_int64
+    dev = torch.device("cuda:0")
+    means, values, covs, conics = syn.gaussians(3000, 2, 3, seed=91)
+    m, v, cv, c = (t.to(dev) for t in (means, values, covs, conics))
+    s = syn.samples(20000, 2, seed=92).to(dev)
+    dL = syn.grad_out(20000, 1, 3, seed=93).to(dev)
+
+    def run(samples, mm):
+        R, gb, sb, rg, srg, radii = dgs._C.preprocess_gaussians(mm, v, cv, c, samples, False)
+        out = dgs._C.sample_gaussians(mm, v, c, samples, R, gb, sb, rg, srg, False)
+        grads = dgs._C.sample_gaussians_backward(mm, v, c, samples, R, dL, gb, sb, rg, srg, False)
+        return R, (rg, srg, radii, out), grads
+
+    def same(a, b):
+        assert a[0] == b[0]
+        for x, y in zip(a[1], b[1]):
+            assert torch.equal(x, y)
+        for x, y in zip(a[2], b[2]):
+            np.testing.assert_allclose(x.cpu().numpy(), y.cpu().numpy(), rtol=1e-5, atol=1e-6 * float(y.abs().max()))
+
+    run(s, m)
+    for step in range(3):
+        mm = m + 0.003 * step
+        n0 = lib.dgs_sample_reuse_count()
+        a = run(s, mm)
+        assert lib.dgs_sample_reuse_count() == n0 + 1, "the unchanged samples were sorted again"
+        b = run(s.clone(), mm)
+        assert lib.dgs_sample_reuse_count() == n0 + 1
+        same(a, b)
+    for change in (lambda t: t.add_(0.0), lambda t: t[:100].mul_(0.5)):
+        change(s)
+        n0 = lib.dgs_sample_reuse_count()
+        a = run(s, m)
+        assert lib.dgs_sample_reuse_count() == n0, "changed samples took the copied sample side"
+        same(a, run(s.clone(), m))
+
+
 def test_preprocess_grid_changes_between_calls(dgs, oracle):
     """preprocess_gaussians computes the tile grid on the device and bins with the previous
     call's grid until the one host sync confirms it (dgs_preprocess_auto): a call whose domain
