@@ -1433,7 +1433,7 @@ __device__ __forceinline__ uint32_t sub_mask(uint32_t ent, const float2 &mm, con
 // sub-cells whose sample box its cut meets (sub_mask).  Sub list k of the cell has the region
 // [4 gbeg + k n, + n) of sub_ent (n = the cell list's length: an entry is in at most every sub
 // list of its cell); it is written in cell-list order, so [lbeg, lmid) holds the flag-free
-// entries, [lmid, lend) the flagged ones and, of those, [lthin, lend) the kThin ones.  The next group's Gaussian rows and the one
+// entries, [lmid, lend) the flagged ones (lthin = lend: no kThin entries since round 6).  The next group's Gaussian rows and the one
 // after's entries are loaded while a group is tested (one stage: waves parked on the row
 // gathers half their cycles, PMC SQ_WAIT_ANY).  (A block-per-cell form -- masks
 // of the whole list in parallel into LDS, then one compacting wave per sub list -- was slower:
@@ -1458,7 +1458,7 @@ __device__ __forceinline__ void sub_lists_wave(const SubListArgs &A, int c, int 
     uint32_t *__restrict__ sub_ent = A.sub_ent;
     const int CT = A.CT;
     const int b = gbeg[c], m_ = gmid[c], e = gend[c], n = e - b;
-    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0}, nth[kSubPerCell] = {0, 0, 0, 0};
+    uint32_t nff[kSubPerCell] = {0, 0, 0, 0}, nfl[kSubPerCell] = {0, 0, 0, 0};
     const int64_t base = (int64_t)kSubPerCell * b;
     if (b < e && (c % CT) != CT - 1) {  // (the fallback cell: every entry is kUnsafe)
         const float4 bx = box[c];
@@ -1498,12 +1498,11 @@ __device__ __forceinline__ void sub_lists_wave(const SubListArgs &A, int c, int 
             ent_n = j + 2 * kWave < e ? entries[j + 2 * kWave] : kUnsafe;
 #endif
             const uint32_t mask = j < e ? sub_mask(ent, mm, cc, bx, ctr, sb) : 0u;
-            const bool ff = j < m_, thin = (ent & kThin) != 0;
+            const bool ff = j < m_;
 #pragma unroll
             for (int k = 0; k < kSubPerCell; ++k) {
                 const bool hit = (mask >> k) & 1u;
                 const uint64_t bf = __ballot(hit && ff), bl = __ballot(hit && !ff);
-                nth[k] += (uint32_t)__popcll(__ballot(hit && thin));
                 if (hit) {
                     const uint32_t below = (uint32_t)__popcll((ff ? bf : bl) & ((1ull << lane) - 1ull));
                     // flag-free entries precede the flagged ones in the cell list, so once a group
@@ -1524,8 +1523,7 @@ __device__ __forceinline__ void sub_lists_wave(const SubListArgs &A, int c, int 
             lbeg[c * kSubPerCell + k] = a;
             lmid[c * kSubPerCell + k] = a + (int)nff[k];
             lend[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);
-            // (the kThin entries sort last in the cell list: the last nth of the flagged part)
-            lthin[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k] - nth[k]);
+            lthin[c * kSubPerCell + k] = a + (int)(nff[k] + nfl[k]);  // (no kThin entries since round 6: = lend)
         }
 }
 
