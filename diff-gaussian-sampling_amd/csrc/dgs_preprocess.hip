@@ -1717,10 +1717,26 @@ __global__ __launch_bounds__(kBlock) void k_sample_reuse(ReuseSpec r) {
         }
         for (int64_t i = done + t; i < r.n[k]; i += st) r.dst[k][i] = r.src[k][i];
     }
-    for (int64_t c = t; c < r.ncells; c += st) {
-        const int cnt = r.send[c] - r.sbeg[c];
-        if (cnt > 0) atomicAdd(&r.stile[(size_t)(c % kShards) * (r.T + 1) + c / r.CT], (uint32_t)cnt);
-        set_fb_bit((int)c, r.CT, cnt > 0, r.fbg);
+    // per tile (a block each, grid-strided): its sample count into copy 0 of stile (the others
+    // stay zero-filled) and its fallback cell's bit.  (Per-cell atomics put ~1.7k adds on each
+    // copy's one cache line: 41 us for this launch at the headline.)
+    __shared__ uint32_t part[kBlock / kWave];
+    for (int tile = blockIdx.x; tile < r.T; tile += gridDim.x) {
+        const int64_t c0 = (int64_t)tile * r.CT;
+        uint32_t sum = 0;
+        for (int k = threadIdx.x; k < r.CT; k += blockDim.x) sum += (uint32_t)(r.send[c0 + k] - r.sbeg[c0 + k]);
+#pragma unroll
+        for (int off = kWave / 2; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+        if ((threadIdx.x & (kWave - 1)) == 0) part[threadIdx.x / kWave] = sum;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tot = 0;
+            for (int w = 0; w < (int)(blockDim.x / kWave); ++w) tot += part[w];
+            r.stile[tile] = tot;
+            const int64_t fb = c0 + r.CT - 1;
+            set_fb_bit((int)fb, r.CT, r.send[fb] > r.sbeg[fb], r.fbg);
+        }
+        __syncthreads();
     }
 }
 
