@@ -523,9 +523,11 @@ def bench_sample(args, world, rank, dev, torch, dist):
             R2, gb2, sb2, rg2, srg2, _ = dgs._C.preprocess_gaussians(md, vd, covs, cd, samples, False)
             fwd(means, values, conics, samples, R2, gb2, sb2, rg2, srg2, False).backward(dLv)
 
+        fixed_sb = sb  # (the collocation points stay put: the captured binning copies their sample side)
+
         def pigs_body():
             R2, gb2, sb2, rg2, srg2, _, st2 = dgs.preprocess_gaussians_capturable(md, vd, covs, cd, samples, grid,
-                                                                                    off, cap)
+                                                                                    off, cap, samples_binned=fixed_sb)
             fwd(means, values, conics, samples, cap[2], gb2, sb2, rg2, srg2, False).backward(dLv)
             return st2
 
@@ -558,7 +560,8 @@ def bench_sample(args, world, rank, dev, torch, dist):
                                 "graph_status": int(g_st.item()), "capacity": cap,
                                 "note": "re-binning + fwd + bwd per step, host-timed medians; graph = one "
                                         "torch.cuda.graph replay of preprocess_gaussians_capturable + the sample "
-                                        "call + backward"}
+                                        "call + backward; both copy the fixed samples' sample side from an "
+                                        "earlier binning (samples_binned) instead of sorting them per step"}
         del graph
     if rank == 0 and world == 1 and not args.no_cpu and not multi:
         cpu_baselines(result, means.detach().cpu(), values.detach().cpu(), covs.cpu(),

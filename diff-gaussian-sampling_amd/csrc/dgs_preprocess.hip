@@ -1662,7 +1662,7 @@ __global__ __launch_bounds__(kBlock) void k_binning_tail(CopySpec c, TailSpec ts
             if (threadIdx.x == 0) {
                 const int64_t R = ts.totals[0], E = ts.totals[1], Es = ts.totals[4];
                 uint32_t st = (E > ts.Ecap ? 1u : 0u) | (Es > ts.Escap ? 2u : 0u) | (R > ts.Rcap ? 4u : 0u);
-                for (int d = 0; d < ts.D; ++d)
+                for (int d = 0; ts.dgrid && d < ts.D; ++d)
                     if (ts.dgrid[d] != ts.grid[d] || __float_as_uint(ts.doff[d]) != __float_as_uint(ts.off[d])) st |= 8u;
                 for (char *b : {ts.gbuf, ts.sbuf}) {
                     Header *hh = reinterpret_cast<Header *>(b);
@@ -2055,7 +2055,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
     const int home_w = G.grid[0] * G.n, home_h = D == 2 ? G.grid[1] * G.n : 1;
     // an earlier binning of the same samples on this grid and these fine cells: its sample side
     UnitHint prev;
-    const bool reuse = !capmode && copt && copt->samples_binned &&
+    const bool reuse = copt && copt->samples_binned && (!capmode || (copt->flags & DGS_BIN_SAMPLES_FIXED)) &&
                        hint_by_sbuf(copt->samples_binned, copt->samples_binned_bytes, &prev) &&
                        prev.hdr.N == N && prev.hdr.D == D && prev.hdr.T == G.T && prev.hdr.n == G.n &&
                        prev.hdr.CT == G.CT && prev.hdr.ncells == G.ncells && prev.hdr.grid[0] == G.grid[0] &&
@@ -2177,7 +2177,7 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         DGS_LAUNCH_CHECK(s, debug);
     }
 
-    if (capmode) {
+    if (capmode && !reuse) {  // (fixed samples: their grid is the reused binning's)
         k_bounds_partial<<<nparts, kBlock, 0, s>>>(N, D, samples, bpart);
         k_bounds_final<<<1, kBlock, 0, s>>>(nparts, D, bpart, cgrid, coff);
         DGS_LAUNCH_CHECK(s, debug);
@@ -2620,8 +2620,8 @@ static int preprocess_body(int P, int D, int N, const float *means, const float 
         ts.D = D;
         ts.totals = totals;
         ts.Rcap = R; ts.Ecap = E; ts.Escap = Es;
-        ts.dgrid = cgrid;
-        ts.doff = coff;
+        ts.dgrid = reuse ? nullptr : cgrid;  // (no grid check for fixed samples)
+        ts.doff = reuse ? nullptr : coff;
         for (int d = 0; d < 2; ++d) { ts.grid[d] = G.grid[d]; ts.off[d] = G.off[d]; }
         ts.R_out = copt->num_rendered_device;
         ts.status = copt->status_device;
@@ -2798,13 +2798,14 @@ extern "C" int dgs_preprocess_ex(int P, int D, int N, const float *means, const 
     if (opts && opts->struct_size != sizeof(dgs_bin_options))
         return fail(DGS_ERR_ARG, "dgs_preprocess_ex: dgs_bin_options.struct_size must be sizeof(dgs_bin_options) "
                                  "(a caller built against another dgs.h; see DGS_ABI_VERSION)");
-    if (opts && (opts->flags & ~(uint32_t)DGS_BIN_STATUS_STICKY))
+    if (opts && (opts->flags & ~(uint32_t)(DGS_BIN_STATUS_STICKY | DGS_BIN_SAMPLES_FIXED)))
         return fail(DGS_ERR_ARG, "dgs_preprocess_ex: unknown dgs_bin_options.flags");
     const uint8_t *present = opts ? opts->present : nullptr;
     const double area = opts ? opts->sample_area : 0.0;
     if (!(area >= 0.0)) return fail(DGS_ERR_ARG, "dgs_preprocess_ex: sample_area must be >= 0");
-    if (opts && opts->samples_binned && opts->capacity_E > 0)
-        return fail(DGS_ERR_ARG, "dgs_preprocess_ex: samples_binned is not for the capturable binning (capacity_E > 0)");
+    if (opts && opts->samples_binned && opts->capacity_E > 0 && !(opts->flags & DGS_BIN_SAMPLES_FIXED))
+        return fail(DGS_ERR_ARG, "dgs_preprocess_ex: samples_binned with the capturable binning (capacity_E > 0) "
+                                 "needs DGS_BIN_SAMPLES_FIXED");
     return preprocess_body(P, D, N, means, covariances, conics, samples, grid, grid_offset, radii, alloc,
                            alloc_ctx, num_rendered, stream, debug, nullptr, nullptr, nullptr, nullptr, present,
                            area, opts);

@@ -273,7 +273,7 @@ std::tuple<Tensor, Tensor, Tensor, Tensor, Tensor, Tensor, Tensor>
 PreprocessCapturableCUDA(const Tensor &means, const Tensor &values, const Tensor &covariances, const Tensor &conics,
                          const Tensor &samples, std::vector<int> grid, std::vector<float> offset,
                          std::vector<int64_t> capacity, const bool debug,
-                         const c10::optional<Tensor> &status_in) {
+                         const c10::optional<Tensor> &status_in, const c10::optional<Tensor> &samples_binned) {
     TORCH_CHECK(capacity.size() == 3 && capacity[0] > 0 && capacity[2] > 0 && capacity[1] >= 0,
                 "capacity must be [E > 0, Es >= 0, R > 0]");
     Tensor rdev = torch::zeros({1}, means.options().dtype(torch::kInt64));
@@ -288,6 +288,14 @@ PreprocessCapturableCUDA(const Tensor &means, const Tensor &values, const Tensor
         o.flags = DGS_BIN_STATUS_STICKY;
     } else {
         status = torch::zeros({1}, means.options().dtype(torch::kInt32));
+    }
+    if (samples_binned.has_value() && samples_binned->defined()) {  // fixed samples (the caller's word)
+        TORCH_CHECK(samples_binned->scalar_type() == torch::kUInt8 && samples_binned->is_cuda() &&
+                        samples_binned->is_contiguous(),
+                    "samples_binned must be the sample_binning_buffer of an eager binning of these samples");
+        o.samples_binned = samples_binned->data_ptr();
+        o.samples_binned_bytes = (size_t)samples_binned->numel();
+        o.flags |= DGS_BIN_SAMPLES_FIXED;
     }
     o.capacity_E = capacity[0];
     o.capacity_Es = std::min(capacity[1], capacity[0]);

@@ -105,7 +105,13 @@ enum {
     /* the capturable binning ORs its status into *status_device instead of storing it: a
      * status word allocated once, outside the captured step, then records every overflow of
      * every replay until the caller clears it (diff_gaussian_sampling.BinningStatusMonitor) */
-    DGS_BIN_STATUS_STICKY = 1
+    DGS_BIN_STATUS_STICKY = 1,
+    /* the capturable binning with samples_binned: the caller guarantees that the samples hold, at
+     * every replay, the values they had when samples_binned's binning was made (a training loop's
+     * fixed collocation points), and keeps that buffer allocated as long as the graph.  The
+     * captured binning then copies the sample side instead of sorting the samples at every replay,
+     * and status bit 8 (the samples' own grid) is not computed. */
+    DGS_BIN_SAMPLES_FIXED = 2
 };
 
 /* Options of dgs_preprocess_ex (zero-initialise, set struct_size = sizeof(dgs_bin_options), then
@@ -113,7 +119,7 @@ enum {
  * refused with DGS_ERR_ARG). */
 typedef struct dgs_bin_options {
     uint32_t struct_size;
-    uint32_t flags; /* DGS_BIN_STATUS_STICKY */
+    uint32_t flags; /* DGS_BIN_STATUS_STICKY, DGS_BIN_SAMPLES_FIXED */
     /* device uint8[P] or NULL.  Gaussians with present[g] == 0 are left out of the binning the
      * way a det == 0 Gaussian is (radius 0, no tiles, no pairs; radii[g] = 0 and they do not
      * count in num_rendered).  A rank of a spatially sharded run bins only the rows it holds
@@ -147,8 +153,8 @@ typedef struct dgs_bin_options {
      * recomputed: the samples' sort, cell keys and boxes, ~0.15 ms of a 1M x 2M binning, are
      * skipped.  Results are bit-identical either way.  The caller vouches for the contents (the
      * torch layer: the samples tensor's identity and version counter); otherwise it is
-     * ignored.  Not with the capturable form (capacity_E > 0: a replay cannot see whether the
-     * captured samples changed). */
+     * ignored.  With the capturable form (capacity_E > 0) only under DGS_BIN_SAMPLES_FIXED: a
+     * replay cannot see whether the captured samples changed. */
     const void *samples_binned;
     size_t samples_binned_bytes;
 } dgs_bin_options;

@@ -72,12 +72,14 @@ def forward_backward(fname):
     assert not torch.equal(new_out, ref_out)
 
 
-def rebin_step(fname):
+def rebin_step(fname, fixed=False):
     """the whole PIGS step -- re-binning (preprocess_gaussians_capturable),
     forward, loss and loss.backward() into .grad -- captured as ONE graph with torch's
     whole-network recipe (warm-up on a side stream, grads set to None before the capture), then
     replayed after in-place steps of the means (the optimizer's move): every replay must match an
-    eager preprocess + forward + backward of the moved means at the parity bound, with status 0."""
+    eager preprocess + forward + backward of the moved means at the parity bound, with status 0.
+    fixed: the captured binning copies the sample side of the first eager binning
+    (samples_binned, DGS_BIN_SAMPLES_FIXED) instead of sorting the unchanged samples per replay."""
     dev = torch.device("cuda")
     P, N, C = 20000, 60000, 1
     means, values, covs, conics = (t.to(dev) for t in syn.gaussians(P, 2, C, seed=3))
@@ -93,7 +95,8 @@ def rebin_step(fname):
 
     def step():
         R, gb, sb, rg, srg, _, st = dgs.preprocess_gaussians_capturable(means.detach(), values.detach(), covs,
-                                                                         conics.detach(), samples, grid, off, cap)
+                                                                         conics.detach(), samples, grid, off, cap,
+                                                                         samples_binned=sb0 if fixed else None)
         out = fwd(means, values, conics, samples, cap[2], gb, sb, rg, srg, False)
         (out - target).square().sum().backward()
         return out, st, R
@@ -239,7 +242,7 @@ if __name__ == "__main__":
     if sys.argv[1] == "forward_backward":
         forward_backward(sys.argv[2])
     elif sys.argv[1] == "rebin_step":
-        rebin_step(sys.argv[2])
+        rebin_step(sys.argv[2], fixed=len(sys.argv) > 3 and sys.argv[3] == "fixed")
     elif sys.argv[1] == "overflow_monitor":
         overflow_monitor()
     else:

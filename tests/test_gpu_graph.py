@@ -41,6 +41,12 @@ def test_graph_capture_rebin_step(fname):
     _child("rebin_step", fname)
 
 
+def test_graph_capture_rebin_step_fixed_samples():
+    """The same with the captured binning copying an eager binning's sample side at every replay
+    (preprocess_gaussians_capturable(samples_binned=...): fixed collocation points)."""
+    _child("rebin_step", "gaussian", "fixed")
+
+
 def test_graph_capture_requires_binned_tensors():
     _child("requires_binned")
 
