@@ -42,7 +42,7 @@ def main(root, key, note):
     out = {}
     for what, prefixes, excl in (("forward_render", ["void dgs::k_forward_s<", "void dgs::k_forward_t<",
                                                      "void dgs::k_forward_mx<"], ("true>",)),
-                                 ("backward_render", ["void dgs::k_backward<"], ())):
+                                 ("backward_render", ["void dgs::k_backward<", "void dgs::k_backward_mx<"], ())):
         name, c = pick(k, prefixes, excl)
         if name is None or "FETCH_SIZE" not in c or "WRITE_SIZE" not in c:
             continue
