@@ -35,7 +35,8 @@ import sys
 import time
 
 REPO = os.path.dirname(os.path.abspath(__file__))
-sys.path.insert(0, os.path.join(REPO, "diff-gaussian-sampling_amd"))
+# (DGS_TEST_PKG_ROOT: time a tools/variant.sh build, variants/NAME, as the tests can)
+sys.path.insert(0, os.environ.get("DGS_TEST_PKG_ROOT") or os.path.join(REPO, "diff-gaussian-sampling_amd"))
 sys.path.insert(0, REPO)
 
 PEAK_FP32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: peak FP32 vector (= f32 MFMA) rate

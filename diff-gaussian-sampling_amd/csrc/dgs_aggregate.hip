@@ -822,6 +822,16 @@ __device__ __forceinline__ float dot_row(const float *__restrict__ q, const floa
     for (int k = 0; k < K; ++k) v += q[k] * row[k];
     return v;
 }
+// The same sum, order and roundings for a compile-time length: the LDS row is then read as
+// 16-byte pieces (a lane's row at a stride of SK floats; the runtime loop's 4-byte reads at that
+// stride were 4-way bank conflicts, PMC SQ_LDS_BANK_CONFLICT).
+template <int N>
+__device__ __forceinline__ float dot_fixed(const float *__restrict__ q, const float *row) {
+    float v = 0.0f;
+#pragma unroll
+    for (int k = 0; k < N; ++k) v += q[k] * row[k];
+    return v;
+}
 
 // Pipelined staging (L, K <= 16, 16-byte rows: at most 4 pieces of each row array per lane):
 // the next batch's pieces are loaded into registers before the current batch's arithmetic
@@ -906,7 +916,7 @@ __global__ __launch_bounds__(kBlock) void k_agg_forward_s(AggArgs A, AggStage G)
         // one slot of the batch: weight, embedding, factor and the lane's share of a
         auto slot = [&](int64_t s, int64_t idx, const float *X, float dn) {
             if (idx >= 0) {
-                const float weight = dot_row(q, sk + lane * G.SK, K);
+                const float weight = K == NB ? dot_fixed<NB>(q, sk + lane * G.SK) : dot_row(q, sk + lane * G.SK, K);
                 float emb, fac;
                 agg_embed(D, F, E, A.freq, A.dt, X, &emb, &fac);
                 A.weights[s] = weight;
@@ -1097,7 +1107,12 @@ __global__ __launch_bounds__(kBlock) void k_agg_backward_s(AggArgs A, AggStage G
                 const float dc = dn * inv;
                 const float dcw = dc * wt;
                 float S2 = 0.0f;
-                for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
+                if (L == NB) {  // (16-byte LDS reads of the lane's row: see dot_fixed)
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) S2 += st[j] * feat[j];
+                } else {
+                    for (int j = 0; j < L; ++j) S2 += st[j] * feat[j];
+                }
                 te = (dc * emb) * S1 + (dc * fac) * S2;  // sum_j te_j
                 c = dcw * fac;
                 const float dwe = dcw * emb, dwf = dcw * fac;
