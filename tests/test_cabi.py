@@ -114,3 +114,64 @@ def test_volume_host_validation(lib):
     p = lib.dgs_volume_preprocess
     p.restype = ctypes.c_int
     assert p(-1, 1, None, None, None, None, None, None, 0) == DGS_ERR_ARG
+
+
+class BinOptions(ctypes.Structure):
+    """dgs_bin_options (include/dgs.h, ABI 12)."""
+    _fields_ = [("struct_size", ctypes.c_uint32), ("flags", ctypes.c_uint32), ("present", ctypes.c_void_p),
+                ("sample_area", ctypes.c_double), ("capacity_E", ctypes.c_int64), ("capacity_Es", ctypes.c_int64),
+                ("capacity_R", ctypes.c_int64), ("num_rendered_device", ctypes.c_void_p),
+                ("status_device", ctypes.c_void_p), ("samples_binned", ctypes.c_void_p),
+                ("samples_binned_bytes", ctypes.c_size_t)]
+
+
+def test_bin_options_layout_and_validation(lib, tmp_path):
+    """dgs_bin_options as C lays it out, and the option checks of dgs_preprocess_ex /
+    dgs_preprocess_auto_ex (ABI 12: samples_binned, DGS_BIN_SAMPLES_FIXED), all before any device
+    work: a struct of another size, flags on the auto form, samples_binned with the capturable form
+    but without DGS_BIN_SAMPLES_FIXED."""
+    import subprocess
+    src = tmp_path / "s.c"
+    src.write_text('#include <stdio.h>\n#include "dgs.h"\n'
+                   'int main(void) { printf("%zu %d %d\\n", sizeof(dgs_bin_options), DGS_ABI_VERSION, '
+                   'DGS_BIN_SAMPLES_FIXED); return 0; }\n')
+    exe = tmp_path / "s"
+    r = subprocess.run(["gcc", "-std=c99", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    size, abi, fixed = map(int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
+    assert size == ctypes.sizeof(BinOptions) and fixed == 2
+    lib.dgs_version.restype = ctypes.c_int
+    assert lib.dgs_version() == abi == 12
+    lib.dgs_last_error.restype = ctypes.c_char_p
+    alloc_t = ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t)
+    alloc = alloc_t(lambda ctx, which, nbytes: None)  # (never reached)
+    nr = ctypes.c_int64(0)
+    grid = (ctypes.c_int * 2)()
+    off = (ctypes.c_float * 2)()
+    auto = lib.dgs_preprocess_auto_ex
+    auto.restype = ctypes.c_int
+    P = ctypes.c_void_p
+    auto.argtypes = [ctypes.c_int] * 3 + [P] * 4 + [ctypes.POINTER(BinOptions), P, alloc_t, P, P, P, P, P, ctypes.c_int]
+    o = BinOptions()
+    o.struct_size = ctypes.sizeof(BinOptions) - 8
+    args = lambda opts: (10, 2, 10, None, None, None, None, ctypes.byref(opts), None, alloc, None,  # noqa: E731
+                         ctypes.byref(nr), grid, off, None, 0)
+    assert auto(*args(o)) == DGS_ERR_ARG and b"struct_size" in lib.dgs_last_error()
+    o.struct_size = ctypes.sizeof(BinOptions)
+    o.flags = 1
+    assert auto(*args(o)) == DGS_ERR_ARG and b"flags" in lib.dgs_last_error()
+    ex = lib.dgs_preprocess_ex
+    ex.restype = ctypes.c_int
+    ex.argtypes = [ctypes.c_int] * 3 + [P] * 6 + [ctypes.POINTER(BinOptions), P, alloc_t, P, P, P, ctypes.c_int]
+    o.flags = 0
+    o.capacity_E, o.capacity_Es, o.capacity_R = 100, 10, 100
+    o.samples_binned, o.samples_binned_bytes = 4096, 4096
+    assert ex(10, 2, 10, None, None, None, None, grid, off, ctypes.byref(o), None, alloc, None,
+              ctypes.byref(nr), None, 0) == DGS_ERR_ARG
+    assert b"DGS_BIN_SAMPLES_FIXED" in lib.dgs_last_error()
+    o.flags = 4
+    assert ex(10, 2, 10, None, None, None, None, grid, off, ctypes.byref(o), None, alloc, None,
+              ctypes.byref(nr), None, 0) == DGS_ERR_ARG and b"flags" in lib.dgs_last_error()
+    lib.dgs_sample_reuse_count.restype = ctypes.c_int64
+    assert lib.dgs_sample_reuse_count() >= 0
