@@ -407,7 +407,8 @@ def test_preprocess_speculation_per_sample_set(dgs, oracle):
         both(inplace)
 
 
-def test_sample_side_reuse(dgs):
+@pytest.mark.parametrize("D", [1, 2])
+def test_sample_side_reuse(dgs, D):
     """Re-binning the same, unchanged samples tensor copies the previous binning's sample side
     (dgs_bin_options.samples_binned; dgs_sample_reuse_count counts it): num_rendered, both range
     arrays, the radii and the forward equal a fresh binning's (of a clone of the samples: another
@@ -419,9 +420,9 @@ def test_sample_side_reuse(dgs):
     lib = ctypes.CDLL(os.path.join(os.path.dirname(dgs.__file__), "libdgs.so"))
     lib.dgs_sample_reuse_count.restype = ctypes.c_int64
     dev = torch.device("cuda:0")
-    means, values, covs, conics = syn.gaussians(3000, 2, 3, seed=91)
+    means, values, covs, conics = syn.gaussians(3000, D, 3, seed=91)
     m, v, cv, c = (t.to(dev) for t in (means, values, covs, conics))
-    s = syn.samples(20000, 2, seed=92).to(dev)
+    s = syn.samples(20000, D, seed=92).to(dev)
     dL = syn.grad_out(20000, 1, 3, seed=93).to(dev)
 
     def run(samples, mm):
